@@ -1,0 +1,198 @@
+"""ctypes binding of oracle/_build/liboracle.so -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import
+this module, and only as the checker.  See oracle/oracle.h for the reference
+lines each function restates.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+F32P = np.ctypeslib.ndpointer(np.float32, flags='C_CONTIGUOUS')
+I32P = np.ctypeslib.ndpointer(np.int32, flags='C_CONTIGUOUS')
+I64P = np.ctypeslib.ndpointer(np.int64, flags='C_CONTIGUOUS')
+
+
+class Model(C.Structure):
+    _fields_ = [
+        ('initialDistribution', C.c_float * 5),
+        ('transProb', C.c_float * 25),
+        ('matchProb', C.c_float * 65536),
+        ('insProb', C.c_float * 1280),
+        ('local_transProb', C.c_float * 9),
+        ('random_transProb', C.c_float * 2),
+    ]
+
+
+def build():
+    subprocess.check_call(['make', '-s', '-C', _HERE, 'oracle'])
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, '_build', 'liboracle.so')
+        if not os.path.exists(path):
+            build()
+        L = C.CDLL(path)
+        L.orc_model_init.argtypes = [C.POINTER(Model), C.c_float]
+        L.orc_forward.argtypes = [C.POINTER(Model), C.c_char_p, C.c_int, C.c_char_p, C.c_int, C.c_int, F32P]
+        L.orc_backward.argtypes = L.orc_forward.argtypes
+        L.orc_total.argtypes = [C.POINTER(Model), C.c_char_p, C.c_int, C.c_char_p, C.c_int, F32P, F32P, C.c_int]
+        L.orc_total.restype = C.c_float
+        L.orc_posterior.argtypes = [C.POINTER(Model), C.c_char_p, C.c_int, C.c_char_p, C.c_int, F32P, F32P, C.c_int, F32P]
+        L.orc_pf_posterior.argtypes = [C.c_char_p, C.c_int, C.c_char_p, C.c_int, F32P]
+        L.orc_pair_posterior.argtypes = [C.POINTER(Model), C.c_char_p, C.c_int, C.c_char_p, C.c_int, C.c_int, F32P]
+        L.orc_mea.argtypes = [C.c_int, C.c_int, F32P, C.c_char_p, C.POINTER(C.c_int)]
+        L.orc_mea.restype = C.c_float
+        L.orc_sparsify.argtypes = [C.c_int, C.c_int, F32P, I32P, C.c_void_p, C.c_void_p]
+        L.orc_sparsify.restype = C.c_int64
+        L.orc_relax.argtypes = [C.c_int, I32P, I64P, I64P, I32P, I32P, F32P, I32P, I64P, I32P, F32P, C.c_int64]
+        L.orc_relax.restype = C.c_int64
+        L.orc_viterbi.argtypes = [C.POINTER(Model), C.c_char_p, C.c_int, C.c_char_p, C.c_int, C.c_char_p, C.POINTER(C.c_int)]
+        L.orc_viterbi.restype = C.c_float
+        L.orc_model_adjustment.argtypes = [C.POINTER(Model), C.c_int, C.POINTER(C.c_char_p), I32P,
+                                           C.POINTER(C.c_float), C.POINTER(C.c_float)]
+        L.orc_pf_tables.argtypes = [np.ctypeslib.ndpointer(np.float64, flags='C_CONTIGUOUS'), I32P]
+        L.orc_pair_loop.argtypes = [C.POINTER(Model), C.c_int, C.POINTER(C.c_char_p), I32P, C.c_int,
+                                    C.c_int64, C.c_int, F32P, I64P]
+        L.orc_pair_loop.restype = C.c_int64
+        _LIB = L
+    return _LIB
+
+
+def model(delta=-1.0):
+    m = Model()
+    lib().orc_model_init(C.byref(m), float(delta))
+    return m
+
+
+def _s(seq):
+    return b'@' + seq.encode()
+
+
+def forward(m, s1, s2, flag):
+    out = np.empty((5 if flag else 3) * (len(s1) + 1) * (len(s2) + 1), np.float32)
+    lib().orc_forward(C.byref(m), _s(s1), len(s1), _s(s2), len(s2), int(flag), out)
+    return out
+
+
+def backward(m, s1, s2, flag):
+    out = np.empty((5 if flag else 3) * (len(s1) + 1) * (len(s2) + 1), np.float32)
+    lib().orc_backward(C.byref(m), _s(s1), len(s1), _s(s2), len(s2), int(flag), out)
+    return out
+
+
+def total(m, s1, s2, f, b, flag):
+    return lib().orc_total(C.byref(m), _s(s1), len(s1), _s(s2), len(s2), f, b, int(flag))
+
+
+def posterior(m, s1, s2, f, b, flag):
+    out = np.empty((len(s1) + 1) * (len(s2) + 1), np.float32)
+    lib().orc_posterior(C.byref(m), _s(s1), len(s1), _s(s2), len(s2), f, b, int(flag), out)
+    return out
+
+
+def pf_posterior(s1, s2):
+    out = np.empty((len(s1) + 1) * (len(s2) + 1), np.float32)
+    rc = lib().orc_pf_posterior(_s(s1), len(s1), _s(s2), len(s2), out)
+    if rc:
+        raise OverflowError('partition function overflow')
+    return out
+
+
+def pair_posterior(m, s1, s2, pid):
+    out = np.empty((len(s1) + 1) * (len(s2) + 1), np.float32)
+    lib().orc_pair_posterior(C.byref(m), _s(s1), len(s1), _s(s2), len(s2), int(pid), out)
+    return out
+
+
+def mea(L1, L2, post, with_path=False):
+    if with_path:
+        buf = C.create_string_buffer(L1 + L2 + 2)
+        n = C.c_int(0)
+        sc = lib().orc_mea(L1, L2, np.ascontiguousarray(post, np.float32), buf, C.byref(n))
+        return sc, buf.raw[: n.value].decode()
+    return lib().orc_mea(L1, L2, np.ascontiguousarray(post, np.float32), None, None)
+
+
+def sparsify(L1, L2, post):
+    post = np.ascontiguousarray(post, np.float32)
+    rp = np.zeros(L1 + 2, np.int32)
+    n = lib().orc_sparsify(L1, L2, post, rp, None, None)
+    cols = np.empty(max(n, 1), np.int32)
+    vals = np.empty(max(n, 1), np.float32)
+    lib().orc_sparsify(L1, L2, post, rp, cols.ctypes.data, vals.ctypes.data)
+    return rp, cols[:n], vals[:n]
+
+
+def viterbi(m, s1, s2):
+    buf = C.create_string_buffer(len(s1) + len(s2) + 2)
+    n = C.c_int(0)
+    sc = lib().orc_viterbi(C.byref(m), _s(s1), len(s1), _s(s2), len(s2), buf, C.byref(n))
+    return sc, buf.raw[: n.value].decode()
+
+
+def model_adjustment(m, seqs):
+    arr = (C.c_char_p * len(seqs))(*[_s(s) for s in seqs])
+    lens = np.array([len(s) for s in seqs], np.int32)
+    ident = C.c_float(0)
+    delta = C.c_float(0)
+    vm = lib().orc_model_adjustment(C.byref(m), len(seqs), arr, lens, C.byref(ident), C.byref(delta))
+    return vm, ident.value, delta.value
+
+
+def pf_tables():
+    sm = np.zeros((26, 26), np.float64)
+    si = np.zeros(26, np.int32)
+    lib().orc_pf_tables(sm, si)
+    return sm, si
+
+
+def pair_loop(m, seqs, pid, max_pairs=-1, threads=0):
+    arr = (C.c_char_p * len(seqs))(*[_s(s) for s in seqs])
+    lens = np.array([len(s) for s in seqs], np.int32)
+    P = len(seqs) * (len(seqs) - 1) // 2
+    if 0 <= max_pairs < P:
+        P = max_pairs
+    dist = np.zeros(max(P, 1), np.float32)
+    nnz = np.zeros(max(P, 1), np.int64)
+    tot = lib().orc_pair_loop(C.byref(m), len(seqs), arr, lens, int(pid), int(max_pairs), int(threads), dist, nnz)
+    return dist[:P], nnz[:P], tot
+
+
+def relax(lens, csrs):
+    """csrs: list over pairs (a<b row-major) of (rowptr[L_a+2], cols, vals)."""
+    N = len(lens)
+    lens = np.asarray(lens, np.int32)
+    row_off = np.zeros(len(csrs), np.int64)
+    ent_off = np.zeros(len(csrs), np.int64)
+    r = e = 0
+    for p, (rp, c, v) in enumerate(csrs):
+        row_off[p] = r
+        ent_off[p] = e
+        r += len(rp)
+        e += len(c)
+    in_rp = np.concatenate([c[0] for c in csrs]).astype(np.int32) if csrs else np.zeros(1, np.int32)
+    in_c = np.concatenate([c[1] for c in csrs] + [np.zeros(1, np.int32)]).astype(np.int32)
+    in_v = np.concatenate([c[2] for c in csrs] + [np.zeros(1, np.float32)]).astype(np.float32)
+    out_rp = np.zeros_like(in_rp)
+    out_off = np.zeros(max(len(csrs), 1), np.int64)
+    cap = max(e, 1)
+    out_c = np.zeros(cap, np.int32)
+    out_v = np.zeros(cap, np.float32)
+    tot = lib().orc_relax(N, lens, row_off, ent_off, in_rp, in_c, in_v, out_rp, out_off, out_c, out_v, cap)
+    assert tot >= 0
+    res = []
+    for p in range(len(csrs)):
+        a = row_off[p]
+        rp = out_rp[a: a + len(csrs[p][0])].copy()
+        o = out_off[p]
+        n = rp[-1]
+        res.append((rp, out_c[o:o + n].copy(), out_v[o:o + n].copy()))
+    return res
