@@ -1,0 +1,112 @@
+/* mlpgpu.h -- C ABI of libmlpgpu, the MI355X (gfx950) pairwise-posterior and
+ * consistency engine that replaces the hot path of kuangmeng/MLProbs'
+ * baseMSA/C_P_NP_Aln.
+ *
+ * The reference has no library boundary on this path: its pair loop calls
+ * C++ member functions of a shared ProbabilisticModel from OpenMP threads and
+ * keeps heap-allocated SparseMatrix objects.  Each entry
+ * point below names the reference code it replaces.  Plain pointers and sizes
+ * only; no C++ or torch types cross this boundary.
+ *
+ * Conventions
+ *  - A family is n sequences of uppercase letters 'A'..'Z' (gaps stripped,
+ *    as after MultiSequence::LoadMFA(..., true), CPNP/MSA.cpp:136).
+ *  - Pair index p enumerates (a, b), a < b, row-major: the order of the
+ *    reference's seqsPairs table (CPNP/MSA.cpp:907-919).
+ *  - The posterior of pair p is the sparse matrix sparseMatrices[a][b]
+ *    (CPNP/MSA.cpp:1023-1025): rows = residues 1..L_a of a, 1-based columns
+ *    of b, entries >= 0.01 (CPNP/SparseMatrix.h:14), columns ascending.
+ *  - Sparse set layout ("canonical CSR"): for pair p, row_ptr has L_a + 2
+ *    int32 entries at row offset R(p) = sum_{q<p} (L_{a_q} + 2); row i
+ *    (1..L_a) spans pair-local entries [row_ptr[i], row_ptr[i+1]);
+ *    row_ptr[0] = row_ptr[1] = 0.  Entries of all pairs are concatenated
+ *    in pair order; ent_off[p] is the first entry of pair p, ent_off[P]
+ *    the total.  Columns are uint16 (L <= 65535), values float.
+ *  - Every call returns MLP_OK (0) or an error code; never exit().
+ *    mlp_last_error() gives a message.  One context per host thread.
+ */
+#ifndef MLPGPU_H
+#define MLPGPU_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MLP_OK 0
+#define MLP_ERR_ARG 1       /* bad argument */
+#define MLP_ERR_HIP 2       /* HIP runtime / device error */
+#define MLP_ERR_OVERFLOW 3  /* partition function overflow (reference: exit(1), CPNP/MSAPartProbs.cpp:547-589) */
+#define MLP_ERR_STATE 4     /* call sequence error (e.g. no family loaded) */
+#define MLP_ERR_COMM 5      /* RCCL error */
+#define MLP_ERR_MEMORY 6    /* device allocation failed */
+
+typedef struct mlp_ctx mlp_ctx;
+
+/* Create a context bound to HIP device `device`. */
+int mlp_ctx_create(int device, mlp_ctx **out);
+void mlp_ctx_destroy(mlp_ctx *ctx);
+const char *mlp_last_error(const mlp_ctx *ctx);
+
+/* Upload a family (replaces the sequence side of MultiSequence, CPNP/MultiSequence.h:267-315).
+ * residues: concatenated uppercase letters; offsets[n+1] delimit sequence k. */
+int mlp_family_load(mlp_ctx *ctx, int n, const char *residues, const int64_t *offsets);
+int64_t mlp_family_npairs(const mlp_ctx *ctx);
+
+/* Posterior stage for pairs [p_begin, p_end) in pair order.  Replaces the
+ * body of the pdoAlign / ArrangePosteriorProbs pair loop
+ * (CPNP/MSA.cpp:927-1032, 1652-1765): per pid, the 5-state + partition
+ * function + local posteriors merged by RMS (pid 0/1), local only (pid 2) or
+ * partition function only (pid >= 3); the MEA distance
+ * 1 - score / min(L_a, L_b); and the sparse matrix (>= 0.01).
+ * delta = initDistrib[2] after ModelAdjustmentTest (CPNP/MSA.cpp:861-870).
+ * Results stay in device memory in the context's canonical CSR store. */
+int mlp_posteriors(mlp_ctx *ctx, int pid, float delta, int64_t p_begin, int64_t p_end);
+
+/* Per-pair scalars of pairs [p_begin, p_end) (host arrays, may be NULL):
+ * distance, MEA score, nnz. */
+int mlp_pair_results(mlp_ctx *ctx, int64_t p_begin, int64_t p_end, float *dist, float *mea,
+                     int64_t *nnz);
+
+/* Total entries of the canonical CSR store (all pairs currently held). */
+int mlp_csr_total(mlp_ctx *ctx, int64_t *total);
+/* Host copy of the full canonical CSR store (see layout above):
+ * row_ptr: sum_p (L_a + 2) int32; ent_off: P + 1 int64; cols/vals: total. */
+int mlp_csr_export(mlp_ctx *ctx, int32_t *row_ptr, int64_t *ent_off, uint16_t *cols, float *vals);
+/* Replace the store with host data in the same layout (e.g. to relax a
+ * sparse set computed elsewhere). */
+int mlp_csr_import(mlp_ctx *ctx, const int32_t *row_ptr, const int64_t *ent_off,
+                   const uint16_t *cols, const float *vals);
+
+/* `iters` rounds of the consistency transformation over the whole store.
+ * Replaces MSA::DoRelaxation x numConsistencyReps (CPNP/MSA.cpp:1041-1051,
+ * 1119-1129, 1172-1360).  With a communicator, each rank relaxes pairs
+ * [p_begin, p_end) of its shard (mlp_set_shard) and the new store is
+ * all-gathered after every round. */
+int mlp_relax(mlp_ctx *ctx, int iters);
+
+/* Multi-GPU (one process per GPU): RCCL over xGMI. */
+int mlp_comm_unique_id(unsigned char id[128]);
+int mlp_comm_init(mlp_ctx *ctx, const unsigned char id[128], int nranks, int rank);
+/* This rank's contiguous pair range (cost-balanced split). */
+int mlp_shard_range(mlp_ctx *ctx, int nranks, int rank, int64_t *p_begin, int64_t *p_end);
+/* After every rank ran mlp_posteriors on its shard: all-gather the CSR
+ * store and the per-pair scalars so every rank holds the whole family. */
+int mlp_allgather(mlp_ctx *ctx);
+
+/* Wait for all device work of the context. */
+int mlp_synchronize(mlp_ctx *ctx);
+
+/* Per-kernel device time accumulated since the last reset (HIP events on
+ * the context stream), enabled by mlp_profile(ctx, 1).  Kernel ids:
+ * 0 forward, 1 backward, 2 local totals, 3 merge/MEA/sparsify, 4 compact,
+ * 5 relax, 6 transpose, 7 filter, 8 allgather. */
+#define MLP_NKERNELS 9
+int mlp_profile(mlp_ctx *ctx, int enable);
+int mlp_kernel_times(mlp_ctx *ctx, double *ms, int64_t *launches, int64_t *cells);
+int mlp_profile_reset(mlp_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,48 @@
+"""Build libmlpgpu.so (HIP kernels for gfx950 + C-ABI host runtime) in-tree.
+
+    python -m mlprobs_amd.build
+
+hipcc flags: -ffp-contract=off keeps every float operation unfused so the
+DP reproduces the reference's scalar-SSE rounding sequence (no FMA); no
+fast-math; fp32 division / sqrt stay correctly rounded (hipcc default).
+"""
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, 'csrc')
+LIBDIR = os.path.join(HERE, 'lib')
+LIB = os.path.join(LIBDIR, 'libmlpgpu.so')
+SOURCES = ['posterior.hip', 'relax.hip', 'mlpgpu.cpp']
+HEADERS = ['mlp_kernels.h', 'mlp_numerics.h', 'mlp_params_default.inc']
+HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
+FLAGS = ['--offload-arch=gfx950', '-O3', '-ffp-contract=off', '-fno-fast-math', '-fPIC',
+         '-std=c++17', '-Wno-unused-result', '-Wno-unused-value']
+
+
+def _stale():
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(ROOT, 'include', 'mlpgpu.h')]
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(force=False, verbose=False):
+    if not force and not _stale():
+        return LIB
+    os.makedirs(LIBDIR, exist_ok=True)
+    cmd = [HIPCC] + FLAGS + ['-shared', '-I', os.path.join(ROOT, 'include')]
+    cmd += [os.path.join(CSRC, f) for f in SOURCES] + ['-lrccl', '-o', LIB + '.tmp']
+    if verbose:
+        print(' '.join(cmd))
+    subprocess.check_call(cmd)
+    os.replace(LIB + '.tmp', LIB)
+    return LIB
+
+
+if __name__ == '__main__':
+    build(force='--force' in sys.argv, verbose=True)
+    print(LIB)

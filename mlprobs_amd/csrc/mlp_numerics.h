@@ -1,0 +1,127 @@
+// mlp_numerics.h -- device-side log-space arithmetic for gfx950.
+//
+// Bit-faithful to the reference's scalar float sequence (CPNP/ScoreType.h):
+// every function below performs exactly the IEEE operations of its reference
+// counterpart, in the same order.  The translation unit MUST be compiled with
+// -ffp-contract=off (no FMA contraction) and without fast-math; fp32 division
+// and sqrt stay correctly rounded (hipcc default).  Branches of the reference
+// are expressed as selects so a wave never diverges inside the DP inner loop.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define MLP_LOG_ZERO (-2e20f)
+#define MLP_LOG_ONE (0.0f)
+
+// LOOKUP: log(1 + e^x) on [0, 7.5], piecewise cubic (CPNP/ScoreType.h:196-216).
+// Coefficients are selected, then the cubic is evaluated in the reference's
+// Horner order; d outside [0, 7.5) only occurs on lanes whose result is
+// discarded by mlp_log_add.
+__device__ __forceinline__ float mlp_lookup(float x) {
+  const bool p1 = x <= 1.00f, p2 = x <= 2.50f, p3 = x <= 4.50f;
+  const float a = p1 ? -0.009350833524763f : p2 ? -0.014532321752540f : p3 ? -0.004605031767994f : -0.000458661602210f;
+  const float b = p1 ? 0.130659527668286f : p2 ? 0.139942324101744f : p3 ? 0.063427417320019f : 0.009695946122598f;
+  const float c = p1 ? 0.498799810682272f : p2 ? 0.495635523139337f : p3 ? 0.695956496475118f : 0.930734667215156f;
+  const float d = p1 ? 0.693203116424741f : p2 ? 0.692140569840976f : p3 ? 0.514272634594009f : 0.168037164329057f;
+  return ((a * x + b) * x + c) * x + d;
+}
+
+// LOG_ADD (CPNP/ScoreType.h:279-285): exact LOG_ZERO sentinel test and the
+// 7.5 underflow cutoff; the result adds LOOKUP(hi - lo) to lo.
+__device__ __forceinline__ float mlp_log_add(float x, float y) {
+  const bool lt = x < y;
+  const float hi = lt ? y : x;
+  const float lo = lt ? x : y;
+  const float d = hi - lo;
+  const float r = mlp_lookup(d) + lo;
+  return (lo == MLP_LOG_ZERO || d >= 7.5f) ? hi : r;
+}
+
+// EXP (CPNP/ScoreType.h:36-68) for x <= 0 (the only domain the posterior
+// uses: min(LOG_ONE, .) clamps, CPNP/ProbabilisticModel.h:484).  The quartic
+// runs in double on the float argument, like the reference.
+__device__ __forceinline__ float mlp_exp_nonpos(float xf) {
+  const double x = (double)xf;
+  double c4, c3, c2, c1, c0;
+  if (x > -2) {
+    if (x > -0.5) {
+      c4 = 0.03254409303190190000; c3 = 0.16280432765779600000; c2 = 0.49929760485974900000;
+      c1 = 0.99995149601363700000; c0 = 0.99999925508501600000;
+    } else if (x > -1) {
+      c4 = 0.01973899026052090000; c3 = 0.13822379685007000000; c2 = 0.48056651562365000000;
+      c1 = 0.99326940370383500000; c0 = 0.99906756856399500000;
+    } else {
+      c4 = 0.00940528203591384000; c3 = 0.09414963667859410000; c2 = 0.40825793595877300000;
+      c1 = 0.93933625499130400000; c0 = 0.98369508190545300000;
+    }
+  } else if (x > -8) {
+    if (x > -4) {
+      c4 = 0.00217245711583303000; c3 = 0.03484829428350620000; c2 = 0.22118199801337800000;
+      c1 = 0.67049462206469500000; c0 = 0.83556950223398500000;
+    } else {
+      c4 = 0.00012398771025456900; c3 = 0.00349155785951272000; c2 = 0.03727721426017900000;
+      c1 = 0.17974997741536900000; c0 = 0.33249299994217400000;
+    }
+  } else {
+    c4 = 0.00000051741713416603; c3 = 0.00002721456879608080; c2 = 0.00053418601865636800;
+    c1 = 0.00464101989351936000; c0 = 0.01507447981459420000;
+  }
+  const float r = (float)((((c4 * x + c3) * x + c2) * x + c1) * x + c0);
+  return (x > -16) ? r : 0.0f;
+}
+
+// Posterior from (f + b) and the pair total (CPNP/ProbabilisticModel.h:484):
+// EXP(min(LOG_ONE, (f + b) - T)); `s` is the stored float sum f + b.
+__device__ __forceinline__ float mlp_post_from_sum(float s, float T) {
+  const float v = s - T;
+  return mlp_exp_nonpos(v < MLP_LOG_ONE ? v : MLP_LOG_ONE);
+}
+
+// ---- wave-level neighbour exchange (DPP wave shifts, gfx9 family) --------
+// lane l receives lane l-1's value; lane 0 keeps `old`.
+__device__ __forceinline__ float mlp_shr1(float v, float old) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(v), 0x138, 0xf, 0xf, false));
+}
+__device__ __forceinline__ int mlp_shr1i(int v, int old) {
+  return __builtin_amdgcn_update_dpp(old, v, 0x138, 0xf, 0xf, false);
+}
+// lane l receives lane l+1's value; lane 63 keeps `old`.
+__device__ __forceinline__ float mlp_shl1(float v, float old) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(v), 0x130, 0xf, 0xf, false));
+}
+__device__ __forceinline__ int mlp_shl1i(int v, int old) {
+  return __builtin_amdgcn_update_dpp(old, v, 0x130, 0xf, 0xf, false);
+}
+__device__ __forceinline__ double mlp_shr1d(double v, double old) {
+  const int2 vv = *reinterpret_cast<const int2*>(&v), oo = *reinterpret_cast<const int2*>(&old);
+  int2 r;
+  r.x = __builtin_amdgcn_update_dpp(oo.x, vv.x, 0x138, 0xf, 0xf, false);
+  r.y = __builtin_amdgcn_update_dpp(oo.y, vv.y, 0x138, 0xf, 0xf, false);
+  return *reinterpret_cast<double*>(&r);
+}
+__device__ __forceinline__ double mlp_shl1d(double v, double old) {
+  const int2 vv = *reinterpret_cast<const int2*>(&v), oo = *reinterpret_cast<const int2*>(&old);
+  int2 r;
+  r.x = __builtin_amdgcn_update_dpp(oo.x, vv.x, 0x130, 0xf, 0xf, false);
+  r.y = __builtin_amdgcn_update_dpp(oo.y, vv.y, 0x130, 0xf, 0xf, false);
+  return *reinterpret_cast<double*>(&r);
+}
+
+// ---- scaled fp64 for the partition function ------------------------------
+// The reference runs the partition function in x87 long double
+// (CPNP/MSAPartProbs.cpp).  We run it in fp64 with a per-lane power-of-two
+// frame: stored value = true value * 2^(-MLP_PF_STEP * e).  Power-of-two
+// rescaling is exact, so every product/sum rounds like unscaled fp64.
+#define MLP_PF_STEP 200
+#define MLP_PF_HUGE 0x1p200
+// Packed storage of (value, e): e in the 8 low mantissa bits (2^-44 rel.).
+__device__ __forceinline__ double mlp_pf_pack(double v, int e) {
+  unsigned long long b = (unsigned long long)__double_as_longlong(v);
+  b = (b & ~0xFFull) | (unsigned long long)(e & 0xFF);
+  return __longlong_as_double((long long)b);
+}
+__device__ __forceinline__ double mlp_pf_unpack(double p, int* e) {
+  unsigned long long b = (unsigned long long)__double_as_longlong(p);
+  *e = (int)(b & 0xFF);
+  return __longlong_as_double((long long)(b & ~0xFFull));
+}

@@ -1,0 +1,933 @@
+// mlpgpu.cpp -- host runtime of libmlpgpu (C ABI in include/mlpgpu.h).
+//
+// Owns the device-resident family (residues, canonical CSR store, per-pair
+// scalars), the batch scratch for the posterior pipeline, the relaxation
+// buffers and the optional RCCL communicator.  The pipeline per batch is
+//   k_forward -> k_backward -> k_local_totals -> k_merge -> k_compact
+// (posterior.hip) and per relaxation round k_transpose -> k_relax ->
+// k_filter (relax.hip).  Parameter tables are built on the host exactly as
+// the reference builds them (CPNP/MSA.cpp:444-500, ProbabilisticModel.h:58-135,
+// MSAReadMatrix.cpp:85-116) and are bit-identical to the reference's
+// (tests/test_lib.py::test_tables).
+#include "../../include/mlpgpu.h"
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cctype>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "mlp_kernels.h"
+#include "mlp_params_default.inc"
+
+using namespace mlp;
+
+namespace {
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+};
+
+enum KernelId { KFWD = 0, KBWD, KTOT, KMERGE, KCOMPACT, KRELAX, KTRANS, KFILTER, KGATHER };
+
+}  // namespace
+
+struct mlp_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  // parameter tables
+  Tables* d_tables = nullptr;
+  Tables h_tables;
+  // family
+  int n = 0;
+  int max_len = 0;
+  int64_t P = 0;
+  std::vector<int32_t> lens;
+  std::vector<int64_t> offs;
+  std::vector<int32_t> pa, pb;        // per pair
+  std::vector<int64_t> rp_off;        // canonical row_ptr offsets (P + 1)
+  std::vector<int64_t> trp_off;       // transposed row_ptr offsets (P + 1)
+  uint8_t* d_res = nullptr;
+  int64_t* d_off = nullptr;
+  int32_t* d_len = nullptr;
+  int64_t* d_rp_off = nullptr;
+  int64_t* d_trp_off = nullptr;
+  // canonical CSR store
+  int32_t* d_rowptr = nullptr;        // rp_off[P] ints
+  int64_t* d_ent_off = nullptr;       // P + 1
+  uint16_t* d_cols = nullptr;
+  float* d_vals = nullptr;
+  int64_t ent_cap = 0;
+  std::vector<int64_t> ent_off;       // host mirror (P + 1)
+  int64_t store_p0 = 0, store_p1 = 0; // pairs currently held (contiguous)
+  int64_t store_total = 0;
+  std::vector<float> dist, mea;
+  std::vector<int64_t> nnz;
+  // batch scratch
+  DevBuf scratch;
+  size_t scratch_budget = 0;
+  // relaxation buffers
+  DevBuf r_trowptr, r_tcols, r_tvals, r_raw, r_newrp, r_newcols, r_newvals, r_tasks_p, r_tasks_r,
+      r_pairs, r_nnz, r_newoff;
+  // comm
+  ncclComm_t comm = nullptr;
+  int nranks = 1, rank = 0;
+  // profiling
+  bool profile = false;
+  double kms[MLP_NKERNELS] = {0};
+  int64_t klaunch[MLP_NKERNELS] = {0};
+  int64_t kcells[MLP_NKERNELS] = {0};
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+};
+
+// ------------------------------------------------------------------ helpers
+#define HIPCHK(ctx, expr)                                                          \
+  do {                                                                             \
+    hipError_t e_ = (expr);                                                        \
+    if (e_ != hipSuccess) {                                                        \
+      (ctx)->err = std::string(#expr) + ": " + hipGetErrorString(e_);              \
+      return MLP_ERR_HIP;                                                          \
+    }                                                                              \
+  } while (0)
+
+#define NCCLCHK(ctx, expr)                                                         \
+  do {                                                                             \
+    ncclResult_t r_ = (expr);                                                      \
+    if (r_ != ncclSuccess) {                                                       \
+      (ctx)->err = std::string(#expr) + ": " + ncclGetErrorString(r_);             \
+      return MLP_ERR_COMM;                                                         \
+    }                                                                              \
+  } while (0)
+
+static int ensure(mlp_ctx* c, DevBuf& b, size_t bytes) {
+  if (b.bytes >= bytes) return MLP_OK;
+  if (b.p) hipFree(b.p);
+  b.p = nullptr;
+  b.bytes = 0;
+  size_t want = std::max<size_t>(bytes, 256);
+  if (hipMalloc(&b.p, want) != hipSuccess) {
+    c->err = "hipMalloc failed (" + std::to_string(want) + " bytes)";
+    b.p = nullptr;
+    return MLP_ERR_MEMORY;
+  }
+  b.bytes = want;
+  return MLP_OK;
+}
+
+template <class T>
+static int dalloc(mlp_ctx* c, T** p, size_t count) {
+  if (*p) hipFree(*p);
+  *p = nullptr;
+  if (hipMalloc((void**)p, std::max<size_t>(count, 1) * sizeof(T)) != hipSuccess) {
+    c->err = "hipMalloc failed";
+    *p = nullptr;
+    return MLP_ERR_MEMORY;
+  }
+  return MLP_OK;
+}
+
+struct Timer {
+  mlp_ctx* c;
+  int id;
+  int64_t cells;
+  Timer(mlp_ctx* c_, int id_, int64_t cells_) : c(c_), id(id_), cells(cells_) {
+    if (c->profile) hipEventRecord(c->ev0, c->stream);
+  }
+  ~Timer() {
+    if (!c->profile) return;
+    hipEventRecord(c->ev1, c->stream);
+    hipEventSynchronize(c->ev1);
+    float ms = 0;
+    hipEventElapsedTime(&ms, c->ev0, c->ev1);
+    c->kms[id] += ms;
+    c->klaunch[id] += 1;
+    c->kcells[id] += cells;
+  }
+};
+
+// Parameter tables exactly as the reference builds them.
+static void build_tables(Tables& T, ModelScalars& ms, float delta) {
+  static float emitPairs[256][256];
+  static float emitSingle[256];
+  for (int i = 0; i < 256; i++) {
+    emitSingle[i] = (float)1e-5;
+    for (int j = 0; j < 256; j++) emitPairs[i][j] = (float)1e-10;
+  }
+  float initDistrib[5], gapOpen[4], gapExtend[4];
+  memcpy(initDistrib, mlp_init_distrib, sizeof initDistrib);
+  memcpy(gapOpen, mlp_gap_open, sizeof gapOpen);
+  memcpy(gapExtend, mlp_gap_extend, sizeof gapExtend);
+  if (delta >= 0) initDistrib[2] = delta;
+  const char* alpha = MLP_ALPHABET;
+  int tri = 0;
+  for (int i = 0; i < 20; i++) {
+    unsigned char ui = (unsigned char)toupper(alpha[i]);
+    emitSingle[ui] = mlp_emit_single[i];
+    for (int j = 0; j <= i; j++, tri++) {
+      unsigned char uj = (unsigned char)toupper(alpha[j]);
+      emitPairs[ui][uj] = emitPairs[uj][ui] = mlp_emit_pairs_lower[tri];
+    }
+  }
+  // CPNP/ProbabilisticModel.h:75-99
+  float tm[5][5] = {{0}};
+  tm[0][0] = 1;
+  for (int i = 0; i < 2; i++) {
+    tm[0][2 * i + 1] = gapOpen[2 * i];
+    tm[0][2 * i + 2] = gapOpen[2 * i];
+    tm[0][0] -= (gapOpen[2 * i] + gapOpen[2 * i]);
+    tm[2 * i + 1][2 * i + 1] = gapExtend[2 * i];
+    tm[2 * i + 2][2 * i + 2] = gapExtend[2 * i];
+    tm[2 * i + 1][0] = 1 - gapExtend[2 * i];
+    tm[2 * i + 2][0] = 1 - gapExtend[2 * i];
+  }
+  for (int i = 0; i < 5; i++) {
+    ms.init[i] = logf(initDistrib[i]);
+    for (int j = 0; j < 5; j++) ms.t[i][j] = logf(tm[i][j]);
+  }
+  ms.init[2] = logf(initDistrib[1]);
+  float lt[3][3] = {{0}};
+  lt[0][0] = 1;
+  lt[0][1] = gapOpen[1];
+  lt[0][2] = gapOpen[1];
+  lt[0][0] -= (gapOpen[1] + gapOpen[1]);
+  lt[1][1] = gapExtend[1];
+  lt[2][2] = gapExtend[1];
+  lt[1][0] = 1 - gapExtend[1];
+  lt[2][0] = 1 - gapExtend[1];
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++) ms.lt[i][j] = logf(lt[i][j]);
+  ms.rt1 = logf(1 - initDistrib[2]);
+  for (int r = 0; r < 26; r++) {
+    T.ins[r] = logf(emitSingle['A' + r]);
+    for (int c = 0; c < 26; c++) T.match[r * 26 + c] = logf(emitPairs['A' + r]['A' + c]);
+  }
+  // Partition function (CPNP/MSAReadMatrix.cpp:85-116, MSAPartProbs.cpp:698-709)
+  const char* bases = MLP_GONNET_MONOMERS;
+  const int nb = (int)strlen(bases);
+  static double sm[26][26];
+  int si[26];
+  for (int i = 0; i < 26; i++) si[i] = -1;
+  for (int i = 0; i < nb; i++) si[bases[i] - 'A'] = i;
+  const float beta = (float)(1.0 / 5.0f);
+  int pos = 0;
+  for (int i = 0; i < nb; i++)
+    for (int j = 0; j <= i; j++) {
+      const double v = expf(beta * mlp_gonnet160_lower[pos++]);
+      sm[i][j] = sm[j][i] = v;
+    }
+  // J, O, U have subst_index -1 in the reference (an out-of-bounds read);
+  // they are scored as X here.
+  const int xi = si['X' - 'A'];
+  for (int r = 0; r < 26; r++)
+    for (int c = 0; c < 26; c++) {
+      const int a = si[r] >= 0 ? si[r] : xi, b = si[c] >= 0 ? si[c] : xi;
+      T.sub[r * 26 + c] = sm[a][b];
+    }
+  const double beta_d = beta;
+  ms.pf_open = exp(beta_d * -22.0);
+  ms.pf_ext = exp(beta_d * -1.0);
+}
+
+static int pair_cost_cells(const mlp_ctx* c, int64_t p) {
+  return (c->lens[c->pa[p]] + 1) * (c->lens[c->pb[p]] + 1);
+}
+
+// ------------------------------------------------------------------ C ABI
+extern "C" {
+
+int mlp_ctx_create(int device, mlp_ctx** out) {
+  if (!out) return MLP_ERR_ARG;
+  *out = nullptr;
+  mlp_ctx* c = new mlp_ctx();
+  c->device = device;
+  if (hipSetDevice(device) != hipSuccess) {
+    delete c;
+    return MLP_ERR_HIP;
+  }
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return MLP_ERR_HIP;
+  }
+  hipEventCreate(&c->ev0);
+  hipEventCreate(&c->ev1);
+  if (hipMalloc((void**)&c->d_tables, sizeof(Tables)) != hipSuccess) {
+    delete c;
+    return MLP_ERR_MEMORY;
+  }
+  size_t freeb = 0, total = 0;
+  hipMemGetInfo(&freeb, &total);
+  c->scratch_budget = std::min<size_t>(freeb / 3, (size_t)48 << 30);
+  if (const char* s = getenv("MLP_SCRATCH_GB")) c->scratch_budget = (size_t)(atof(s) * (1ull << 30));
+  *out = c;
+  return MLP_OK;
+}
+
+void mlp_ctx_destroy(mlp_ctx* c) {
+  if (!c) return;
+  hipSetDevice(c->device);
+  hipStreamSynchronize(c->stream);
+  void* ptrs[] = {c->d_tables, c->d_res, c->d_off, c->d_len, c->d_rp_off, c->d_trp_off,
+                  c->d_rowptr, c->d_ent_off, c->d_cols, c->d_vals};
+  for (void* p : ptrs)
+    if (p) hipFree(p);
+  DevBuf* bufs[] = {&c->scratch, &c->r_trowptr, &c->r_tcols, &c->r_tvals, &c->r_raw, &c->r_newrp,
+                    &c->r_newcols, &c->r_newvals, &c->r_tasks_p, &c->r_tasks_r, &c->r_pairs,
+                    &c->r_nnz, &c->r_newoff};
+  for (DevBuf* b : bufs)
+    if (b->p) hipFree(b->p);
+  if (c->comm) ncclCommDestroy(c->comm);
+  hipEventDestroy(c->ev0);
+  hipEventDestroy(c->ev1);
+  hipStreamDestroy(c->stream);
+  delete c;
+}
+
+const char* mlp_last_error(const mlp_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int mlp_family_load(mlp_ctx* c, int n, const char* residues, const int64_t* offsets) {
+  if (!c || n < 1 || !residues || !offsets) return MLP_ERR_ARG;
+  hipSetDevice(c->device);
+  c->n = n;
+  c->lens.assign(n, 0);
+  c->offs.assign(offsets, offsets + n + 1);
+  c->max_len = 0;
+  const int64_t tot = offsets[n];
+  std::vector<uint8_t> codes(std::max<int64_t>(tot, 1));
+  for (int k = 0; k < n; k++) {
+    const int64_t L = offsets[k + 1] - offsets[k];
+    if (L < 1 || L > 65535) {
+      c->err = "sequence length must be in [1, 65535]";
+      return MLP_ERR_ARG;
+    }
+    c->lens[k] = (int32_t)L;
+    c->max_len = std::max(c->max_len, (int)L);
+    for (int64_t q = offsets[k]; q < offsets[k + 1]; q++) {
+      const unsigned char ch = (unsigned char)residues[q];
+      if (ch < 'A' || ch > 'Z') {
+        c->err = "residues must be uppercase letters A-Z";
+        return MLP_ERR_ARG;
+      }
+      codes[q] = (uint8_t)(ch - 'A');
+    }
+  }
+  c->P = (int64_t)n * (n - 1) / 2;
+  c->pa.resize(c->P);
+  c->pb.resize(c->P);
+  c->rp_off.assign(c->P + 1, 0);
+  c->trp_off.assign(c->P + 1, 0);
+  int64_t p = 0;
+  for (int a = 0; a < n; a++)
+    for (int b = a + 1; b < n; b++, p++) {
+      c->pa[p] = a;
+      c->pb[p] = b;
+      c->rp_off[p + 1] = c->rp_off[p] + c->lens[a] + 2;
+      c->trp_off[p + 1] = c->trp_off[p] + c->lens[b] + 2;
+    }
+  int rc;
+  if ((rc = dalloc(c, &c->d_res, codes.size()))) return rc;
+  if ((rc = dalloc(c, &c->d_off, n + 1))) return rc;
+  if ((rc = dalloc(c, &c->d_len, n))) return rc;
+  if ((rc = dalloc(c, &c->d_rp_off, c->P + 1))) return rc;
+  if ((rc = dalloc(c, &c->d_trp_off, c->P + 1))) return rc;
+  if ((rc = dalloc(c, &c->d_rowptr, c->rp_off[c->P]))) return rc;
+  if ((rc = dalloc(c, &c->d_ent_off, c->P + 1))) return rc;
+  HIPCHK(c, hipMemcpy(c->d_res, codes.data(), codes.size(), hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(c->d_off, offsets, sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(c->d_len, c->lens.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(c->d_rp_off, c->rp_off.data(), sizeof(int64_t) * (c->P + 1), hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(c->d_trp_off, c->trp_off.data(), sizeof(int64_t) * (c->P + 1), hipMemcpyHostToDevice));
+  c->ent_off.assign(c->P + 1, 0);
+  c->dist.assign(c->P, 0.f);
+  c->mea.assign(c->P, 0.f);
+  c->nnz.assign(c->P, 0);
+  c->store_p0 = c->store_p1 = 0;
+  c->store_total = 0;
+  return MLP_OK;
+}
+
+int64_t mlp_family_npairs(const mlp_ctx* c) { return c ? c->P : 0; }
+
+// grow the entry store to hold `need` entries, keeping `keep` existing ones
+static int grow_store(mlp_ctx* c, int64_t need, int64_t keep) {
+  if (need <= c->ent_cap) return MLP_OK;
+  int64_t cap = std::max<int64_t>(need, c->ent_cap + c->ent_cap / 2);
+  uint16_t* nc = nullptr;
+  float* nv = nullptr;
+  if (hipMalloc((void**)&nc, sizeof(uint16_t) * cap) != hipSuccess ||
+      hipMalloc((void**)&nv, sizeof(float) * cap) != hipSuccess) {
+    if (nc) hipFree(nc);
+    c->err = "hipMalloc (CSR store) failed";
+    return MLP_ERR_MEMORY;
+  }
+  if (keep > 0) {
+    HIPCHK(c, hipMemcpyAsync(nc, c->d_cols, sizeof(uint16_t) * keep, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(nv, c->d_vals, sizeof(float) * keep, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
+  if (c->d_cols) hipFree(c->d_cols);
+  if (c->d_vals) hipFree(c->d_vals);
+  c->d_cols = nc;
+  c->d_vals = nv;
+  c->ent_cap = cap;
+  return MLP_OK;
+}
+
+int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
+  if (!c) return MLP_ERR_ARG;
+  if (c->n < 2) { c->err = "family needs >= 2 sequences"; return MLP_ERR_STATE; }
+  if (p0 < 0 || p1 > c->P || p0 > p1) { c->err = "bad pair range"; return MLP_ERR_ARG; }
+  if (p0 != c->store_p1 && !(c->store_p0 == c->store_p1)) {
+    c->err = "pair ranges must be appended contiguously";
+    return MLP_ERR_STATE;
+  }
+  hipSetDevice(c->device);
+  if (c->store_p0 == c->store_p1) {  // empty store: start at p0
+    c->store_p0 = c->store_p1 = p0;
+    c->store_total = 0;
+  }
+  ModelScalars ms;
+  build_tables(c->h_tables, ms, delta);
+  HIPCHK(c, hipMemcpyAsync(c->d_tables, &c->h_tables, sizeof(Tables), hipMemcpyHostToDevice, c->stream));
+  const int models = model_set_for_pid(pid);
+  SeqSet seqs{c->d_res, c->d_off, c->d_len};
+
+  int64_t p = p0;
+  while (p < p1) {
+    // ---- batch: contiguous pairs within the scratch budget
+    int64_t q = p, cells = 0, rm = 0, bnd = 0, rows = 0;
+    size_t bytes = 0;
+    const size_t per_slot = 6 * sizeof(int64_t) + 2 * sizeof(int32_t) + sizeof(PairRec) + 16;
+    while (q < p1) {
+      const int L1 = c->lens[c->pa[q]], L2 = c->lens[c->pb[q]];
+      const int64_t S = (L1 + 64) >> 6;
+      const int64_t cl = S * (L2 + 64) * 64;
+      const int64_t rmc = (int64_t)L1 * ((L2 + 3) & ~3);
+      const size_t add = cl * 20 + rmc * 8 + (L2 + 2) * (5 * 4 + 3 * 4 + 3 * 8 + 4 + 4) +
+                         (size_t)L1 * (kEll * 6 + 4) + per_slot;
+      if (q > p && bytes + add > c->scratch_budget) break;
+      bytes += add;
+      cells += cl;
+      rm += rmc;
+      bnd += L2 + 2;
+      rows += L1;
+      ++q;
+    }
+    const int64_t np = q - p;
+    // slot order: most expensive pair first (LPT) inside the batch
+    std::vector<int64_t> order(np);
+    std::iota(order.begin(), order.end(), p);
+    std::stable_sort(order.begin(), order.end(), [&](int64_t x, int64_t y) {
+      return pair_cost_cells(c, x) > pair_cost_cells(c, y);
+    });
+    std::vector<int32_t> h_pa(np), h_pb(np);
+    std::vector<int64_t> h_cell(np), h_rm(np), h_bnd(np), h_ell(np), h_entb(np), h_rpb(np);
+    // offsets follow pair order (so storage is independent of slot order)
+    std::vector<int64_t> cell_of(np), rm_of(np), bnd_of(np), ell_of(np);
+    {
+      int64_t co = 0, ro = 0, bo = 0, eo = 0;
+      for (int64_t k = 0; k < np; k++) {
+        const int L1 = c->lens[c->pa[p + k]], L2 = c->lens[c->pb[p + k]];
+        cell_of[k] = co;
+        rm_of[k] = ro;
+        bnd_of[k] = bo;
+        ell_of[k] = eo;
+        co += (int64_t)((L1 + 64) >> 6) * (L2 + 64) * 64;
+        ro += (int64_t)L1 * ((L2 + 3) & ~3);
+        bo += L2 + 2;
+        eo += L1;
+      }
+    }
+    for (int64_t s = 0; s < np; s++) {
+      const int64_t pp = order[s], k = pp - p;
+      h_pa[s] = c->pa[pp];
+      h_pb[s] = c->pb[pp];
+      h_cell[s] = cell_of[k];
+      h_rm[s] = rm_of[k];
+      h_bnd[s] = bnd_of[k];
+      h_ell[s] = ell_of[k];
+    }
+    // ---- carve scratch
+    size_t off = 0;
+    auto carve = [&](size_t b) {
+      size_t o = off;
+      off += (b + 255) & ~(size_t)255;
+      return o;
+    };
+    const size_t o_f5 = carve(cells * 4), o_fl = carve(cells * 4), o_pg = carve(cells * 4),
+                 o_zm = carve(cells * 8), o_chf = carve(rm * 4), o_chb = carve(rm * 4),
+                 o_b5 = carve(bnd * 20), o_bl = carve(bnd * 12), o_bz = carve(bnd * 24),
+                 o_be = carve(bnd * 4), o_bm = carve(bnd * 4), o_ec = carve(rows * kEll * 2),
+                 o_ev = carve(rows * kEll * 4), o_en = carve(rows * 4), o_pa = carve(np * 4),
+                 o_pb = carve(np * 4), o_cell = carve(np * 8), o_rm = carve(np * 8),
+                 o_bnd = carve(np * 8), o_ell = carve(np * 8), o_entb = carve(np * 8),
+                 o_rpb = carve(np * 8), o_rec = carve(np * sizeof(PairRec));
+    int rc;
+    if ((rc = ensure(c, c->scratch, off))) return rc;
+    char* base = (char*)c->scratch.p;
+    Scratch sc;
+    sc.f5 = (float*)(base + o_f5);
+    sc.fl = (float*)(base + o_fl);
+    sc.pg = (float*)(base + o_pg);
+    sc.zm = (double*)(base + o_zm);
+    sc.chf = (float*)(base + o_chf);
+    sc.chb = (float*)(base + o_chb);
+    sc.bnd5 = (float*)(base + o_b5);
+    sc.bndl = (float*)(base + o_bl);
+    sc.bndz = (double*)(base + o_bz);
+    sc.bnde = (int32_t*)(base + o_be);
+    sc.bndm = (float*)(base + o_bm);
+    sc.ell_col = (uint16_t*)(base + o_ec);
+    sc.ell_val = (float*)(base + o_ev);
+    sc.ell_cnt = (int32_t*)(base + o_en);
+    PairRec* d_rec = (PairRec*)(base + o_rec);
+    PairMeta pm;
+    pm.pa = (const int32_t*)(base + o_pa);
+    pm.pb = (const int32_t*)(base + o_pb);
+    pm.cell_off = (const int64_t*)(base + o_cell);
+    pm.rm_off = (const int64_t*)(base + o_rm);
+    pm.bnd_off = (const int64_t*)(base + o_bnd);
+    pm.ell_row = (const int64_t*)(base + o_ell);
+    HIPCHK(c, hipMemcpyAsync(base + o_pa, h_pa.data(), np * 4, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(base + o_pb, h_pb.data(), np * 4, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(base + o_cell, h_cell.data(), np * 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(base + o_rm, h_rm.data(), np * 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(base + o_bnd, h_bnd.data(), np * 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(base + o_ell, h_ell.data(), np * 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemsetAsync(d_rec, 0, np * sizeof(PairRec), c->stream));
+    int64_t bcells = 0;
+    for (int64_t k = p; k < q; k++) bcells += pair_cost_cells(c, k);
+    {
+      Timer t(c, KFWD, bcells);
+      HIPCHK(c, launch_forward(models, ms, c->d_tables, seqs, pm, d_rec, sc, np, c->stream));
+    }
+    {
+      Timer t(c, KBWD, bcells);
+      HIPCHK(c, launch_backward(models, ms, c->d_tables, seqs, pm, d_rec, sc, np, c->stream));
+    }
+    if (models & kLocal) {
+      Timer t(c, KTOT, bcells);
+      HIPCHK(c, launch_local_totals(seqs, pm, d_rec, sc, np, c->stream));
+    }
+    {
+      Timer t(c, KMERGE, bcells);
+      HIPCHK(c, launch_merge(models, pid, ms, seqs, pm, d_rec, sc, np, c->stream));
+    }
+    std::vector<PairRec> rec(np);
+    HIPCHK(c, hipMemcpyAsync(rec.data(), d_rec, np * sizeof(PairRec), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    for (int64_t s = 0; s < np; s++) {
+      if (rec[s].flags & 1) {
+        c->err = "partition function overflow (pair " + std::to_string(order[s]) + ")";
+        return MLP_ERR_OVERFLOW;
+      }
+      if (rec[s].flags & 2) {
+        c->err = "posterior row exceeds " + std::to_string(kEll) + " entries >= 0.01 (pair " +
+                 std::to_string(order[s]) + "); unsupported input";
+        return MLP_ERR_STATE;
+      }
+    }
+    // ---- canonical entry offsets (pair order) and compaction
+    std::vector<int64_t> slot_of(np);
+    for (int64_t s = 0; s < np; s++) slot_of[order[s] - p] = s;
+    int64_t run = c->store_total;
+    for (int64_t k = 0; k < np; k++) {
+      const int64_t s = slot_of[k];
+      const int64_t pp = p + k;
+      c->ent_off[pp] = run;
+      c->nnz[pp] = rec[s].nnz;
+      c->dist[pp] = rec[s].dist;
+      c->mea[pp] = rec[s].mea;
+      h_entb[s] = run;
+      h_rpb[s] = c->rp_off[pp];
+      run += rec[s].nnz;
+    }
+    c->ent_off[q] = run;
+    if ((rc = grow_store(c, run, c->store_total))) return rc;
+    HIPCHK(c, hipMemcpyAsync(base + o_entb, h_entb.data(), np * 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(base + o_rpb, h_rpb.data(), np * 8, hipMemcpyHostToDevice, c->stream));
+    {
+      Timer t(c, KCOMPACT, bcells);
+      HIPCHK(c, launch_compact(seqs, pm, d_rec, sc, (const int64_t*)(base + o_entb), c->d_rowptr,
+                               (const int64_t*)(base + o_rpb), c->d_cols, c->d_vals, np, c->stream));
+    }
+    c->store_total = run;
+    c->store_p1 = q;
+    p = q;
+  }
+  HIPCHK(c, hipMemcpyAsync(c->d_ent_off, c->ent_off.data(), sizeof(int64_t) * (c->P + 1),
+                           hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return MLP_OK;
+}
+
+int mlp_pair_results(mlp_ctx* c, int64_t p0, int64_t p1, float* dist, float* mea, int64_t* nnz) {
+  if (!c || p0 < 0 || p1 > c->P || p0 > p1) return MLP_ERR_ARG;
+  for (int64_t p = p0; p < p1; p++) {
+    if (dist) dist[p - p0] = c->dist[p];
+    if (mea) mea[p - p0] = c->mea[p];
+    if (nnz) nnz[p - p0] = c->nnz[p];
+  }
+  return MLP_OK;
+}
+
+int mlp_csr_total(mlp_ctx* c, int64_t* total) {
+  if (!c || !total) return MLP_ERR_ARG;
+  *total = c->store_total;
+  return MLP_OK;
+}
+
+int mlp_csr_export(mlp_ctx* c, int32_t* row_ptr, int64_t* ent_off, uint16_t* cols, float* vals) {
+  if (!c) return MLP_ERR_ARG;
+  hipSetDevice(c->device);
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (row_ptr) HIPCHK(c, hipMemcpy(row_ptr, c->d_rowptr, sizeof(int32_t) * c->rp_off[c->P], hipMemcpyDeviceToHost));
+  if (ent_off) memcpy(ent_off, c->ent_off.data(), sizeof(int64_t) * (c->P + 1));
+  if (cols && c->store_total) HIPCHK(c, hipMemcpy(cols, c->d_cols, sizeof(uint16_t) * c->store_total, hipMemcpyDeviceToHost));
+  if (vals && c->store_total) HIPCHK(c, hipMemcpy(vals, c->d_vals, sizeof(float) * c->store_total, hipMemcpyDeviceToHost));
+  return MLP_OK;
+}
+
+int mlp_csr_import(mlp_ctx* c, const int32_t* row_ptr, const int64_t* ent_off, const uint16_t* cols,
+                   const float* vals) {
+  if (!c || !row_ptr || !ent_off) return MLP_ERR_ARG;
+  if (c->n < 2) return MLP_ERR_STATE;
+  hipSetDevice(c->device);
+  const int64_t total = ent_off[c->P];
+  int rc;
+  if ((rc = grow_store(c, total, 0))) return rc;
+  HIPCHK(c, hipMemcpy(c->d_rowptr, row_ptr, sizeof(int32_t) * c->rp_off[c->P], hipMemcpyHostToDevice));
+  if (total) {
+    HIPCHK(c, hipMemcpy(c->d_cols, cols, sizeof(uint16_t) * total, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(c->d_vals, vals, sizeof(float) * total, hipMemcpyHostToDevice));
+  }
+  c->ent_off.assign(ent_off, ent_off + c->P + 1);
+  HIPCHK(c, hipMemcpy(c->d_ent_off, ent_off, sizeof(int64_t) * (c->P + 1), hipMemcpyHostToDevice));
+  for (int64_t p = 0; p < c->P; p++) c->nnz[p] = ent_off[p + 1] - ent_off[p];
+  c->store_p0 = 0;
+  c->store_p1 = c->P;
+  c->store_total = total;
+  return MLP_OK;
+}
+
+// ------------------------------------------------------------------ shards
+int mlp_shard_range(mlp_ctx* c, int nranks, int rank, int64_t* b, int64_t* e) {
+  if (!c || nranks < 1 || rank < 0 || rank >= nranks || !b || !e) return MLP_ERR_ARG;
+  // contiguous pair ranges balanced by DP cells
+  double total = 0;
+  for (int64_t p = 0; p < c->P; p++) total += pair_cost_cells(c, p);
+  auto cut = [&](int r) -> int64_t {
+    if (r <= 0) return 0;
+    if (r >= nranks) return c->P;
+    const double target = total * r / nranks;
+    double acc = 0;
+    for (int64_t p = 0; p < c->P; p++) {
+      if (acc >= target) return p;
+      acc += pair_cost_cells(c, p);
+    }
+    return c->P;
+  };
+  *b = cut(rank);
+  *e = cut(rank + 1);
+  return MLP_OK;
+}
+
+// ------------------------------------------------------------------ comm
+int mlp_comm_unique_id(unsigned char id[128]) {
+  ncclUniqueId u;
+  if (ncclGetUniqueId(&u) != ncclSuccess) return MLP_ERR_COMM;
+  static_assert(sizeof(u) == 128, "nccl id size");
+  memcpy(id, &u, 128);
+  return MLP_OK;
+}
+
+int mlp_comm_init(mlp_ctx* c, const unsigned char id[128], int nranks, int rank) {
+  if (!c || !id || nranks < 1 || rank < 0 || rank >= nranks) return MLP_ERR_ARG;
+  hipSetDevice(c->device);
+  ncclUniqueId u;
+  memcpy(&u, id, 128);
+  NCCLCHK(c, ncclCommInitRank(&c->comm, nranks, u, rank));
+  c->nranks = nranks;
+  c->rank = rank;
+  return MLP_OK;
+}
+
+// Every rank holds pairs [store_p0, store_p1) with entries from 0; after the
+// gather every rank holds [0, P) in canonical layout.
+int mlp_allgather(mlp_ctx* c) {
+  if (!c) return MLP_ERR_ARG;
+  if (!c->comm || c->nranks == 1) return MLP_OK;
+  hipSetDevice(c->device);
+  const int R = c->nranks;
+  Timer tm(c, KGATHER, 0);
+  // 1. exchange ranges and entry counts (tiny; through device memory)
+  std::vector<int64_t> mine = {c->store_p0, c->store_p1, c->store_total, 0};
+  int64_t* d_info = nullptr;
+  HIPCHK(c, hipMalloc((void**)&d_info, sizeof(int64_t) * 4 * R));
+  HIPCHK(c, hipMemcpyAsync(d_info + 4 * c->rank, mine.data(), 32, hipMemcpyHostToDevice, c->stream));
+  NCCLCHK(c, ncclAllGather(d_info + 4 * c->rank, d_info, 4, ncclInt64, c->comm, c->stream));
+  std::vector<int64_t> info(4 * R);
+  HIPCHK(c, hipMemcpyAsync(info.data(), d_info, sizeof(int64_t) * 4 * R, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  hipFree(d_info);
+  // ranges must tile [0, P) in rank order
+  std::vector<int64_t> ebase(R + 1, 0);
+  for (int r = 0; r < R; r++) {
+    if (info[4 * r] != (r == 0 ? 0 : info[4 * (r - 1) + 1])) {
+      c->err = "shards must tile the pair range in rank order";
+      return MLP_ERR_STATE;
+    }
+    ebase[r + 1] = ebase[r] + info[4 * r + 2];
+  }
+  if (info[4 * (R - 1) + 1] != c->P) {
+    c->err = "shards do not cover all pairs";
+    return MLP_ERR_STATE;
+  }
+  const int64_t total = ebase[R];
+  // 2. new entry arrays; my block moves to its global place
+  uint16_t* nc = nullptr;
+  float* nv = nullptr;
+  if (hipMalloc((void**)&nc, sizeof(uint16_t) * std::max<int64_t>(total, 1)) != hipSuccess ||
+      hipMalloc((void**)&nv, sizeof(float) * std::max<int64_t>(total, 1)) != hipSuccess) {
+    c->err = "hipMalloc (gather) failed";
+    return MLP_ERR_MEMORY;
+  }
+  // per-pair scalars through device memory
+  float* d_sc = nullptr;
+  int64_t* d_nz = nullptr;
+  HIPCHK(c, hipMalloc((void**)&d_sc, sizeof(float) * 2 * std::max<int64_t>(c->P, 1)));
+  HIPCHK(c, hipMalloc((void**)&d_nz, sizeof(int64_t) * std::max<int64_t>(c->P, 1)));
+  const int64_t mp0 = c->store_p0, mp1 = c->store_p1;
+  HIPCHK(c, hipMemcpyAsync(d_sc + mp0, c->dist.data() + mp0, sizeof(float) * (mp1 - mp0), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(d_sc + c->P + mp0, c->mea.data() + mp0, sizeof(float) * (mp1 - mp0), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(d_nz + mp0, c->nnz.data() + mp0, sizeof(int64_t) * (mp1 - mp0), hipMemcpyHostToDevice, c->stream));
+  NCCLCHK(c, ncclGroupStart());
+  for (int r = 0; r < R; r++) {
+    const int64_t rp0 = info[4 * r], rp1 = info[4 * r + 1], cnt = info[4 * r + 2];
+    const bool me = r == c->rank;
+    if (cnt > 0) {
+      NCCLCHK(c, ncclBroadcast(me ? (const void*)c->d_cols : nullptr, nc + ebase[r], cnt * 2, ncclUint8, r, c->comm, c->stream));
+      NCCLCHK(c, ncclBroadcast(me ? (const void*)c->d_vals : nullptr, nv + ebase[r], cnt, ncclFloat32, r, c->comm, c->stream));
+    }
+    const int64_t rb = c->rp_off[rp0], re = c->rp_off[rp1];
+    if (re > rb) NCCLCHK(c, ncclBroadcast(c->d_rowptr + rb, c->d_rowptr + rb, re - rb, ncclInt32, r, c->comm, c->stream));
+    if (rp1 > rp0) {
+      NCCLCHK(c, ncclBroadcast(d_sc + rp0, d_sc + rp0, rp1 - rp0, ncclFloat32, r, c->comm, c->stream));
+      NCCLCHK(c, ncclBroadcast(d_sc + c->P + rp0, d_sc + c->P + rp0, rp1 - rp0, ncclFloat32, r, c->comm, c->stream));
+      NCCLCHK(c, ncclBroadcast(d_nz + rp0, d_nz + rp0, rp1 - rp0, ncclInt64, r, c->comm, c->stream));
+    }
+  }
+  NCCLCHK(c, ncclGroupEnd());
+  HIPCHK(c, hipMemcpyAsync(c->dist.data(), d_sc, sizeof(float) * c->P, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->mea.data(), d_sc + c->P, sizeof(float) * c->P, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->nnz.data(), d_nz, sizeof(int64_t) * c->P, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  hipFree(d_sc);
+  hipFree(d_nz);
+  if (c->d_cols) hipFree(c->d_cols);
+  if (c->d_vals) hipFree(c->d_vals);
+  c->d_cols = nc;
+  c->d_vals = nv;
+  c->ent_cap = std::max<int64_t>(total, 1);
+  c->ent_off[0] = 0;
+  for (int64_t p = 0; p < c->P; p++) c->ent_off[p + 1] = c->ent_off[p] + c->nnz[p];
+  HIPCHK(c, hipMemcpyAsync(c->d_ent_off, c->ent_off.data(), sizeof(int64_t) * (c->P + 1), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->store_p0 = 0;
+  c->store_p1 = c->P;
+  c->store_total = total;
+  return MLP_OK;
+}
+
+// ------------------------------------------------------------------ relax
+int mlp_relax(mlp_ctx* c, int iters) {
+  if (!c || iters < 0) return MLP_ERR_ARG;
+  if (c->n < 2) return MLP_ERR_STATE;
+  if (c->store_p0 != 0 || c->store_p1 != c->P) {
+    c->err = "relaxation needs every pair (all-gather first)";
+    return MLP_ERR_STATE;
+  }
+  hipSetDevice(c->device);
+  int64_t r0 = 0, r1 = c->P;
+  if (c->comm && c->nranks > 1) mlp_shard_range(c, c->nranks, c->rank, &r0, &r1);
+  const int64_t nout = r1 - r0;
+  int rc;
+  for (int it = 0; it < iters; it++) {
+    const int64_t total = c->store_total;
+    if ((rc = ensure(c, c->r_trowptr, sizeof(int32_t) * c->trp_off[c->P]))) return rc;
+    if ((rc = ensure(c, c->r_tcols, sizeof(uint16_t) * std::max<int64_t>(total, 1)))) return rc;
+    if ((rc = ensure(c, c->r_tvals, sizeof(float) * std::max<int64_t>(total, 1)))) return rc;
+    if ((rc = ensure(c, c->r_raw, sizeof(float) * std::max<int64_t>(total, 1)))) return rc;
+    if ((rc = ensure(c, c->r_pairs, sizeof(int64_t) * std::max<int64_t>(c->P, 1)))) return rc;
+    if ((rc = ensure(c, c->r_nnz, sizeof(int64_t) * std::max<int64_t>(c->P, 1)))) return rc;
+    if ((rc = ensure(c, c->r_newoff, sizeof(int64_t) * (c->P + 1)))) return rc;
+    if ((rc = ensure(c, c->r_newrp, sizeof(int32_t) * c->rp_off[c->P]))) return rc;
+    // all pairs are transposed (every rank reads every block)
+    std::vector<int64_t> allp(c->P);
+    std::iota(allp.begin(), allp.end(), 0);
+    HIPCHK(c, hipMemcpyAsync(c->r_pairs.p, allp.data(), sizeof(int64_t) * c->P, hipMemcpyHostToDevice, c->stream));
+    TransposeArgs ta;
+    ta.n = c->n;
+    ta.lens = c->d_len;
+    ta.rp_off = c->d_rp_off;
+    ta.rowptr = c->d_rowptr;
+    ta.ent_off = c->d_ent_off;
+    ta.cols = c->d_cols;
+    ta.vals = c->d_vals;
+    ta.trp_off = c->d_trp_off;
+    ta.trowptr = (int32_t*)c->r_trowptr.p;
+    ta.tcols = (uint16_t*)c->r_tcols.p;
+    ta.tvals = (float*)c->r_tvals.p;
+    ta.pairs = (const int64_t*)c->r_pairs.p;
+    ta.npairs = c->P;
+    ta.max_len = c->max_len;
+    {
+      Timer t(c, KTRANS, total);
+      HIPCHK(c, launch_transpose(ta, c->stream));
+    }
+    // row tasks of my output pairs
+    std::vector<int64_t> tp;
+    std::vector<int32_t> tr;
+    for (int64_t p = r0; p < r1; p++) {
+      const int La = c->lens[c->pa[p]];
+      for (int g = 1; g <= La; g += 64) {
+        tp.push_back(p);
+        tr.push_back(g);
+      }
+    }
+    const int64_t nt = (int64_t)tp.size();
+    if ((rc = ensure(c, c->r_tasks_p, sizeof(int64_t) * std::max<int64_t>(nt, 1)))) return rc;
+    if ((rc = ensure(c, c->r_tasks_r, sizeof(int32_t) * std::max<int64_t>(nt, 1)))) return rc;
+    HIPCHK(c, hipMemcpyAsync(c->r_tasks_p.p, tp.data(), sizeof(int64_t) * nt, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->r_tasks_r.p, tr.data(), sizeof(int32_t) * nt, hipMemcpyHostToDevice, c->stream));
+    RelaxArgs ra;
+    ra.n = c->n;
+    ra.lens = c->d_len;
+    ra.rp_off = c->d_rp_off;
+    ra.rowptr = c->d_rowptr;
+    ra.ent_off = c->d_ent_off;
+    ra.cols = c->d_cols;
+    ra.vals = c->d_vals;
+    ra.trp_off = c->d_trp_off;
+    ra.trowptr = (const int32_t*)c->r_trowptr.p;
+    ra.tcols = (const uint16_t*)c->r_tcols.p;
+    ra.tvals = (const float*)c->r_tvals.p;
+    ra.task_pair = (const int64_t*)c->r_tasks_p.p;
+    ra.task_row0 = (const int32_t*)c->r_tasks_r.p;
+    ra.ntasks = nt;
+    ra.out = (float*)c->r_raw.p;
+    {
+      Timer t(c, KRELAX, c->ent_off[r1] - c->ent_off[r0]);
+      HIPCHK(c, launch_relax_tasks(ra, c->stream));
+    }
+    // filter: count, host scan, write
+    std::vector<int64_t> outp(nout);
+    std::iota(outp.begin(), outp.end(), r0);
+    HIPCHK(c, hipMemcpyAsync(c->r_pairs.p, outp.data(), sizeof(int64_t) * nout, hipMemcpyHostToDevice, c->stream));
+    FilterArgs fa;
+    fa.n = c->n;
+    fa.lens = c->d_len;
+    fa.rp_off = c->d_rp_off;
+    fa.rowptr = c->d_rowptr;
+    fa.ent_off = c->d_ent_off;
+    fa.cols = c->d_cols;
+    fa.raw = (const float*)c->r_raw.p;
+    fa.pair_nnz = (int64_t*)c->r_nnz.p;
+    fa.new_ent_off = (const int64_t*)c->r_newoff.p;
+    fa.new_rowptr = (int32_t*)c->r_newrp.p;
+    fa.new_cols = nullptr;
+    fa.new_vals = nullptr;
+    fa.pairs = (const int64_t*)c->r_pairs.p;
+    fa.npairs = nout;
+    fa.write = 0;
+    {
+      Timer t(c, KFILTER, 0);
+      HIPCHK(c, launch_filter(fa, c->stream));
+    }
+    std::vector<int64_t> pn(nout);
+    HIPCHK(c, hipMemcpyAsync(pn.data(), c->r_nnz.p, sizeof(int64_t) * nout, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    // new canonical offsets of my pairs, starting at 0 (gathered below)
+    std::vector<int64_t> noff(c->P + 1, 0);
+    int64_t run = 0;
+    for (int64_t k = 0; k < nout; k++) {
+      noff[r0 + k] = run;
+      run += pn[k];
+    }
+    if ((rc = ensure(c, c->r_newcols, sizeof(uint16_t) * std::max<int64_t>(run, 1)))) return rc;
+    if ((rc = ensure(c, c->r_newvals, sizeof(float) * std::max<int64_t>(run, 1)))) return rc;
+    HIPCHK(c, hipMemcpyAsync(c->r_newoff.p, noff.data(), sizeof(int64_t) * (c->P + 1), hipMemcpyHostToDevice, c->stream));
+    fa.new_cols = (uint16_t*)c->r_newcols.p;
+    fa.new_vals = (float*)c->r_newvals.p;
+    fa.write = 1;
+    {
+      Timer t(c, KFILTER, 0);
+      HIPCHK(c, launch_filter(fa, c->stream));
+    }
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    // swap in the new store (my shard), keep row_ptr canonical
+    std::swap(c->d_rowptr, *(int32_t**)&c->r_newrp.p);
+    {
+      // sizes of the swapped buffers: both are rp_off[P] ints
+      size_t bsz = c->r_newrp.bytes;
+      (void)bsz;
+    }
+    if ((rc = grow_store(c, run, 0))) return rc;
+    HIPCHK(c, hipMemcpyAsync(c->d_cols, c->r_newcols.p, sizeof(uint16_t) * run, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->d_vals, c->r_newvals.p, sizeof(float) * run, hipMemcpyDeviceToDevice, c->stream));
+    for (int64_t k = 0; k < nout; k++) c->nnz[r0 + k] = pn[k];
+    for (int64_t p = r0; p <= r1; p++) c->ent_off[p] = noff[p];
+    c->ent_off[r1] = run;
+    c->store_p0 = r0;
+    c->store_p1 = r1;
+    c->store_total = run;
+    HIPCHK(c, hipMemcpyAsync(c->d_ent_off, c->ent_off.data(), sizeof(int64_t) * (c->P + 1), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (c->comm && c->nranks > 1) {
+      if ((rc = mlp_allgather(c))) return rc;
+    }
+  }
+  return MLP_OK;
+}
+
+int mlp_synchronize(mlp_ctx* c) {
+  if (!c) return MLP_ERR_ARG;
+  hipSetDevice(c->device);
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return MLP_OK;
+}
+
+int mlp_profile(mlp_ctx* c, int enable) {
+  if (!c) return MLP_ERR_ARG;
+  c->profile = enable != 0;
+  return MLP_OK;
+}
+
+int mlp_profile_reset(mlp_ctx* c) {
+  if (!c) return MLP_ERR_ARG;
+  for (int k = 0; k < MLP_NKERNELS; k++) {
+    c->kms[k] = 0;
+    c->klaunch[k] = 0;
+    c->kcells[k] = 0;
+  }
+  return MLP_OK;
+}
+
+int mlp_kernel_times(mlp_ctx* c, double* ms, int64_t* launches, int64_t* cells) {
+  if (!c) return MLP_ERR_ARG;
+  for (int k = 0; k < MLP_NKERNELS; k++) {
+    if (ms) ms[k] = c->kms[k];
+    if (launches) launches[k] = c->klaunch[k];
+    if (cells) cells[k] = c->kcells[k];
+  }
+  return MLP_OK;
+}
+
+}  // extern "C"

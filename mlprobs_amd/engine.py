@@ -1,0 +1,227 @@
+"""Python mirror of the C_P_NP_Aln posterior / consistency interface, running
+on the MI355X through libmlpgpu's C ABI (include/mlpgpu.h).
+
+Reference interface (kuangmeng/MLProbs baseMSA/C_P_NP_Aln):
+  - pdoAlign pair loop (CPNP/MSA.cpp:927-1032): per pair posterior, distance
+    1 - MEA/min(L_a, L_b), SparseMatrix (>= 0.01)   -> Family.posteriors()
+  - MSA::DoRelaxation x numConsistencyReps (CPNP/MSA.cpp:1041-1051)
+                                                    -> Family.relax()
+  - SparseMatrix rows/columns (CPNP/SparseMatrix.h) -> Family.sparse(a, b)
+
+There is deliberately no CPU fallback: if the HIP library is missing or no
+GPU is visible every entry point raises.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import build as _build
+
+_LIB = None
+
+I64 = C.c_int64
+F32P = np.ctypeslib.ndpointer(np.float32, flags='C_CONTIGUOUS')
+I32P = np.ctypeslib.ndpointer(np.int32, flags='C_CONTIGUOUS')
+I64P = np.ctypeslib.ndpointer(np.int64, flags='C_CONTIGUOUS')
+U16P = np.ctypeslib.ndpointer(np.uint16, flags='C_CONTIGUOUS')
+
+ERRORS = {1: 'bad argument', 2: 'HIP error', 3: 'partition function overflow', 4: 'state error',
+          5: 'RCCL error', 6: 'device memory'}
+KERNELS = ['forward', 'backward', 'local_totals', 'merge_mea_sparsify', 'compact', 'relax',
+           'transpose', 'filter', 'allgather']
+
+
+class MlpError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f'{ERRORS.get(code, code)}: {msg}')
+        self.code = code
+
+
+def lib_path():
+    return _build.LIB
+
+
+def lib():
+    """Load libmlpgpu.so (in-tree).  Raises if it is missing."""
+    global _LIB
+    if _LIB is None:
+        path = _build.LIB
+        if not os.path.exists(path):
+            raise RuntimeError(f'{path} missing: run `python -m mlprobs_amd.build` (hipcc, gfx950)')
+        L = C.CDLL(path)
+        P = C.c_void_p
+        L.mlp_ctx_create.argtypes = [C.c_int, C.POINTER(P)]
+        L.mlp_ctx_destroy.argtypes = [P]
+        L.mlp_ctx_destroy.restype = None
+        L.mlp_last_error.argtypes = [P]
+        L.mlp_last_error.restype = C.c_char_p
+        L.mlp_family_load.argtypes = [P, C.c_int, C.c_char_p, I64P]
+        L.mlp_family_npairs.argtypes = [P]
+        L.mlp_family_npairs.restype = I64
+        L.mlp_posteriors.argtypes = [P, C.c_int, C.c_float, I64, I64]
+        L.mlp_pair_results.argtypes = [P, I64, I64, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.mlp_csr_total.argtypes = [P, C.POINTER(I64)]
+        L.mlp_csr_export.argtypes = [P, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.mlp_csr_import.argtypes = [P, I32P, I64P, U16P, F32P]
+        L.mlp_relax.argtypes = [P, C.c_int]
+        L.mlp_comm_unique_id.argtypes = [C.c_char_p]
+        L.mlp_comm_init.argtypes = [P, C.c_char_p, C.c_int, C.c_int]
+        L.mlp_shard_range.argtypes = [P, C.c_int, C.c_int, C.POINTER(I64), C.POINTER(I64)]
+        L.mlp_allgather.argtypes = [P]
+        L.mlp_synchronize.argtypes = [P]
+        L.mlp_profile.argtypes = [P, C.c_int]
+        L.mlp_profile_reset.argtypes = [P]
+        L.mlp_kernel_times.argtypes = [P, C.c_void_p, C.c_void_p, C.c_void_p]
+        _LIB = L
+    return _LIB
+
+
+EXPORTED = ['mlp_ctx_create', 'mlp_ctx_destroy', 'mlp_last_error', 'mlp_family_load',
+            'mlp_family_npairs', 'mlp_posteriors', 'mlp_pair_results', 'mlp_csr_total',
+            'mlp_csr_export', 'mlp_csr_import', 'mlp_relax', 'mlp_comm_unique_id', 'mlp_comm_init',
+            'mlp_shard_range', 'mlp_allgather', 'mlp_synchronize', 'mlp_profile',
+            'mlp_kernel_times', 'mlp_profile_reset']
+
+
+def pair_index(n, a, b):
+    """Row-major index of pair (a, b), a < b (CPNP/MSA.cpp:907-919)."""
+    return a * n - a * (a + 1) // 2 + (b - a - 1)
+
+
+def pairs_of(n):
+    return [(a, b) for a in range(n) for b in range(a + 1, n)]
+
+
+class Family:
+    """One MLProbs family resident on one GPU."""
+
+    def __init__(self, seqs, device=0):
+        self._L = lib()
+        self._ctx = C.c_void_p()
+        self._chk(self._L.mlp_ctx_create(int(device), C.byref(self._ctx)), ctx=False)
+        self.seqs = [s.upper() for s in seqs]
+        self.n = len(self.seqs)
+        self.lens = np.array([len(s) for s in self.seqs], np.int64)
+        offs = np.zeros(self.n + 1, np.int64)
+        offs[1:] = np.cumsum(self.lens)
+        self._chk(self._L.mlp_family_load(self._ctx, self.n, ''.join(self.seqs).encode(), offs))
+        self.npairs = self.n * (self.n - 1) // 2
+        rp = np.zeros(self.npairs + 1, np.int64)
+        k = 0
+        for a in range(self.n):
+            for b in range(a + 1, self.n):
+                rp[k + 1] = rp[k] + self.lens[a] + 2
+                k += 1
+        self.rp_off = rp
+        self._csr = None
+
+    def _chk(self, rc, ctx=True):
+        if rc != 0:
+            msg = self._L.mlp_last_error(self._ctx).decode() if ctx else 'context creation failed'
+            raise MlpError(rc, msg)
+
+    def close(self):
+        if self._ctx:
+            self._L.mlp_ctx_destroy(self._ctx)
+            self._ctx = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- posterior stage
+    def posteriors(self, pid, delta, p_begin=0, p_end=None):
+        p_end = self.npairs if p_end is None else p_end
+        self._csr = None
+        self._chk(self._L.mlp_posteriors(self._ctx, int(pid), float(delta), int(p_begin), int(p_end)))
+
+    def results(self, p_begin=0, p_end=None):
+        p_end = self.npairs if p_end is None else p_end
+        m = p_end - p_begin
+        d = np.zeros(m, np.float32)
+        e = np.zeros(m, np.float32)
+        z = np.zeros(m, np.int64)
+        self._chk(self._L.mlp_pair_results(self._ctx, p_begin, p_end, d.ctypes.data, e.ctypes.data, z.ctypes.data))
+        return d, e, z
+
+    def distances(self):
+        d, _, _ = self.results()
+        D = np.zeros((self.n, self.n), np.float32)
+        k = 0
+        for a in range(self.n):
+            for b in range(a + 1, self.n):
+                D[a, b] = D[b, a] = d[k]
+                k += 1
+        return D
+
+    def export(self):
+        tot = I64(0)
+        self._chk(self._L.mlp_csr_total(self._ctx, C.byref(tot)))
+        rp = np.zeros(int(self.rp_off[-1]), np.int32)
+        eo = np.zeros(self.npairs + 1, np.int64)
+        cols = np.zeros(max(tot.value, 1), np.uint16)
+        vals = np.zeros(max(tot.value, 1), np.float32)
+        self._chk(self._L.mlp_csr_export(self._ctx, rp.ctypes.data, eo.ctypes.data, cols.ctypes.data, vals.ctypes.data))
+        self._csr = (rp, eo, cols[:tot.value], vals[:tot.value])
+        return self._csr
+
+    def import_csr(self, rp, eo, cols, vals):
+        self._csr = None
+        self._chk(self._L.mlp_csr_import(self._ctx, np.ascontiguousarray(rp, np.int32),
+                                         np.ascontiguousarray(eo, np.int64),
+                                         np.ascontiguousarray(cols, np.uint16),
+                                         np.ascontiguousarray(vals, np.float32)))
+
+    def sparse(self, p):
+        """(row_ptr[L_a+2], cols, vals) of pair index p (SparseMatrix layout)."""
+        if self._csr is None:
+            self.export()
+        rp, eo, cols, vals = self._csr
+        r = rp[self.rp_off[p]:self.rp_off[p + 1]]
+        e0, e1 = eo[p], eo[p + 1]
+        return r, cols[e0:e1].astype(np.int32), vals[e0:e1]
+
+    # ---- consistency
+    def relax(self, iters):
+        self._csr = None
+        self._chk(self._L.mlp_relax(self._ctx, int(iters)))
+
+    # ---- multi-GPU
+    @staticmethod
+    def unique_id():
+        buf = C.create_string_buffer(128)
+        rc = lib().mlp_comm_unique_id(buf)
+        if rc:
+            raise MlpError(rc, 'ncclGetUniqueId')
+        return buf.raw
+
+    def comm_init(self, uid, nranks, rank):
+        self._chk(self._L.mlp_comm_init(self._ctx, uid, int(nranks), int(rank)))
+
+    def shard(self, nranks, rank):
+        b, e = I64(0), I64(0)
+        self._chk(self._L.mlp_shard_range(self._ctx, nranks, rank, C.byref(b), C.byref(e)))
+        return b.value, e.value
+
+    def allgather(self):
+        self._csr = None
+        self._chk(self._L.mlp_allgather(self._ctx))
+
+    def synchronize(self):
+        self._chk(self._L.mlp_synchronize(self._ctx))
+
+    # ---- profiling
+    def profile(self, enable=True):
+        self._chk(self._L.mlp_profile(self._ctx, 1 if enable else 0))
+        self._chk(self._L.mlp_profile_reset(self._ctx))
+
+    def kernel_times(self):
+        ms = np.zeros(len(KERNELS), np.float64)
+        nl = np.zeros(len(KERNELS), np.int64)
+        cells = np.zeros(len(KERNELS), np.int64)
+        self._chk(self._L.mlp_kernel_times(self._ctx, ms.ctypes.data, nl.ctypes.data, cells.ctypes.data))
+        return {k: {'ms': float(ms[i]), 'launches': int(nl[i]), 'cells': int(cells[i])}
+                for i, k in enumerate(KERNELS)}
