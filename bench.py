@@ -1,0 +1,206 @@
+"""bench.py -- all-pairs posterior stage of C_P_NP_Aln on MI355X.
+
+One step = the whole posterior stage over the family:
+every pair's 5-state + partition-function + local posteriors, RMS merge,
+MEA distance and sparsification into the canonical CSR store, inputs already
+resident in HBM.  With N GPUs the pairs are split into N contiguous,
+cell-balanced shards (one process per GPU) and the step ends with the RCCL
+all-gather of the sparse posteriors over xGMI (the exchange step before
+consistency).  Value = pair-cells of the whole family / max-over-ranks time.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--n 512] [--len 400]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = 'pair-HMM DP cell updates/s (all-pairs) + end-to-end MSA sec/family'
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+# Algorithmic HBM bytes per pair-cell for each kernel of the pid-0 pipeline
+# ("Kernels and their rooflines").
+ALGO_BYTES = {'forward': 20, 'backward': 32, 'local_totals': 8, 'merge_mea_sparsify': 12}
+STAGE_BYTES = 56  # pid 0/1 algorithmic bytes per pair-cell
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=3)
+    ap.add_argument('--warmup', type=int, default=1)
+    ap.add_argument('--n', type=int, default=512)
+    ap.add_argument('--len', type=int, default=400)
+    ap.add_argument('--s', type=float, default=0.7)
+    ap.add_argument('--seed', type=int, default=11)
+    ap.add_argument('--pid', type=int, default=0)
+    ap.add_argument('--delta', type=float, default=0.132548)
+    ap.add_argument('--cpu-pairs', type=int, default=768, help='reference CPU baseline sample (pairs)')
+    ap.add_argument('--cpu-threads', type=int, default=16)
+    ap.add_argument('--no-cpu', action='store_true')
+    ap.add_argument('--relax', type=int, default=0, help='also time N relaxation rounds (reported separately)')
+    return ap.parse_args()
+
+
+def cpu_baseline(fasta, pid, pairs, threads, cells_per_pair):
+    """Time the reference's own pair loop (oracle/_ref/ref_probe, compiled from
+    /root/reference by `make -C oracle ref`) on a bounded sample of the same
+    family; fall back to the plain-C port if the reference build is absent."""
+    probe = os.path.join(ROOT, 'oracle', '_ref', 'ref_probe')
+    if os.path.exists(probe):
+        out = subprocess.run([probe, 'bench', fasta, str(pid), str(pairs), str(threads)],
+                             capture_output=True, text=True, timeout=600)
+        if out.returncode == 0:
+            r = json.loads(out.stdout.strip().splitlines()[-1])
+            return {'value': r['pair_cells_per_s'], 'unit': 'pair-cells/s', 'cores': threads,
+                    'kind': 'reference',
+                    'sample': f"first {r['pairs']} pairs of the same family, {r['seconds']:.1f} s, "
+                              f"reference C_P_NP_Aln pdoAlign pair body (posterior+MEA+sparsify)"}
+    sys.path.insert(0, os.path.join(ROOT, 'oracle'))
+    import orc
+    from mlprobs_amd import synth
+    seqs = [s for _, s in synth.read_fasta(fasta)]
+    m = orc.model(0.132548)
+    t0 = time.perf_counter()
+    d, nz, tot = orc.pair_loop(m, seqs, pid, max_pairs=pairs, threads=threads)
+    dt = time.perf_counter() - t0
+    cells = sum((len(seqs[a]) + 1) * (len(seqs[b]) + 1) for a, b in
+                [(a, b) for a in range(len(seqs)) for b in range(a + 1, len(seqs))][:pairs])
+    return {'value': cells / dt, 'unit': 'pair-cells/s', 'cores': threads, 'kind': 'port',
+            'sample': f'first {pairs} pairs, {dt:.1f} s, oracle port'}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    from mlprobs_amd import synth
+    from mlprobs_amd.engine import Family
+
+    fam_in = synth.family(args.n, args.len, args.s, seed=args.seed)
+    seqs = [s for _, s in fam_in]
+    lens = np.array([len(s) for s in seqs], np.int64)
+    fam = Family(seqs, device=local if world > 1 else 0)
+    if world > 1:
+        uid = Family.unique_id() if rank == 0 else None
+        obj = [uid]
+        dist.broadcast_object_list(obj, src=0)
+        fam.comm_init(obj[0], world, rank)
+    p0, p1 = fam.shard(world, rank)
+    total_cells = 0
+    for a in range(args.n):
+        total_cells += int(((lens[a] + 1) * (lens[a + 1:] + 1)).sum())
+
+    def step():
+        fam.posteriors(args.pid, args.delta, p0, p1)
+        if world > 1:
+            fam.allgather()
+
+    def barrier():
+        fam.synchronize()
+        if world > 1:
+            import torch
+            torch.cuda.synchronize()
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        fam.profile(False)
+        step()
+    fam.profile(True)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        import torch
+        t = torch.tensor([dt], dtype=torch.float64, device='cuda')
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    kt = fam.kernel_times()
+    relax_info = None
+    if args.relax > 0:
+        fam.profile(True)
+        barrier()
+        tr = time.perf_counter()
+        fam.relax(args.relax)
+        barrier()
+        relax_info = {'rounds': args.relax, 'seconds': time.perf_counter() - tr,
+                      'kernels': fam.kernel_times()}
+    _, _, nnz = fam.results()
+    value = total_cells * args.steps / dt
+    # roofline of the dominant kernel (largest accumulated device time)
+    dom = max(ALGO_BYTES, key=lambda k: kt[k]['ms'])
+    launches = max(kt[dom]['launches'], 1)
+    avg_ms = kt[dom]['ms'] / launches
+    bytes_per_launch = ALGO_BYTES[dom] * kt[dom]['cells'] / launches
+    achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
+    traffic = None
+    pmc = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
+    if os.path.exists(pmc):
+        with open(pmc) as fh:
+            traffic = json.load(fh).get(dom)
+    out = None
+    if rank == 0:
+        cpu = None
+        if not args.no_cpu and world == 1:
+            with tempfile.TemporaryDirectory() as td:
+                fa = os.path.join(td, 'fam.fa')
+                synth.write_fasta(fa, fam_in)
+                cpu = cpu_baseline(fa, args.pid, args.cpu_pairs, args.cpu_threads, None)
+        out = {
+            'metric': METRIC,
+            'value': value,
+            'unit': 'pair-cells/s',
+            'n_gpus': world,
+            'steps': args.steps,
+            'warmup': args.warmup,
+            'ms_per_step': dt / args.steps * 1e3,
+            'higher_is_better': True,
+            'scaling': 'strong',
+            'vs_baseline': None,
+            'dtype': 'f32',
+            'data': 'synthetic',
+            'config': {'workload': f'C3 all-pairs posterior stage: {args.n} seqs x {args.len} aa synthetic '
+                                   f'(s={args.s}, seed {args.seed}), pid {args.pid} '
+                                   '(5-state HMM + partition function + local HMM, RMS merge, MEA, sparsify)',
+                       'n_seqs': args.n, 'length': args.len, 'pairs': int(args.n * (args.n - 1) // 2),
+                       'pair_cells': int(total_cells), 'nnz': int(nnz.sum()),
+                       'parallelism': f'pair-sharded dp{world}' + (' + RCCL all-gather' if world > 1 else '')},
+            'roofline': {'bound': 'hbm', 'kernel': dom, 'achieved': achieved, 'peak': HBM_PEAK_GBS,
+                         'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
+                         'algo_bytes_per_cell': ALGO_BYTES[dom], 'avg_launch_ms': avg_ms},
+            'stage_roofline': {'algo_bytes_per_cell': STAGE_BYTES,
+                               'achieved_GBps': value * STAGE_BYTES / 1e9,
+                               'frac': value * STAGE_BYTES / 1e9 / HBM_PEAK_GBS},
+            'kernels_ms_per_step': {k: v['ms'] / args.steps for k, v in kt.items() if v['launches']},
+            'cpu_baseline': cpu,
+        }
+        if cpu:
+            out['speedup_vs_cpu'] = value / cpu['value']
+        if relax_info:
+            out['relax'] = relax_info
+        print(json.dumps(out))
+    fam.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -384,12 +384,9 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
   if (!c) return MLP_ERR_ARG;
   if (c->n < 2) { c->err = "family needs >= 2 sequences"; return MLP_ERR_STATE; }
   if (p0 < 0 || p1 > c->P || p0 > p1) { c->err = "bad pair range"; return MLP_ERR_ARG; }
-  if (p0 != c->store_p1 && !(c->store_p0 == c->store_p1)) {
-    c->err = "pair ranges must be appended contiguously";
-    return MLP_ERR_STATE;
-  }
   hipSetDevice(c->device);
-  if (c->store_p0 == c->store_p1) {  // empty store: start at p0
+  // a range that continues the held one is appended; anything else restarts
+  if (c->store_p0 == c->store_p1 || p0 != c->store_p1) {
     c->store_p0 = c->store_p1 = p0;
     c->store_total = 0;
   }
