@@ -37,6 +37,31 @@ __device__ __forceinline__ float mlp_log_add(float x, float y) {
   return (lo == MLP_LOG_ZERO || d >= 7.5f) ? hi : r;
 }
 
+// LDS-table form of LOOKUP: the interval index selects one float4 of
+// coefficients (filled by mlp_lookup_table), then the same Horner sequence.
+__device__ __forceinline__ void mlp_lookup_table(float4* lk) {
+  lk[0] = make_float4(-0.009350833524763f, 0.130659527668286f, 0.498799810682272f, 0.693203116424741f);
+  lk[1] = make_float4(-0.014532321752540f, 0.139942324101744f, 0.495635523139337f, 0.692140569840976f);
+  lk[2] = make_float4(-0.004605031767994f, 0.063427417320019f, 0.695956496475118f, 0.514272634594009f);
+  lk[3] = make_float4(-0.000458661602210f, 0.009695946122598f, 0.930734667215156f, 0.168037164329057f);
+}
+
+// LOG_ADD with LDS coefficients.  max/min replace the reference's compare
+// (identical results for non-NaN inputs; for x == y both operands are equal).
+__device__ __forceinline__ float mlp_log_add_t(float x, float y, const float4* __restrict__ lk) {
+  const float hi = fmaxf(x, y), lo = fminf(x, y);
+  const float d = hi - lo;
+  const int k = (d > 1.00f) + (d > 2.50f) + (d > 4.50f);
+  const float4 c = lk[k];
+  const float r = (((c.x * d + c.y) * d + c.z) * d + c.w) + lo;
+  return (lo == MLP_LOG_ZERO || d >= 7.5f) ? hi : r;
+}
+
+// LOG_ADD(LOG_ZERO, y) == max(LOG_ZERO, y) exactly: above LOG_ZERO the sentinel
+// returns y; below it the gap to LOG_ZERO exceeds the float spacing at 2e20
+// (1.6e13) and thus the 7.5 cutoff.
+__device__ __forceinline__ float mlp_log_add_from_zero(float y) { return fmaxf(MLP_LOG_ZERO, y); }
+
 // EXP (CPNP/ScoreType.h:36-68) for x <= 0 (the only domain the posterior
 // uses: min(LOG_ONE, .) clamps, CPNP/ProbabilisticModel.h:484).  The quartic
 // runs in double on the float argument, like the reference.
@@ -68,6 +93,33 @@ __device__ __forceinline__ float mlp_exp_nonpos(float xf) {
   }
   const float r = (float)((((c4 * x + c3) * x + c2) * x + c1) * x + c0);
   return (x > -16) ? r : 0.0f;
+}
+
+// LDS-table form of EXP for x <= 0: row k of `ex` (6 doubles, 5 used) holds
+// the coefficients of interval k; row 6 is all zero (x <= -16 -> 0).
+__device__ __forceinline__ void mlp_exp_table(double* ex) {
+  const double c[7][5] = {
+      {0.03254409303190190000, 0.16280432765779600000, 0.49929760485974900000, 0.99995149601363700000, 0.99999925508501600000},
+      {0.01973899026052090000, 0.13822379685007000000, 0.48056651562365000000, 0.99326940370383500000, 0.99906756856399500000},
+      {0.00940528203591384000, 0.09414963667859410000, 0.40825793595877300000, 0.93933625499130400000, 0.98369508190545300000},
+      {0.00217245711583303000, 0.03484829428350620000, 0.22118199801337800000, 0.67049462206469500000, 0.83556950223398500000},
+      {0.00012398771025456900, 0.00349155785951272000, 0.03727721426017900000, 0.17974997741536900000, 0.33249299994217400000},
+      {0.00000051741713416603, 0.00002721456879608080, 0.00053418601865636800, 0.00464101989351936000, 0.01507447981459420000},
+      {0, 0, 0, 0, 0}};
+  for (int k = 0; k < 7; ++k) {
+    for (int q = 0; q < 5; ++q) ex[k * 6 + q] = c[k][q];
+    ex[k * 6 + 5] = 0;
+  }
+}
+__device__ __forceinline__ float mlp_exp_nonpos_t(float xf, const double* __restrict__ ex) {
+  const double x = (double)xf;
+  const int k = 6 - (x > -16) - (x > -8) - (x > -4) - (x > -2) - (x > -1) - (x > -0.5);
+  const double* c = ex + k * 6;
+  return (float)((((c[0] * x + c[1]) * x + c[2]) * x + c[3]) * x + c[4]);
+}
+__device__ __forceinline__ float mlp_post_from_sum_t(float s, float T, const double* __restrict__ ex) {
+  const float v = s - T;
+  return mlp_exp_nonpos_t(v < MLP_LOG_ONE ? v : MLP_LOG_ONE, ex);
 }
 
 // Posterior from (f + b) and the pair total (CPNP/ProbabilisticModel.h:484):
