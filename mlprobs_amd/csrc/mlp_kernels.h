@@ -9,6 +9,11 @@ namespace mlp {
 constexpr int kWave = 64;        // CDNA wavefront
 constexpr int kWavesPerBlock = 4;  // independent pairs per workgroup
 constexpr int kEll = 64;         // sparse slots per posterior row before overflow
+constexpr int kSeqLds = 2048;    // column residues staged in LDS per wave (longer: LONG kernels)
+
+// Steps of one 64-row strip: columns 0..L2 plus the 63-step skew, padded to
+// a multiple of 8 so the step loops unroll without remainders.
+__host__ __device__ constexpr int strip_steps(int L2) { return (L2 + 64 + 7) & ~7; }
 
 // Model constants (CPNP/ProbabilisticModel.h:42-47 plus the PF factors of
 // CPNP/MSAPartProbs.cpp:698-709).  Letter-indexed tables (26 uppercase
@@ -82,9 +87,11 @@ inline int model_set_for_pid(int pid) {
 
 // launchers (posterior.hip)
 hipError_t launch_forward(int models, const ModelScalars& ms, const Tables* tab, SeqSet seqs,
-                          PairMeta pm, PairRec* rec, Scratch sc, int64_t npairs, hipStream_t st);
+                          PairMeta pm, PairRec* rec, Scratch sc, int64_t npairs, int max_len2,
+                          hipStream_t st);
 hipError_t launch_backward(int models, const ModelScalars& ms, const Tables* tab, SeqSet seqs,
-                           PairMeta pm, PairRec* rec, Scratch sc, int64_t npairs, hipStream_t st);
+                           PairMeta pm, PairRec* rec, Scratch sc, int64_t npairs, int max_len2,
+                           hipStream_t st);
 hipError_t launch_local_totals(SeqSet seqs, PairMeta pm, PairRec* rec, Scratch sc, int64_t npairs,
                                hipStream_t st);
 hipError_t launch_merge(int models, int pid, const ModelScalars& ms, SeqSet seqs, PairMeta pm,

@@ -37,24 +37,33 @@ __device__ __forceinline__ float mlp_log_add(float x, float y) {
   return (lo == MLP_LOG_ZERO || d >= 7.5f) ? hi : r;
 }
 
-// LDS-table form of LOOKUP: the interval index selects one float4 of
-// coefficients (filled by mlp_lookup_table), then the same Horner sequence.
+// LDS-table form of LOOKUP.  The interval is found from
+// q = floor(min(d * (2 - 2^-23), 15)): q <= 1 <=> d <= 1, q <= 4 <=> d <= 2.5,
+// q <= 8 <=> d <= 4.5 for every float d >= 0 (checked exhaustively on [0, 8);
+// the product rounds below the even integer exactly at the three breakpoints),
+// so lk[q] (16 float4 rows, filled by mlp_lookup_table) holds the reference's
+// coefficients of d's interval.  Four VALU ops instead of compare/select chains.
 __device__ __forceinline__ void mlp_lookup_table(float4* lk) {
-  lk[0] = make_float4(-0.009350833524763f, 0.130659527668286f, 0.498799810682272f, 0.693203116424741f);
-  lk[1] = make_float4(-0.014532321752540f, 0.139942324101744f, 0.495635523139337f, 0.692140569840976f);
-  lk[2] = make_float4(-0.004605031767994f, 0.063427417320019f, 0.695956496475118f, 0.514272634594009f);
-  lk[3] = make_float4(-0.000458661602210f, 0.009695946122598f, 0.930734667215156f, 0.168037164329057f);
+  const float4 k0 = make_float4(-0.009350833524763f, 0.130659527668286f, 0.498799810682272f, 0.693203116424741f);
+  const float4 k1 = make_float4(-0.014532321752540f, 0.139942324101744f, 0.495635523139337f, 0.692140569840976f);
+  const float4 k2 = make_float4(-0.004605031767994f, 0.063427417320019f, 0.695956496475118f, 0.514272634594009f);
+  const float4 k3 = make_float4(-0.000458661602210f, 0.009695946122598f, 0.930734667215156f, 0.168037164329057f);
+  for (int q = 0; q < 16; ++q) lk[q] = q < 2 ? k0 : q < 5 ? k1 : q < 9 ? k2 : k3;
 }
+constexpr int kLookupRows = 16;
 
 // LOG_ADD with LDS coefficients.  max/min replace the reference's compare
 // (identical results for non-NaN inputs; for x == y both operands are equal).
+// The reference's `lo == LOG_ZERO` test is implied by `d >= 7.5`: if lo is
+// LOG_ZERO and d < 7.5 then hi == LOG_ZERO too (float spacing at 2e20 is
+// 1.6e13) and LOOKUP(0) + LOG_ZERO rounds back to LOG_ZERO == hi.
 __device__ __forceinline__ float mlp_log_add_t(float x, float y, const float4* __restrict__ lk) {
   const float hi = fmaxf(x, y), lo = fminf(x, y);
   const float d = hi - lo;
-  const int k = (d > 1.00f) + (d > 2.50f) + (d > 4.50f);
-  const float4 c = lk[k];
+  const int q = (int)fminf(d * 0x1.fffffep0f, 15.0f);
+  const float4 c = lk[q];
   const float r = (((c.x * d + c.y) * d + c.z) * d + c.w) + lo;
-  return (lo == MLP_LOG_ZERO || d >= 7.5f) ? hi : r;
+  return (d >= 7.5f) ? hi : r;
 }
 
 // LOG_ADD(LOG_ZERO, y) == max(LOG_ZERO, y) exactly: above LOG_ZERO the sentinel
@@ -111,9 +120,14 @@ __device__ __forceinline__ void mlp_exp_table(double* ex) {
     ex[k * 6 + 5] = 0;
   }
 }
+// The breakpoints -0.5 .. -16 are powers of two, so for x <= 0 the interval
+// follows from the biased exponent E of x: k = clamp(E - 125, 0, 6); e.g.
+// x = -0.5 has E = 126 -> k = 1, as `x > -0.5` fails in the reference chain
+// (checked exhaustively over all non-positive floats).
 __device__ __forceinline__ float mlp_exp_nonpos_t(float xf, const double* __restrict__ ex) {
   const double x = (double)xf;
-  const int k = 6 - (x > -16) - (x > -8) - (x > -4) - (x > -2) - (x > -1) - (x > -0.5);
+  const int e = (int)((__float_as_uint(xf) >> 23) & 0xFF) - 125;
+  const int k = min(max(e, 0), 6);
   const double* c = ex + k * 6;
   return (float)((((c[0] * x + c[1]) * x + c[2]) * x + c[3]) * x + c[4]);
 }

@@ -405,7 +405,7 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
     while (q < p1) {
       const int L1 = c->lens[c->pa[q]], L2 = c->lens[c->pb[q]];
       const int64_t S = (L1 + 64) >> 6;
-      const int64_t cl = S * (L2 + 64) * 64;
+      const int64_t cl = S * strip_steps(L2) * 64;
       const int64_t rmc = (int64_t)L1 * ((L2 + 3) & ~3);
       const size_t add = cl * 20 + rmc * 8 + (L2 + 2) * (5 * 4 + 3 * 4 + 3 * 8 + 4 + 4) +
                          (size_t)L1 * (kEll * 6 + 4) + per_slot;
@@ -436,7 +436,7 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
         rm_of[k] = ro;
         bnd_of[k] = bo;
         ell_of[k] = eo;
-        co += (int64_t)((L1 + 64) >> 6) * (L2 + 64) * 64;
+        co += (int64_t)((L1 + 64) >> 6) * strip_steps(L2) * 64;
         ro += (int64_t)L1 * ((L2 + 3) & ~3);
         bo += L2 + 2;
         eo += L1;
@@ -500,14 +500,18 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
     HIPCHK(c, hipMemcpyAsync(base + o_ell, h_ell.data(), np * 8, hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipMemsetAsync(d_rec, 0, np * sizeof(PairRec), c->stream));
     int64_t bcells = 0;
-    for (int64_t k = p; k < q; k++) bcells += pair_cost_cells(c, k);
+    int maxL2 = 0;
+    for (int64_t k = p; k < q; k++) {
+      bcells += pair_cost_cells(c, k);
+      maxL2 = std::max(maxL2, c->lens[c->pb[k]]);
+    }
     {
       Timer t(c, KFWD, bcells);
-      HIPCHK(c, launch_forward(models, ms, c->d_tables, seqs, pm, d_rec, sc, np, c->stream));
+      HIPCHK(c, launch_forward(models, ms, c->d_tables, seqs, pm, d_rec, sc, np, maxL2, c->stream));
     }
     {
       Timer t(c, KBWD, bcells);
-      HIPCHK(c, launch_backward(models, ms, c->d_tables, seqs, pm, d_rec, sc, np, c->stream));
+      HIPCHK(c, launch_backward(models, ms, c->d_tables, seqs, pm, d_rec, sc, np, maxL2, c->stream));
     }
     if (models & kLocal) {
       Timer t(c, KTOT, bcells);

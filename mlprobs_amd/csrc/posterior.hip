@@ -16,7 +16,7 @@
 // previous step's neighbour value, the left / right value stays in the lane.
 // Strip-to-strip rows go through a small per-pair boundary column buffer.
 // Cell values are stored in a strip-diagonal layout
-//     idx = cell_off + ((s * (L2 + 64)) + t) * 64 + lane
+//     idx = cell_off + ((s * strip_steps(L2)) + t) * 64 + lane
 // so every store / load of a step is one coalesced 256-byte wave access.
 //
 // All float arithmetic reproduces the reference's operation order exactly
@@ -34,28 +34,6 @@ namespace mlp {
 // LDS-resident tables of one workgroup: letter-indexed emissions, the PF
 // score factors and the LOOKUP coefficient sets (one ds_read_b128 per
 // LOG_ADD instead of twelve selects).
-struct LdsTables {
-  float4 lk[4];
-  float match[26 * 26];
-  float ins[26];
-  double sub[26 * 26];
-};
-
-__device__ __forceinline__ void stage_tables(LdsTables& L, const Tables* __restrict__ tab) {
-  for (int k = threadIdx.x; k < 26 * 26; k += blockDim.x) {
-    L.match[k] = tab->match[k];
-    L.sub[k] = tab->sub[k];
-  }
-  if (threadIdx.x < 26) L.ins[threadIdx.x] = tab->ins[threadIdx.x];
-  if (threadIdx.x == 0) mlp_lookup_table(L.lk);
-  __syncthreads();
-}
-
-__device__ __forceinline__ int64_t wave_pair_index() {
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  return (int64_t)blockIdx.x * kWavesPerBlock + w;
-}
-
 // Residue supply: the residue a lane needs at step t is the residue its
 // upper neighbour needed one step earlier, so residues flow down the wave by
 // DPP; only lane 0 / 63 takes a new one, read with v_readlane out of a
@@ -77,6 +55,52 @@ struct ResidueChunk {
   }
 };
 
+struct LdsTables {
+  float4 lk[kLookupRows];
+  float match[26 * 26];
+  float ins[26];
+  double sub[26 * 26];
+  uint8_t seq[kWavesPerBlock][kSeqLds];
+};
+
+// Column residues of this wave's pair: staged in LDS (no VMEM wait in the
+// step loop); LONG kernels (L2 > kSeqLds) use the chunked global path.
+template <bool LONG>
+struct ColumnResidues {
+  const uint8_t* lds;
+  const uint8_t* glob;
+  int len;
+  ResidueChunk rc;
+  __device__ __forceinline__ void init(uint8_t* buf, const uint8_t* g, int L) {
+    lds = buf; glob = g; len = L; rc.init();
+    if constexpr (!LONG) {
+      for (int k = threadIdx.x & 63; k < L; k += 64) buf[k] = g[k];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+  }
+  __device__ __forceinline__ int get(int q) {
+    if constexpr (!LONG) return (q >= 0 && q < len) ? (int)lds[q] : 0;
+    else return rc.get(glob, len, q);
+  }
+};
+
+__device__ __forceinline__ void stage_tables(LdsTables& L, const Tables* __restrict__ tab) {
+  for (int k = threadIdx.x; k < 26 * 26; k += blockDim.x) {
+    L.match[k] = tab->match[k];
+    L.sub[k] = tab->sub[k];
+  }
+  if (threadIdx.x < 26) L.ins[threadIdx.x] = tab->ins[threadIdx.x];
+  if (threadIdx.x == 0) mlp_lookup_table(L.lk);
+  __syncthreads();
+}
+
+__device__ __forceinline__ int64_t wave_pair_index() {
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  return (int64_t)blockIdx.x * kWavesPerBlock + w;
+}
+
 __device__ __forceinline__ float readlane_f(float v, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
@@ -87,6 +111,71 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
   r.y = __builtin_amdgcn_readlane(w.y, l);
   return *reinterpret_cast<double*>(&r);
 }
+
+// Boundary row of the neighbouring strip, read 64 columns at a time (one per
+// lane) and double-buffered: the sweeps run their steps in chunks of 64 and
+// switch buffers between chunks, so the chunk in use is loop-invariant in the
+// step loop and was loaded a whole chunk earlier -- reading it never waits on
+// the loads and stores issued since (vmcnt is in order on gfx9).  Loads use
+// clamped addresses; out-of-range columns are masked at take().
+template <int M>
+struct BoundaryChunks {
+  float c5[5], n5[5], cl[3], nl[3];
+  double cz[3], nz[3];
+  int ce, ne;
+  __device__ __forceinline__ void load_next(const Scratch& sc, int64_t bo, int L2, int col0, int lane) {
+    const int col = col0 + lane;
+    const int64_t bi = bo + min(max(col, 0), L2);
+    if constexpr ((M & kHmm5) != 0) {
+#pragma unroll
+      for (int k = 0; k < 5; ++k) n5[k] = sc.bnd5[bi * 5 + k];
+    }
+    if constexpr ((M & kLocal) != 0) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) nl[k] = sc.bndl[bi * 3 + k];
+    }
+    if constexpr ((M & kPF) != 0) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) nz[k] = sc.bndz[bi * 3 + k];
+      ne = sc.bnde[bi];
+    }
+  }
+  __device__ __forceinline__ void advance() {
+#pragma unroll
+    for (int k = 0; k < 5; ++k) c5[k] = n5[k];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) { cl[k] = nl[k]; cz[k] = nz[k]; }
+    ce = ne;
+  }
+  // the value of column q of the current chunk into lane `who`'s neighbour
+  // state; `ok` (wave-uniform) = the column lies inside 0..L2
+  __device__ __forceinline__ void take(int q, bool ok, bool who, float* X5, float* XL,
+                                       double& Zm, double& Ze, double& Zf, int& e) const {
+    if constexpr ((M & kHmm5) != 0) {
+#pragma unroll
+      for (int k = 0; k < 5; ++k) {
+        const float v = ok ? readlane_f(c5[k], q) : LZ;
+        X5[k] = who ? v : X5[k];
+      }
+    }
+    if constexpr ((M & kLocal) != 0) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const float v = ok ? readlane_f(cl[k], q) : LZ;
+        XL[k] = who ? v : XL[k];
+      }
+    }
+    if constexpr ((M & kPF) != 0) {
+      const double z0 = ok ? readlane_d(cz[0], q) : 0.0, z1 = ok ? readlane_d(cz[1], q) : 0.0;
+      const double z2 = ok ? readlane_d(cz[2], q) : 0.0;
+      const int ee = ok ? __builtin_amdgcn_readlane(ce, q) : 0;
+      Zm = who ? z0 : Zm; Ze = who ? z1 : Ze; Zf = who ? z2 : Zf; e = who ? ee : e;
+    }
+  }
+};
+
+// Depth of the software-pipelined loads of the backward step loop.
+constexpr int kPrefetch = 4;
 
 // Bring three scaled-fp64 frames to their common maximum (exact: powers of two).
 __device__ __forceinline__ int pf_align(double& a0, double& a1, double& a2, int ea,
@@ -111,7 +200,7 @@ __device__ __forceinline__ void pf_rescale(double& zm, double& ze, double& zf, i
 // 2..L2-1) take a branch-free path; the others evaluate the reference's
 // boundary conditions per lane.
 // =====================================================================
-template <int M>
+template <int M, bool LONG>
 __global__ __launch_bounds__(256) void k_forward(ModelScalars ms, const Tables* __restrict__ tab,
                                                  SeqSet sq, PairMeta pm, PairRec* __restrict__ rec,
                                                  Scratch sc, int64_t npairs) {
@@ -126,7 +215,7 @@ __global__ __launch_bounds__(256) void k_forward(ModelScalars ms, const Tables* 
   const uint8_t* __restrict__ s1 = sq.res + sq.off[a];
   const uint8_t* __restrict__ s2 = sq.res + sq.off[b];
   const int S = (L1 + 64) >> 6;
-  const int T = L2 + 64;
+  const int T = strip_steps(L2);
   const int64_t cbase = pm.cell_off[p];
   const int64_t rmb = pm.rm_off[p];
   const int Wp = (L2 + 3) & ~3;
@@ -134,6 +223,8 @@ __global__ __launch_bounds__(256) void k_forward(ModelScalars ms, const Tables* 
   const float rt1 = ms.rt1, two_rt1 = 2 * ms.rt1;
   const double pfo = ms.pf_open, pfe = ms.pf_ext;
   int pf_over = 0;
+  ColumnResidues<LONG> cres;
+  cres.init(T_.seq[(threadIdx.x >> 6)], s2, L2);
 
   for (int s = 0; s < S; ++s) {
     const int i = (s << 6) + lane;
@@ -150,18 +241,25 @@ __global__ __launch_bounds__(256) void k_forward(ModelScalars ms, const Tables* 
     for (int k = 0; k < 5; ++k) L5[k] = U5[k] = D5[k] = LZ;
 #pragma unroll
     for (int k = 0; k < 3; ++k) LL[k] = UL[k] = DL[k] = LZ;
-    float cb0 = 0, cb1 = 0, cb2 = 0, cb3 = 0;  // row-major chain staging
+    // row-major chain staging; unused slots stay LOG_ZERO, a no-op in the chain
+    float cb0 = LZ, cb1 = LZ, cb2 = LZ, cb3 = LZ;
     int c2 = 0;
-    ResidueChunk rc2;
-    rc2.init();
-    float bch5[5], bchl[3];
-    double bchz[3];
-    int bche = 0;
-    int bbase = -(1 << 30);
+    BoundaryChunks<M> bc;
+    if (s > 0) {
+      bc.load_next(sc, bo, L2, 0, lane);
+      bc.advance();
+      bc.load_next(sc, bo, L2, 64, lane);
+    }
 
-    for (int t = 0; t < T; ++t) {
+    for (int c = 0; (c << 6) < T; ++c) {
+    if (s > 0 && c > 0) {
+      bc.advance();
+      bc.load_next(sc, bo, L2, (c + 1) << 6, lane);
+    }
+    const int tend = min(T, (c << 6) + 64);
+    for (int t = c << 6; t < tend; ++t) {
       const int j = t - lane;
-      const int c2new = rc2.get(s2, L2, t - 1);   // residue j: s2[j-1]
+      const int c2new = cres.get(t - 1);   // residue j: s2[j-1]
       c2 = mlp_shr1i(c2, c2new);
       if constexpr ((M & kHmm5) != 0) {
 #pragma unroll
@@ -178,41 +276,7 @@ __global__ __launch_bounds__(256) void k_forward(ModelScalars ms, const Tables* 
       }
       if (s > 0) {
         // lane 0 takes row 64*s-1, column t, from the boundary buffer
-        const int cbk = t & ~63;
-        if (cbk != bbase) {
-          bbase = cbk;
-          const int col = cbk + lane;
-          const bool ok = col <= L2;
-          const int64_t bi = bo + col;
-          if constexpr ((M & kHmm5) != 0) {
-#pragma unroll
-            for (int k = 0; k < 5; ++k) bch5[k] = ok ? sc.bnd5[bi * 5 + k] : LZ;
-          }
-          if constexpr ((M & kLocal) != 0) {
-#pragma unroll
-            for (int k = 0; k < 3; ++k) bchl[k] = ok ? sc.bndl[bi * 3 + k] : LZ;
-          }
-          if constexpr ((M & kPF) != 0) {
-#pragma unroll
-            for (int k = 0; k < 3; ++k) bchz[k] = ok ? sc.bndz[bi * 3 + k] : 0.0;
-            bche = ok ? sc.bnde[bi] : 0;
-          }
-        }
-        const int q = t & 63;
-        if (lane == 0) {
-          if constexpr ((M & kHmm5) != 0) {
-#pragma unroll
-            for (int k = 0; k < 5; ++k) U5[k] = readlane_f(bch5[k], q);
-          }
-          if constexpr ((M & kLocal) != 0) {
-#pragma unroll
-            for (int k = 0; k < 3; ++k) UL[k] = readlane_f(bchl[k], q);
-          }
-          if constexpr ((M & kPF) != 0) {
-            UZm = readlane_d(bchz[0], q); UZe = readlane_d(bchz[1], q); UZf = readlane_d(bchz[2], q);
-            Ue = __builtin_amdgcn_readlane(bche, q);
-          }
-        }
+        bc.take(t & 63, t <= L2, lane == 0, U5, UL, UZm, UZe, UZf, Ue);
       }
 
       const int64_t idx = cbase + ((int64_t)s * T + t) * 64 + lane;
@@ -251,8 +315,8 @@ __global__ __launch_bounds__(256) void k_forward(ModelScalars ms, const Tables* 
               if (j > 0) { C[2] = vy1; C[4] = vy2; }
             }
           }
+          sc.f5[idx] = C[0];   // every lane: inactive slots of the strip are never read
           if (act) {
-            sc.f5[idx] = C[0];
             if (!INT && i == L1 && j == L2) {  // CPNP/ProbabilisticModel.h:415-419 (forward half)
               float tf = LZ;
 #pragma unroll
@@ -288,8 +352,8 @@ __global__ __launch_bounds__(256) void k_forward(ModelScalars ms, const Tables* 
               if (j > 0) Cy = vy;
             }
           }
+          sc.fl[idx] = Cm;
           if (act) {
-            sc.fl[idx] = Cm;
             if (lane == 63) {
               sc.bndl[(bo + j) * 3 + 0] = Cm;
               sc.bndl[(bo + j) * 3 + 1] = Cx;
@@ -306,6 +370,7 @@ __global__ __launch_bounds__(256) void k_forward(ModelScalars ms, const Tables* 
             if (q == 3 || (!INT && j == L2)) {
               *reinterpret_cast<float4*>(sc.chf + rmb + (int64_t)(i - 1) * Wp + ((j - 1) & ~3)) =
                   make_float4(cb0, cb1, cb2, cb3);
+              cb0 = cb1 = cb2 = cb3 = LZ;
             }
           }
           LL[0] = Cm; LL[1] = Cx; LL[2] = Cy;
@@ -335,9 +400,9 @@ __global__ __launch_bounds__(256) void k_forward(ModelScalars ms, const Tables* 
             Zm = (DZm + DZe + DZf) * score;
             pf_rescale(Zm, Ze, Zf, E);
           }
+          sc.zm[idx] = mlp_pf_pack(Zm, E);
           if (act) {
             pf_over |= (E > 250);
-            sc.zm[idx] = mlp_pf_pack(Zm, E);
             if (!INT && i == L1 && j == L2) {  // CPNP/MSAPartProbs.cpp:591,612
               rec[p].zmant = (Zm + Ze) + Zf;
               rec[p].zexp = E;
@@ -355,6 +420,7 @@ __global__ __launch_bounds__(256) void k_forward(ModelScalars ms, const Tables* 
       if (strip_interior && t >= 65 && t <= L2 - 1) cell(std::true_type{});
       else cell(std::false_type{});
     }
+    }
     // the next strip's lane 0 reads what lane 63 wrote
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
   }
@@ -369,7 +435,7 @@ __global__ __launch_bounds__(256) void k_forward(ModelScalars ms, const Tables* 
 // Backward: reverse sweep; emits f+b (in place), PF posterior, chains.
 // Interior steps: rows 2..L1-1, columns 2..L2-1 on every lane.
 // =====================================================================
-template <int M>
+template <int M, bool LONG>
 __global__ __launch_bounds__(256) void k_backward(ModelScalars ms, const Tables* __restrict__ tab,
                                                   SeqSet sq, PairMeta pm, PairRec* __restrict__ rec,
                                                   Scratch sc, int64_t npairs) {
@@ -384,7 +450,7 @@ __global__ __launch_bounds__(256) void k_backward(ModelScalars ms, const Tables*
   const uint8_t* __restrict__ s1 = sq.res + sq.off[a];
   const uint8_t* __restrict__ s2 = sq.res + sq.off[b];
   const int S = (L1 + 64) >> 6;
-  const int T = L2 + 64;
+  const int T = strip_steps(L2);
   const int64_t cbase = pm.cell_off[p];
   const int64_t rmb = pm.rm_off[p];
   const int Wp = (L2 + 3) & ~3;
@@ -393,6 +459,8 @@ __global__ __launch_bounds__(256) void k_backward(ModelScalars ms, const Tables*
   const double pfo = ms.pf_open, pfe = ms.pf_ext;
   const double zmant = (M & kPF) ? rec[p].zmant : 1.0;
   const int zexp = (M & kPF) ? rec[p].zexp : 0;
+  ColumnResidues<LONG> cres;
+  cres.init(T_.seq[(threadIdx.x >> 6)], s2, L2);
 
   for (int s = S - 1; s >= 0; --s) {
     const int i = (s << 6) + lane;
@@ -410,22 +478,48 @@ __global__ __launch_bounds__(256) void k_backward(ModelScalars ms, const Tables*
     for (int k = 0; k < 5; ++k) R5[k] = N5[k] = G5[k] = LZ;
 #pragma unroll
     for (int k = 0; k < 3; ++k) RL[k] = NL[k] = GL[k] = LZ;
-    float cb0 = 0, cb1 = 0, cb2 = 0, cb3 = 0;
+    float cb0 = LZ, cb1 = LZ, cb2 = LZ, cb3 = LZ;
     int c2n = 0;  // residue j+1
-    ResidueChunk rcn, rcc;
-    rcn.init();
-    rcc.init();
-    float bch5[5], bchl[3];
-    double bchz[3];
-    int bche = 0;
-    int bbase = -(1 << 30);
+    BoundaryChunks<M> bc;
+    const int c_top = (T - 1) >> 6;
+    if (s < S - 1) {
+      bc.load_next(sc, bo, L2, (c_top << 6) - 63, lane);
+      bc.advance();
+      bc.load_next(sc, bo, L2, ((c_top - 1) << 6) - 63, lane);
+    }
+    // the step-t loads of f5 / fl / zm are issued kPrefetch steps earlier;
+    // every slot of the strip was written by the forward sweep, values of
+    // inactive cells are never used
+    const int64_t sbase = cbase + (int64_t)s * T * 64 + lane;
+    // queue slot u always serves steps t0 - u: the loop is unrolled by
+    // kPrefetch (T is a multiple of 8) so every slot is a fixed register
+    float q5[kPrefetch] = {}, ql[kPrefetch] = {};
+    double qz[kPrefetch] = {};
+#pragma unroll
+    for (int k = 0; k < kPrefetch; ++k) {
+      const int tt = T - 1 - k;
+      if constexpr ((M & kHmm5) != 0) q5[k] = sc.f5[sbase + (int64_t)tt * 64];
+      if constexpr ((M & kLocal) != 0) ql[k] = sc.fl[sbase + (int64_t)tt * 64];
+      if constexpr ((M & kPF) != 0) qz[k] = sc.zm[sbase + (int64_t)tt * 64];
+    }
 
-    for (int t = T - 1; t >= 0; --t) {
+    for (int c = c_top; c >= 0; --c) {
+    if (s < S - 1 && c < c_top) {
+      bc.advance();
+      bc.load_next(sc, bo, L2, ((c - 1) << 6) - 63, lane);
+    }
+    // T - 1 = 7 (mod 8): every chunk holds a whole number of unrolled groups
+    for (int t0 = min(T - 1, (c << 6) + 63); t0 >= (c << 6); t0 -= kPrefetch)
+#pragma unroll
+    for (int u = 0; u < kPrefetch; ++u) {
+      const int t = t0 - u;
       const int j = t - lane;
+      const float f5v = q5[u], flv = ql[u];
+      const double zmv = qz[u];
       // residues: lane 63 takes s2[j] for its column j = t - 63
-      c2n = mlp_shl1i(c2n, rcn.get(s2, L2, t - 63));
+      c2n = mlp_shl1i(c2n, cres.get(t - 63));
       // residue j (current column) = c2n of lane+1 at this step
-      const int c2 = mlp_shl1i(c2n, rcc.get(s2, L2, t - 64));
+      const int c2 = mlp_shl1i(c2n, cres.get(t - 64));
       if constexpr ((M & kHmm5) != 0) {
 #pragma unroll
         for (int k = 0; k < 5; ++k) { G5[k] = N5[k]; N5[k] = mlp_shl1(R5[k], LZ); }
@@ -442,41 +536,7 @@ __global__ __launch_bounds__(256) void k_backward(ModelScalars ms, const Tables*
       if (s < S - 1) {
         // lane 63 takes row 64*(s+1), column t-63, from the boundary buffer
         const int col = t - 63;
-        const int cbk = col & ~63;
-        if (cbk != bbase) {
-          bbase = cbk;
-          const int cc = cbk + lane;
-          const bool ok = cc >= 0 && cc <= L2;
-          const int64_t bi = bo + cc;
-          if constexpr ((M & kHmm5) != 0) {
-#pragma unroll
-            for (int k = 0; k < 5; ++k) bch5[k] = ok ? sc.bnd5[bi * 5 + k] : LZ;
-          }
-          if constexpr ((M & kLocal) != 0) {
-#pragma unroll
-            for (int k = 0; k < 3; ++k) bchl[k] = ok ? sc.bndl[bi * 3 + k] : LZ;
-          }
-          if constexpr ((M & kPF) != 0) {
-#pragma unroll
-            for (int k = 0; k < 3; ++k) bchz[k] = ok ? sc.bndz[bi * 3 + k] : 0.0;
-            bche = ok ? sc.bnde[bi] : 0;
-          }
-        }
-        const int q = col & 63;
-        if (lane == 63) {
-          if constexpr ((M & kHmm5) != 0) {
-#pragma unroll
-            for (int k = 0; k < 5; ++k) N5[k] = readlane_f(bch5[k], q);
-          }
-          if constexpr ((M & kLocal) != 0) {
-#pragma unroll
-            for (int k = 0; k < 3; ++k) NL[k] = readlane_f(bchl[k], q);
-          }
-          if constexpr ((M & kPF) != 0) {
-            NZm = readlane_d(bchz[0], q); NZe = readlane_d(bchz[1], q); NZf = readlane_d(bchz[2], q);
-            Ne = __builtin_amdgcn_readlane(bche, q);
-          }
-        }
+        bc.take(t & 63, col >= 0 && col <= L2, lane == 63, N5, NL, NZm, NZe, NZf, Ne);
       }
 
       const int64_t idx = cbase + ((int64_t)s * T + t) * 64 + lane;
@@ -513,8 +573,8 @@ __global__ __launch_bounds__(256) void k_backward(ModelScalars ms, const Tables*
             B[0] = mlp_log_add_t(B[0], R5[4] + ins2n + ms.t[0][4], lk);
             B[4] = mlp_log_add_t(B[4], R5[4] + ins2n + ms.t[4][4], lk);
           }
+          sc.f5[idx] = f5v + B[0];   // f + b (CPNP/ProbabilisticModel.h:484)
           if (act) {
-            sc.f5[idx] = sc.f5[idx] + B[0];   // f + b (CPNP/ProbabilisticModel.h:484)
             if (!INT) {
               if (i == 1 && j == 1) rec[p].b5[0] = B[0];
               if (i == 1 && j == 0) { rec[p].b5[1] = B[1]; rec[p].b5[3] = B[3]; }
@@ -547,8 +607,8 @@ __global__ __launch_bounds__(256) void k_backward(ModelScalars ms, const Tables*
             Bm = mlp_log_add_t(Bm, RL[2] + ms.lt[0][2] - rt1, lk);
             By = mlp_log_add_t(By, RL[2] + ms.lt[2][2] - rt1, lk);
           }
+          sc.fl[idx] = flv + Bm;
           if (act) {
-            sc.fl[idx] = sc.fl[idx] + Bm;
             if (lane == 0) {
               sc.bndl[(bo + j) * 3 + 0] = Bm;
               sc.bndl[(bo + j) * 3 + 1] = Bx;
@@ -566,6 +626,7 @@ __global__ __launch_bounds__(256) void k_backward(ModelScalars ms, const Tables*
             if (q == 0) {
               *reinterpret_cast<float4*>(sc.chb + rmb + (int64_t)(i - 1) * Wp + (j - 1)) =
                   make_float4(cb0, cb1, cb2, cb3);
+              cb0 = cb1 = cb2 = cb3 = LZ;
             }
           }
           RL[0] = Bm; RL[1] = Bx; RL[2] = By;
@@ -602,13 +663,13 @@ __global__ __launch_bounds__(256) void k_backward(ModelScalars ms, const Tables*
             pf_rescale(Zm, Ze, Zf, E);
             if (act) {
               int ef;
-              const double zf = mlp_pf_unpack(sc.zm[idx], &ef);
+              const double zf = mlp_pf_unpack(zmv, &ef);
               const double q = (zf * Zm) / (score * zmant);
               post = (float)ldexp(q, MLP_PF_STEP * (ef + E - zexp));
             }
           }
+          sc.pg[idx] = post;
           if (act) {
-            sc.pg[idx] = post;
             if (lane == 0) {
               sc.bndz[(bo + j) * 3 + 0] = Zm;
               sc.bndz[(bo + j) * 3 + 1] = Ze;
@@ -621,6 +682,13 @@ __global__ __launch_bounds__(256) void k_backward(ModelScalars ms, const Tables*
       };
       if (strip_interior && t >= 65 && t <= L2 - 1) cell(std::true_type{});
       else cell(std::false_type{});
+      // refill slot u after its value is dead, so the load reuses the register
+      // (a loop-carried copy of a pending load would drain vmcnt)
+      const int tt = max(t - kPrefetch, 0);
+      if constexpr ((M & kHmm5) != 0) q5[u] = sc.f5[sbase + (int64_t)tt * 64];
+      if constexpr ((M & kLocal) != 0) ql[u] = sc.fl[sbase + (int64_t)tt * 64];
+      if constexpr ((M & kPF) != 0) qz[u] = sc.zm[sbase + (int64_t)tt * 64];
+    }
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
   }
@@ -631,49 +699,163 @@ __global__ __launch_bounds__(256) void k_backward(ModelScalars ms, const Tables*
 // cells in row-major order (CPNP/ProbabilisticModel.h:435-450), a single
 // non-associative chain, for the forward and the backward half.
 //
-// One wave per pair streams 64 consecutive row-major elements at a time.  An
-// element x leaves the running sum acc unchanged iff acc - x >= 7.5 (the
-// LOG_ADD cutoff), and acc never decreases (LOOKUP(d) - d >= 4.46e-4 for
-// every float d in [0, 7.5), checked exhaustively), so an element that is
-// skippable against the current acc is skippable at its turn too.  Only the
-// remaining candidates are folded in, serially and in order, with the exact
-// LOG_ADD: the result is bit-identical to the reference's chain.
+// One lane per pair walks its two chains serially (the exact reference
+// order; rows are padded to a multiple of 4 with LOG_ZERO, a no-op element).
+// A wave owns 64 pairs and stages 16-element tiles of all 64 chains through
+// LDS with coalesced loads.  Inside a tile an element x is folded with the
+// exact LOG_ADD unless acc - x >= 7.5, where LOG_ADD returns acc unchanged
+// (CPNP/ScoreType.h:279-285), so the skip is exact.
 // =====================================================================
-__global__ __launch_bounds__(256) void k_local_totals(SeqSet sq, PairMeta pm, PairRec* __restrict__ rec,
-                                                      Scratch sc, int64_t npairs) {
+constexpr int kTile = 32;
+__global__ __launch_bounds__(64) void k_local_totals_lane(SeqSet sq, PairMeta pm, PairRec* __restrict__ rec,
+                                                          Scratch sc, int64_t npairs) {
+  __shared__ float tf_t[64][kTile + 1];
+  __shared__ float tb_t[64][kTile + 1];
+  const int lane = threadIdx.x;
+  const int64_t g0 = (int64_t)blockIdx.x * 64;
+  const int64_t p = g0 + lane;
+  int64_t ne = 0, base = 0;
+  if (p < npairs) {
+    const int L1 = sq.len[pm.pa[p]], L2 = sq.len[pm.pb[p]];
+    ne = (int64_t)L1 * ((L2 + 3) & ~3);
+    base = pm.rm_off[p];
+  }
+  int64_t emax = ne;
+  for (int off = 32; off >= 1; off >>= 1) emax = max(emax, (int64_t)__shfl_xor(emax, off));
+  // loader geometry: 8 lanes x float4 cover one pair's 32-element tile;
+  // 8 rounds cover the 64 pairs
+  const int part = lane & 7;
+  int64_t nq[8], bq[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int q = k * 8 + (lane >> 3);
+    nq[k] = __shfl(ne, q);
+    bq[k] = __shfl(base, q);
+  }
+  float4 pf[8], pb[8];
+  auto load = [&](int64_t e0) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int64_t e = e0 + part * 4;
+      pf[k] = make_float4(LZ, LZ, LZ, LZ);
+      pb[k] = pf[k];
+      if (e < nq[k]) {
+        pf[k] = *reinterpret_cast<const float4*>(sc.chf + bq[k] + e);
+        pb[k] = *reinterpret_cast<const float4*>(sc.chb + bq[k] + e);
+      }
+    }
+  };
+  float tf = LZ, tb = LZ;
+  load(0);
+  for (int64_t e0 = 0; e0 < emax; e0 += kTile) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int q = k * 8 + (lane >> 3);
+      tf_t[q][part * 4 + 0] = pf[k].x; tf_t[q][part * 4 + 1] = pf[k].y;
+      tf_t[q][part * 4 + 2] = pf[k].z; tf_t[q][part * 4 + 3] = pf[k].w;
+      tb_t[q][part * 4 + 0] = pb[k].x; tb_t[q][part * 4 + 1] = pb[k].y;
+      tb_t[q][part * 4 + 2] = pb[k].z; tb_t[q][part * 4 + 3] = pb[k].w;
+    }
+    __syncthreads();
+    if (e0 + kTile < emax) load(e0 + kTile);  // prefetch the next tile meanwhile
+#pragma unroll 8
+    for (int u = 0; u < kTile; ++u) {
+      const float xf = tf_t[lane][u], xb = tb_t[lane][u];
+      tf = mlp_log_add(tf, xf);
+      tb = mlp_log_add(tb, xb);
+    }
+    __syncthreads();
+  }
+  if (p < npairs) {
+    rec[p].tfl = tf;
+    rec[p].tbl = tb;
+  }
+}
+
+// Variant: 8 lanes per pair, 8 pairs per wave.  Each group streams 8
+// consecutive elements of its pair; every lane evaluates the exact LOG_ADD of
+// the group's running total with its own element and the group adopts the
+// result of its first pending candidate (a shuffle), so one wave instruction
+// stream folds eight chains at once.
+__device__ __forceinline__ float fold_group(float acc, float x, int sub, int gbase) {
+  bool cand = !(acc - x >= 7.5f);
+  while (true) {
+    const uint64_t m = __ballot(cand);
+    if (m == 0) break;
+    const uint32_t gm = (uint32_t)(m >> gbase) & 0xFFu;
+    const int first = gm ? __builtin_ctz(gm) : 8;
+    const float v = mlp_log_add(acc, x);
+    const float nv = __shfl(v, gbase + (first & 7));
+    if (gm) acc = nv;
+    cand = cand && (sub > first) && !(acc - x >= 7.5f);
+  }
+  return acc;
+}
+
+__global__ __launch_bounds__(256) void k_local_totals_grp(SeqSet sq, PairMeta pm, PairRec* __restrict__ rec,
+                                                          Scratch sc, int64_t npairs) {
+  const int lane = threadIdx.x & 63;
+  const int sub = lane & 7, gbase = lane & ~7;
+  const int64_t wave = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  const int64_t p = wave * 8 + (lane >> 3);
+  int64_t ne = 0, base = 0;
+  if (p < npairs) {
+    const int L1 = sq.len[pm.pa[p]], L2 = sq.len[pm.pb[p]];
+    ne = (int64_t)L1 * ((L2 + 3) & ~3);
+    base = pm.rm_off[p];
+  }
+  int64_t emax = ne;
+  for (int off = 32; off >= 8; off >>= 1) emax = max(emax, (int64_t)__shfl_xor(emax, off));
+  const float* __restrict__ cf = sc.chf + base;
+  const float* __restrict__ cbk = sc.chb + base;
+  float tf = LZ, tb = LZ;
+  float xf = (sub < ne) ? cf[sub] : LZ, xb = (sub < ne) ? cbk[sub] : LZ;
+  for (int64_t e0 = 0; e0 < emax; e0 += 8) {
+    const float cxf = xf, cxb = xb;
+    const int64_t en = e0 + 8 + sub;
+    xf = LZ; xb = LZ;
+    if (en < ne) { xf = cf[en]; xb = cbk[en]; }  // prefetch the next chunk
+    tf = fold_group(tf, cxf, sub, gbase);
+    tb = fold_group(tb, cxb, sub, gbase);
+  }
+  if (p < npairs && sub == 0) {
+    rec[p].tfl = tf;
+    rec[p].tbl = tb;
+  }
+}
+
+// Variant: one wave per pair, candidates folded serially (see above).
+__global__ __launch_bounds__(256) void k_local_totals_wave(SeqSet sq, PairMeta pm, PairRec* __restrict__ rec,
+                                                           Scratch sc, int64_t npairs) {
   const int64_t p = wave_pair_index();
   if (p >= npairs) return;
   const int lane = threadIdx.x & 63;
   const int L1 = sq.len[pm.pa[p]], L2 = sq.len[pm.pb[p]];
-  const int Wp = (L2 + 3) & ~3;
+  const int64_t ne = (int64_t)L1 * ((L2 + 3) & ~3);
   const float* __restrict__ cf = sc.chf + pm.rm_off[p];
   const float* __restrict__ cbk = sc.chb + pm.rm_off[p];
   float tf = LZ, tb = LZ;
-  for (int i = 0; i < L1; ++i) {
-    const float* rf = cf + (int64_t)i * Wp;
-    const float* rb = cbk + (int64_t)i * Wp;
-    for (int c0 = 0; c0 < L2; c0 += 64) {
-      const int j = c0 + lane;
-      const bool ok = j < L2;
-      const float xf = ok ? rf[j] : LZ;
-      const float xb = ok ? rb[j] : LZ;
-      uint64_t mf = __ballot(ok && !(tf - xf >= 7.5f));
-      uint64_t mb = __ballot(ok && !(tb - xb >= 7.5f));
-      while (mf | mb) {
-        if (mf) {
-          const int l = __builtin_ctzll(mf);
-          const float v = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xf), l));
-          tf = mlp_log_add(tf, v);
-          mf &= mf - 1;
-          mf &= __ballot(!(tf - xf >= 7.5f));
-        }
-        if (mb) {
-          const int l = __builtin_ctzll(mb);
-          const float v = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xb), l));
-          tb = mlp_log_add(tb, v);
-          mb &= mb - 1;
-          mb &= __ballot(!(tb - xb >= 7.5f));
-        }
+  float xf = LZ, xb = LZ;
+  if (lane < ne) { xf = cf[lane]; xb = cbk[lane]; }
+  for (int64_t c0 = 0; c0 < ne; c0 += 64) {
+    const float cxf = xf, cxb = xb;
+    const int64_t nx = c0 + 64 + lane;
+    xf = LZ; xb = LZ;
+    if (nx < ne) { xf = cf[nx]; xb = cbk[nx]; }   // prefetch next chunk
+    uint64_t mf = __ballot(!(tf - cxf >= 7.5f));
+    uint64_t mb = __ballot(!(tb - cxb >= 7.5f));
+    while (mf | mb) {
+      if (mf) {
+        const int l = __builtin_ctzll(mf);
+        tf = mlp_log_add(tf, __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cxf), l)));
+        mf &= mf - 1;
+        mf &= __ballot(!(tf - cxf >= 7.5f));
+      }
+      if (mb) {
+        const int l = __builtin_ctzll(mb);
+        tb = mlp_log_add(tb, __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cxb), l)));
+        mb &= mb - 1;
+        mb &= __ballot(!(tb - cxb >= 7.5f));
       }
     }
   }
@@ -697,7 +879,7 @@ __global__ __launch_bounds__(256) void k_merge(ModelScalars ms, SeqSet sq, PairM
   const int lane = threadIdx.x & 63;
   const int L1 = sq.len[pm.pa[p]], L2 = sq.len[pm.pb[p]];
   const int S = (L1 + 64) >> 6;
-  const int T = L2 + 64;
+  const int T = strip_steps(L2);
   const int64_t cbase = pm.cell_off[p];
   const int64_t bo = pm.bnd_off[p];
   const int64_t er0 = pm.ell_row[p];
@@ -723,20 +905,40 @@ __global__ __launch_bounds__(256) void k_merge(ModelScalars ms, SeqSet sq, PairM
     float Lv = 0.f, Uv = 0.f, Dv = 0.f;
     int cnt = 0;
     const int64_t erow = er0 + (i - 1);
-    float bch = 0.f;
-    int bbase = -(1 << 30);
-    for (int t = 0; t < T; ++t) {
+    // boundary row 64s-1 (MEA values), double-buffered as in BoundaryChunks
+    float bch = 0.f, bnx = 0.f;
+    if (s > 0) {
+      bch = sc.bndm[bo + min(lane, L2)];
+      bnx = sc.bndm[bo + min(64 + lane, L2)];
+    }
+    // slots of the strip written by the backward sweep; values of inactive
+    // cells are never used
+    const int64_t sbase = cbase + (int64_t)s * T * 64 + lane;
+    constexpr int QD = 8;
+    // fixed-register load queue: slot u serves steps t0 + u (T % QD == 0)
+    float q5[QD] = {}, ql[QD] = {}, qg[QD] = {};
+#pragma unroll
+    for (int k = 0; k < QD; ++k) {
+      if constexpr ((M & kHmm5) != 0) q5[k] = sc.f5[sbase + (int64_t)k * 64];
+      if constexpr ((M & kLocal) != 0) ql[k] = sc.fl[sbase + (int64_t)k * 64];
+      if constexpr ((M & kPF) != 0) qg[k] = sc.pg[sbase + (int64_t)k * 64];
+    }
+    for (int c = 0; (c << 6) < T; ++c) {
+    if (s > 0 && c > 0) {
+      bch = bnx;
+      bnx = sc.bndm[bo + min(((c + 1) << 6) + lane, L2)];
+    }
+    const int tend = min(T, (c << 6) + 64);
+    for (int t0 = c << 6; t0 < tend; t0 += QD)
+#pragma unroll
+    for (int u = 0; u < QD; ++u) {
+      const int t = t0 + u;
       const int j = t - lane;
+      const float f5v = q5[u], flv = ql[u], pgv = qg[u];
       Dv = Uv;
       Uv = mlp_shr1(Lv, 0.f);
       if (s > 0) {
-        const int cbk = t & ~63;
-        if (cbk != bbase) {
-          bbase = cbk;
-          const int col = cbk + lane;
-          bch = (col <= L2) ? sc.bndm[bo + col] : 0.f;
-        }
-        const float v = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(bch), t & 63));
+        const float v = (t <= L2) ? readlane_f(bch, t & 63) : 0.f;
         if (lane == 0) Uv = v;
       }
       const bool act = row_ok && j >= 1 && j <= L2;
@@ -744,13 +946,13 @@ __global__ __launch_bounds__(256) void k_merge(ModelScalars ms, SeqSet sq, PairM
       float P = 0.f;
       if (act) {
         if constexpr (PID == 2) {
-          P = mlp_post_from_sum_t(sc.fl[idx], TL, ex);
+          P = mlp_post_from_sum_t(flv, TL, ex);
         } else if constexpr (PID >= 3) {
-          P = sc.pg[idx];
+          P = pgv;
         } else {
-          const float v1 = mlp_post_from_sum_t(sc.f5[idx], T5, ex);
-          const float v2 = sc.pg[idx];
-          const float v3 = mlp_post_from_sum_t(sc.fl[idx], TL, ex);
+          const float v1 = mlp_post_from_sum_t(f5v, T5, ex);
+          const float v2 = pgv;
+          const float v3 = mlp_post_from_sum_t(flv, TL, ex);
           P = sqrtf((v1 * v1 + v2 * v2 + v3 * v3) / 3);
         }
       }
@@ -772,6 +974,12 @@ __global__ __launch_bounds__(256) void k_merge(ModelScalars ms, SeqSet sq, PairM
       }
       if (lane == 63 && i <= L1 && j >= 0 && j <= L2) sc.bndm[bo + j] = Cv;
       Lv = Cv;
+      // refill slot u once its value is dead (see k_backward)
+      const int tt = min(t + QD, T - 1);
+      if constexpr ((M & kHmm5) != 0) q5[u] = sc.f5[sbase + (int64_t)tt * 64];
+      if constexpr ((M & kLocal) != 0) ql[u] = sc.fl[sbase + (int64_t)tt * 64];
+      if constexpr ((M & kPF) != 0) qg[u] = sc.pg[sbase + (int64_t)tt * 64];
+    }
     }
     if (row_ok) {
       sc.ell_cnt[erow] = cnt;
@@ -856,35 +1064,66 @@ __global__ void k_fold_totals(ModelScalars ms, SeqSet sq, PairMeta pm, PairRec* 
 }
 
 // ------------------------------------------------------------ launchers
+// MLP_FUSE=1 runs all three models in one sweep (default: two sweeps).
+static bool fuse_models() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("MLP_FUSE");
+    v = (e && e[0] == '1') ? 1 : 0;
+  }
+  return v == 1;
+}
+
 static inline dim3 wave_grid(int64_t npairs) {
   return dim3((unsigned)((npairs + kWavesPerBlock - 1) / kWavesPerBlock));
 }
 
-hipError_t launch_forward(int models, const ModelScalars& ms, const Tables* tab, SeqSet seqs,
-                          PairMeta pm, PairRec* rec, Scratch sc, int64_t npairs, hipStream_t st) {
-  if (npairs <= 0) return hipSuccess;
+// One sweep kernel K<M, LONG> per model set; LONG when a column sequence of
+// the batch does not fit the per-wave LDS residue buffer.
+template <template <int, bool> class K>
+static hipError_t launch_sweep(int models, bool long_seq, const ModelScalars& ms, const Tables* tab,
+                               SeqSet seqs, PairMeta pm, PairRec* rec, Scratch sc, int64_t npairs,
+                               hipStream_t st) {
   const dim3 g = wave_grid(npairs), b(64 * kWavesPerBlock);
+  auto go = [&](auto m_tag) {
+    constexpr int Mv = decltype(m_tag)::value;
+    if (long_seq) hipLaunchKernelGGL((K<Mv, true>::fn), g, b, 0, st, ms, tab, seqs, pm, rec, sc, npairs);
+    else hipLaunchKernelGGL((K<Mv, false>::fn), g, b, 0, st, ms, tab, seqs, pm, rec, sc, npairs);
+  };
   switch (models) {
-    case kHmm5 | kLocal | kPF: hipLaunchKernelGGL(k_forward<kHmm5 | kLocal | kPF>, g, b, 0, st, ms, tab, seqs, pm, rec, sc, npairs); break;
-    case kLocal: hipLaunchKernelGGL(k_forward<kLocal>, g, b, 0, st, ms, tab, seqs, pm, rec, sc, npairs); break;
-    case kPF: hipLaunchKernelGGL(k_forward<kPF>, g, b, 0, st, ms, tab, seqs, pm, rec, sc, npairs); break;
-    case kHmm5: hipLaunchKernelGGL(k_forward<kHmm5>, g, b, 0, st, ms, tab, seqs, pm, rec, sc, npairs); break;
+    case kHmm5 | kLocal | kPF:
+      if (fuse_models()) {
+        go(std::integral_constant<int, kHmm5 | kLocal | kPF>{});
+      } else {  // fp32 HMMs and the fp64 partition function as two sweeps: fewer VGPRs each
+        go(std::integral_constant<int, kHmm5 | kLocal>{});
+        go(std::integral_constant<int, kPF>{});
+      }
+      break;
+    case kLocal: go(std::integral_constant<int, kLocal>{}); break;
+    case kPF: go(std::integral_constant<int, kPF>{}); break;
+    case kHmm5: go(std::integral_constant<int, kHmm5>{}); break;
     default: return hipErrorInvalidValue;
   }
+  return hipSuccess;
+}
+template <int M, bool LONG> struct ForwardK { static constexpr auto fn = k_forward<M, LONG>; };
+template <int M, bool LONG> struct BackwardK { static constexpr auto fn = k_backward<M, LONG>; };
+
+hipError_t launch_forward(int models, const ModelScalars& ms, const Tables* tab, SeqSet seqs,
+                          PairMeta pm, PairRec* rec, Scratch sc, int64_t npairs, int max_len2,
+                          hipStream_t st) {
+  if (npairs <= 0) return hipSuccess;
+  const hipError_t e = launch_sweep<ForwardK>(models, max_len2 > kSeqLds, ms, tab, seqs, pm, rec, sc, npairs, st);
+  if (e != hipSuccess) return e;
   return hipGetLastError();
 }
 
 hipError_t launch_backward(int models, const ModelScalars& ms, const Tables* tab, SeqSet seqs,
-                           PairMeta pm, PairRec* rec, Scratch sc, int64_t npairs, hipStream_t st) {
+                           PairMeta pm, PairRec* rec, Scratch sc, int64_t npairs, int max_len2,
+                           hipStream_t st) {
   if (npairs <= 0) return hipSuccess;
-  const dim3 g = wave_grid(npairs), b(64 * kWavesPerBlock);
-  switch (models) {
-    case kHmm5 | kLocal | kPF: hipLaunchKernelGGL(k_backward<kHmm5 | kLocal | kPF>, g, b, 0, st, ms, tab, seqs, pm, rec, sc, npairs); break;
-    case kLocal: hipLaunchKernelGGL(k_backward<kLocal>, g, b, 0, st, ms, tab, seqs, pm, rec, sc, npairs); break;
-    case kPF: hipLaunchKernelGGL(k_backward<kPF>, g, b, 0, st, ms, tab, seqs, pm, rec, sc, npairs); break;
-    case kHmm5: hipLaunchKernelGGL(k_backward<kHmm5>, g, b, 0, st, ms, tab, seqs, pm, rec, sc, npairs); break;
-    default: return hipErrorInvalidValue;
-  }
+  const hipError_t e = launch_sweep<BackwardK>(models, max_len2 > kSeqLds, ms, tab, seqs, pm, rec, sc, npairs, st);
+  if (e != hipSuccess) return e;
   if (models & kHmm5) {
     // fold the 5-state backward total (needs Tables for the initial cells)
     hipLaunchKernelGGL(k_fold_totals, dim3((unsigned)((npairs + 255) / 256)), dim3(256), 0, st, ms, seqs, pm, rec, tab, npairs);
@@ -895,7 +1134,13 @@ hipError_t launch_backward(int models, const ModelScalars& ms, const Tables* tab
 hipError_t launch_local_totals(SeqSet seqs, PairMeta pm, PairRec* rec, Scratch sc, int64_t npairs,
                                hipStream_t st) {
   if (npairs <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_local_totals, wave_grid(npairs), dim3(64 * kWavesPerBlock), 0, st, seqs, pm, rec, sc, npairs);
+  const char* v = getenv("MLP_TOTALS");
+  if (v && v[0] == 'g')
+    hipLaunchKernelGGL(k_local_totals_grp, dim3((unsigned)((npairs + 8 * kWavesPerBlock - 1) / (8 * kWavesPerBlock))), dim3(64 * kWavesPerBlock), 0, st, seqs, pm, rec, sc, npairs);
+  else if (!v || v[0] == 'w')
+    hipLaunchKernelGGL(k_local_totals_wave, wave_grid(npairs), dim3(64 * kWavesPerBlock), 0, st, seqs, pm, rec, sc, npairs);
+  else
+    hipLaunchKernelGGL(k_local_totals_lane, dim3((unsigned)((npairs + 63) / 64)), dim3(64), 0, st, seqs, pm, rec, sc, npairs);
   return hipGetLastError();
 }
 
