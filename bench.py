@@ -26,6 +26,9 @@ sys.path.insert(0, ROOT)
 
 METRIC = 'pair-HMM DP cell updates/s (all-pairs) + end-to-end MSA sec/family'
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+# VALU issue peak: 256 CUs x 4 SIMDs x 2.4 GHz, one wave64 VALU instruction per
+# 4 cycles per SIMD (16 lanes wide) -- the bound the DP sweeps actually hit
+VALU_PEAK_WAVE_INSTS = 256 * 4 * 2.4e9 / 4
 # Algorithmic HBM bytes per pair-cell for each kernel of the pid-0 pipeline
 # ("Kernels and their rooflines").
 ALGO_BYTES = {'forward': 20, 'backward': 32, 'local_totals': 8, 'merge_mea_sparsify': 12}
@@ -43,7 +46,7 @@ def parse():
     ap.add_argument('--seed', type=int, default=11)
     ap.add_argument('--pid', type=int, default=0)
     ap.add_argument('--delta', type=float, default=0.132548)
-    ap.add_argument('--cpu-pairs', type=int, default=768, help='reference CPU baseline sample (pairs)')
+    ap.add_argument('--cpu-pairs', type=int, default=6144, help='reference CPU baseline sample (pairs)')
     ap.add_argument('--cpu-threads', type=int, default=16)
     ap.add_argument('--no-cpu', action='store_true')
     ap.add_argument('--relax', type=int, default=0, help='also time N relaxation rounds (reported separately)')
@@ -151,11 +154,21 @@ def main():
     avg_ms = kt[dom]['ms'] / launches
     bytes_per_launch = ALGO_BYTES[dom] * kt[dom]['cells'] / launches
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
-    traffic = None
+    # measured HBM bytes and VALU instructions per pair-cell of this kernel
+    # group from the committed PMC passes (tools/pmc_run.sh), scaled to the
+    # cells of one launch here
+    traffic, valu = None, None
     pmc = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
     if os.path.exists(pmc):
         with open(pmc) as fh:
-            traffic = json.load(fh).get(dom)
+            g = json.load(fh).get(dom)
+        if g:
+            cells_per_launch = kt[dom]['cells'] / launches
+            traffic = g['traffic_bytes_per_cell'] * cells_per_launch / 1e9
+            issued = g['valu_insts_per_cell'] * cells_per_launch / (avg_ms * 1e-3)
+            valu = {'achieved': issued, 'peak': VALU_PEAK_WAVE_INSTS, 'unit': 'wave-instr/s',
+                    'frac': issued / VALU_PEAK_WAVE_INSTS,
+                    'insts_per_cell': g['valu_insts_per_cell']}
     out = None
     if rank == 0:
         cpu = None
@@ -185,7 +198,9 @@ def main():
                        'parallelism': f'pair-sharded dp{world}' + (' + RCCL all-gather' if world > 1 else '')},
             'roofline': {'bound': 'hbm', 'kernel': dom, 'achieved': achieved, 'peak': HBM_PEAK_GBS,
                          'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
-                         'algo_bytes_per_cell': ALGO_BYTES[dom], 'avg_launch_ms': avg_ms},
+                         'traffic_unit': 'GB per launch (2 x FETCH_SIZE + WRITE_SIZE)',
+                         'algo_bytes_per_cell': ALGO_BYTES[dom], 'avg_launch_ms': avg_ms,
+                         'valu_issue': valu},
             'stage_roofline': {'algo_bytes_per_cell': STAGE_BYTES,
                                'achieved_GBps': value * STAGE_BYTES / 1e9,
                                'frac': value * STAGE_BYTES / 1e9 / HBM_PEAK_GBS},

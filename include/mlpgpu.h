@@ -81,7 +81,7 @@ int mlp_csr_import(mlp_ctx *ctx, const int32_t *row_ptr, const int64_t *ent_off,
 /* `iters` rounds of the consistency transformation over the whole store.
  * Replaces MSA::DoRelaxation x numConsistencyReps (CPNP/MSA.cpp:1041-1051,
  * 1119-1129, 1172-1360).  With a communicator, each rank relaxes pairs
- * [p_begin, p_end) of its shard (mlp_set_shard) and the new store is
+ * [p_begin, p_end) of its shard (mlp_shard_range) and the new store is
  * all-gathered after every round. */
 int mlp_relax(mlp_ctx *ctx, int iters);
 

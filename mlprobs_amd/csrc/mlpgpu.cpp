@@ -264,7 +264,10 @@ int mlp_ctx_create(int device, mlp_ctx** out) {
   }
   size_t freeb = 0, total = 0;
   hipMemGetInfo(&freeb, &total);
-  c->scratch_budget = std::min<size_t>(freeb / 3, (size_t)48 << 30);
+  // half of the free HBM for per-batch scratch (the rest: CSR store, relaxation
+  // buffers): larger batches keep every SIMD busy through the serial
+  // local-total chains and shorten the per-batch tails
+  c->scratch_budget = freeb / 2;
   if (const char* s = getenv("MLP_SCRATCH_GB")) c->scratch_budget = (size_t)(atof(s) * (1ull << 30));
   *out = c;
   return MLP_OK;
@@ -396,20 +399,34 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
   const int models = model_set_for_pid(pid);
   SeqSet seqs{c->d_res, c->d_off, c->d_len};
 
+  const size_t per_slot = 6 * sizeof(int64_t) + 2 * sizeof(int32_t) + sizeof(PairRec) + 16;
+  auto pair_bytes = [&](int64_t q) {
+    const int L1 = c->lens[c->pa[q]], L2 = c->lens[c->pb[q]];
+    const int64_t cl = (int64_t)((L1 + 64) >> 6) * strip_steps(L2) * 64;
+    const int64_t rmc = (int64_t)L1 * ((L2 + 3) & ~3);
+    return (size_t)(cl * 20 + rmc * 8) + (size_t)(L2 + 2) * (5 * 4 + 3 * 4 + 3 * 8 + 4 + 4) +
+           (size_t)L1 * (kEll * 6 + 4) + per_slot;
+  };
+  // equal-sized batches (no small tail batch that leaves the GPU half idle)
+  size_t batch_target = c->scratch_budget;
+  {
+    size_t all = 0;
+    for (int64_t q = p0; q < p1; q++) all += pair_bytes(q);
+    const size_t nb = (all + c->scratch_budget - 1) / std::max<size_t>(c->scratch_budget, 1);
+    if (nb > 1) batch_target = std::min(c->scratch_budget, all / nb + all / (nb * 64) + 1);
+  }
   int64_t p = p0;
   while (p < p1) {
     // ---- batch: contiguous pairs within the scratch budget
     int64_t q = p, cells = 0, rm = 0, bnd = 0, rows = 0;
     size_t bytes = 0;
-    const size_t per_slot = 6 * sizeof(int64_t) + 2 * sizeof(int32_t) + sizeof(PairRec) + 16;
     while (q < p1) {
       const int L1 = c->lens[c->pa[q]], L2 = c->lens[c->pb[q]];
       const int64_t S = (L1 + 64) >> 6;
       const int64_t cl = S * strip_steps(L2) * 64;
       const int64_t rmc = (int64_t)L1 * ((L2 + 3) & ~3);
-      const size_t add = cl * 20 + rmc * 8 + (L2 + 2) * (5 * 4 + 3 * 4 + 3 * 8 + 4 + 4) +
-                         (size_t)L1 * (kEll * 6 + 4) + per_slot;
-      if (q > p && bytes + add > c->scratch_budget) break;
+      const size_t add = pair_bytes(q);
+      if (q > p && bytes + add > batch_target) break;
       bytes += add;
       cells += cl;
       rm += rmc;

@@ -827,6 +827,9 @@ __global__ __launch_bounds__(256) void k_local_totals_grp(SeqSet sq, PairMeta pm
 // Variant: one wave per pair, candidates folded serially (see above).
 __global__ __launch_bounds__(256) void k_local_totals_wave(SeqSet sq, PairMeta pm, PairRec* __restrict__ rec,
                                                            Scratch sc, int64_t npairs) {
+  __shared__ float4 lk[kLookupRows];
+  if (threadIdx.x == 0) mlp_lookup_table(lk);
+  __syncthreads();
   const int64_t p = wave_pair_index();
   if (p >= npairs) return;
   const int lane = threadIdx.x & 63;
@@ -834,7 +837,11 @@ __global__ __launch_bounds__(256) void k_local_totals_wave(SeqSet sq, PairMeta p
   const int64_t ne = (int64_t)L1 * ((L2 + 3) & ~3);
   const float* __restrict__ cf = sc.chf + pm.rm_off[p];
   const float* __restrict__ cbk = sc.chb + pm.rm_off[p];
-  float tf = LZ, tb = LZ;
+  // lane 0 carries the forward chain, lane 1 the backward chain: one LOG_ADD
+  // sequence advances both (LOG_ADD(acc, LOG_ZERO) == acc keeps an idle
+  // chain unchanged)
+  float acc = LZ;
+  float tf = LZ, tb = LZ;   // wave-uniform copies
   float xf = LZ, xb = LZ;
   if (lane < ne) { xf = cf[lane]; xb = cbk[lane]; }
   for (int64_t c0 = 0; c0 < ne; c0 += 64) {
@@ -845,21 +852,126 @@ __global__ __launch_bounds__(256) void k_local_totals_wave(SeqSet sq, PairMeta p
     uint64_t mf = __ballot(!(tf - cxf >= 7.5f));
     uint64_t mb = __ballot(!(tb - cxb >= 7.5f));
     while (mf | mb) {
-      if (mf) {
-        const int l = __builtin_ctzll(mf);
-        tf = mlp_log_add(tf, __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cxf), l)));
-        mf &= mf - 1;
-        mf &= __ballot(!(tf - cxf >= 7.5f));
-      }
-      if (mb) {
-        const int l = __builtin_ctzll(mb);
-        tb = mlp_log_add(tb, __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cxb), l)));
-        mb &= mb - 1;
-        mb &= __ballot(!(tb - cxb >= 7.5f));
-      }
+      const float vf = mf ? readlane_f(cxf, __builtin_ctzll(mf)) : LZ;
+      const float vb = mb ? readlane_f(cxb, __builtin_ctzll(mb)) : LZ;
+      acc = mlp_log_add_t(acc, lane == 0 ? vf : vb, lk);
+      tf = readlane_f(acc, 0);
+      tb = readlane_f(acc, 1);
+      if (mf) mf = (mf & (mf - 1)) & __ballot(!(tf - cxf >= 7.5f));
+      if (mb) mb = (mb & (mb - 1)) & __ballot(!(tb - cxb >= 7.5f));
     }
   }
   if (lane == 0) {
+    rec[p].tfl = tf;
+    rec[p].tbl = tb;
+  }
+}
+
+// Variant (default): 8 pairs per wave, 8 lanes per pair.  Chunks of 64
+// elements per chain (8 per lane, two float4 loads); candidates of each
+// chain (elements with acc - x < 7.5, acc = chain value at the chunk start)
+// are compacted in order into LDS, then lanes 0..15 fold the 16 chains of the
+// wave in parallel.  The candidate list is a superset of the elements that
+// change acc: LOG_ADD(acc, x) for acc - x >= 7.5 returns acc exactly, so
+// folding every listed element reproduces the reference's serial chain.
+constexpr int kTotPairs = 8;   // pairs per wave
+__global__ __launch_bounds__(256) void k_local_totals_multi(SeqSet sq, PairMeta pm, PairRec* __restrict__ rec,
+                                                            Scratch sc, int64_t npairs) {
+  __shared__ float4 lk[kLookupRows];
+  __shared__ float list[kWavesPerBlock][2 * kTotPairs][64];
+  if (threadIdx.x == 0) mlp_lookup_table(lk);
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int g = lane >> 3, sub = lane & 7;
+  const int64_t p = ((int64_t)blockIdx.x * kWavesPerBlock + w) * kTotPairs + g;
+  int64_t ne = 0, base = 0;
+  if (p < npairs) {
+    const int L1 = sq.len[pm.pa[p]], L2 = sq.len[pm.pb[p]];
+    ne = (int64_t)L1 * ((L2 + 3) & ~3);
+    base = pm.rm_off[p];
+  }
+  int64_t emax = ne;
+  for (int off = 32; off >= 8; off >>= 1) emax = max(emax, (int64_t)__shfl_xor(emax, off));
+  const float* __restrict__ cf = sc.chf + base;
+  const float* __restrict__ cb = sc.chb + base;
+  // chain c = 2g (forward) / 2g+1 (backward) is folded on lane c
+  float acc = LZ;
+  float nf[8], nb[8];
+  auto load = [&](int64_t e0, float* f, float* b) {
+    const int64_t e = e0 + sub * 8;   // ne is a multiple of 4: float4 pieces are all-in or all-out
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      float4 vf = make_float4(LZ, LZ, LZ, LZ), vb = vf;
+      if (e + 4 * h < ne) {
+        vf = *reinterpret_cast<const float4*>(cf + e + 4 * h);
+        vb = *reinterpret_cast<const float4*>(cb + e + 4 * h);
+      }
+      f[4 * h + 0] = vf.x; f[4 * h + 1] = vf.y; f[4 * h + 2] = vf.z; f[4 * h + 3] = vf.w;
+      b[4 * h + 0] = vb.x; b[4 * h + 1] = vb.y; b[4 * h + 2] = vb.z; b[4 * h + 3] = vb.w;
+    }
+  };
+  // two chunks in flight: HBM latency exceeds one chunk's fold
+  float nf2[8], nb2[8];
+  load(0, nf, nb);
+  load(64, nf2, nb2);
+  // exclusive prefix of a per-lane count over the 8 lanes of its group
+  auto group_scan = [&](int c) {
+    int x = c;
+#pragma unroll
+    for (int d = 1; d < 8; d <<= 1) {
+      const int y = __shfl_up(x, d, 8);
+      x += (sub >= d) ? y : 0;
+    }
+    return x - c;
+  };
+  auto chunk = [&](int64_t e0, float* xf, float* xb) {
+    const float af = __shfl(acc, 2 * g), ab = __shfl(acc, 2 * g + 1);
+    const int64_t e = e0 + sub * 8;
+    unsigned ff = 0, fb = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const bool in = e + k < ne;
+      ff |= (in && !(af - xf[k] >= 7.5f)) ? (1u << k) : 0u;
+      fb |= (in && !(ab - xb[k] >= 7.5f)) ? (1u << k) : 0u;
+    }
+    const int cf_n = __popc(ff), cb_n = __popc(fb);
+    int pf = group_scan(cf_n), pb = group_scan(cb_n);
+    float* lf = list[w][2 * g];
+    float* lb = list[w][2 * g + 1];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (ff & (1u << k)) lf[pf++] = xf[k];
+      if (fb & (1u << k)) lb[pb++] = xb[k];
+    }
+    // totals per chain: last lane of the group holds the inclusive sums
+    const int tot_f = __shfl(pf, g * 8 + 7), tot_b = __shfl(pb, g * 8 + 7);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // chain `lane` (< 16) folds its list; count from its group's last lane
+    const int cnt_f = __shfl(tot_f, (lane >> 1) * 8), cnt_b = __shfl(tot_b, (lane >> 1) * 8);
+    const int cnt = lane < 2 * kTotPairs ? ((lane & 1) ? cnt_b : cnt_f) : 0;
+    const float* my = list[w][lane & (2 * kTotPairs - 1)];
+    for (int k = 0; __any(k < cnt); ++k) {
+      if (k < cnt) acc = mlp_log_add_t(acc, my[k], lk);
+    }
+    __builtin_amdgcn_wave_barrier();
+  };
+  for (int64_t e0 = 0; e0 < emax; e0 += 128) {
+    float xf[8], xb[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { xf[k] = nf[k]; xb[k] = nb[k]; }
+    if (e0 + 128 < emax) load(e0 + 128, nf, nb);
+    chunk(e0, xf, xb);
+    if (e0 + 64 >= emax) break;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { xf[k] = nf2[k]; xb[k] = nb2[k]; }
+    if (e0 + 192 < emax) load(e0 + 192, nf2, nb2);
+    chunk(e0 + 64, xf, xb);
+  }
+  const float tf = __shfl(acc, 2 * g), tb = __shfl(acc, 2 * g + 1);
+  if (p < npairs && sub == 0) {
     rec[p].tfl = tf;
     rec[p].tbl = tb;
   }
@@ -1137,7 +1249,10 @@ hipError_t launch_local_totals(SeqSet seqs, PairMeta pm, PairRec* rec, Scratch s
   const char* v = getenv("MLP_TOTALS");
   if (v && v[0] == 'g')
     hipLaunchKernelGGL(k_local_totals_grp, dim3((unsigned)((npairs + 8 * kWavesPerBlock - 1) / (8 * kWavesPerBlock))), dim3(64 * kWavesPerBlock), 0, st, seqs, pm, rec, sc, npairs);
-  else if (!v || v[0] == 'w')
+  else if (!v || v[0] == 'm')
+    hipLaunchKernelGGL(k_local_totals_multi, dim3((unsigned)((npairs + kTotPairs * kWavesPerBlock - 1) / (kTotPairs * kWavesPerBlock))),
+                       dim3(64 * kWavesPerBlock), 0, st, seqs, pm, rec, sc, npairs);
+  else if (v[0] == 'w')
     hipLaunchKernelGGL(k_local_totals_wave, wave_grid(npairs), dim3(64 * kWavesPerBlock), 0, st, seqs, pm, rec, sc, npairs);
   else
     hipLaunchKernelGGL(k_local_totals_lane, dim3((unsigned)((npairs + 63) / 64)), dim3(64), 0, st, seqs, pm, rec, sc, npairs);

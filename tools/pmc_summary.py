@@ -3,6 +3,13 @@
 FETCH_SIZE is reported in KB and, on gfx950, counts half the bytes of wide
 coalesced streaming reads (MI355X_MICROARCH.md, HBM section): we report both
 the raw value and the x2-corrected one; WRITE_SIZE is taken as is.
+
+    python tools/pmc_summary.py DIR [per-kernel.json] [traffic.json]
+
+traffic.json (read by bench.py) holds, per bench kernel group (the HIP-event
+timed launch groups of bench.py), the measured HBM bytes and VALU wave
+instructions per pair-cell of the profiled run, so bench.py can scale them
+to its own launches.
 """
 import csv
 import json
@@ -64,6 +71,39 @@ def main(d):
     return out
 
 
+GROUPS = {'forward': ('k_forward',), 'backward': ('k_backward', 'k_fold_totals'),
+          'local_totals': ('k_local_totals',), 'merge_mea_sparsify': ('k_merge',), 'compact': ('k_compact',)}
+
+
+def groups(o, d):
+    """Per bench kernel group: bytes and VALU instructions per pair-cell."""
+    cells = None
+    for log in ('p1.log', 'p2.log', 'p3.log', 'stats.log'):
+        f = os.path.join(d, log)
+        if not os.path.exists(f):
+            continue
+        for line in open(f):
+            if line.startswith('{"metric"'):
+                b = json.loads(line)
+                cells = b['config']['pair_cells'] * (b['steps'] + b['warmup'])
+        if cells:
+            break
+    out = {'_source': os.path.basename(os.path.normpath(d)), '_pair_cells': cells,
+           '_note': 'read bytes = 2 x FETCH_SIZE (gfx950 correction), write bytes = WRITE_SIZE'}
+    for g, pre in GROUPS.items():
+        ks = [k for k in o if k.startswith(pre)]
+        if not ks or not cells:
+            continue
+        rd = sum(o[k].get('fetch_bytes_per_launch_x2', 0) * o[k].get('calls', 1) for k in ks)
+        wr = sum(o[k].get('write_bytes_per_launch', 0) * o[k].get('calls', 1) for k in ks)
+        vi = sum(o[k].get('SQ_INSTS_VALU', 0) for k in ks)
+        ns = sum(o[k]['total_ns'] for k in ks)
+        out[g] = {'kernels': ks, 'read_bytes_per_cell': rd / cells, 'write_bytes_per_cell': wr / cells,
+                  'traffic_bytes_per_cell': (rd + wr) / cells, 'valu_insts_per_cell': vi / cells,
+                  'profiled_ms': ns / 1e6}
+    return out
+
+
 if __name__ == '__main__':
     o = main(sys.argv[1])
     for k, e in sorted(o.items(), key=lambda kv: -kv[1]['total_ns']):
@@ -74,3 +114,6 @@ if __name__ == '__main__':
     if len(sys.argv) > 2:
         with open(sys.argv[2], 'w') as fh:
             json.dump(o, fh, indent=1)
+    if len(sys.argv) > 3:
+        with open(sys.argv[3], 'w') as fh:
+            json.dump(groups(o, sys.argv[1]), fh, indent=1)
