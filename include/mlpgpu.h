@@ -90,6 +90,14 @@ int mlp_comm_unique_id(unsigned char id[128]);
 int mlp_comm_init(mlp_ctx *ctx, const unsigned char id[128], int nranks, int rank);
 /* This rank's contiguous pair range (cost-balanced split). */
 int mlp_shard_range(mlp_ctx *ctx, int nranks, int rank, int64_t *p_begin, int64_t *p_end);
+/* Host-only planning (no device needed; what mlp_shard_range and
+ * mlp_allgather use).  mlp_shard_plan: contiguous pair range of `rank` for a
+ * family with lengths lens[n], balanced by DP cells (L_a + 1)(L_b + 1).
+ * mlp_gather_layout: info[3r..3r+2] = (p_begin, p_end, entries) of rank r;
+ * checks that the ranges tile [0, npairs) in rank order and writes the
+ * first global entry of every rank's block to ebase[nranks + 1]. */
+int mlp_shard_plan(int n, const int32_t *lens, int nranks, int rank, int64_t *p_begin, int64_t *p_end);
+int mlp_gather_layout(int nranks, int64_t npairs, const int64_t *info, int64_t *ebase);
 /* After every rank ran mlp_posteriors on its shard: all-gather the CSR
  * store and the per-pair scalars so every rank holds the whole family. */
 int mlp_allgather(mlp_ctx *ctx);

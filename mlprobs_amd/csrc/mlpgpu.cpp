@@ -636,25 +636,47 @@ int mlp_csr_import(mlp_ctx* c, const int32_t* row_ptr, const int64_t* ent_off, c
 }
 
 // ------------------------------------------------------------------ shards
-int mlp_shard_range(mlp_ctx* c, int nranks, int rank, int64_t* b, int64_t* e) {
-  if (!c || nranks < 1 || rank < 0 || rank >= nranks || !b || !e) return MLP_ERR_ARG;
-  // contiguous pair ranges balanced by DP cells
+int mlp_shard_plan(int n, const int32_t* lens, int nranks, int rank, int64_t* b, int64_t* e) {
+  if (n < 0 || (n > 0 && !lens) || nranks < 1 || rank < 0 || rank >= nranks || !b || !e) return MLP_ERR_ARG;
+  // contiguous ranges of the row-major pair order, balanced by DP cells
+  const int64_t P = (int64_t)n * (n - 1) / 2;
+  auto cost = [&](int a, int bb) { return (double)(lens[a] + 1) * (double)(lens[bb] + 1); };
   double total = 0;
-  for (int64_t p = 0; p < c->P; p++) total += pair_cost_cells(c, p);
+  for (int a = 0; a < n; a++)
+    for (int bb = a + 1; bb < n; bb++) total += cost(a, bb);
   auto cut = [&](int r) -> int64_t {
     if (r <= 0) return 0;
-    if (r >= nranks) return c->P;
+    if (r >= nranks) return P;
     const double target = total * r / nranks;
     double acc = 0;
-    for (int64_t p = 0; p < c->P; p++) {
-      if (acc >= target) return p;
-      acc += pair_cost_cells(c, p);
-    }
-    return c->P;
+    int64_t p = 0;
+    for (int a = 0; a < n; a++)
+      for (int bb = a + 1; bb < n; bb++, p++) {
+        if (acc >= target) return p;
+        acc += cost(a, bb);
+      }
+    return P;
   };
   *b = cut(rank);
   *e = cut(rank + 1);
   return MLP_OK;
+}
+
+int mlp_shard_range(mlp_ctx* c, int nranks, int rank, int64_t* b, int64_t* e) {
+  if (!c) return MLP_ERR_ARG;
+  return mlp_shard_plan(c->n, c->lens.data(), nranks, rank, b, e);
+}
+
+int mlp_gather_layout(int nranks, int64_t npairs, const int64_t* info, int64_t* ebase) {
+  if (nranks < 1 || !info || !ebase) return MLP_ERR_ARG;
+  ebase[0] = 0;
+  for (int r = 0; r < nranks; r++) {
+    if (info[3 * r] != (r == 0 ? 0 : info[3 * (r - 1) + 1]) || info[3 * r + 1] < info[3 * r] ||
+        info[3 * r + 2] < 0)
+      return MLP_ERR_STATE;
+    ebase[r + 1] = ebase[r] + info[3 * r + 2];
+  }
+  return info[3 * (nranks - 1) + 1] == npairs ? MLP_OK : MLP_ERR_STATE;
 }
 
 // ------------------------------------------------------------------ comm
@@ -696,16 +718,11 @@ int mlp_allgather(mlp_ctx* c) {
   HIPCHK(c, hipStreamSynchronize(c->stream));
   hipFree(d_info);
   // ranges must tile [0, P) in rank order
-  std::vector<int64_t> ebase(R + 1, 0);
-  for (int r = 0; r < R; r++) {
-    if (info[4 * r] != (r == 0 ? 0 : info[4 * (r - 1) + 1])) {
-      c->err = "shards must tile the pair range in rank order";
-      return MLP_ERR_STATE;
-    }
-    ebase[r + 1] = ebase[r] + info[4 * r + 2];
-  }
-  if (info[4 * (R - 1) + 1] != c->P) {
-    c->err = "shards do not cover all pairs";
+  std::vector<int64_t> ebase(R + 1, 0), tri(3 * R);
+  for (int r = 0; r < R; r++)
+    for (int k = 0; k < 3; k++) tri[3 * r + k] = info[4 * r + k];
+  if (mlp_gather_layout(R, c->P, tri.data(), ebase.data()) != MLP_OK) {
+    c->err = "shards must tile the pair range [0, P) in rank order";
     return MLP_ERR_STATE;
   }
   const int64_t total = ebase[R];

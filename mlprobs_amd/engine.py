@@ -68,6 +68,8 @@ def lib():
         L.mlp_comm_unique_id.argtypes = [C.c_char_p]
         L.mlp_comm_init.argtypes = [P, C.c_char_p, C.c_int, C.c_int]
         L.mlp_shard_range.argtypes = [P, C.c_int, C.c_int, C.POINTER(I64), C.POINTER(I64)]
+        L.mlp_shard_plan.argtypes = [C.c_int, I32P, C.c_int, C.c_int, C.POINTER(I64), C.POINTER(I64)]
+        L.mlp_gather_layout.argtypes = [C.c_int, I64, I64P, I64P]
         L.mlp_allgather.argtypes = [P]
         L.mlp_synchronize.argtypes = [P]
         L.mlp_profile.argtypes = [P, C.c_int]
@@ -80,8 +82,31 @@ def lib():
 EXPORTED = ['mlp_ctx_create', 'mlp_ctx_destroy', 'mlp_last_error', 'mlp_family_load',
             'mlp_family_npairs', 'mlp_posteriors', 'mlp_pair_results', 'mlp_csr_total',
             'mlp_csr_export', 'mlp_csr_import', 'mlp_relax', 'mlp_comm_unique_id', 'mlp_comm_init',
-            'mlp_shard_range', 'mlp_allgather', 'mlp_synchronize', 'mlp_profile',
+            'mlp_shard_range', 'mlp_shard_plan', 'mlp_gather_layout', 'mlp_allgather', 'mlp_synchronize', 'mlp_profile',
             'mlp_kernel_times', 'mlp_profile_reset']
+
+
+def shard_plan(lens, nranks, rank):
+    """Contiguous, cell-balanced pair range [p0, p1) of `rank` (host only:
+    the split mlp_shard_range applies on the GPU path)."""
+    lens = np.ascontiguousarray(lens, np.int32)
+    b, e = I64(), I64()
+    rc = lib().mlp_shard_plan(len(lens), lens, int(nranks), int(rank), C.byref(b), C.byref(e))
+    if rc != 0:
+        raise MlpError(rc, 'mlp_shard_plan')
+    return b.value, e.value
+
+
+def gather_layout(npairs, shards):
+    """shards: [(p0, p1, entries)] per rank.  Returns ebase[nranks + 1], the
+    global first entry of every rank's block (as mlp_allgather places them);
+    raises if the ranges do not tile [0, npairs) in rank order."""
+    info = np.ascontiguousarray(np.array(shards, np.int64).reshape(-1))
+    eb = np.zeros(len(shards) + 1, np.int64)
+    rc = lib().mlp_gather_layout(len(shards), int(npairs), info, eb)
+    if rc != 0:
+        raise MlpError(rc, 'shards must tile the pair range in rank order')
+    return eb
 
 
 def pair_index(n, a, b):

@@ -1,0 +1,142 @@
+"""Multi-rank path on CPU (gloo): the pair sharding and the all-gather layout
+of libmlpgpu (mlp_shard_plan / mlp_gather_layout, the host logic behind
+mlp_shard_range and mlp_allgather) with real process-group exchange.
+
+Each rank computes the posteriors of its own shard (here with the oracle, the
+checker, standing in for the GPU kernels), the ranks exchange (p0, p1,
+entries) and their CSR blocks over gloo, place them where the library's
+layout says, and every rank must end up with the single-process store
+(bit-identical results for any rank count).
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, 'oracle'))
+
+DELTA = 0.132548
+
+
+def _family():
+    from mlprobs_amd import synth
+    fam = [s for _, s in synth.family(7, 40, 0.6, seed=23)]
+    fam[2] = fam[2][:17]   # ragged lengths
+    fam[5] = fam[5] + fam[1][:9]
+    return fam
+
+
+def _pair_block(m, s1, s2, pid):
+    import orc
+    post = orc.pair_posterior(m, s1, s2, pid)
+    rp, cols, vals = orc.sparsify(len(s1), len(s2), post)
+    score = orc.mea(len(s1), len(s2), post)
+    dist_ = np.float32(1.0) - np.float32(score) / np.float32(min(len(s1), len(s2)))
+    return rp.astype(np.int32), cols.astype(np.uint16), vals.astype(np.float32), np.float32(dist_)
+
+
+def _store(fam, pid, p0, p1):
+    """Canonical CSR pieces of pairs [p0, p1): row_ptr blocks, entries, distances."""
+    import orc
+    from mlprobs_amd.engine import pairs_of
+    m = orc.model(DELTA)
+    rps, cols, vals, dists = [], [], [], []
+    for a, b in pairs_of(len(fam))[p0:p1]:
+        rp, c, v, d = _pair_block(m, fam[a], fam[b], pid)
+        rps.append(rp)
+        cols.append(c)
+        vals.append(v)
+        dists.append(d)
+    cat = lambda xs, dt: np.concatenate(xs) if xs else np.zeros(0, dt)
+    return cat(rps, np.int32), cat(cols, np.uint16), cat(vals, np.float32), np.array(dists, np.float32)
+
+
+def _worker(rank, world, port, pid, q):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from mlprobs_amd import engine
+        fam = _family()
+        lens = np.array([len(s) for s in fam], np.int32)
+        P = len(fam) * (len(fam) - 1) // 2
+        p0, p1 = engine.shard_plan(lens, world, rank)
+        rp, cols, vals, dists = _store(fam, pid, p0, p1)
+        shards = [None] * world
+        dist.all_gather_object(shards, (p0, p1, int(len(cols))))
+        ebase = engine.gather_layout(P, shards)
+        blocks = [None] * world
+        dist.all_gather_object(blocks, (rp, cols, vals, dists))
+        # place every rank's block where mlp_allgather puts it
+        total = int(ebase[-1])
+        g_cols = np.zeros(total, np.uint16)
+        g_vals = np.zeros(total, np.float32)
+        g_rp = np.concatenate([b[0] for b in blocks])
+        g_d = np.concatenate([b[3] for b in blocks])
+        for r, b in enumerate(blocks):
+            g_cols[ebase[r]:ebase[r + 1]] = b[1]
+            g_vals[ebase[r]:ebase[r + 1]] = b[2]
+        q.put((rank, shards, g_rp, g_cols, g_vals, g_d))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize('world,pid', [(2, 2), (3, 0)])
+def test_sharded_store_matches_single_process(world, pid):
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, pid, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    fam = _family()
+    P = len(fam) * (len(fam) - 1) // 2
+    rp, cols, vals, dists = _store(fam, pid, 0, P)
+    for rank, shards, g_rp, g_cols, g_vals, g_d in got:
+        # shards tile [0, P) and are balanced by cells
+        assert shards[0][0] == 0 and shards[-1][1] == P
+        assert all(shards[r][1] == shards[r + 1][0] for r in range(world - 1))
+        assert np.array_equal(g_rp, rp)
+        assert np.array_equal(g_cols, cols)
+        assert np.array_equal(g_vals, vals)
+        assert np.array_equal(g_d, dists)
+
+
+def test_shard_plan_balance():
+    from mlprobs_amd import engine
+    rng = np.random.default_rng(5)
+    lens = rng.integers(20, 600, size=61).astype(np.int32)
+    n = len(lens)
+    cost = np.array([(lens[a] + 1) * (lens[b] + 1) for a in range(n) for b in range(a + 1, n)], np.float64)
+    for R in (1, 2, 4, 8):
+        cuts = [engine.shard_plan(lens, R, r) for r in range(R)]
+        assert cuts[0][0] == 0 and cuts[-1][1] == len(cost)
+        for r in range(R - 1):
+            assert cuts[r][1] == cuts[r + 1][0]
+        loads = [cost[a:b].sum() for a, b in cuts]
+        assert max(loads) - cost.sum() / R <= cost.max() + 1e-6
+
+
+def test_gather_layout_rejects_gaps():
+    from mlprobs_amd import engine
+    assert list(engine.gather_layout(10, [(0, 3, 5), (3, 10, 2)])) == [0, 5, 7]
+    with pytest.raises(engine.MlpError):
+        engine.gather_layout(10, [(0, 3, 5), (4, 10, 2)])
+    with pytest.raises(engine.MlpError):
+        engine.gather_layout(10, [(0, 3, 5), (3, 9, 2)])
