@@ -15,7 +15,7 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, 'csrc')
 LIBDIR = os.path.join(HERE, 'lib')
 LIB = os.path.join(LIBDIR, 'libmlpgpu.so')
-SOURCES = ['posterior.hip', 'relax.hip', 'mlpgpu.cpp']
+SOURCES = ['posterior.hip', 'totals.hip', 'relax.hip', 'mlpgpu.cpp']
 HEADERS = ['mlp_kernels.h', 'mlp_numerics.h', 'mlp_params_default.inc']
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 FLAGS = ['--offload-arch=gfx950', '-O3', '-ffp-contract=off', '-fno-fast-math', '-fPIC',
@@ -30,19 +30,29 @@ def _stale():
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force=False, verbose=False):
-    if not force and not _stale():
+def variant_path(name):
+    return os.path.join(LIBDIR, f'libmlpgpu_{name}.so')
+
+
+def build(force=False, verbose=False, variant=None, defines=()):
+    """Build the library; `variant` builds an experiment copy
+    lib/libmlpgpu_<variant>.so with extra -D defines (loaded when
+    MLP_LIB_VARIANT=<variant>; never the default)."""
+    out = variant_path(variant) if variant else LIB
+    if not variant and not force and not _stale():
         return LIB
     os.makedirs(LIBDIR, exist_ok=True)
-    cmd = [HIPCC] + FLAGS + ['-shared', '-I', os.path.join(ROOT, 'include')]
-    cmd += [os.path.join(CSRC, f) for f in SOURCES] + ['-lrccl', '-o', LIB + '.tmp']
+    cmd = [HIPCC] + FLAGS + ['-D' + d for d in defines] + ['-shared', '-I', os.path.join(ROOT, 'include')]
+    cmd += [os.path.join(CSRC, f) for f in SOURCES] + ['-lrccl', '-o', out + '.tmp']
     if verbose:
         print(' '.join(cmd))
     subprocess.check_call(cmd)
-    os.replace(LIB + '.tmp', LIB)
-    return LIB
+    os.replace(out + '.tmp', out)
+    return out
 
 
 if __name__ == '__main__':
-    build(force='--force' in sys.argv, verbose=True)
-    print(LIB)
+    args = sys.argv[1:]
+    var = args[args.index('--variant') + 1] if '--variant' in args else None
+    defs = [a[2:] for a in args if a.startswith('-D')]
+    print(build(force='--force' in args, verbose=True, variant=var, defines=defs))

@@ -7,13 +7,37 @@
 namespace mlp {
 
 constexpr int kWave = 64;        // CDNA wavefront
-constexpr int kWavesPerBlock = 4;  // independent pairs per workgroup
+constexpr int kWavesPerBlock = 4;  // independent chains (waves) per workgroup
 constexpr int kEll = 64;         // sparse slots per posterior row before overflow
-constexpr int kSeqLds = 2048;    // column residues staged in LDS per wave (longer: LONG kernels)
 
-// Steps of one 64-row strip: columns 0..L2 plus the 63-step skew, padded to
-// a multiple of 8 so the step loops unroll without remainders.
-__host__ __device__ constexpr int strip_steps(int L2) { return (L2 + 64 + 7) & ~7; }
+// Chains.  One wave sweeps a chain of pairs whose rows are stacked: global
+// row g of the chain is row i = g - row0[q] of member q.  Lane r owns rows
+// g = r (mod 64) and walks them one after another, W steps per row (W >= every
+// member's L2 + 1; the extra columns are idle), so lane r works on column
+// j = (tau - r) mod W of row 64 * floor((tau - r) / W) + r at step tau: an
+// anti-diagonal wavefront that wraps from one 64-row strip into the next and
+// from one pair into the next without draining.
+constexpr int kChainMax = 32;    // pairs per chain
+constexpr int kChainSeqSoft = 8192;   // residue bytes per chain (LDS) when stacking pairs
+constexpr int kChainSeqMax = 50000;   // residue bytes of a single-pair chain (one wave per block)
+constexpr int kMinWidth = 192;   // W floor: boundary chunks are loaded 64 columns ahead
+// W for a chain whose widest member has L2 columns (+1): multiple of 8 so the
+// unrolled step loops never straddle a boundary-chunk switch
+__host__ __device__ constexpr int chain_width(int maxL2) {
+  return ((maxL2 + 1 < kMinWidth ? kMinWidth : maxL2 + 1) + 7) & ~7;
+}
+// LDS residue bytes of a chain of `n` members with sum of L1 = `sum_l1`:
+// a zero area of W + 2, then per member the padded row (L1 + 2) and column
+// (W + 1) sequences
+__host__ __device__ constexpr int chain_seq_bytes(int W, int sum_l1, int n) {
+  return W + 2 + sum_l1 + n * (W + 3);
+}
+// strips of a chain with `rows` stacked rows
+__host__ __device__ constexpr int chain_strips(int rows) { return (rows + 63) >> 6; }
+// step slots of a chain: steps tau = -1 .. S*W + 63, rounded up to 8
+__host__ __device__ constexpr int64_t chain_steps(int rows, int W) {
+  return ((int64_t)chain_strips(rows) * W + 65 + 7) & ~(int64_t)7;
+}
 
 // Model constants (CPNP/ProbabilisticModel.h:42-47 plus the PF factors of
 // CPNP/MSAPartProbs.cpp:698-709).  Letter-indexed tables (26 uppercase
@@ -32,14 +56,25 @@ struct Tables {
   double sub[26 * 26];    // PF score factor, [seq2 letter][seq1 letter]
 };
 
-// Per-pair bookkeeping of one batch (device arrays, length npairs).
+// Per-pair bookkeeping of one batch (device arrays indexed by slot; slots
+// are ordered chain by chain).
 struct PairMeta {
   const int32_t* pa;       // seq index of row sequence (seq1)
   const int32_t* pb;       // seq index of column sequence (seq2)
-  const int64_t* cell_off; // base of the pair's strip-diagonal region
-  const int64_t* rm_off;   // base of the pair's row-major chain region
-  const int64_t* bnd_off;  // base of the pair's boundary columns
+  const int32_t* row0;     // first stacked row of the pair in its chain
+  const int64_t* rm_off;   // base of the pair's row-major local-chain region
   const int64_t* ell_row;  // first ELL row of the pair (rows 1..L1)
+};
+
+// Per-chain bookkeeping (device arrays indexed by chain = wave).
+struct ChainMeta {
+  const int32_t* first;    // first slot
+  const int32_t* count;    // members (<= kChainMax)
+  const int32_t* width;    // W
+  const int32_t* rows;     // stacked rows (sum of L1 + 1)
+  const int32_t* seq_bytes;// residues of all members (LDS staging)
+  const int64_t* cell_off; // base of the chain's step-diagonal region (chain_steps * 64 slots)
+  const int64_t* bnd_off;  // base of the chain's boundary row (W entries)
 };
 
 struct PairRec {           // per-pair scalars produced along the pipeline
@@ -61,13 +96,13 @@ struct SeqSet {
 };
 
 struct Scratch {
-  float* f5;               // strip-diagonal: 5-state fwd M, then f+b (in place)
+  float* f5;               // step-diagonal: 5-state fwd M, then f+b (in place)
   float* fl;               // local fwd M, then f+b
   double* zm;              // PF forward Zm (packed with frame)
   float* pg;               // PF posterior
   float* chf;              // row-major local fwd M   (chain for total)
   float* chb;              // row-major local bwd M + emission
-  float* bnd5;             // boundary columns: 5 floats per column
+  float* bnd5;             // chain boundary row: 5 floats per column
   float* bndl;             // 3 floats per column
   double* bndz;            // 3 doubles per column
   int32_t* bnde;           // 1 int per column
@@ -85,17 +120,20 @@ inline int model_set_for_pid(int pid) {
   return kHmm5 | kLocal | kPF;
 }
 
-// launchers (posterior.hip)
+// launchers (posterior.hip).  lds_seq: max seq_bytes over the chains.
 hipError_t launch_forward(int models, const ModelScalars& ms, const Tables* tab, SeqSet seqs,
-                          PairMeta pm, PairRec* rec, Scratch sc, int64_t npairs, int max_len2,
-                          hipStream_t st);
+                          PairMeta pm, ChainMeta cm, PairRec* rec, Scratch sc, int64_t nchains,
+                          int lds_seq, hipStream_t st);
 hipError_t launch_backward(int models, const ModelScalars& ms, const Tables* tab, SeqSet seqs,
-                           PairMeta pm, PairRec* rec, Scratch sc, int64_t npairs, int max_len2,
-                           hipStream_t st);
+                           PairMeta pm, ChainMeta cm, PairRec* rec, Scratch sc, int64_t nchains,
+                           int lds_seq, int64_t npairs, hipStream_t st);
 hipError_t launch_local_totals(SeqSet seqs, PairMeta pm, PairRec* rec, Scratch sc, int64_t npairs,
                                hipStream_t st);
+hipError_t launch_fold_totals(const ModelScalars& ms, const Tables* tab, SeqSet seqs, PairMeta pm,
+                              PairRec* rec, int64_t npairs, hipStream_t st);
 hipError_t launch_merge(int models, int pid, const ModelScalars& ms, SeqSet seqs, PairMeta pm,
-                        PairRec* rec, Scratch sc, int64_t npairs, hipStream_t st);
+                        ChainMeta cm, PairRec* rec, Scratch sc, int64_t nchains, int lds_seq,
+                        hipStream_t st);
 hipError_t launch_compact(SeqSet seqs, PairMeta pm, PairRec* rec, Scratch sc,
                           const int64_t* ent_base, int32_t* out_rowptr, const int64_t* rowptr_base,
                           uint16_t* out_cols, float* out_vals, int64_t npairs, hipStream_t st);

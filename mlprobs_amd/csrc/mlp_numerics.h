@@ -158,6 +158,30 @@ __device__ __forceinline__ float mlp_shl1(float v, float old) {
 __device__ __forceinline__ int mlp_shl1i(int v, int old) {
   return __builtin_amdgcn_update_dpp(old, v, 0x130, 0xf, 0xf, false);
 }
+// Shifts whose vacated lane (0 for shr, 63 for shl) reads 0 (DPP bound_ctrl):
+// no old-value copy; for when that lane's result is overwritten or unused.
+__device__ __forceinline__ float mlp_shr1z(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x138, 0xf, 0xf, true));
+}
+__device__ __forceinline__ float mlp_shl1z(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x130, 0xf, 0xf, true));
+}
+__device__ __forceinline__ int mlp_shr1zi(int v) { return __builtin_amdgcn_mov_dpp(v, 0x138, 0xf, 0xf, true); }
+__device__ __forceinline__ int mlp_shl1zi(int v) { return __builtin_amdgcn_mov_dpp(v, 0x130, 0xf, 0xf, true); }
+__device__ __forceinline__ double mlp_shr1zd(double v) {
+  const int2 vv = *reinterpret_cast<const int2*>(&v);
+  int2 r;
+  r.x = __builtin_amdgcn_mov_dpp(vv.x, 0x138, 0xf, 0xf, true);
+  r.y = __builtin_amdgcn_mov_dpp(vv.y, 0x138, 0xf, 0xf, true);
+  return *reinterpret_cast<double*>(&r);
+}
+__device__ __forceinline__ double mlp_shl1zd(double v) {
+  const int2 vv = *reinterpret_cast<const int2*>(&v);
+  int2 r;
+  r.x = __builtin_amdgcn_mov_dpp(vv.x, 0x130, 0xf, 0xf, true);
+  r.y = __builtin_amdgcn_mov_dpp(vv.y, 0x130, 0xf, 0xf, true);
+  return *reinterpret_cast<double*>(&r);
+}
 __device__ __forceinline__ double mlp_shr1d(double v, double old) {
   const int2 vv = *reinterpret_cast<const int2*>(&v), oo = *reinterpret_cast<const int2*>(&old);
   int2 r;

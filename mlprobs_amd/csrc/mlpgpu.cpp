@@ -399,12 +399,15 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
   const int models = model_set_for_pid(pid);
   SeqSet seqs{c->d_res, c->d_off, c->d_len};
 
-  const size_t per_slot = 6 * sizeof(int64_t) + 2 * sizeof(int32_t) + sizeof(PairRec) + 16;
+  const size_t per_slot = 4 * sizeof(int64_t) + 3 * sizeof(int32_t) + sizeof(PairRec) + 7 * 8 + 16;
+  // upper bound of one pair's scratch (as if it were alone in a chain whose
+  // width may exceed its own by kWidthSlack)
   auto pair_bytes = [&](int64_t q) {
     const int L1 = c->lens[c->pa[q]], L2 = c->lens[c->pb[q]];
-    const int64_t cl = (int64_t)((L1 + 64) >> 6) * strip_steps(L2) * 64;
+    const int64_t Wb = chain_width(L2) + chain_width(L2) / 8 + 8;
+    const int64_t cl = (int64_t)(L1 + 1 + 64) * Wb + 80 * 64;
     const int64_t rmc = (int64_t)L1 * ((L2 + 3) & ~3);
-    return (size_t)(cl * 20 + rmc * 8) + (size_t)(L2 + 2) * (5 * 4 + 3 * 4 + 3 * 8 + 4 + 4) +
+    return (size_t)(cl * 20 + rmc * 8) + (size_t)Wb * (5 * 4 + 3 * 4 + 3 * 8 + 4 + 4) +
            (size_t)L1 * (kEll * 6 + 4) + per_slot;
   };
   // equal-sized batches (no small tail batch that leaves the GPU half idle)
@@ -418,55 +421,94 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
   int64_t p = p0;
   while (p < p1) {
     // ---- batch: contiguous pairs within the scratch budget
-    int64_t q = p, cells = 0, rm = 0, bnd = 0, rows = 0;
+    int64_t q = p;
     size_t bytes = 0;
     while (q < p1) {
-      const int L1 = c->lens[c->pa[q]], L2 = c->lens[c->pb[q]];
-      const int64_t S = (L1 + 64) >> 6;
-      const int64_t cl = S * strip_steps(L2) * 64;
-      const int64_t rmc = (int64_t)L1 * ((L2 + 3) & ~3);
       const size_t add = pair_bytes(q);
       if (q > p && bytes + add > batch_target) break;
+      if (chain_seq_bytes(chain_width(c->lens[c->pb[q]]), c->lens[c->pa[q]], 1) > kChainSeqMax) {
+        c->err = "pair " + std::to_string(q) + ": sequences too long for the LDS residue staging";
+        return MLP_ERR_ARG;
+      }
       bytes += add;
-      cells += cl;
-      rm += rmc;
-      bnd += L2 + 2;
-      rows += L1;
       ++q;
     }
     const int64_t np = q - p;
-    // slot order: most expensive pair first (LPT) inside the batch
-    std::vector<int64_t> order(np);
-    std::iota(order.begin(), order.end(), p);
-    std::stable_sort(order.begin(), order.end(), [&](int64_t x, int64_t y) {
-      return pair_cost_cells(c, x) > pair_cost_cells(c, y);
+    // ---- chains: pairs sorted by column count, stacked greedily
+    std::vector<int64_t> byw(np);
+    std::iota(byw.begin(), byw.end(), p);
+    std::stable_sort(byw.begin(), byw.end(), [&](int64_t x, int64_t y) {
+      const int ax = c->lens[c->pb[x]], ay = c->lens[c->pb[y]];
+      if (ax != ay) return ax > ay;
+      return c->lens[c->pa[x]] > c->lens[c->pa[y]];
     });
-    std::vector<int32_t> h_pa(np), h_pb(np);
-    std::vector<int64_t> h_cell(np), h_rm(np), h_bnd(np), h_ell(np), h_entb(np), h_rpb(np);
-    // offsets follow pair order (so storage is independent of slot order)
-    std::vector<int64_t> cell_of(np), rm_of(np), bnd_of(np), ell_of(np);
+    int64_t total_rows = 0;
+    for (int64_t k = p; k < q; k++) total_rows += c->lens[c->pa[k]] + 1;
+    // enough chains to fill the device a few times over, long enough that the
+    // 63-step skew and the last partial strip stay small
+    const int64_t target_rows = std::max<int64_t>(512, std::min<int64_t>(4096, total_rows / 8192));
+    struct ChainH { int64_t begin, end; int W, rows, seq; int64_t cost; };
+    std::vector<ChainH> chains;
     {
-      int64_t co = 0, ro = 0, bo = 0, eo = 0;
+      ChainH cur{0, 0, 0, 0, 0, 0};
       for (int64_t k = 0; k < np; k++) {
-        const int L1 = c->lens[c->pa[p + k]], L2 = c->lens[c->pb[p + k]];
-        cell_of[k] = co;
-        rm_of[k] = ro;
-        bnd_of[k] = bo;
-        ell_of[k] = eo;
-        co += (int64_t)((L1 + 64) >> 6) * strip_steps(L2) * 64;
-        ro += (int64_t)L1 * ((L2 + 3) & ~3);
-        bo += L2 + 2;
-        eo += L1;
+        const int64_t x = byw[k];
+        const int L1 = c->lens[c->pa[x]], L2 = c->lens[c->pb[x]];
+        const int w = chain_width(L2);
+        const int n_in = (int)(cur.end - cur.begin);
+        const bool fits = n_in > 0 && n_in < kChainMax && cur.rows + L1 + 1 <= target_rows &&
+                          chain_seq_bytes(cur.W, cur.rows - n_in + L1, n_in + 1) <= kChainSeqSoft &&
+                          cur.W - w <= std::max(8, cur.W / 16);
+        if (!fits) {
+          if (cur.end > cur.begin) chains.push_back(cur);
+          cur = ChainH{k, k, w, 0, 0, 0};
+        }
+        cur.end = k + 1;
+        cur.rows += L1 + 1;
+        cur.seq = chain_seq_bytes(cur.W, cur.rows - (int)(cur.end - cur.begin), (int)(cur.end - cur.begin));
       }
+      if (cur.end > cur.begin) chains.push_back(cur);
+      for (auto& h : chains) h.cost = (int64_t)chain_strips(h.rows) * h.W;
+      std::stable_sort(chains.begin(), chains.end(), [](const ChainH& x, const ChainH& y) { return x.cost > y.cost; });
     }
-    for (int64_t s = 0; s < np; s++) {
-      const int64_t pp = order[s], k = pp - p;
-      h_pa[s] = c->pa[pp];
-      h_pb[s] = c->pb[pp];
-      h_cell[s] = cell_of[k];
-      h_rm[s] = rm_of[k];
-      h_bnd[s] = bnd_of[k];
-      h_ell[s] = ell_of[k];
+    const int64_t nch = (int64_t)chains.size();
+    // slots: chain members in chain order
+    std::vector<int64_t> order(np);
+    std::vector<int32_t> h_pa(np), h_pb(np), h_row0(np);
+    std::vector<int64_t> h_rm(np), h_ell(np), h_entb(np), h_rpb(np);
+    std::vector<int32_t> h_first(nch), h_count(nch), h_width(nch), h_rows(nch), h_seqb(nch);
+    std::vector<int64_t> h_cell(nch), h_bndo(nch);
+    int64_t cells = 0, rm = 0, bnd = 0, rows = 0;
+    int lds_seq = 0;
+    {
+      int64_t s = 0;
+      for (int64_t h = 0; h < nch; h++) {
+        const ChainH& ch = chains[h];
+        h_first[h] = (int32_t)s;
+        h_count[h] = (int32_t)(ch.end - ch.begin);
+        h_width[h] = ch.W;
+        h_rows[h] = ch.rows;
+        h_seqb[h] = ch.seq;
+        h_cell[h] = cells;
+        h_bndo[h] = bnd;
+        cells += chain_steps(ch.rows, ch.W) * 64;
+        bnd += ch.W;
+        lds_seq = std::max(lds_seq, ch.seq);
+        int row0 = 0;
+        for (int64_t k = ch.begin; k < ch.end; k++, s++) {
+          const int64_t x = byw[k];
+          const int L1 = c->lens[c->pa[x]], L2 = c->lens[c->pb[x]];
+          order[s] = x;
+          h_pa[s] = c->pa[x];
+          h_pb[s] = c->pb[x];
+          h_row0[s] = row0;
+          h_rm[s] = rm;
+          h_ell[s] = rows;
+          row0 += L1 + 1;
+          rm += (int64_t)L1 * ((L2 + 3) & ~3);
+          rows += L1;
+        }
+      }
     }
     // ---- carve scratch
     size_t off = 0;
@@ -480,9 +522,11 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
                  o_b5 = carve(bnd * 20), o_bl = carve(bnd * 12), o_bz = carve(bnd * 24),
                  o_be = carve(bnd * 4), o_bm = carve(bnd * 4), o_ec = carve(rows * kEll * 2),
                  o_ev = carve(rows * kEll * 4), o_en = carve(rows * 4), o_pa = carve(np * 4),
-                 o_pb = carve(np * 4), o_cell = carve(np * 8), o_rm = carve(np * 8),
-                 o_bnd = carve(np * 8), o_ell = carve(np * 8), o_entb = carve(np * 8),
-                 o_rpb = carve(np * 8), o_rec = carve(np * sizeof(PairRec));
+                 o_pb = carve(np * 4), o_r0 = carve(np * 4), o_rm = carve(np * 8),
+                 o_ell = carve(np * 8), o_entb = carve(np * 8), o_rpb = carve(np * 8),
+                 o_rec = carve(np * sizeof(PairRec)), o_cf = carve(nch * 4), o_cc = carve(nch * 4),
+                 o_cw = carve(nch * 4), o_cr = carve(nch * 4), o_cs = carve(nch * 4),
+                 o_cco = carve(nch * 8), o_cbo = carve(nch * 8);
     int rc;
     if ((rc = ensure(c, c->scratch, off))) return rc;
     char* base = (char*)c->scratch.p;
@@ -505,30 +549,42 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
     PairMeta pm;
     pm.pa = (const int32_t*)(base + o_pa);
     pm.pb = (const int32_t*)(base + o_pb);
-    pm.cell_off = (const int64_t*)(base + o_cell);
+    pm.row0 = (const int32_t*)(base + o_r0);
     pm.rm_off = (const int64_t*)(base + o_rm);
-    pm.bnd_off = (const int64_t*)(base + o_bnd);
     pm.ell_row = (const int64_t*)(base + o_ell);
-    HIPCHK(c, hipMemcpyAsync(base + o_pa, h_pa.data(), np * 4, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(c, hipMemcpyAsync(base + o_pb, h_pb.data(), np * 4, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(c, hipMemcpyAsync(base + o_cell, h_cell.data(), np * 8, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(c, hipMemcpyAsync(base + o_rm, h_rm.data(), np * 8, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(c, hipMemcpyAsync(base + o_bnd, h_bnd.data(), np * 8, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(c, hipMemcpyAsync(base + o_ell, h_ell.data(), np * 8, hipMemcpyHostToDevice, c->stream));
+    ChainMeta cm;
+    cm.first = (const int32_t*)(base + o_cf);
+    cm.count = (const int32_t*)(base + o_cc);
+    cm.width = (const int32_t*)(base + o_cw);
+    cm.rows = (const int32_t*)(base + o_cr);
+    cm.seq_bytes = (const int32_t*)(base + o_cs);
+    cm.cell_off = (const int64_t*)(base + o_cco);
+    cm.bnd_off = (const int64_t*)(base + o_cbo);
+    auto up = [&](size_t o, const void* h, size_t n) {
+      return hipMemcpyAsync(base + o, h, n, hipMemcpyHostToDevice, c->stream);
+    };
+    HIPCHK(c, up(o_pa, h_pa.data(), np * 4));
+    HIPCHK(c, up(o_pb, h_pb.data(), np * 4));
+    HIPCHK(c, up(o_r0, h_row0.data(), np * 4));
+    HIPCHK(c, up(o_rm, h_rm.data(), np * 8));
+    HIPCHK(c, up(o_ell, h_ell.data(), np * 8));
+    HIPCHK(c, up(o_cf, h_first.data(), nch * 4));
+    HIPCHK(c, up(o_cc, h_count.data(), nch * 4));
+    HIPCHK(c, up(o_cw, h_width.data(), nch * 4));
+    HIPCHK(c, up(o_cr, h_rows.data(), nch * 4));
+    HIPCHK(c, up(o_cs, h_seqb.data(), nch * 4));
+    HIPCHK(c, up(o_cco, h_cell.data(), nch * 8));
+    HIPCHK(c, up(o_cbo, h_bndo.data(), nch * 8));
     HIPCHK(c, hipMemsetAsync(d_rec, 0, np * sizeof(PairRec), c->stream));
     int64_t bcells = 0;
-    int maxL2 = 0;
-    for (int64_t k = p; k < q; k++) {
-      bcells += pair_cost_cells(c, k);
-      maxL2 = std::max(maxL2, c->lens[c->pb[k]]);
-    }
+    for (int64_t k = p; k < q; k++) bcells += pair_cost_cells(c, k);
     {
       Timer t(c, KFWD, bcells);
-      HIPCHK(c, launch_forward(models, ms, c->d_tables, seqs, pm, d_rec, sc, np, maxL2, c->stream));
+      HIPCHK(c, launch_forward(models, ms, c->d_tables, seqs, pm, cm, d_rec, sc, nch, lds_seq, c->stream));
     }
     {
       Timer t(c, KBWD, bcells);
-      HIPCHK(c, launch_backward(models, ms, c->d_tables, seqs, pm, d_rec, sc, np, maxL2, c->stream));
+      HIPCHK(c, launch_backward(models, ms, c->d_tables, seqs, pm, cm, d_rec, sc, nch, lds_seq, np, c->stream));
     }
     if (models & kLocal) {
       Timer t(c, KTOT, bcells);
@@ -536,7 +592,7 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
     }
     {
       Timer t(c, KMERGE, bcells);
-      HIPCHK(c, launch_merge(models, pid, ms, seqs, pm, d_rec, sc, np, c->stream));
+      HIPCHK(c, launch_merge(models, pid, ms, seqs, pm, cm, d_rec, sc, nch, lds_seq, c->stream));
     }
     std::vector<PairRec> rec(np);
     HIPCHK(c, hipMemcpyAsync(rec.data(), d_rec, np * sizeof(PairRec), hipMemcpyDeviceToHost, c->stream));

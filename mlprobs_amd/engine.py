@@ -46,7 +46,8 @@ def lib():
     """Load libmlpgpu.so (in-tree).  Raises if it is missing."""
     global _LIB
     if _LIB is None:
-        path = _build.LIB
+        var = os.environ.get('MLP_LIB_VARIANT')
+        path = _build.variant_path(var) if var else _build.LIB
         if not os.path.exists(path):
             raise RuntimeError(f'{path} missing: run `python -m mlprobs_amd.build` (hipcc, gfx950)')
         L = C.CDLL(path)
