@@ -111,3 +111,55 @@ def test_vs_oracle(s, L, n, pid, seed):
     for k in range(len(ref1)):
         csr_equal(ref1[k], fam.sparse(k), f'relax p{k}')
     fam.close()
+
+
+def _ragged_family(n, lo, hi, seed):
+    rng = np.random.default_rng(seed)
+    base = [x for _, x in synth.family(n, hi, 0.5, seed=seed)]
+    return [x[: int(rng.integers(lo, hi + 1))] or 'A' for x in base]
+
+
+def _check_family_vs_oracle(seqs, pid, tag):
+    delta = 0.132548
+    m = orc.model(delta)
+    fam = Family(seqs)
+    fam.posteriors(pid, delta)
+    D = fam.distances()
+    k = 0
+    for a in range(len(seqs)):
+        for b in range(a + 1, len(seqs)):
+            post = orc.pair_posterior(m, seqs[a], seqs[b], pid)
+            ref = orc.sparsify(len(seqs[a]), len(seqs[b]), post)
+            _check_pair_csr(ref, fam.sparse(k), pid, f'{tag} p{k}')
+            sc = orc.mea(len(seqs[a]), len(seqs[b]), post)
+            dist = np.float32(1) - np.float32(sc) / np.float32(min(len(seqs[a]), len(seqs[b])))
+            if pid in EXACT_PIDS:
+                assert D[a, b] == dist, (tag, k)
+            else:
+                assert close_scalar(dist, D[a, b]), (tag, k)
+            k += 1
+    fam.close()
+
+
+@pytest.mark.parametrize('pid', [2, 0])
+def test_chains_many_short(pid):
+    """Many short ragged pairs: chains of up to kChainMax members whose rows
+    cross 64-row strips and member boundaries inside one strip."""
+    _check_family_vs_oracle(_ragged_family(16, 2, 90, 41), pid, 'short')
+
+
+def test_chains_long():
+    """Long rows: W spans many 64-column boundary chunks."""
+    _check_family_vs_oracle([x for _, x in synth.family(3, 900, 0.6, seed=42)], 2, 'long')
+
+
+def test_chains_mixed_widths():
+    """Column counts far apart: pairs go to different chains (width slack)."""
+    seqs = _ragged_family(9, 150, 420, 43)
+    _check_family_vs_oracle(seqs, 2, 'mixed')
+
+
+def test_batches_of_one(monkeypatch):
+    """A scratch budget below one pair: every batch holds a single pair."""
+    monkeypatch.setenv('MLP_SCRATCH_GB', '0.0001')
+    _check_family_vs_oracle([x for _, x in synth.family(5, 70, 0.6, seed=44)], 2, 'batch1')
