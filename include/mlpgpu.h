@@ -68,6 +68,24 @@ int mlp_posteriors(mlp_ctx *ctx, int pid, float delta, int64_t p_begin, int64_t 
 int mlp_pair_results(mlp_ctx *ctx, int64_t p_begin, int64_t p_end, float *dist, float *mea,
                      int64_t *nnz);
 
+/* Family test (replaces ModelAdjustmentTest / Alter_ModelAdjustmentTest,
+ * CPNP/MSA.cpp:646-882): the Viterbi alignment of every pair
+ * (CPNP/ProbabilisticModel.h:1043-1170).  mlp_viterbi runs pairs
+ * [p_begin, p_end); keep_paths keeps every path on the host (needed by
+ * mlp_family_features). */
+int mlp_viterbi(mlp_ctx *ctx, int64_t p_begin, int64_t p_end, int keep_paths);
+/* Per pair: identical residues in match columns and path length. */
+int mlp_viterbi_results(mlp_ctx *ctx, int64_t p_begin, int64_t p_end, float *match, int32_t *len);
+/* Path of pair p, forward order: 0 = 'B' (both), 1 = 'X', 2 = 'Y'. */
+int mlp_viterbi_path(mlp_ctx *ctx, int64_t p, uint8_t *codes, int32_t *len);
+/* ModelAdjustmentTest: average identity, its standard deviation, the
+ * initDistrib[2] it selects and the returned code (variance_mean + class),
+ * the per-pair identities summed in pair order. */
+int mlp_model_adjustment(mlp_ctx *ctx, float *identity, float *variance, float *delta, int32_t *code);
+/* Alter_ModelAdjustmentTest (the `-G` line): f = {identity, variance,
+ * tmp_sp, peak_ratio, factor}, ints = {N, avg_len}, serial in pair order. */
+int mlp_family_features(mlp_ctx *ctx, float theta, float *f, int32_t *ints);
+
 /* Total entries of the canonical CSR store (all pairs currently held). */
 int mlp_csr_total(mlp_ctx *ctx, int64_t *total);
 /* Host copy of the full canonical CSR store (see layout above):
@@ -108,8 +126,8 @@ int mlp_synchronize(mlp_ctx *ctx);
 /* Per-kernel device time accumulated since the last reset (HIP events on
  * the context stream), enabled by mlp_profile(ctx, 1).  Kernel ids:
  * 0 forward, 1 backward, 2 local totals, 3 merge/MEA/sparsify, 4 compact,
- * 5 relax, 6 transpose, 7 filter, 8 allgather. */
-#define MLP_NKERNELS 9
+ * 5 relax, 6 transpose, 7 filter, 8 allgather, 9 viterbi. */
+#define MLP_NKERNELS 10
 int mlp_profile(mlp_ctx *ctx, int enable);
 int mlp_kernel_times(mlp_ctx *ctx, double *ms, int64_t *launches, int64_t *cells);
 int mlp_profile_reset(mlp_ctx *ctx);

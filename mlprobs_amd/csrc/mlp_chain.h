@@ -1,0 +1,317 @@
+// mlp_chain.h -- device-side machinery shared by the chained-wavefront
+// sweeps (posterior.hip, viterbi.hip): LDS tables, chain staging, the per-lane
+// cursor over stacked rows and the double-buffered strip boundary.  See
+// mlp_kernels.h ("Chains") for the schedule.
+#pragma once
+#include "mlp_kernels.h"
+#include "mlp_numerics.h"
+
+namespace mlp {
+
+#define LZ MLP_LOG_ZERO
+
+// LDS-resident tables of one workgroup: letter-indexed emissions, the PF
+// score factors and the LOOKUP coefficient rows (one ds_read_b128 per
+// LOG_ADD instead of compare/select chains).
+struct LdsTables {
+  float4 lk[kLookupRows];
+  float match[26 * 26];
+  float ins[26];
+  double sub[26 * 26];
+};
+
+__device__ __forceinline__ void stage_tables(LdsTables& L, const Tables* __restrict__ tab) {
+  for (int k = threadIdx.x; k < 26 * 26; k += blockDim.x) {
+    L.match[k] = tab->match[k];
+    L.sub[k] = tab->sub[k];
+  }
+  if (threadIdx.x < 26) L.ins[threadIdx.x] = tab->ins[threadIdx.x];
+  if (threadIdx.x == 0) mlp_lookup_table(L.lk);
+  __syncthreads();
+}
+
+__device__ __forceinline__ int64_t wave_index() {
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  return (int64_t)blockIdx.x * (blockDim.x >> 6) + w;
+}
+
+__device__ __forceinline__ float readlane_f(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  const int2 w = *reinterpret_cast<const int2*>(&v);
+  int2 r;
+  r.x = __builtin_amdgcn_readlane(w.x, l);
+  r.y = __builtin_amdgcn_readlane(w.y, l);
+  return *reinterpret_cast<double*>(&r);
+}
+
+__device__ __forceinline__ void wave_sync_lds() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// ---------------------------------------------------------------- chains
+// LDS copy of one chain member's bookkeeping (64 bytes).
+struct ChainPair {
+  int L1, L2, row0, roff, coff, slot;
+  float T5, TL;      // merge: pair totals
+  int64_t rm, ell;   // local-chain base, first ELL row
+  double zmant;      // backward: PF total
+  int zexp, pad;
+};
+constexpr int kChainLdsMeta = (int)sizeof(ChainPair) * (kChainMax + 1);
+__host__ __device__ constexpr int chain_lds_stride(int lds_seq) {
+  return kChainLdsMeta + ((lds_seq + 15) & ~15);
+}
+
+struct ChainView {
+  const ChainPair* P;   // K + 1 entries, P[K].row0 = rows
+  const uint8_t* seq;   // residues of all members
+  int K, W, rows, S;
+};
+
+enum StageKind { kStageFwd = 0, kStageBwd = 1, kStageMerge = 2 };
+
+// Stage the chain's members (bookkeeping + both residue strings) into this
+// wave's LDS region.
+template <int KIND>
+__device__ ChainView stage_chain(uint8_t* dyn, int lds_seq, int64_t ch, SeqSet sq, PairMeta pm,
+                                 ChainMeta cm, const PairRec* __restrict__ rec) {
+  const int lane = threadIdx.x & 63;
+  uint8_t* region = dyn + (threadIdx.x >> 6) * chain_lds_stride(lds_seq);
+  ChainPair* P = reinterpret_cast<ChainPair*>(region);
+  uint8_t* seq = region + kChainLdsMeta;
+  const int K = cm.count[ch], first = cm.first[ch];
+  int L1 = 0, L2 = 0, a = 0, b = 0;
+  if (lane < K) {
+    a = pm.pa[first + lane];
+    b = pm.pb[first + lane];
+    L1 = sq.len[a];
+    L2 = sq.len[b];
+  }
+  const int W = cm.width[ch];
+  // residue layout: [W + 2 zeros: idle lanes] then per member
+  //   row seq padded  0, s1[0..L1-1], 0          (L1 + 2 bytes; c1 = [i], c1n = [i+1])
+  //   col seq padded  0, s2[0..L2-1], 0 .. 0     (W + 1 bytes; c2 = [j], c2n = [j+1])
+  int x = lane < K ? L1 + W + 3 : 0;
+  for (int d = 1; d < 64; d <<= 1) {
+    const int y = __shfl_up(x, d);
+    if (lane >= d) x += y;
+  }
+  const int roff = W + 2 + x - (lane < K ? L1 + W + 3 : 0);
+  if (lane < K) {
+    const int slot = first + lane;
+    ChainPair c;
+    c.L1 = L1; c.L2 = L2; c.row0 = pm.row0[slot]; c.roff = roff; c.coff = roff + L1 + 2; c.slot = slot;
+    c.T5 = 0.f; c.TL = 0.f; c.rm = pm.rm_off[slot]; c.ell = pm.ell_row[slot];
+    c.zmant = 1.0; c.zexp = 0; c.pad = 0;
+    if constexpr (KIND == kStageBwd) {
+      c.zmant = rec[slot].zmant;
+      c.zexp = rec[slot].zexp;
+    }
+    if constexpr (KIND == kStageMerge) {
+      // CPNP/ProbabilisticModel.h:405-454: T = (T_fwd + T_bwd) / 2; the
+      // 5-state backward total was folded into b5[0] by k_fold_totals
+      const PairRec& r = rec[slot];
+      c.T5 = (r.tf5 + r.b5[0]) / 2;
+      c.TL = (r.tfl + r.tbl) / 2;
+    }
+    P[lane] = c;
+  }
+  if (lane == 0) P[K].row0 = cm.rows[ch];
+  const int total = __shfl(x, 63) + W + 2;
+  for (int k = lane * 4; k < total; k += 256) *reinterpret_cast<uint32_t*>(seq + k) = 0u;
+  wave_sync_lds();
+  for (int q = 0; q < K; ++q) {
+    const int aq = __shfl(a, q), bq = __shfl(b, q);
+    const int l1 = __shfl(L1, q), l2 = __shfl(L2, q), ro = __shfl(roff, q);
+    const uint8_t* s1 = sq.res + sq.off[aq];
+    const uint8_t* s2 = sq.res + sq.off[bq];
+    for (int k = lane; k < l1; k += 64) seq[ro + 1 + k] = s1[k];
+    for (int k = lane; k < l2; k += 64) seq[ro + l1 + 2 + 1 + k] = s2[k];
+  }
+  wave_sync_lds();
+  ChainView v;
+  v.P = P;
+  v.seq = seq;
+  v.K = K;
+  v.W = W;
+  v.rows = cm.rows[ch];
+  v.S = chain_strips(v.rows);
+  return v;
+}
+
+// Where one lane is in the chain: stacked row g (idle outside [0, rows)),
+// column j, member q and its row i, plus the member's values the sweeps need.
+struct Cursor {
+  int g, j, q, i, L1, L2;
+  int ca;          // LDS offset of column residue j (padded column seq + j)
+  int c1, c1n;     // residues i and i + 1 of the row sequence (0 outside)
+  float ins1, ins1n;
+  int slot;
+  int64_t rm, ell;
+  float T5, TL;
+  double zmant;
+  int zexp;
+};
+
+__device__ __forceinline__ void locate(Cursor& c, const ChainView& C, const float* __restrict__ ins) {
+  if (c.g < 0 || c.g >= C.rows) {
+    c.q = -1; c.i = -1; c.L1 = -1; c.L2 = -1; c.c1 = 0; c.c1n = 0;
+    c.ca = c.j;   // the zero area
+    c.ins1 = ins[0]; c.ins1n = ins[0];
+    return;
+  }
+  int q = c.q < 0 ? 0 : c.q;
+  while (C.P[q + 1].row0 <= c.g) ++q;
+  while (C.P[q].row0 > c.g) --q;
+  const ChainPair& m = C.P[q];
+  c.q = q;
+  c.i = c.g - m.row0;
+  c.L1 = m.L1;
+  c.L2 = m.L2;
+  c.ca = m.coff + c.j;
+  c.slot = m.slot;
+  c.rm = m.rm;
+  c.ell = m.ell;
+  c.T5 = m.T5;
+  c.TL = m.TL;
+  c.zmant = m.zmant;
+  c.zexp = m.zexp;
+  c.c1 = C.seq[m.roff + c.i];
+  c.c1n = C.seq[m.roff + c.i + 1];
+  c.ins1 = ins[c.c1];
+  c.ins1n = ins[c.c1n];
+}
+
+// forward-order cursor at step 0: lane r at u = -r
+__device__ __forceinline__ void cursor_start_fwd(Cursor& c, const ChainView& C, const float* ins, int lane) {
+  c.q = -1;
+  c.g = lane == 0 ? 0 : lane - 64;
+  c.j = lane == 0 ? 0 : C.W - lane;
+  locate(c, C, ins);
+}
+__device__ __forceinline__ void cursor_next(Cursor& c, const ChainView& C, const float* ins) {
+  ++c.ca;
+  if (++c.j == C.W) {
+    c.j = 0;
+    c.g += 64;
+    locate(c, C, ins);
+  }
+}
+// reverse-order cursor at step tau (u = tau - lane >= 0)
+__device__ __forceinline__ void cursor_start_bwd(Cursor& c, const ChainView& C, const float* ins, int lane, int tau) {
+  const int u = tau - lane;
+  c.q = -1;
+  c.g = 64 * (u / C.W) + lane;
+  c.j = u % C.W;
+  locate(c, C, ins);
+}
+__device__ __forceinline__ void cursor_prev(Cursor& c, const ChainView& C, const float* ins) {
+  --c.ca;
+  if (--c.j < 0) {
+    c.j = C.W - 1;
+    c.g -= 64;
+    locate(c, C, ins);
+  }
+}
+
+// Boundary row of the neighbouring strip, read 64 columns at a time (one per
+// lane) and double-buffered: the sweeps switch buffers between 64-step
+// segments, so the chunk in use is loop-invariant in the step loop and was
+// loaded a whole segment earlier -- reading it never waits on the loads and
+// stores issued since (vmcnt is in order on gfx9).  Column indices are
+// clamped to the chain's W columns; columns a lane must not use are never
+// consumed by an active cell.
+template <int M>
+struct BoundaryChunks {
+  float c5[5], n5[5], cl[3], nl[3];
+  double cz[3], nz[3];
+  int ce, ne;
+  __device__ __forceinline__ void load_next(const Scratch& sc, int64_t bo, int W, int col0, int lane) {
+    const int64_t bi = bo + min(max(col0 + lane, 0), W - 1);
+    if constexpr ((M & kHmm5) != 0) {
+#pragma unroll
+      for (int k = 0; k < 5; ++k) n5[k] = sc.bnd5[bi * 5 + k];
+    }
+    if constexpr ((M & kLocal) != 0) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) nl[k] = sc.bndl[bi * 3 + k];
+    }
+    if constexpr ((M & kPF) != 0) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) nz[k] = sc.bndz[bi * 3 + k];
+      ne = sc.bnde[bi];
+    }
+  }
+  __device__ __forceinline__ void advance() {
+#pragma unroll
+    for (int k = 0; k < 5; ++k) c5[k] = n5[k];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) { cl[k] = nl[k]; cz[k] = nz[k]; }
+    ce = ne;
+  }
+  // Neighbour shift of one step: X = src shifted by one lane toward higher
+  // lanes (SHR, forward) or lower lanes (backward); the vacated lane (0 / 63)
+  // takes column q of the current chunk when TAKE, else 0 (unused there).
+  template <bool SHR, bool TAKE>
+  __device__ __forceinline__ void shift(int q, const float* S5, float* X5, const float* SL, float* XL,
+                                        double sZm, double sZe, double sZf, int se,
+                                        double& Zm, double& Ze, double& Zf, int& e) const {
+    if constexpr ((M & kHmm5) != 0) {
+#pragma unroll
+      for (int k = 0; k < 5; ++k)
+        X5[k] = TAKE ? (SHR ? mlp_shr1(S5[k], readlane_f(c5[k], q)) : mlp_shl1(S5[k], readlane_f(c5[k], q)))
+                     : (SHR ? mlp_shr1z(S5[k]) : mlp_shl1z(S5[k]));
+    }
+    if constexpr ((M & kLocal) != 0) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k)
+        XL[k] = TAKE ? (SHR ? mlp_shr1(SL[k], readlane_f(cl[k], q)) : mlp_shl1(SL[k], readlane_f(cl[k], q)))
+                     : (SHR ? mlp_shr1z(SL[k]) : mlp_shl1z(SL[k]));
+    }
+    if constexpr ((M & kPF) != 0) {
+      if constexpr (TAKE) {
+        Zm = SHR ? mlp_shr1d(sZm, readlane_d(cz[0], q)) : mlp_shl1d(sZm, readlane_d(cz[0], q));
+        Ze = SHR ? mlp_shr1d(sZe, readlane_d(cz[1], q)) : mlp_shl1d(sZe, readlane_d(cz[1], q));
+        Zf = SHR ? mlp_shr1d(sZf, readlane_d(cz[2], q)) : mlp_shl1d(sZf, readlane_d(cz[2], q));
+        const int ee = __builtin_amdgcn_readlane(ce, q);
+        e = SHR ? mlp_shr1i(se, ee) : mlp_shl1i(se, ee);
+      } else {
+        Zm = SHR ? mlp_shr1zd(sZm) : mlp_shl1zd(sZm);
+        Ze = SHR ? mlp_shr1zd(sZe) : mlp_shl1zd(sZe);
+        Zf = SHR ? mlp_shr1zd(sZf) : mlp_shl1zd(sZf);
+        e = SHR ? mlp_shr1zi(se) : mlp_shl1zi(se);
+      }
+    }
+  }
+};
+
+// Stores of the boundary row before a segment's chunk load must be visible
+// to it (same wave, other lanes): order them once per 64-step segment.
+__device__ __forceinline__ void boundary_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+
+struct ChainLaunch {
+  dim3 grid, block;
+  size_t lds;
+};
+// 4 waves (chains) per workgroup; 1 when a chain's residues need a large
+// LDS region.
+static inline ChainLaunch chain_launch(int64_t nchains, int lds_seq) {
+  const int stride = chain_lds_stride(lds_seq);
+  const int wpb = stride * kWavesPerBlock <= 40 * 1024 ? kWavesPerBlock : 1;
+  ChainLaunch l;
+  l.grid = dim3((unsigned)((nchains + wpb - 1) / wpb));
+  l.block = dim3(64 * wpb);
+  l.lds = (size_t)stride * wpb;
+  return l;
+}
+
+
+}  // namespace mlp

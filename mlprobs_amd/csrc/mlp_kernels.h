@@ -48,6 +48,7 @@ struct ModelScalars {
   float lt[3][3];     // local_transProb
   float rt1;          // random_transProb[1]
   double pf_open, pf_ext;  // exp(beta*gap_open), exp(beta*gap_ext)
+  float vit_init[3];       // Viterbi start/end scores (CPNP/ProbabilisticModel.h:1068-1070)
 };
 
 struct Tables {
@@ -62,6 +63,7 @@ struct PairMeta {
   const int32_t* pa;       // seq index of row sequence (seq1)
   const int32_t* pb;       // seq index of column sequence (seq2)
   const int32_t* row0;     // first stacked row of the pair in its chain
+  const int32_t* chain;    // chain of the pair
   const int64_t* rm_off;   // base of the pair's row-major local-chain region
   const int64_t* ell_row;  // first ELL row of the pair (rows 1..L1)
 };
@@ -110,6 +112,16 @@ struct Scratch {
   uint16_t* ell_col;       // [ell row][kEll]
   float* ell_val;
   int32_t* ell_cnt;        // [ell row]
+  uint8_t* vt;             // step-diagonal Viterbi traceback bits
+};
+
+// Viterbi family test outputs (per slot).
+struct VitOut {
+  uint8_t* path;           // traceback order: 0 = B (match), 1 = X, 2 = Y
+  const int64_t* path_off; // per slot, capacity L1 + L2
+  int32_t* path_len;
+  float* match;            // identical residue pairs in B columns
+  int32_t* state;          // best terminating state (k_viterbi -> k_vit_trace)
 };
 
 enum ModelSet : int { kHmm5 = 1, kLocal = 2, kPF = 4 };
@@ -134,6 +146,9 @@ hipError_t launch_fold_totals(const ModelScalars& ms, const Tables* tab, SeqSet 
 hipError_t launch_merge(int models, int pid, const ModelScalars& ms, SeqSet seqs, PairMeta pm,
                         ChainMeta cm, PairRec* rec, Scratch sc, int64_t nchains, int lds_seq,
                         hipStream_t st);
+hipError_t launch_viterbi(const ModelScalars& ms, const Tables* tab, SeqSet seqs, PairMeta pm,
+                          ChainMeta cm, Scratch sc, VitOut vo, int64_t nchains, int lds_seq,
+                          int64_t npairs, hipStream_t st);
 hipError_t launch_compact(SeqSet seqs, PairMeta pm, PairRec* rec, Scratch sc,
                           const int64_t* ent_base, int32_t* out_rowptr, const int64_t* rowptr_base,
                           uint16_t* out_cols, float* out_vals, int64_t npairs, hipStream_t st);

@@ -35,7 +35,7 @@ struct DevBuf {
   size_t bytes = 0;
 };
 
-enum KernelId { KFWD = 0, KBWD, KTOT, KMERGE, KCOMPACT, KRELAX, KTRANS, KFILTER, KGATHER };
+enum KernelId { KFWD = 0, KBWD, KTOT, KMERGE, KCOMPACT, KRELAX, KTRANS, KFILTER, KGATHER, KVITERBI };
 
 }  // namespace
 
@@ -52,6 +52,7 @@ struct mlp_ctx {
   int64_t P = 0;
   std::vector<int32_t> lens;
   std::vector<int64_t> offs;
+  std::vector<uint8_t> h_res;         // residue letters of the family (host)
   std::vector<int32_t> pa, pb;        // per pair
   std::vector<int64_t> rp_off;        // canonical row_ptr offsets (P + 1)
   std::vector<int64_t> trp_off;       // transposed row_ptr offsets (P + 1)
@@ -71,6 +72,12 @@ struct mlp_ctx {
   int64_t store_total = 0;
   std::vector<float> dist, mea;
   std::vector<int64_t> nnz;
+  // Viterbi family test (per pair, pair order)
+  std::vector<int32_t> vit_len;
+  std::vector<float> vit_match;
+  std::vector<int64_t> vit_off;       // path offsets (P + 1), capacity L_a + L_b
+  std::vector<uint8_t> vit_path;      // forward order, 0 = B, 1 = X, 2 = Y (when kept)
+  bool vit_done = false, vit_paths = false;
   // batch scratch
   DevBuf scratch;
   size_t scratch_budget = 0;
@@ -234,6 +241,10 @@ static void build_tables(Tables& T, ModelScalars& ms, float delta) {
   const double beta_d = beta;
   ms.pf_open = exp(beta_d * -22.0);
   ms.pf_ext = exp(beta_d * -1.0);
+  // CPNP/ProbabilisticModel.h:1068-1070: LOG(0.6080327034), LOG(0.1959836632) x 2
+  ms.vit_init[0] = logf(0.6080327034f);
+  ms.vit_init[1] = logf(0.1959836632f);
+  ms.vit_init[2] = logf(0.1959836632f);
 }
 
 static int pair_cost_cells(const mlp_ctx* c, int64_t p) {
@@ -321,6 +332,7 @@ int mlp_family_load(mlp_ctx* c, int n, const char* residues, const int64_t* offs
       codes[q] = (uint8_t)(ch - 'A');
     }
   }
+  c->h_res.assign(residues, residues + tot);
   c->P = (int64_t)n * (n - 1) / 2;
   c->pa.resize(c->P);
   c->pb.resize(c->P);
@@ -353,6 +365,12 @@ int mlp_family_load(mlp_ctx* c, int n, const char* residues, const int64_t* offs
   c->nnz.assign(c->P, 0);
   c->store_p0 = c->store_p1 = 0;
   c->store_total = 0;
+  c->vit_len.assign(c->P, 0);
+  c->vit_match.assign(c->P, 0.f);
+  c->vit_off.assign(c->P + 1, 0);
+  for (int64_t q = 0; q < c->P; q++) c->vit_off[q + 1] = c->vit_off[q] + c->lens[c->pa[q]] + c->lens[c->pb[q]];
+  c->vit_path.clear();
+  c->vit_done = c->vit_paths = false;
   return MLP_OK;
 }
 
@@ -383,6 +401,196 @@ static int grow_store(mlp_ctx* c, int64_t need, int64_t keep) {
   return MLP_OK;
 }
 
+}  // extern "C"
+
+// ------------------------------------------------------------ batch planning
+// Equal-sized batches of a pair range under the scratch budget, given an
+// upper bound of one pair's scratch bytes.
+template <class F>
+static size_t batch_target_for(mlp_ctx* c, int64_t p0, int64_t p1, F pair_bytes) {
+  size_t all = 0;
+  for (int64_t q = p0; q < p1; q++) all += pair_bytes(q);
+  const size_t nb = (all + c->scratch_budget - 1) / std::max<size_t>(c->scratch_budget, 1);
+  if (nb > 1) return std::min(c->scratch_budget, all / nb + all / (nb * 64) + 1);
+  return c->scratch_budget;
+}
+template <class F>
+static int next_batch(mlp_ctx* c, int64_t p, int64_t p1, size_t target, F pair_bytes, int64_t* q_out) {
+  int64_t q = p;
+  size_t bytes = 0;
+  while (q < p1) {
+    const size_t add = pair_bytes(q);
+    if (q > p && bytes + add > target) break;
+    if (chain_seq_bytes(chain_width(c->lens[c->pb[q]]), c->lens[c->pa[q]], 1) > kChainSeqMax) {
+      c->err = "pair " + std::to_string(q) + ": sequences too long for the LDS residue staging";
+      return MLP_ERR_ARG;
+    }
+    bytes += add;
+    ++q;
+  }
+  *q_out = q;
+  return MLP_OK;
+}
+
+// Chains of one batch (mlp_kernels.h, "Chains"): pairs sorted by column
+// count, stacked greedily; slots ordered chain by chain, chains longest first.
+struct ChainPlan {
+  int64_t np = 0, nch = 0;
+  std::vector<int64_t> order;                       // slot -> pair
+  std::vector<int32_t> pa, pb, row0, chain;         // per slot
+  std::vector<int64_t> rm, ell;                     // per slot
+  std::vector<int32_t> first, count, width, rows, seqb;  // per chain
+  std::vector<int64_t> cell, bndo;                  // per chain
+  int64_t cells = 0, rm_total = 0, bnd = 0, ell_rows = 0;
+  int lds_seq = 0;
+};
+
+static void plan_chains(const mlp_ctx* c, int64_t p, int64_t q, ChainPlan& P) {
+  const int64_t np = q - p;
+  std::vector<int64_t> byw(np);
+  std::iota(byw.begin(), byw.end(), p);
+  std::stable_sort(byw.begin(), byw.end(), [&](int64_t x, int64_t y) {
+    const int ax = c->lens[c->pb[x]], ay = c->lens[c->pb[y]];
+    if (ax != ay) return ax > ay;
+    return c->lens[c->pa[x]] > c->lens[c->pa[y]];
+  });
+  int64_t total_rows = 0;
+  for (int64_t k = p; k < q; k++) total_rows += c->lens[c->pa[k]] + 1;
+  // enough chains to fill the device a few times over, long enough that the
+  // 63-step skew and the last partial strip stay small
+  const int64_t target_rows = std::max<int64_t>(512, std::min<int64_t>(4096, total_rows / 8192));
+  struct ChainH { int64_t begin, end; int W, rows, seq; int64_t cost; };
+  std::vector<ChainH> chains;
+  ChainH cur{0, 0, 0, 0, 0, 0};
+  for (int64_t k = 0; k < np; k++) {
+    const int64_t x = byw[k];
+    const int L1 = c->lens[c->pa[x]], L2 = c->lens[c->pb[x]];
+    const int w = chain_width(L2);
+    const int n_in = (int)(cur.end - cur.begin);
+    const bool fits = n_in > 0 && n_in < kChainMax && cur.rows + L1 + 1 <= target_rows &&
+                      chain_seq_bytes(cur.W, cur.rows - n_in + L1, n_in + 1) <= kChainSeqSoft &&
+                      cur.W - w <= std::max(8, cur.W / 16);
+    if (!fits) {
+      if (cur.end > cur.begin) chains.push_back(cur);
+      cur = ChainH{k, k, w, 0, 0, 0};
+    }
+    cur.end = k + 1;
+    cur.rows += L1 + 1;
+    cur.seq = chain_seq_bytes(cur.W, cur.rows - (int)(cur.end - cur.begin), (int)(cur.end - cur.begin));
+  }
+  if (cur.end > cur.begin) chains.push_back(cur);
+  for (auto& h : chains) h.cost = (int64_t)chain_strips(h.rows) * h.W;
+  std::stable_sort(chains.begin(), chains.end(), [](const ChainH& x, const ChainH& y) { return x.cost > y.cost; });
+  P = ChainPlan();
+  P.np = np;
+  P.nch = (int64_t)chains.size();
+  P.order.resize(np); P.pa.resize(np); P.pb.resize(np); P.row0.resize(np); P.chain.resize(np);
+  P.rm.resize(np); P.ell.resize(np);
+  P.first.resize(P.nch); P.count.resize(P.nch); P.width.resize(P.nch); P.rows.resize(P.nch);
+  P.seqb.resize(P.nch); P.cell.resize(P.nch); P.bndo.resize(P.nch);
+  int64_t s = 0;
+  for (int64_t h = 0; h < P.nch; h++) {
+    const ChainH& ch = chains[h];
+    P.first[h] = (int32_t)s;
+    P.count[h] = (int32_t)(ch.end - ch.begin);
+    P.width[h] = ch.W;
+    P.rows[h] = ch.rows;
+    P.seqb[h] = ch.seq;
+    P.cell[h] = P.cells;
+    P.bndo[h] = P.bnd;
+    P.cells += chain_steps(ch.rows, ch.W) * 64;
+    P.bnd += ch.W;
+    P.lds_seq = std::max(P.lds_seq, ch.seq);
+    int row0 = 0;
+    for (int64_t k = ch.begin; k < ch.end; k++, s++) {
+      const int64_t x = byw[k];
+      const int L1 = c->lens[c->pa[x]], L2 = c->lens[c->pb[x]];
+      P.order[s] = x;
+      P.pa[s] = c->pa[x];
+      P.pb[s] = c->pb[x];
+      P.row0[s] = row0;
+      P.chain[s] = (int32_t)h;
+      P.rm[s] = P.rm_total;
+      P.ell[s] = P.ell_rows;
+      row0 += L1 + 1;
+      P.rm_total += (int64_t)L1 * ((L2 + 3) & ~3);
+      P.ell_rows += L1;
+    }
+  }
+}
+
+// Scratch carving: 256-byte aligned sub-buffers of one device allocation.
+struct Carver {
+  size_t off = 0;
+  size_t take(size_t b) {
+    const size_t o = off;
+    off += (b + 255) & ~(size_t)255;
+    return o;
+  }
+};
+
+// Upload the plan's per-slot / per-chain metadata; returns device views.
+struct PlanDev {
+  size_t o_pa, o_pb, o_r0, o_ch, o_rm, o_ell, o_cf, o_cc, o_cw, o_cr, o_cs, o_cco, o_cbo;
+};
+static PlanDev carve_plan(Carver& cv, const ChainPlan& P) {
+  PlanDev d;
+  d.o_pa = cv.take(P.np * 4); d.o_pb = cv.take(P.np * 4); d.o_r0 = cv.take(P.np * 4);
+  d.o_ch = cv.take(P.np * 4); d.o_rm = cv.take(P.np * 8); d.o_ell = cv.take(P.np * 8);
+  d.o_cf = cv.take(P.nch * 4); d.o_cc = cv.take(P.nch * 4); d.o_cw = cv.take(P.nch * 4);
+  d.o_cr = cv.take(P.nch * 4); d.o_cs = cv.take(P.nch * 4); d.o_cco = cv.take(P.nch * 8);
+  d.o_cbo = cv.take(P.nch * 8);
+  return d;
+}
+static int upload_plan(mlp_ctx* c, char* base, const PlanDev& d, const ChainPlan& P, PairMeta& pm,
+                       ChainMeta& cm) {
+  auto up = [&](size_t o, const void* h, size_t n) {
+    return hipMemcpyAsync(base + o, h, n, hipMemcpyHostToDevice, c->stream);
+  };
+  HIPCHK(c, up(d.o_pa, P.pa.data(), P.np * 4));
+  HIPCHK(c, up(d.o_pb, P.pb.data(), P.np * 4));
+  HIPCHK(c, up(d.o_r0, P.row0.data(), P.np * 4));
+  HIPCHK(c, up(d.o_ch, P.chain.data(), P.np * 4));
+  HIPCHK(c, up(d.o_rm, P.rm.data(), P.np * 8));
+  HIPCHK(c, up(d.o_ell, P.ell.data(), P.np * 8));
+  HIPCHK(c, up(d.o_cf, P.first.data(), P.nch * 4));
+  HIPCHK(c, up(d.o_cc, P.count.data(), P.nch * 4));
+  HIPCHK(c, up(d.o_cw, P.width.data(), P.nch * 4));
+  HIPCHK(c, up(d.o_cr, P.rows.data(), P.nch * 4));
+  HIPCHK(c, up(d.o_cs, P.seqb.data(), P.nch * 4));
+  HIPCHK(c, up(d.o_cco, P.cell.data(), P.nch * 8));
+  HIPCHK(c, up(d.o_cbo, P.bndo.data(), P.nch * 8));
+  pm.pa = (const int32_t*)(base + d.o_pa);
+  pm.pb = (const int32_t*)(base + d.o_pb);
+  pm.row0 = (const int32_t*)(base + d.o_r0);
+  pm.chain = (const int32_t*)(base + d.o_ch);
+  pm.rm_off = (const int64_t*)(base + d.o_rm);
+  pm.ell_row = (const int64_t*)(base + d.o_ell);
+  cm.first = (const int32_t*)(base + d.o_cf);
+  cm.count = (const int32_t*)(base + d.o_cc);
+  cm.width = (const int32_t*)(base + d.o_cw);
+  cm.rows = (const int32_t*)(base + d.o_cr);
+  cm.seq_bytes = (const int32_t*)(base + d.o_cs);
+  cm.cell_off = (const int64_t*)(base + d.o_cco);
+  cm.bnd_off = (const int64_t*)(base + d.o_cbo);
+  return MLP_OK;
+}
+
+// upper bound of one pair's step-diagonal slots (as if alone in a chain whose
+// width may exceed its own by the stacking slack)
+static int64_t pair_slots_bound(const mlp_ctx* c, int64_t q) {
+  const int L1 = c->lens[c->pa[q]], L2 = c->lens[c->pb[q]];
+  const int64_t Wb = chain_width(L2) + chain_width(L2) / 8 + 8;
+  return (int64_t)(L1 + 1 + 64) * Wb + 80 * 64;
+}
+static int64_t pair_width_bound(const mlp_ctx* c, int64_t q) {
+  const int L2 = c->lens[c->pb[q]];
+  return chain_width(L2) + chain_width(L2) / 8 + 8;
+}
+static const size_t kPerSlotMeta = 4 * sizeof(int64_t) + 4 * sizeof(int32_t) + sizeof(PairRec) + 7 * 8 + 16;
+
+extern "C" {
+
 int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
   if (!c) return MLP_ERR_ARG;
   if (c->n < 2) { c->err = "family needs >= 2 sequences"; return MLP_ERR_STATE; }
@@ -399,138 +607,36 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
   const int models = model_set_for_pid(pid);
   SeqSet seqs{c->d_res, c->d_off, c->d_len};
 
-  const size_t per_slot = 4 * sizeof(int64_t) + 3 * sizeof(int32_t) + sizeof(PairRec) + 7 * 8 + 16;
-  // upper bound of one pair's scratch (as if it were alone in a chain whose
-  // width may exceed its own by kWidthSlack)
   auto pair_bytes = [&](int64_t q) {
     const int L1 = c->lens[c->pa[q]], L2 = c->lens[c->pb[q]];
-    const int64_t Wb = chain_width(L2) + chain_width(L2) / 8 + 8;
-    const int64_t cl = (int64_t)(L1 + 1 + 64) * Wb + 80 * 64;
     const int64_t rmc = (int64_t)L1 * ((L2 + 3) & ~3);
-    return (size_t)(cl * 20 + rmc * 8) + (size_t)Wb * (5 * 4 + 3 * 4 + 3 * 8 + 4 + 4) +
-           (size_t)L1 * (kEll * 6 + 4) + per_slot;
+    return (size_t)(pair_slots_bound(c, q) * 20 + rmc * 8) +
+           (size_t)pair_width_bound(c, q) * (5 * 4 + 3 * 4 + 3 * 8 + 4 + 4) +
+           (size_t)L1 * (kEll * 6 + 4) + kPerSlotMeta;
   };
-  // equal-sized batches (no small tail batch that leaves the GPU half idle)
-  size_t batch_target = c->scratch_budget;
-  {
-    size_t all = 0;
-    for (int64_t q = p0; q < p1; q++) all += pair_bytes(q);
-    const size_t nb = (all + c->scratch_budget - 1) / std::max<size_t>(c->scratch_budget, 1);
-    if (nb > 1) batch_target = std::min(c->scratch_budget, all / nb + all / (nb * 64) + 1);
-  }
+  const size_t batch_target = batch_target_for(c, p0, p1, pair_bytes);
   int64_t p = p0;
+  ChainPlan P;
   while (p < p1) {
-    // ---- batch: contiguous pairs within the scratch budget
-    int64_t q = p;
-    size_t bytes = 0;
-    while (q < p1) {
-      const size_t add = pair_bytes(q);
-      if (q > p && bytes + add > batch_target) break;
-      if (chain_seq_bytes(chain_width(c->lens[c->pb[q]]), c->lens[c->pa[q]], 1) > kChainSeqMax) {
-        c->err = "pair " + std::to_string(q) + ": sequences too long for the LDS residue staging";
-        return MLP_ERR_ARG;
-      }
-      bytes += add;
-      ++q;
-    }
-    const int64_t np = q - p;
-    // ---- chains: pairs sorted by column count, stacked greedily
-    std::vector<int64_t> byw(np);
-    std::iota(byw.begin(), byw.end(), p);
-    std::stable_sort(byw.begin(), byw.end(), [&](int64_t x, int64_t y) {
-      const int ax = c->lens[c->pb[x]], ay = c->lens[c->pb[y]];
-      if (ax != ay) return ax > ay;
-      return c->lens[c->pa[x]] > c->lens[c->pa[y]];
-    });
-    int64_t total_rows = 0;
-    for (int64_t k = p; k < q; k++) total_rows += c->lens[c->pa[k]] + 1;
-    // enough chains to fill the device a few times over, long enough that the
-    // 63-step skew and the last partial strip stay small
-    const int64_t target_rows = std::max<int64_t>(512, std::min<int64_t>(4096, total_rows / 8192));
-    struct ChainH { int64_t begin, end; int W, rows, seq; int64_t cost; };
-    std::vector<ChainH> chains;
-    {
-      ChainH cur{0, 0, 0, 0, 0, 0};
-      for (int64_t k = 0; k < np; k++) {
-        const int64_t x = byw[k];
-        const int L1 = c->lens[c->pa[x]], L2 = c->lens[c->pb[x]];
-        const int w = chain_width(L2);
-        const int n_in = (int)(cur.end - cur.begin);
-        const bool fits = n_in > 0 && n_in < kChainMax && cur.rows + L1 + 1 <= target_rows &&
-                          chain_seq_bytes(cur.W, cur.rows - n_in + L1, n_in + 1) <= kChainSeqSoft &&
-                          cur.W - w <= std::max(8, cur.W / 16);
-        if (!fits) {
-          if (cur.end > cur.begin) chains.push_back(cur);
-          cur = ChainH{k, k, w, 0, 0, 0};
-        }
-        cur.end = k + 1;
-        cur.rows += L1 + 1;
-        cur.seq = chain_seq_bytes(cur.W, cur.rows - (int)(cur.end - cur.begin), (int)(cur.end - cur.begin));
-      }
-      if (cur.end > cur.begin) chains.push_back(cur);
-      for (auto& h : chains) h.cost = (int64_t)chain_strips(h.rows) * h.W;
-      std::stable_sort(chains.begin(), chains.end(), [](const ChainH& x, const ChainH& y) { return x.cost > y.cost; });
-    }
-    const int64_t nch = (int64_t)chains.size();
-    // slots: chain members in chain order
-    std::vector<int64_t> order(np);
-    std::vector<int32_t> h_pa(np), h_pb(np), h_row0(np);
-    std::vector<int64_t> h_rm(np), h_ell(np), h_entb(np), h_rpb(np);
-    std::vector<int32_t> h_first(nch), h_count(nch), h_width(nch), h_rows(nch), h_seqb(nch);
-    std::vector<int64_t> h_cell(nch), h_bndo(nch);
-    int64_t cells = 0, rm = 0, bnd = 0, rows = 0;
-    int lds_seq = 0;
-    {
-      int64_t s = 0;
-      for (int64_t h = 0; h < nch; h++) {
-        const ChainH& ch = chains[h];
-        h_first[h] = (int32_t)s;
-        h_count[h] = (int32_t)(ch.end - ch.begin);
-        h_width[h] = ch.W;
-        h_rows[h] = ch.rows;
-        h_seqb[h] = ch.seq;
-        h_cell[h] = cells;
-        h_bndo[h] = bnd;
-        cells += chain_steps(ch.rows, ch.W) * 64;
-        bnd += ch.W;
-        lds_seq = std::max(lds_seq, ch.seq);
-        int row0 = 0;
-        for (int64_t k = ch.begin; k < ch.end; k++, s++) {
-          const int64_t x = byw[k];
-          const int L1 = c->lens[c->pa[x]], L2 = c->lens[c->pb[x]];
-          order[s] = x;
-          h_pa[s] = c->pa[x];
-          h_pb[s] = c->pb[x];
-          h_row0[s] = row0;
-          h_rm[s] = rm;
-          h_ell[s] = rows;
-          row0 += L1 + 1;
-          rm += (int64_t)L1 * ((L2 + 3) & ~3);
-          rows += L1;
-        }
-      }
-    }
-    // ---- carve scratch
-    size_t off = 0;
-    auto carve = [&](size_t b) {
-      size_t o = off;
-      off += (b + 255) & ~(size_t)255;
-      return o;
-    };
-    const size_t o_f5 = carve(cells * 4), o_fl = carve(cells * 4), o_pg = carve(cells * 4),
-                 o_zm = carve(cells * 8), o_chf = carve(rm * 4), o_chb = carve(rm * 4),
-                 o_b5 = carve(bnd * 20), o_bl = carve(bnd * 12), o_bz = carve(bnd * 24),
-                 o_be = carve(bnd * 4), o_bm = carve(bnd * 4), o_ec = carve(rows * kEll * 2),
-                 o_ev = carve(rows * kEll * 4), o_en = carve(rows * 4), o_pa = carve(np * 4),
-                 o_pb = carve(np * 4), o_r0 = carve(np * 4), o_rm = carve(np * 8),
-                 o_ell = carve(np * 8), o_entb = carve(np * 8), o_rpb = carve(np * 8),
-                 o_rec = carve(np * sizeof(PairRec)), o_cf = carve(nch * 4), o_cc = carve(nch * 4),
-                 o_cw = carve(nch * 4), o_cr = carve(nch * 4), o_cs = carve(nch * 4),
-                 o_cco = carve(nch * 8), o_cbo = carve(nch * 8);
+    int64_t q;
     int rc;
-    if ((rc = ensure(c, c->scratch, off))) return rc;
+    if ((rc = next_batch(c, p, p1, batch_target, pair_bytes, &q))) return rc;
+    plan_chains(c, p, q, P);
+    const int64_t np = P.np, nch = P.nch;
+    const std::vector<int64_t>& order = P.order;
+    std::vector<int64_t> h_entb(np), h_rpb(np);
+    // ---- carve scratch
+    Carver cv;
+    const size_t o_f5 = cv.take(P.cells * 4), o_fl = cv.take(P.cells * 4), o_pg = cv.take(P.cells * 4),
+                 o_zm = cv.take(P.cells * 8), o_chf = cv.take(P.rm_total * 4), o_chb = cv.take(P.rm_total * 4),
+                 o_b5 = cv.take(P.bnd * 20), o_bl = cv.take(P.bnd * 12), o_bz = cv.take(P.bnd * 24),
+                 o_be = cv.take(P.bnd * 4), o_bm = cv.take(P.bnd * 4), o_ec = cv.take(P.ell_rows * kEll * 2),
+                 o_ev = cv.take(P.ell_rows * kEll * 4), o_en = cv.take(P.ell_rows * 4),
+                 o_entb = cv.take(np * 8), o_rpb = cv.take(np * 8), o_rec = cv.take(np * sizeof(PairRec));
+    const PlanDev pd = carve_plan(cv, P);
+    if ((rc = ensure(c, c->scratch, cv.off))) return rc;
     char* base = (char*)c->scratch.p;
-    Scratch sc;
+    Scratch sc{};
     sc.f5 = (float*)(base + o_f5);
     sc.fl = (float*)(base + o_fl);
     sc.pg = (float*)(base + o_pg);
@@ -547,34 +653,9 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
     sc.ell_cnt = (int32_t*)(base + o_en);
     PairRec* d_rec = (PairRec*)(base + o_rec);
     PairMeta pm;
-    pm.pa = (const int32_t*)(base + o_pa);
-    pm.pb = (const int32_t*)(base + o_pb);
-    pm.row0 = (const int32_t*)(base + o_r0);
-    pm.rm_off = (const int64_t*)(base + o_rm);
-    pm.ell_row = (const int64_t*)(base + o_ell);
     ChainMeta cm;
-    cm.first = (const int32_t*)(base + o_cf);
-    cm.count = (const int32_t*)(base + o_cc);
-    cm.width = (const int32_t*)(base + o_cw);
-    cm.rows = (const int32_t*)(base + o_cr);
-    cm.seq_bytes = (const int32_t*)(base + o_cs);
-    cm.cell_off = (const int64_t*)(base + o_cco);
-    cm.bnd_off = (const int64_t*)(base + o_cbo);
-    auto up = [&](size_t o, const void* h, size_t n) {
-      return hipMemcpyAsync(base + o, h, n, hipMemcpyHostToDevice, c->stream);
-    };
-    HIPCHK(c, up(o_pa, h_pa.data(), np * 4));
-    HIPCHK(c, up(o_pb, h_pb.data(), np * 4));
-    HIPCHK(c, up(o_r0, h_row0.data(), np * 4));
-    HIPCHK(c, up(o_rm, h_rm.data(), np * 8));
-    HIPCHK(c, up(o_ell, h_ell.data(), np * 8));
-    HIPCHK(c, up(o_cf, h_first.data(), nch * 4));
-    HIPCHK(c, up(o_cc, h_count.data(), nch * 4));
-    HIPCHK(c, up(o_cw, h_width.data(), nch * 4));
-    HIPCHK(c, up(o_cr, h_rows.data(), nch * 4));
-    HIPCHK(c, up(o_cs, h_seqb.data(), nch * 4));
-    HIPCHK(c, up(o_cco, h_cell.data(), nch * 8));
-    HIPCHK(c, up(o_cbo, h_bndo.data(), nch * 8));
+    if ((rc = upload_plan(c, base, pd, P, pm, cm))) return rc;
+    const int lds_seq = P.lds_seq;
     HIPCHK(c, hipMemsetAsync(d_rec, 0, np * sizeof(PairRec), c->stream));
     int64_t bcells = 0;
     for (int64_t k = p; k < q; k++) bcells += pair_cost_cells(c, k);
@@ -649,6 +730,230 @@ int mlp_pair_results(mlp_ctx* c, int64_t p0, int64_t p1, float* dist, float* mea
     if (mea) mea[p - p0] = c->mea[p];
     if (nnz) nnz[p - p0] = c->nnz[p];
   }
+  return MLP_OK;
+}
+
+// ------------------------------------------------------------ Viterbi family test
+int mlp_viterbi(mlp_ctx* c, int64_t p0, int64_t p1, int keep_paths) {
+  if (!c) return MLP_ERR_ARG;
+  if (c->n < 2) { c->err = "family needs >= 2 sequences"; return MLP_ERR_STATE; }
+  if (p0 < 0 || p1 > c->P || p0 > p1) { c->err = "bad pair range"; return MLP_ERR_ARG; }
+  hipSetDevice(c->device);
+  ModelScalars ms;
+  build_tables(c->h_tables, ms, -1.0f);
+  HIPCHK(c, hipMemcpyAsync(c->d_tables, &c->h_tables, sizeof(Tables), hipMemcpyHostToDevice, c->stream));
+  SeqSet seqs{c->d_res, c->d_off, c->d_len};
+  if (keep_paths && c->vit_path.size() != (size_t)c->vit_off[c->P]) c->vit_path.assign(c->vit_off[c->P], 0);
+  auto pair_bytes = [&](int64_t q) {
+    const int L1 = c->lens[c->pa[q]], L2 = c->lens[c->pb[q]];
+    return (size_t)pair_slots_bound(c, q) + (size_t)pair_width_bound(c, q) * 12 + (size_t)(L1 + L2) +
+           kPerSlotMeta + 24;
+  };
+  const size_t batch_target = batch_target_for(c, p0, p1, pair_bytes);
+  int64_t p = p0;
+  ChainPlan P;
+  while (p < p1) {
+    int64_t q;
+    int rc;
+    if ((rc = next_batch(c, p, p1, batch_target, pair_bytes, &q))) return rc;
+    plan_chains(c, p, q, P);
+    const int64_t np = P.np;
+    std::vector<int64_t> h_poff(np + 1, 0);
+    for (int64_t s = 0; s < np; s++) {
+      const int64_t x = P.order[s];
+      h_poff[s + 1] = h_poff[s] + c->lens[c->pa[x]] + c->lens[c->pb[x]];
+    }
+    Carver cv;
+    const size_t o_vt = cv.take(P.cells), o_bl = cv.take(P.bnd * 12), o_path = cv.take(h_poff[np]),
+                 o_poff = cv.take(np * 8), o_plen = cv.take(np * 4), o_match = cv.take(np * 4),
+                 o_state = cv.take(np * 4);
+    const PlanDev pd = carve_plan(cv, P);
+    if ((rc = ensure(c, c->scratch, cv.off))) return rc;
+    char* base = (char*)c->scratch.p;
+    Scratch sc{};
+    sc.vt = (uint8_t*)(base + o_vt);
+    sc.bndl = (float*)(base + o_bl);
+    VitOut vo;
+    vo.path = (uint8_t*)(base + o_path);
+    vo.path_off = (const int64_t*)(base + o_poff);
+    vo.path_len = (int32_t*)(base + o_plen);
+    vo.match = (float*)(base + o_match);
+    vo.state = (int32_t*)(base + o_state);
+    PairMeta pm;
+    ChainMeta cm;
+    if ((rc = upload_plan(c, base, pd, P, pm, cm))) return rc;
+    HIPCHK(c, hipMemcpyAsync(base + o_poff, h_poff.data(), np * 8, hipMemcpyHostToDevice, c->stream));
+    int64_t bcells = 0;
+    for (int64_t k = p; k < q; k++) bcells += pair_cost_cells(c, k);
+    {
+      Timer t(c, KVITERBI, bcells);
+      HIPCHK(c, launch_viterbi(ms, c->d_tables, seqs, pm, cm, sc, vo, P.nch, P.lds_seq, np, c->stream));
+    }
+    std::vector<int32_t> len(np);
+    std::vector<float> match(np);
+    std::vector<uint8_t> paths;
+    HIPCHK(c, hipMemcpyAsync(len.data(), vo.path_len, np * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(match.data(), vo.match, np * 4, hipMemcpyDeviceToHost, c->stream));
+    if (keep_paths) {
+      paths.resize(h_poff[np]);
+      HIPCHK(c, hipMemcpyAsync(paths.data(), vo.path, h_poff[np], hipMemcpyDeviceToHost, c->stream));
+    }
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    for (int64_t s = 0; s < np; s++) {
+      const int64_t x = P.order[s];
+      c->vit_len[x] = len[s];
+      c->vit_match[x] = match[s];
+      if (keep_paths) {  // traceback order -> forward order
+        uint8_t* dst = c->vit_path.data() + c->vit_off[x];
+        const uint8_t* src = paths.data() + h_poff[s];
+        for (int k = 0; k < len[s]; k++) dst[k] = src[len[s] - 1 - k];
+      }
+    }
+    p = q;
+  }
+  if (p0 == 0 && p1 == c->P) {
+    c->vit_done = true;
+    c->vit_paths = keep_paths != 0;
+  }
+  return MLP_OK;
+}
+
+int mlp_viterbi_results(mlp_ctx* c, int64_t p0, int64_t p1, float* match, int32_t* len) {
+  if (!c || p0 < 0 || p1 > c->P || p0 > p1) return MLP_ERR_ARG;
+  for (int64_t p = p0; p < p1; p++) {
+    if (match) match[p - p0] = c->vit_match[p];
+    if (len) len[p - p0] = c->vit_len[p];
+  }
+  return MLP_OK;
+}
+
+int mlp_viterbi_path(mlp_ctx* c, int64_t p, uint8_t* codes, int32_t* len) {
+  if (!c || p < 0 || p >= c->P) return MLP_ERR_ARG;
+  if (c->vit_path.empty()) { c->err = "paths not kept (mlp_viterbi keep_paths = 0)"; return MLP_ERR_STATE; }
+  if (len) *len = c->vit_len[p];
+  if (codes) memcpy(codes, c->vit_path.data() + c->vit_off[p], c->vit_len[p]);
+  return MLP_OK;
+}
+
+// initDistrib[2] by average identity (CPNP/MSA.cpp:851-861)
+static float delta_for_identity(float identity) {
+  if (identity <= 0.125) return 0.108854f;
+  if (identity <= 0.15) return 0.132548f;
+  if (identity <= 0.175) return 0.165248f;
+  if (identity <= 0.2) return 0.168284f;
+  if (identity <= 0.25) return 0.170705f;
+  if (identity <= 0.3) return 0.100675f;
+  if (identity <= 0.35) return 0.090755f;
+  if (identity <= 0.4) return 0.146188f;
+  if (identity <= 0.45) return 0.167858f;
+  if (identity <= 0.5) return 0.250769f;
+  return mlp_init_distrib[2];
+}
+
+int mlp_model_adjustment(mlp_ctx* c, float* identity_out, float* variance_out, float* delta_out,
+                         int32_t* code_out) {
+  if (!c) return MLP_ERR_ARG;
+  if (c->n < 2) { c->err = "family needs >= 2 sequences"; return MLP_ERR_STATE; }
+  int rc;
+  if (!c->vit_done && (rc = mlp_viterbi(c, 0, c->P, 0))) return rc;
+  // CPNP/MSA.cpp:775-882; identities summed in pair order (the reference's
+  // OpenMP `identity +=` is unsynchronised; one thread gives this order)
+  const int P = (int)c->P;
+  std::vector<float> pids(P);
+  float identity = 0;
+  for (int k = 0; k < P; k++) {
+    pids[k] = c->vit_match[k] / (float)c->vit_len[k];
+    identity += pids[k];
+  }
+  identity /= (float)P;
+  float variance = 0;
+  for (int k = 0; k < P; k++) variance += (pids[k] - identity) * (pids[k] - identity);
+  variance /= (float)P;
+  variance = sqrtf(variance);
+  const int vm = variance > 0.115 ? 10 : 0;
+  int code;
+  if (identity <= 0.18) code = vm + 0;
+  else if (identity <= 0.25) code = vm + 1;
+  else if (identity <= 0.4) code = vm + 2;
+  else if (identity <= 0.7) code = vm + 3;
+  else code = vm + 4;
+  if (identity_out) *identity_out = identity;
+  if (variance_out) *variance_out = variance;
+  if (delta_out) *delta_out = delta_for_identity(identity);
+  if (code_out) *code_out = code;
+  return MLP_OK;
+}
+
+int mlp_family_features(mlp_ctx* c, float theta, float* f, int32_t* ints) {
+  if (!c || !f || !ints) return MLP_ERR_ARG;
+  if (c->n < 2) { c->err = "family needs >= 2 sequences"; return MLP_ERR_STATE; }
+  int rc;
+  if (!(c->vit_done && c->vit_paths) && (rc = mlp_viterbi(c, 0, c->P, 1))) return rc;
+  // CPNP/MSA.cpp:646-772 (Alter_ModelAdjustmentTest), serial in pair order.
+  // BLOSUM62 is indexed through alphabetDefault.find(); a letter outside the
+  // 20-letter alphabet gives index -1, i.e. a read just before the row / the
+  // table.  The reference build lays emitPairsDefault[20][20] out directly
+  // before BLOSUM62 (CPNP/Defaults.h:36-104), so those reads return
+  // emitPairsDefault entries; `mem` reproduces that layout (pinned by the
+  // BB11028 `-G` golden line, whose sequences contain X).
+  int idx[26];
+  for (int k = 0; k < 26; k++) idx[k] = -1;
+  for (int k = 0; k < 20; k++) idx[MLP_ALPHABET[k] - 'A'] = k;
+  float mem[800] = {0};
+  for (int i = 0, t = 0; i < 20; i++)
+    for (int j = 0; j <= i; j++) mem[i * 20 + j] = mlp_emit_pairs_lower[t++];
+  for (int k = 0; k < 400; k++) mem[400 + k] = (float)mlp_blosum62[k];
+  const int P = (int)c->P;
+  std::vector<float> finals(10000, 0.f);   // MAX_ARR (CPNP/MSA.cpp:17)
+  float identity = 0, tmp_sp = 0;
+  int max_len = 0, tmp_sp_idx = 0, avg_length = 0;
+  std::vector<float> pids(P);
+  for (int p = 0; p < P; p++) {
+    const int a = c->pa[p], b = c->pb[p];
+    const char* s1 = (const char*)c->h_res.data() + c->offs[a];
+    const char* s2 = (const char*)c->h_res.data() + c->offs[b];
+    const uint8_t* path = c->vit_path.data() + c->vit_off[p];
+    const int n = c->vit_len[p];
+    avg_length += n;
+    if (n > max_len) max_len = n;
+    float nmatch = 0;
+    int i = 0, j = 0, num = 0;
+    for (int k = 0; k < n; k++) {
+      if (path[k] == 0) {
+        const char c1 = s1[i++], c2 = s2[j++];
+        if (c1 == c2) nmatch += 1;
+        const float bl = mem[400 + idx[c1 - 'A'] * 20 + idx[c2 - 'A']];
+        if (bl < 10) {
+          if (num < (int)finals.size()) finals[num] += bl;
+          tmp_sp += bl;
+        }
+      } else if (path[k] == 1) {
+        ++i;
+      } else {
+        ++j;
+      }
+      ++num;
+      ++tmp_sp_idx;
+    }
+    pids[p] = nmatch / (float)n;
+    identity += nmatch / (float)n;
+  }
+  tmp_sp /= (float)tmp_sp_idx;
+  identity /= (float)P;
+  avg_length /= P;
+  float peak = 0;
+  for (int k = 0; k < max_len && k < (int)finals.size(); k++) {
+    finals[k] /= (float)P;
+    if (theta <= finals[k]) peak += 1;
+  }
+  peak /= (float)max_len;
+  float variance = 0;
+  for (int k = 0; k < P; k++) variance += (pids[k] - identity) * (pids[k] - identity);
+  variance /= (float)P;
+  variance = sqrtf(variance);
+  const float factor = 2 * (float)c->n - (float)avg_length;
+  f[0] = identity; f[1] = variance; f[2] = tmp_sp; f[3] = peak; f[4] = factor;
+  ints[0] = c->n; ints[1] = avg_length;
   return MLP_OK;
 }
 

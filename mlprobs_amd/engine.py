@@ -29,7 +29,7 @@ U16P = np.ctypeslib.ndpointer(np.uint16, flags='C_CONTIGUOUS')
 ERRORS = {1: 'bad argument', 2: 'HIP error', 3: 'partition function overflow', 4: 'state error',
           5: 'RCCL error', 6: 'device memory'}
 KERNELS = ['forward', 'backward', 'local_totals', 'merge_mea_sparsify', 'compact', 'relax',
-           'transpose', 'filter', 'allgather']
+           'transpose', 'filter', 'allgather', 'viterbi']
 
 
 class MlpError(RuntimeError):
@@ -66,6 +66,11 @@ def lib():
         L.mlp_csr_export.argtypes = [P, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
         L.mlp_csr_import.argtypes = [P, I32P, I64P, U16P, F32P]
         L.mlp_relax.argtypes = [P, C.c_int]
+        L.mlp_viterbi.argtypes = [P, I64, I64, C.c_int]
+        L.mlp_viterbi_results.argtypes = [P, I64, I64, C.c_void_p, C.c_void_p]
+        L.mlp_viterbi_path.argtypes = [P, I64, C.c_void_p, C.c_void_p]
+        L.mlp_model_adjustment.argtypes = [P, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.mlp_family_features.argtypes = [P, C.c_float, C.c_void_p, C.c_void_p]
         L.mlp_comm_unique_id.argtypes = [C.c_char_p]
         L.mlp_comm_init.argtypes = [P, C.c_char_p, C.c_int, C.c_int]
         L.mlp_shard_range.argtypes = [P, C.c_int, C.c_int, C.POINTER(I64), C.POINTER(I64)]
@@ -82,7 +87,8 @@ def lib():
 
 EXPORTED = ['mlp_ctx_create', 'mlp_ctx_destroy', 'mlp_last_error', 'mlp_family_load',
             'mlp_family_npairs', 'mlp_posteriors', 'mlp_pair_results', 'mlp_csr_total',
-            'mlp_csr_export', 'mlp_csr_import', 'mlp_relax', 'mlp_comm_unique_id', 'mlp_comm_init',
+            'mlp_csr_export', 'mlp_csr_import', 'mlp_relax', 'mlp_viterbi', 'mlp_viterbi_results',
+            'mlp_viterbi_path', 'mlp_model_adjustment', 'mlp_family_features', 'mlp_comm_unique_id', 'mlp_comm_init',
             'mlp_shard_range', 'mlp_shard_plan', 'mlp_gather_layout', 'mlp_allgather', 'mlp_synchronize', 'mlp_profile',
             'mlp_kernel_times', 'mlp_profile_reset']
 
@@ -243,6 +249,51 @@ class Family:
     def profile(self, enable=True):
         self._chk(self._L.mlp_profile(self._ctx, 1 if enable else 0))
         self._chk(self._L.mlp_profile_reset(self._ctx))
+
+    # ---- family test (CPNP/MSA.cpp:646-882)
+    def viterbi(self, keep_paths=False, p_begin=0, p_end=None):
+        """Viterbi alignment of pairs [p_begin, p_end) (ComputeViterbiAlignment,
+        CPNP/ProbabilisticModel.h:1043-1170)."""
+        p_end = self.npairs if p_end is None else p_end
+        self._chk(self._L.mlp_viterbi(self._ctx, int(p_begin), int(p_end), int(bool(keep_paths))))
+
+    def viterbi_results(self):
+        """(identical residues in match columns, path length) per pair."""
+        m = np.zeros(self.npairs, np.float32)
+        n = np.zeros(self.npairs, np.int32)
+        self._chk(self._L.mlp_viterbi_results(self._ctx, 0, self.npairs, m.ctypes.data, n.ctypes.data))
+        return m, n
+
+    def viterbi_path(self, p):
+        """Path of pair p as the reference's string of 'B' / 'X' / 'Y'."""
+        a, b = pairs_of(self.n)[p]
+        buf = np.zeros(self.lens[a] + self.lens[b], np.uint8)
+        n = C.c_int32()
+        self._chk(self._L.mlp_viterbi_path(self._ctx, int(p), buf.ctypes.data, C.byref(n)))
+        return ''.join('BXY'[x] for x in buf[: n.value])
+
+    def model_adjustment(self):
+        """ModelAdjustmentTest (CPNP/MSA.cpp:775-882): (identity, variance,
+        delta, code) with code = variance_mean + identity class."""
+        idn, var, dl = C.c_float(), C.c_float(), C.c_float()
+        code = C.c_int32()
+        self._chk(self._L.mlp_model_adjustment(self._ctx, C.byref(idn), C.byref(var), C.byref(dl), C.byref(code)))
+        return idn.value, var.value, dl.value, code.value
+
+    def family_features(self, theta=1.0):
+        """Alter_ModelAdjustmentTest (CPNP/MSA.cpp:646-772), the `-G` line:
+        (identity, variance, N, avg_len, tmp_sp, peak_ratio, factor)."""
+        f = np.zeros(5, np.float32)
+        ints = np.zeros(2, np.int32)
+        self._chk(self._L.mlp_family_features(self._ctx, C.c_float(theta), f.ctypes.data, ints.ctypes.data))
+        return (float(f[0]), float(f[1]), int(ints[0]), int(ints[1]), float(f[2]), float(f[3]), float(f[4]))
+
+    @staticmethod
+    def features_line(feat):
+        """The `-G` output line (std::to_string of each field, tab-separated,
+        CPNP/MSA.cpp:771)."""
+        i, v, n, al, sp, pk, fa = feat
+        return '\t'.join(['%f' % i, '%f' % v, str(n), str(al), '%f' % sp, '%f' % pk, '%f' % fa])
 
     def kernel_times(self):
         ms = np.zeros(len(KERNELS), np.float64)

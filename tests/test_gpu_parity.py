@@ -2,11 +2,12 @@
 (tests/golden/, produced by the reference's own objects) and against the CPU
 oracle at larger sizes.  All calls go through the C ABI (include/mlpgpu.h).
 """
+import os
 import numpy as np
 import pytest
 
 import orc
-from goldens import family_csrs, family_names, load_family, load_pair, pair_names
+from goldens import GOLDEN, family_csrs, family_names, load_family, load_pair, pair_names
 from mlprobs_amd import synth
 from mlprobs_amd.engine import Family
 from parity import close_scalar, csr_close, csr_equal
@@ -163,3 +164,58 @@ def test_batches_of_one(monkeypatch):
     """A scratch budget below one pair: every batch holds a single pair."""
     monkeypatch.setenv('MLP_SCRATCH_GB', '0.0001')
     _check_family_vs_oracle([x for _, x in synth.family(5, 70, 0.6, seed=44)], 2, 'batch1')
+
+
+# ---- family test: Viterbi alignments (CPNP/MSA.cpp:646-882)
+@pytest.mark.parametrize('name', family_names())
+def test_model_adjustment_golden(name):
+    """pid class and delta from the reference's ModelAdjustmentTest (one thread)."""
+    d = load_family(name)
+    fam = Family(list(d['seqs']))
+    ident, var, delta, code = fam.model_adjustment()
+    assert code == int(d['variance_mean']), (name, ident, var, code)
+    assert np.float32(delta) == np.float32(d['delta']), name
+    fam.close()
+
+
+@pytest.mark.parametrize('s,L,n,seed', [(0.6, 90, 6, 51), (0.3, 200, 4, 52), (0.8, 300, 3, 53)])
+def test_viterbi_paths_vs_oracle(s, L, n, seed):
+    seqs = _ragged_family(n, L // 3, L, seed)
+    m = orc.model(0.132548)
+    fam = Family(seqs)
+    fam.viterbi(keep_paths=True)
+    match, length = fam.viterbi_results()
+    k = 0
+    for a in range(n):
+        for b in range(a + 1, n):
+            _, ref = orc.viterbi(m, seqs[a], seqs[b])
+            got = fam.viterbi_path(k)
+            assert got == ref, (k, len(got), len(ref))
+            assert length[k] == len(ref)
+            i = j = 0
+            same = 0
+            for ch in ref:
+                if ch == 'B':
+                    same += seqs[a][i] == seqs[b][j]
+                    i += 1
+                    j += 1
+                elif ch == 'X':
+                    i += 1
+                else:
+                    j += 1
+            assert match[k] == same
+            k += 1
+    fam.close()
+
+
+@pytest.mark.parametrize('name', ['bb11028', 'div12', 'sim8'])
+def test_family_features_cli_golden(name):
+    """The `c_p_np_aln -G` line of the reference CLI (single thread)."""
+    fa = os.path.join(GOLDEN, 'cli', f'{name}.fa')
+    seqs = [x for _, x in synth.read_fasta(fa)]
+    fam = Family(seqs)
+    line = Family.features_line(fam.family_features(1.0))
+    with open(os.path.join(GOLDEN, 'cli', f'{name}_G.out')) as fh:
+        ref = fh.read().strip()
+    assert line == ref, (line, ref)
+    fam.close()
