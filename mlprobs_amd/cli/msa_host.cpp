@@ -1,0 +1,413 @@
+// msa_host.cpp -- see msa_host.h.
+#include "msa_host.h"
+
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <algorithm>
+#include <cctype>
+#include <set>
+
+namespace cpnp {
+
+// ------------------------------------------------------------------ FASTA
+// Byte reader with the reference FileBuffer's Get / UnGet / GetLine
+// (FileBuffer.h): a line ends at '\n' only, so '\r' stays in the line.
+namespace {
+struct Reader {
+  std::string buf;
+  size_t pos = 0;
+  bool eof() const { return pos >= buf.size(); }
+  bool get(char& ch) {
+    if (pos >= buf.size()) return false;
+    ch = buf[pos++];
+    return true;
+  }
+  void unget() { --pos; }
+  void line(std::string& s) {
+    s.clear();
+    char ch;
+    while (get(ch) && ch != '\n') s += ch;
+  }
+};
+}  // namespace
+
+bool load_fasta(const std::string& path, std::vector<Row>& out, std::string& err) {
+  FILE* f = fopen(path.c_str(), "rb");
+  if (!f) {
+    err = "ERROR: Could not open file '" + path + "' for reading.";
+    return false;
+  }
+  Reader in;
+  char tmp[1 << 16];
+  size_t got;
+  while ((got = fread(tmp, 1, sizeof tmp, f)) > 0) in.buf.append(tmp, got);
+  fclose(f);
+  out.clear();
+  // MultiSequence::LoadMFA: sequences until the first record that fails
+  while (true) {
+    std::string header;
+    while (!in.eof()) {
+      in.line(header);
+      if (!header.empty()) break;
+    }
+    if (header.empty() || header[0] != '>') {
+      if (out.empty() && !header.empty()) {
+        err = "ERROR: MSF input is not supported by this build";
+        return false;
+      }
+      break;
+    }
+    header = header.substr(1);
+    while (!header.empty() && isspace((unsigned char)header[0])) header = header.substr(1);
+    while (!header.empty() && isspace((unsigned char)header.back())) header.pop_back();
+    Row r;
+    r.header = header;
+    r.data = "@";
+    char ch;
+    while (in.get(ch)) {
+      if (ch == '>') {
+        in.unget();
+        break;
+      }
+      if (isspace((unsigned char)ch)) continue;
+      if (ch == '.') ch = '-';
+      if (ch == '-') continue;   // stripGaps
+      if (!((ch >= 'A' && ch <= 'Z') || (ch >= 'a' && ch <= 'z'))) {
+        err = std::string("ERROR: Unknown character encountered: ") + ch;
+        return false;
+      }
+      if (ch >= 'a' && ch <= 'z') ch = ch - 'a' + 'A';
+      r.data += ch;
+    }
+    if (r.length() == 0) break;   // an empty record ends the input (Sequence::Fail)
+    r.label = r.sort_label = (int)out.size();
+    out.push_back(std::move(r));
+  }
+  if (out.empty()) {
+    err = "ERROR: No sequences read.";
+    return false;
+  }
+  return true;
+}
+
+void write_mfa(std::string& out, const Profile& p, int columns) {
+  for (const Row& r : p) {
+    out += '>';
+    out += r.header;
+    out += '\n';
+    int ct = 1;
+    for (; ct <= r.length(); ct++) {
+      out += r.data[ct];
+      if (ct % columns == 0) out += '\n';
+    }
+    if ((ct - 1) % columns != 0) out += '\n';
+  }
+}
+
+// ------------------------------------------------------------------ tree
+GuideTree build_tree(std::vector<std::vector<float>> dist, int varianceid) {
+  const int n = (int)dist.size();
+  GuideTree t;
+  t.nodes.assign(2 * n + 1, GuideTree::Node());
+  for (int i = 0; i < n; i++) t.nodes[i].leaf = true;
+  // active clusters in a list ordered by their matrix index; each cluster
+  // keeps the node it currently stands for (MSAClusterTree.cpp:164-295)
+  std::vector<int> active(n), node_of(n), size_of(2 * n + 1, 0);
+  for (int i = 0; i < n; i++) {
+    active[i] = i;
+    node_of[i] = i;
+    size_of[i] = 1;
+  }
+  std::vector<float> joins(n + 1, 0.f);
+  const int first = n, last = 2 * n - 1;
+  for (int node = first; node < last; node++) {
+    float best = 1.1f;
+    int bi = -1, bj = -1;   // positions in `active`
+    for (size_t x = 0; x < active.size(); x++) {
+      const int mi = active[x];
+      for (size_t y = 0; y < active.size() && active[y] < mi; y++) {
+        float d = dist[mi][active[y]];
+        if (d < 0) {
+          fprintf(stderr, "ERROR: It is impossible to have distance value less than zero\n");
+          d = 0;
+        }
+        if (d < best) {
+          best = d;
+          bi = (int)x;
+          bj = (int)y;
+        }
+      }
+    }
+    if (bi < 0) {
+      fprintf(stderr, "OOPS: Error occurred while constructing the cluster tree\n\n");
+      exit(-1);
+    }
+    const int mi = active[bi], mj = active[bj];
+    const float half = best * 0.5f;
+    GuideTree::Node& par = t.nodes[node];
+    par.left = node_of[mi];
+    par.right = node_of[mj];
+    t.nodes[node_of[mi]].parent = node;
+    t.nodes[node_of[mi]].dist = half;
+    t.nodes[node_of[mj]].parent = node;
+    t.nodes[node_of[mj]].dist = half;
+    size_of[node] = size_of[node_of[mi]] + size_of[node_of[mj]];
+    active.erase(active.begin() + bj);
+    const unsigned isize = size_of[node_of[mi]], jsize = size_of[node_of[mj]];
+    for (int idx : active) {
+      const float idist = dist[mi][idx], jdist = dist[mj][idx];
+      if (varianceid == 0) joins[idx] = (idist + jdist) / 2;
+      else joins[idx] = (idist * isize + jdist * jsize) / (isize + jsize);
+    }
+    node_of[mi] = node;
+    for (int idx : active) {
+      dist[mi][idx] = joins[idx];
+      dist[idx][mi] = joins[idx];
+    }
+  }
+  t.root = n >= 1 ? (n == 1 ? 0 : last - 1) : -1;
+  // sequence weights (MSAGuideTree.cpp getSeqsWeights)
+  for (int i = 0; i < n; i++)
+    for (int cur = i; cur >= 0; cur = t.nodes[cur].parent) t.nodes[cur].order++;
+  t.weights.assign(n, 0);
+  for (int i = 0; i < n; i++) {
+    float w = 0;
+    for (int cur = i; t.nodes[cur].parent >= 0; cur = t.nodes[cur].parent)
+      w += t.nodes[cur].dist / t.nodes[cur].order;
+    t.weights[i] = (int)(100 * w);
+  }
+  int wsum = 0;
+  for (int i = 0; i < n; i++) wsum += t.weights[i];
+  if (wsum == 0) {
+    for (int i = 0; i < n; i++) t.weights[i] = 1;
+    wsum = n;
+  }
+  for (int i = 0; i < n; i++) {
+    t.weights[i] = (t.weights[i] * 1000) / wsum;   // INT_MULTIPLY (MSADef.h)
+    if (t.weights[i] < 1) t.weights[i] = 1;
+  }
+  return t;
+}
+
+// ------------------------------------------------------------------ profiles
+static std::vector<int> mapping(const Row& r) {   // Sequence::GetMapping
+  std::vector<int> m(1, 0);
+  for (int i = 1; i <= r.length(); i++)
+    if (r.data[i] != '-') m.push_back(i);
+  return m;
+}
+
+std::vector<float> build_posterior(const Profile& A, const Profile& B, const SparseSet& sp,
+                                   const int* weights, float cutoff) {
+  const int len1 = A[0].length(), len2 = B[0].length();
+  const int64_t W2 = len2 + 1;
+  std::vector<float> post((size_t)(len1 + 1) * W2, 0.f);
+  float total = 0;
+  if (weights)
+    for (const Row& x : A)
+      for (const Row& y : B) total += weights[x.label] * weights[y.label];
+  for (const Row& x : A) {
+    const std::vector<int> m1 = mapping(x);
+    for (const Row& y : B) {
+      const std::vector<int> m2 = mapping(y);
+      const int first = x.label, second = y.label;
+      const float w = weights ? (float)(weights[first] * weights[second]) / total : 1.f;
+      const int lo = std::min(first, second), hi = std::max(first, second);
+      const int64_t p = sp.pair(lo, hi);
+      const int32_t* rp = sp.row_ptr.data() + sp.rp_off[p];
+      const uint16_t* cols = sp.cols.data() + sp.ent_off[p];
+      const float* vals = sp.vals.data() + sp.ent_off[p];
+      const int rows = sp.lens[lo], ncols = sp.lens[hi];
+      if (first < second) {
+        for (int ii = 1; ii <= rows; ii++) {
+          const int64_t base = (int64_t)m1[ii] * W2;
+          for (int32_t e = rp[ii]; e < rp[ii + 1]; e++)
+            post[base + m2[cols[e]]] += weights ? w * vals[e] : vals[e];
+          for (int jj = 0; jj < ncols; jj++) post[base + m2[jj]] -= weights ? w * cutoff : cutoff;
+        }
+      } else {
+        for (int jj = 1; jj <= rows; jj++) {
+          const int64_t base = m2[jj];
+          for (int32_t e = rp[jj]; e < rp[jj + 1]; e++)
+            post[base + (int64_t)m1[cols[e]] * W2] += weights ? w * vals[e] : vals[e];
+          for (int ii = 0; ii < ncols; ii++) post[base + (int64_t)m1[ii] * W2] -= weights ? w * cutoff : cutoff;
+        }
+      }
+    }
+  }
+  return post;
+}
+
+std::string mea_path(int len1, int len2, const std::vector<float>& post, float* score) {
+  const int W2 = len2 + 1;
+  std::vector<float> rows(2 * (size_t)W2);
+  float* oldr = rows.data();
+  float* newr = rows.data() + W2;
+  std::vector<char> tb((size_t)(len1 + 1) * W2);
+  for (int j = 0; j <= len2; j++) {
+    oldr[j] = 0;
+    tb[j] = 'L';
+  }
+  for (int i = 1; i <= len1; i++) {
+    newr[0] = 0;
+    tb[(size_t)i * W2] = 'U';
+    const float* pr = post.data() + (size_t)i * W2;
+    for (int j = 1; j <= len2; j++) {
+      // ChooseBestOfThree (ScoreType.h:347-366): D, L, U
+      const float x1 = pr[j] + oldr[j - 1], x2 = newr[j - 1], x3 = oldr[j];
+      float v;
+      char b;
+      if (x1 >= x2) {
+        if (x1 >= x3) { v = x1; b = 'D'; } else { v = x3; b = 'U'; }
+      } else if (x2 >= x3) {
+        v = x2; b = 'L';
+      } else {
+        v = x3; b = 'U';
+      }
+      newr[j] = v;
+      tb[(size_t)i * W2 + j] = b;
+    }
+    std::swap(oldr, newr);
+  }
+  if (score) *score = oldr[len2];
+  std::string path;
+  int r = len1, c = len2;
+  while (r != 0 || c != 0) {
+    switch (tb[(size_t)r * W2 + c]) {
+      case 'L': c--; path += 'Y'; break;
+      case 'U': r--; path += 'X'; break;
+      default: c--; r--; path += 'B'; break;
+    }
+  }
+  std::reverse(path.begin(), path.end());
+  return path;
+}
+
+static Row add_gaps(const Row& r, const std::string& path, char id) {   // Sequence::AddGaps
+  Row o;
+  o.header = r.header;
+  o.label = r.label;
+  o.sort_label = r.sort_label;
+  o.data.reserve(path.size() + 1);
+  o.data = "@";
+  size_t k = 1;
+  for (char c : path) {
+    if (c == 'B' || c == id) o.data += r.data[k++];
+    else o.data += '-';
+  }
+  return o;
+}
+
+Profile merge(const Profile& a, const Profile& b, const std::string& path, bool sort_by_label) {
+  Profile out;
+  out.reserve(a.size() + b.size());
+  for (const Row& r : a) out.push_back(add_gaps(r, path, 'X'));
+  for (const Row& r : b) out.push_back(add_gaps(r, path, 'Y'));
+  if (sort_by_label) {   // MultiSequence::SortByLabel: O(n^2) swap sort
+    for (size_t i = 0; i + 1 < out.size(); i++)
+      for (size_t j = i + 1; j < out.size(); j++)
+        if (out[i].sort_label > out[j].sort_label) std::swap(out[i], out[j]);
+  }
+  return out;
+}
+
+// MultiSequence::Project (MultiSequence.h:662-734)
+static Profile project(const Profile& p, const std::set<int>& idx) {
+  const int L = p[*idx.begin()].length();
+  std::vector<int> keep;
+  for (int i = 1; i <= L; i++) {
+    bool found = false;
+    for (int k : idx)
+      if (p[k].data[i] != '-') { found = true; break; }
+    if (found) keep.push_back(i);
+  }
+  Profile out;
+  for (int k : idx) {
+    Row r;
+    r.header = p[k].header;
+    r.label = p[k].label;
+    r.sort_label = p[k].sort_label;
+    r.data = "@";
+    for (int i : keep) r.data += p[k].data[i];
+    out.push_back(std::move(r));
+  }
+  return out;
+}
+
+static Profile process_tree(const GuideTree& t, int node, const std::vector<Row>& seqs,
+                            const SparseSet& sp, const Options& opt) {
+  const GuideTree::Node& nd = t.nodes[node];
+  if (nd.leaf) return Profile{seqs[node]};
+  Profile left = process_tree(t, nd.left, seqs, sp, opt);
+  Profile right = process_tree(t, nd.right, seqs, sp, opt);
+  // AlignAlignments (MSA.cpp:1410-1474) with the tree weights
+  const std::vector<float> post = build_posterior(left, right, sp, t.weights.data(), opt.cutoff);
+  float sc;
+  const std::string path = mea_path(left[0].length(), right[0].length(), post, &sc);
+  return merge(left, right, path, !opt.align_order);
+}
+
+// DoIterativeRefinement (MSA.cpp:1537-1625): 2 = no split, 1 = unchanged score
+static int refine_once(Profile& aln, const SparseSet& sp, const Options& opt) {
+  std::set<int> one, two;
+  const int n = (int)aln.size();
+  for (int i = 0; i < n; i++) {
+    if (rand() % 2) one.insert(i);
+    else two.insert(i);
+  }
+  if (one.empty() || two.empty()) return 2;
+  const Profile g1 = project(aln, one), g2 = project(aln, two);
+  const std::vector<float> post = build_posterior(g1, g2, sp, nullptr, opt.cutoff);
+  // accuracy of the current alignment
+  const int L = aln[0].length();
+  const int W2 = g2[0].length() + 1;
+  int i1 = 0, i2 = 0;
+  float before = 0;
+  for (int i = 1; i <= L; i++) {
+    bool f1 = false, f2 = false;
+    for (int k : one)
+      if (aln[k].data[i] != '-') { f1 = true; break; }
+    if (f1) i1++;
+    for (int k : two)
+      if (aln[k].data[i] != '-') { f2 = true; break; }
+    if (f2) i2++;
+    if (f1 && f2) before += post[(size_t)i1 * W2 + i2];
+  }
+  float after;
+  const std::string path = mea_path(g1[0].length(), g2[0].length(), post, &after);
+  aln = merge(g1, g2, path, false);
+  return before == after ? 1 : 0;
+}
+
+Profile progressive_alignment(const std::vector<Row>& seqs, const SparseSet& sp, const GuideTree& tree,
+                              int pid, Options& opt) {
+  Profile aln = process_tree(tree, tree.root, seqs, sp, opt);
+  const int n = (int)aln.size();
+  if (opt.align_order) {   // ComputeFinalAlignment: SaveOrdering, then sorted merges stay off
+    for (int i = 0; i < n; i++) aln[i].sort_label = i;
+    opt.align_order = false;
+  }
+  int reps = opt.refinement;
+  if (pid > 3 || n > 150) reps = 0;
+  if (n <= 50) reps = 2 * reps;
+  int ineffective = 0;
+  const int warmup = 100;
+  for (int i = 0; i < reps; i++) {
+    const int flag = refine_once(aln, sp, opt);
+    if (n > 20) {
+      if (n < 200) {
+        if (flag > 0) {
+          if (reps < 4 * n) reps++;
+          if (flag == 1) ineffective++;
+        }
+        if (ineffective > 2 * n && i > warmup) break;
+      } else if (n > 200) {
+        reps = 10;
+      }
+    }
+  }
+  return aln;
+}
+
+}  // namespace cpnp

@@ -1,0 +1,90 @@
+// msa_host.h -- host side of the c_p_np_aln drop-in: sequence I/O, the guide
+// tree, profile-profile posteriors from the sparse set, MEA alignment of two
+// profiles and iterative refinement.  These stages run once per family (the
+// all-pairs stages they consume run on the GPU through libmlpgpu); each
+// function cites the reference code whose behaviour it reproduces
+// (kuangmeng/MLProbs baseMSA/C_P_NP_Aln).
+#pragma once
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+namespace cpnp {
+
+// One (possibly gapped) row of an alignment: data[0] is unused ('@'),
+// residues / '-' at 1..length (Sequence.h:24-125).
+struct Row {
+  std::string header;
+  std::string data;   // data[0] = '@'
+  int label = 0;      // input position (GetLabel)
+  int sort_label = 0; // GetSortLabel
+  int length() const { return (int)data.size() - 1; }
+};
+
+using Profile = std::vector<Row>;
+
+// FASTA in the reference's MultiSequence::LoadMFA(..., stripGaps = true)
+// semantics (Sequence.h:56-119, MultiSequence.h:267-312).  Returns false
+// and sets `err` on the conditions where the reference exits with status 1.
+bool load_fasta(const std::string& path, std::vector<Row>& out, std::string& err);
+
+// MultiSequence::WriteMFA, 60 columns (Sequence.h:281-303).
+void write_mfa(std::string& out, const Profile& p, int columns = 60);
+
+// Canonical sparse set of libmlpgpu (include/mlpgpu.h): pair (a < b) has
+// row_ptr[rp_off[p] .. + L_a + 2) and entries from ent_off[p].
+struct SparseSet {
+  int n = 0;
+  std::vector<int> lens;
+  std::vector<int64_t> rp_off, ent_off;
+  std::vector<int32_t> row_ptr;
+  std::vector<uint16_t> cols;
+  std::vector<float> vals;
+  int64_t pair(int a, int b) const {  // a < b, row-major (CPNP/MSA.cpp:907-919)
+    return (int64_t)a * n - (int64_t)a * (a + 1) / 2 + (b - a - 1);
+  }
+};
+
+// UPGMA-style cluster tree over the distance matrix (MSAClusterTree.cpp:
+// generateClusterTree(varianceid)) and the sequence weights derived from it
+// (MSAGuideTree.cpp getSeqsWeights).
+struct GuideTree {
+  struct Node {
+    int left = -1, right = -1, parent = -1;
+    float dist = 0;
+    bool leaf = false;
+    int order = 0;
+  };
+  std::vector<Node> nodes;
+  int root = -1;
+  std::vector<int> weights;
+};
+GuideTree build_tree(std::vector<std::vector<float>> dist, int varianceid);
+
+// Profile-profile posterior (ProbabilisticModel.h:1197-1376): weighted when
+// `weights` is non-null.  Returns the dense (len1 + 1) x (len2 + 1) matrix.
+std::vector<float> build_posterior(const Profile& a, const Profile& b, const SparseSet& sp,
+                                   const int* weights, float cutoff);
+
+// MEA alignment of two profiles (ProbabilisticModel.h:804-864): the path
+// ('B', 'X', 'Y') and its score.
+std::string mea_path(int len1, int len2, const std::vector<float>& post, float* score);
+
+// Profile merge along a path (Sequence.h AddGaps) and helpers.
+Profile merge(const Profile& a, const Profile& b, const std::string& path, bool sort_by_label);
+
+struct Options {
+  int consistency = 2;          // -c
+  int refinement = 100;         // -ir
+  float cutoff = 0;             // -co
+  bool align_order = false;     // -a
+  bool verbose = false;         // -v
+};
+
+// Progressive alignment over the guide tree followed by iterative
+// refinement (MSA.cpp:1369-1635, ComputeFinalAlignment).
+Profile progressive_alignment(const std::vector<Row>& seqs, const SparseSet& sp, const GuideTree& tree,
+                              int pid, Options& opt);
+
+}  // namespace cpnp
