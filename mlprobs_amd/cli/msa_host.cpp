@@ -348,12 +348,49 @@ static Profile process_tree(const GuideTree& t, int node, const std::vector<Row>
   return merge(left, right, path, !opt.align_order);
 }
 
+// The refinement splits come from the C library's rand() at its default seed
+// (the -p 0 path never seeds it, CPNP/MSA.cpp:1545).  The GPU runtime
+// libraries of this build may draw from the shared libc generator during
+// initialisation, so the sequence is reproduced here instead: glibc's
+// TYPE_3 additive feedback generator (r[i] = r[i-3] + r[i-31], seeded by
+// the Park-Miller recurrence, first 310 outputs discarded), seed 1.
+namespace {
+struct LibcRand {
+  uint32_t r[34];
+  int k = 0;
+  LibcRand() {
+    int32_t s[34];
+    s[0] = 1;
+    for (int i = 1; i < 31; i++) {
+      const int64_t v = (16807LL * s[i - 1]) % 2147483647;
+      s[i] = (int32_t)(v < 0 ? v + 2147483647 : v);
+    }
+    for (int i = 31; i < 34; i++) s[i] = s[i - 31];
+    for (int i = 0; i < 34; i++) r[i] = (uint32_t)s[i];
+    k = 34;
+    for (int i = 34; i < 344; i++) next_raw();
+  }
+  uint32_t next_raw() {
+    // ring of the last 34 values: r[k % 34]
+    const uint32_t v = r[(k - 31) % 34] + r[(k - 3) % 34];
+    r[k % 34] = v;
+    ++k;
+    return v;
+  }
+  int next() { return (int)(next_raw() >> 1); }
+};
+LibcRand& libc_rand() {
+  static LibcRand g;
+  return g;
+}
+}  // namespace
+
 // DoIterativeRefinement (MSA.cpp:1537-1625): 2 = no split, 1 = unchanged score
 static int refine_once(Profile& aln, const SparseSet& sp, const Options& opt) {
   std::set<int> one, two;
   const int n = (int)aln.size();
   for (int i = 0; i < n; i++) {
-    if (rand() % 2) one.insert(i);
+    if (libc_rand().next() % 2) one.insert(i);
     else two.insert(i);
   }
   if (one.empty() || two.empty()) return 2;
