@@ -13,6 +13,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <chrono>
 #include <iostream>
 #include <string>
 #include <vector>
@@ -55,6 +56,17 @@ static bool get_float(const char* s, float* v) {   // MSA::GetFloat (CPNP/MSA.cp
   if (end == s || *end) return false;
   *v = (float)r;
   return true;
+}
+
+// MLP_CLI_TIMES=1 prints stage times to stderr (off by default: the
+// reference is silent on stderr on success).
+static void stage(const char* name) {
+  static const bool on = getenv("MLP_CLI_TIMES") != nullptr;
+  static auto t0 = std::chrono::steady_clock::now();
+  if (!on) return;
+  const auto t1 = std::chrono::steady_clock::now();
+  std::cerr << "[stage] " << name << " " << std::chrono::duration<double>(t1 - t0).count() << " s" << std::endl;
+  t0 = t1;
 }
 
 [[noreturn]] static void fail(const std::string& msg) {
@@ -150,6 +162,7 @@ int main(int argc, char** argv) {
     off.push_back((int64_t)res.size());
   }
   check(ctx, mlp_family_load(ctx, n, res.data(), off.data()), "family");
+  stage("load");
 
   if (just_features) {   // CPNP/MSA.cpp:153-166 (theta = 1.0)
     float f[5];
@@ -174,6 +187,7 @@ int main(int argc, char** argv) {
     float identity, variance, delta;
     int32_t code;
     check(ctx, mlp_model_adjustment(ctx, &identity, &variance, &delta, &code), "family test");
+    stage("family test (Viterbi)");
     const int pid = code % 10, vpid = code / 10;
     // pdoAlign (CPNP/MSA.cpp:895-1081): posteriors, distances, tree, consistency
     const int64_t P = mlp_family_npairs(ctx);
@@ -183,8 +197,12 @@ int main(int argc, char** argv) {
     std::vector<std::vector<float>> D(n, std::vector<float>(n, 0.f));
     for (int a = 0, p = 0; a < n; a++)
       for (int b = a + 1; b < n; b++, p++) D[a][b] = D[b][a] = dist[p];
+    stage("posteriors");
     const cpnp::GuideTree tree = cpnp::build_tree(D, vpid);
+    stage("guide tree");
     if (opt.consistency > 0) check(ctx, mlp_relax(ctx, opt.consistency), "consistency");
+    check(ctx, mlp_synchronize(ctx), "consistency");
+    stage("consistency");
     cpnp::SparseSet sp;
     sp.n = n;
     sp.lens.resize(n);
@@ -200,7 +218,9 @@ int main(int argc, char** argv) {
     sp.vals.resize(std::max<int64_t>(total, 1));
     check(ctx, mlp_csr_export(ctx, sp.row_ptr.data(), sp.ent_off.data(), sp.cols.data(), sp.vals.data()),
           "sparse set");
+    stage("sparse set to host");
     aln = cpnp::progressive_alignment(seqs, sp, tree, pid, opt);
+    stage("progressive + refinement");
   }
   mlp_ctx_destroy(ctx);
   std::string out;
