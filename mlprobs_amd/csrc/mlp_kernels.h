@@ -204,6 +204,56 @@ struct FilterArgs {
   int64_t npairs;
   int write;
 };
+// Block images for the pair-resident relaxation: every block P(a, b) and its
+// transpose packed as one contiguous, 16-byte aligned record that a workgroup
+// copies into LDS in one pass:
+//   u16 row_ptr[R + 2] | pad to 8 | entries[nnz] {u32 code, f32 val} | pad to 16
+// R = rows of that orientation, row_ptr relative to the block (nnz < 65536).
+// code = col | (byte offset of col's mask word in the workgroup's bitmap,
+// (col >> 5) * threads * 8) << 10, so col < 1024 and threads <= 1024.
+// Image 2p is P(a, b) of pair p, image 2p + 1 its transpose.
+__host__ __device__ inline int64_t img_ent_off(int rows) { return ((int64_t)(rows + 2) * 2 + 7) & ~(int64_t)7; }
+__host__ __device__ inline int64_t img_bytes(int rows, int64_t nnz) {
+  return (img_ent_off(rows) + 8 * nnz + 15) & ~(int64_t)15;
+}
+struct PackArgs {
+  int n;
+  const int32_t* lens;
+  const int64_t* rp_off;
+  const int32_t* rowptr;
+  const int64_t* ent_off;
+  const uint16_t* cols;
+  const float* vals;
+  const int64_t* trp_off;
+  const int32_t* trowptr;
+  const uint16_t* tcols;
+  const float* tvals;
+  const int64_t* img_off;    // 2P + 1 byte offsets
+  uint8_t* img;
+  int64_t nimg;              // 2P
+  int threads;               // workgroup size of k_relax_pair (mask word offsets)
+};
+struct PairRelaxArgs {
+  int n;
+  const int32_t* lens;
+  const int64_t* rp_off;     // the output pair's own pattern (the mask) and values
+  const int32_t* rowptr;
+  const int64_t* ent_off;
+  const uint16_t* cols;
+  const float* vals;
+  const int64_t* img_off;
+  const uint8_t* img;
+  const int64_t* pairs;      // output pairs, one workgroup each
+  int64_t npairs;
+  float* out;                // raw relaxed values at the input entry slots
+  int img_cap;               // LDS bytes per staged image (multiple of 16)
+  int mask_words;            // bitmap words per output row: (max L >> 5) + 1
+  int acc_cap;               // accumulator slots (max nnz of an output pair)
+};
+size_t pair_relax_lds(int threads, int img_cap, int mask_words, int acc_cap);
+int pair_relax_prefetch(int threads, int img_cap);   // chunks per thread, 0 = too large
+hipError_t launch_pack(const PackArgs& a, hipStream_t st);
+hipError_t launch_relax_pairs(const PairRelaxArgs& a, int threads, hipStream_t st);
 hipError_t launch_transpose(const TransposeArgs& a, hipStream_t st);
 hipError_t launch_relax_tasks(const RelaxArgs& a, hipStream_t st);
 hipError_t launch_filter(const FilterArgs& a, hipStream_t st);

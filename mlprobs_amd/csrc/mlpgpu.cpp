@@ -83,7 +83,7 @@ struct mlp_ctx {
   size_t scratch_budget = 0;
   // relaxation buffers
   DevBuf r_trowptr, r_tcols, r_tvals, r_raw, r_newrp, r_newcols, r_newvals, r_tasks_p, r_tasks_r,
-      r_pairs, r_nnz, r_newoff;
+      r_pairs, r_nnz, r_newoff, r_img, r_imgoff, r_fast;
   // comm
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
@@ -294,7 +294,7 @@ void mlp_ctx_destroy(mlp_ctx* c) {
     if (p) hipFree(p);
   DevBuf* bufs[] = {&c->scratch, &c->r_trowptr, &c->r_tcols, &c->r_tvals, &c->r_raw, &c->r_newrp,
                     &c->r_newcols, &c->r_newvals, &c->r_tasks_p, &c->r_tasks_r, &c->r_pairs,
-                    &c->r_nnz, &c->r_newoff};
+                    &c->r_nnz, &c->r_newoff, &c->r_img, &c->r_imgoff, &c->r_fast};
   for (DevBuf* b : bufs)
     if (b->p) hipFree(b->p);
   if (c->comm) ncclCommDestroy(c->comm);
@@ -1188,21 +1188,88 @@ int mlp_relax(mlp_ctx* c, int iters) {
       Timer t(c, KTRANS, total);
       HIPCHK(c, launch_transpose(ta, c->stream));
     }
-    // row tasks of my output pairs
-    std::vector<int64_t> tp;
+    // Pair-resident path (k_relax_pair) for every output pair whose blocks fit
+    // the LDS images; the row-task kernel for the rest (MLP_RELAX=tasks: all).
+    const int64_t LDS_MAX = 160 * 1024;
+    const char* mode = getenv("MLP_RELAX");
+    const bool tasks_only = (mode && !strcmp(mode, "tasks")) || c->max_len > 1023;
+    const int threads = 64 * ((c->max_len + 63) / 64);
+    const int mask_words = (c->max_len >> 5) + 1;
+    std::vector<int64_t> img_off(2 * c->P + 1, 0);
+    int64_t img_max = 0;
+    for (int64_t p = 0; p < c->P; p++) {
+      const int64_t nz = c->ent_off[p + 1] - c->ent_off[p];
+      const int64_t s0 = img_bytes(c->lens[c->pa[p]], nz), s1 = img_bytes(c->lens[c->pb[p]], nz);
+      img_off[2 * p + 1] = img_off[2 * p] + s0;
+      img_off[2 * p + 2] = img_off[2 * p + 1] + s1;
+      if (nz < 65536) img_max = std::max(img_max, std::max(s0, s1));
+    }
+    int64_t acc_cap = 0;
+    for (int64_t p = r0; p < r1; p++) acc_cap = std::max(acc_cap, c->ent_off[p + 1] - c->ent_off[p]);
+    acc_cap = std::min<int64_t>(acc_cap, 16384);
+    const int64_t fixed = pair_relax_lds(threads, 0, mask_words, (int)acc_cap);
+    int64_t img_cap = std::min<int64_t>(img_max, (LDS_MAX - fixed) / 2) & ~(int64_t)15;
+    while (img_cap > 0 && !pair_relax_prefetch(threads, (int)img_cap)) img_cap -= 16 * threads;
+    std::vector<char> big(c->n, 0);
+    for (int64_t p = 0; p < c->P; p++) {
+      const int64_t nz = c->ent_off[p + 1] - c->ent_off[p];
+      if (nz >= 65536 || img_off[2 * p + 2] - img_off[2 * p + 1] > img_cap ||
+          img_off[2 * p + 1] - img_off[2 * p] > img_cap)
+        big[c->pa[p]] = big[c->pb[p]] = 1;
+    }
+    std::vector<int64_t> fast, tp;
     std::vector<int32_t> tr;
     for (int64_t p = r0; p < r1; p++) {
+      const int64_t nz = c->ent_off[p + 1] - c->ent_off[p];
+      if (nz == 0) continue;  // empty mask: the filter writes an empty block
+      if (!tasks_only && img_cap > 0 && !big[c->pa[p]] && !big[c->pb[p]] && nz <= acc_cap) {
+        fast.push_back(p);
+        continue;
+      }
       const int La = c->lens[c->pa[p]];
       for (int g = 1; g <= La; g += 64) {
         tp.push_back(p);
         tr.push_back(g);
       }
     }
+    if (!fast.empty()) {
+      if ((rc = ensure(c, c->r_img, std::max<int64_t>(img_off[2 * c->P], 16)))) return rc;
+      if ((rc = ensure(c, c->r_imgoff, sizeof(int64_t) * (2 * c->P + 1)))) return rc;
+      if ((rc = ensure(c, c->r_fast, sizeof(int64_t) * fast.size()))) return rc;
+      HIPCHK(c, hipMemcpyAsync(c->r_imgoff.p, img_off.data(), sizeof(int64_t) * (2 * c->P + 1),
+                               hipMemcpyHostToDevice, c->stream));
+      HIPCHK(c, hipMemcpyAsync(c->r_fast.p, fast.data(), sizeof(int64_t) * fast.size(), hipMemcpyHostToDevice,
+                               c->stream));
+      PackArgs pk;
+      pk.n = c->n;
+      pk.lens = c->d_len;
+      pk.rp_off = c->d_rp_off;
+      pk.rowptr = c->d_rowptr;
+      pk.ent_off = c->d_ent_off;
+      pk.cols = c->d_cols;
+      pk.vals = c->d_vals;
+      pk.trp_off = c->d_trp_off;
+      pk.trowptr = (const int32_t*)c->r_trowptr.p;
+      pk.tcols = (const uint16_t*)c->r_tcols.p;
+      pk.tvals = (const float*)c->r_tvals.p;
+      pk.img_off = (const int64_t*)c->r_imgoff.p;
+      pk.img = (uint8_t*)c->r_img.p;
+      pk.nimg = 2 * c->P;
+      pk.threads = threads;
+      Timer t(c, KTRANS, total);
+      HIPCHK(c, launch_pack(pk, c->stream));
+    }
     const int64_t nt = (int64_t)tp.size();
+    if (mode && !strcmp(mode, "pairs") && nt) {  // test hook: the pair-resident path must cover all
+      c->err = "MLP_RELAX=pairs: " + std::to_string(nt) + " row tasks fell back";
+      return MLP_ERR_STATE;
+    }
     if ((rc = ensure(c, c->r_tasks_p, sizeof(int64_t) * std::max<int64_t>(nt, 1)))) return rc;
     if ((rc = ensure(c, c->r_tasks_r, sizeof(int32_t) * std::max<int64_t>(nt, 1)))) return rc;
-    HIPCHK(c, hipMemcpyAsync(c->r_tasks_p.p, tp.data(), sizeof(int64_t) * nt, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(c, hipMemcpyAsync(c->r_tasks_r.p, tr.data(), sizeof(int32_t) * nt, hipMemcpyHostToDevice, c->stream));
+    if (nt) {
+      HIPCHK(c, hipMemcpyAsync(c->r_tasks_p.p, tp.data(), sizeof(int64_t) * nt, hipMemcpyHostToDevice, c->stream));
+      HIPCHK(c, hipMemcpyAsync(c->r_tasks_r.p, tr.data(), sizeof(int32_t) * nt, hipMemcpyHostToDevice, c->stream));
+    }
     RelaxArgs ra;
     ra.n = c->n;
     ra.lens = c->d_len;
@@ -1219,8 +1286,25 @@ int mlp_relax(mlp_ctx* c, int iters) {
     ra.task_row0 = (const int32_t*)c->r_tasks_r.p;
     ra.ntasks = nt;
     ra.out = (float*)c->r_raw.p;
+    PairRelaxArgs pr;
+    pr.n = c->n;
+    pr.lens = c->d_len;
+    pr.rp_off = c->d_rp_off;
+    pr.rowptr = c->d_rowptr;
+    pr.ent_off = c->d_ent_off;
+    pr.cols = c->d_cols;
+    pr.vals = c->d_vals;
+    pr.img_off = (const int64_t*)c->r_imgoff.p;
+    pr.img = (const uint8_t*)c->r_img.p;
+    pr.pairs = (const int64_t*)c->r_fast.p;
+    pr.npairs = (int64_t)fast.size();
+    pr.out = (float*)c->r_raw.p;
+    pr.img_cap = (int)img_cap;
+    pr.mask_words = mask_words;
+    pr.acc_cap = (int)acc_cap;
     {
       Timer t(c, KRELAX, c->ent_off[r1] - c->ent_off[r0]);
+      HIPCHK(c, launch_relax_pairs(pr, threads, c->stream));
       HIPCHK(c, launch_relax_tasks(ra, c->stream));
     }
     // filter: count, host scan, write

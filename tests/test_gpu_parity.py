@@ -219,3 +219,45 @@ def test_family_features_cli_golden(name):
         ref = fh.read().strip()
     assert line == ref, (line, ref)
     fam.close()
+
+
+def _relax_both_paths(seqs, pid, iters, tag):
+    """Pair-resident and row-task relaxation vs the oracle, bit-exact, `iters` rounds."""
+    n = len(seqs)
+    fam = Family(seqs)
+    fam.posteriors(pid, 0.132548)
+    rp, eo, cols, vals = [a.copy() for a in fam.export()]
+    cur = [fam.sparse(k) for k in range(n * (n - 1) // 2)]
+    cur = [(r.astype(np.int32), c.astype(np.int32), v) for r, c, v in cur]
+    lens = [len(x) for x in seqs]
+    refs = []
+    for _ in range(iters):
+        cur = orc.relax(lens, cur)
+        refs.append(cur)
+    for mode in ('pairs', 'tasks'):
+        os.environ['MLP_RELAX'] = mode
+        try:
+            fam.import_csr(rp, eo, cols, vals)
+            for it in range(iters):
+                fam.relax(1)
+                for k in range(len(refs[it])):
+                    csr_equal(refs[it][k], fam.sparse(k), f'{tag} {mode} it{it + 1} p{k}')
+        finally:
+            del os.environ['MLP_RELAX']
+    fam.close()
+
+
+def test_relax_pair_path_divergent():
+    seqs = [x for _, x in synth.family(40, 150, 0.7, seed=41)]
+    _relax_both_paths(seqs, 0, 2, 'div')
+
+
+def test_relax_pair_path_ragged():
+    # lengths 1..400: idle waves, images of very different sizes, empty rows
+    seqs = _ragged_family(24, 1, 400, 42)
+    _relax_both_paths(seqs, 1, 2, 'ragged')
+
+
+def test_relax_pair_path_similar():
+    seqs = [x for _, x in synth.family(30, 200, 0.2, seed=43)]
+    _relax_both_paths(seqs, 3, 3, 'similar')

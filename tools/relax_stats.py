@@ -34,7 +34,7 @@ def block(fam, csr, a, b):
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 512
     L = int(sys.argv[2]) if len(sys.argv) > 2 else 400
-    seqs = synth.family(n, L, 0.7, seed=11)
+    seqs = [s for _, s in synth.family(n, L, 0.7, seed=11)]
     fam = engine.Family(seqs)
     fam.posteriors(0, 0.0)
     csr = fam.export()
