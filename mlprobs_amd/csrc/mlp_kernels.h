@@ -204,17 +204,29 @@ struct FilterArgs {
   int64_t npairs;
   int write;
 };
-// Block images for the pair-resident relaxation: every block P(a, b) and its
-// transpose packed as one contiguous, 16-byte aligned record that a workgroup
-// copies into LDS in one pass:
-//   u16 row_ptr[R + 2] | pad to 8 | entries[nnz] {u32 code, f32 val} | pad to 16
-// R = rows of that orientation, row_ptr relative to the block (nnz < 65536).
-// code = col | (byte offset of col's mask word in the workgroup's bitmap,
-// (col >> 5) * threads * 8) << 10, so col < 1024 and threads <= 1024.
-// Image 2p is P(a, b) of pair p, image 2p + 1 its transpose.
-__host__ __device__ inline int64_t img_ent_off(int rows) { return ((int64_t)(rows + 2) * 2 + 7) & ~(int64_t)7; }
-__host__ __device__ inline int64_t img_bytes(int rows, int64_t nnz) {
-  return (img_ent_off(rows) + 8 * nnz + 15) & ~(int64_t)15;
+// Block images for the pair-resident relaxation (relax.hip).  Every block
+// P(a, b) and its transpose is packed once per round as one record, in two
+// overlapping 16-byte aligned ranges that a workgroup stages into LDS:
+//   cols  u16[nnz]                                  \
+//   rp    u16[R + 2]  (row_ptr, relative)            | A range: the block as
+//   vals  f32[nnz]                    \             /  the left factor
+//   bits  {u32 bits, u32 base}[R * W]  | B range: the block as the right
+//                                     /  factor (row bitmaps over columns)
+// R = rows, C = columns of that orientation, W = (C >> 5) + 1 words per row;
+// bits[(k - 1) * W + w] covers columns 32w .. 32w + 31 of row k and base is
+// the entry index of its first set bit.  Image 2p is P(a, b) of pair p,
+// image 2p + 1 its transpose.
+struct ImgLayout {
+  int64_t rp, vals, bits, end;  // byte offsets (cols at 0)
+};
+__host__ __device__ inline int64_t mlp_align16(int64_t v) { return (v + 15) & ~(int64_t)15; }
+__host__ __device__ inline ImgLayout img_layout(int rows, int cols, int64_t nnz) {
+  ImgLayout l;
+  l.rp = mlp_align16(2 * nnz);
+  l.vals = mlp_align16(l.rp + 2 * (int64_t)(rows + 2));
+  l.bits = mlp_align16(l.vals + 4 * nnz);
+  l.end = l.bits + 8 * (int64_t)rows * ((cols >> 5) + 1);
+  return l;
 }
 struct PackArgs {
   int n;
@@ -231,7 +243,6 @@ struct PackArgs {
   const int64_t* img_off;    // 2P + 1 byte offsets
   uint8_t* img;
   int64_t nimg;              // 2P
-  int threads;               // workgroup size of k_relax_pair (mask word offsets)
 };
 struct PairRelaxArgs {
   int n;
@@ -246,14 +257,16 @@ struct PairRelaxArgs {
   const int64_t* pairs;      // output pairs, one workgroup each
   int64_t npairs;
   float* out;                // raw relaxed values at the input entry slots
-  int img_cap;               // LDS bytes per staged image (multiple of 16)
-  int mask_words;            // bitmap words per output row: (max L >> 5) + 1
-  int acc_cap;               // accumulator slots (max nnz of an output pair)
+  int cap_a, cap_b;          // LDS bytes for the staged A and B ranges (multiples of 16)
+  int max_len;               // longest sequence (task-prefix scratch)
 };
-size_t pair_relax_lds(int threads, int img_cap, int mask_words, int acc_cap);
-int pair_relax_prefetch(int threads, int img_cap);   // chunks per thread, 0 = too large
+constexpr int kRelaxThreads = 512;   // workgroup of the pair-resident relaxation
+constexpr int kRelaxCells = 4;       // mask cells of one row per task
+size_t pair_relax_lds(int cap_a, int cap_b, int max_len);
+int pair_relax_prefetch(int cap);              // 16-byte chunks per thread, 0 = too large
+int pair_relax_slots(int64_t tasks);           // tasks per thread, 0 = too many
 hipError_t launch_pack(const PackArgs& a, hipStream_t st);
-hipError_t launch_relax_pairs(const PairRelaxArgs& a, int threads, hipStream_t st);
+hipError_t launch_relax_pairs(const PairRelaxArgs& a, int slots, hipStream_t st);
 hipError_t launch_transpose(const TransposeArgs& a, hipStream_t st);
 hipError_t launch_relax_tasks(const RelaxArgs& a, hipStream_t st);
 hipError_t launch_filter(const FilterArgs& a, hipStream_t st);

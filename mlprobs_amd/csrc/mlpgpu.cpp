@@ -1189,44 +1189,55 @@ int mlp_relax(mlp_ctx* c, int iters) {
       HIPCHK(c, launch_transpose(ta, c->stream));
     }
     // Pair-resident path (k_relax_pair) for every output pair whose blocks fit
-    // the LDS images; the row-task kernel for the rest (MLP_RELAX=tasks: all).
+    // the LDS ranges; the row-task kernel for the rest (MLP_RELAX=tasks: all).
     const int64_t LDS_MAX = 160 * 1024;
     const char* mode = getenv("MLP_RELAX");
-    const bool tasks_only = (mode && !strcmp(mode, "tasks")) || c->max_len > 1023;
-    const int threads = 64 * ((c->max_len + 63) / 64);
-    const int mask_words = (c->max_len >> 5) + 1;
-    std::vector<int64_t> img_off(2 * c->P + 1, 0);
-    int64_t img_max = 0;
+    const bool tasks_only = (mode && !strcmp(mode, "tasks")) || c->max_len > 65000;
+    std::vector<int64_t> img_off(2 * c->P + 1, 0), rng_a(2 * c->P), rng_b(2 * c->P);
+    int64_t max_a = 0, max_b = 0;
     for (int64_t p = 0; p < c->P; p++) {
       const int64_t nz = c->ent_off[p + 1] - c->ent_off[p];
-      const int64_t s0 = img_bytes(c->lens[c->pa[p]], nz), s1 = img_bytes(c->lens[c->pb[p]], nz);
-      img_off[2 * p + 1] = img_off[2 * p] + s0;
-      img_off[2 * p + 2] = img_off[2 * p + 1] + s1;
-      if (nz < 65536) img_max = std::max(img_max, std::max(s0, s1));
+      const int La = c->lens[c->pa[p]], Lb = c->lens[c->pb[p]];
+      const ImgLayout l0 = img_layout(La, Lb, nz), l1 = img_layout(Lb, La, nz);
+      img_off[2 * p + 1] = img_off[2 * p] + mlp_align16(l0.end);
+      img_off[2 * p + 2] = img_off[2 * p + 1] + mlp_align16(l1.end);
+      rng_a[2 * p] = l0.bits;
+      rng_a[2 * p + 1] = l1.bits;
+      rng_b[2 * p] = mlp_align16(l0.end - l0.vals);
+      rng_b[2 * p + 1] = mlp_align16(l1.end - l1.vals);
+      if (nz < 65536) {
+        max_a = std::max(max_a, std::max(rng_a[2 * p], rng_a[2 * p + 1]));
+        max_b = std::max(max_b, std::max(rng_b[2 * p], rng_b[2 * p + 1]));
+      }
     }
-    int64_t acc_cap = 0;
-    for (int64_t p = r0; p < r1; p++) acc_cap = std::max(acc_cap, c->ent_off[p + 1] - c->ent_off[p]);
-    acc_cap = std::min<int64_t>(acc_cap, 16384);
-    const int64_t fixed = pair_relax_lds(threads, 0, mask_words, (int)acc_cap);
-    int64_t img_cap = std::min<int64_t>(img_max, (LDS_MAX - fixed) / 2) & ~(int64_t)15;
-    while (img_cap > 0 && !pair_relax_prefetch(threads, (int)img_cap)) img_cap -= 16 * threads;
+    if (img_off[2 * c->P] >= (1LL << 36)) max_a = max_b = 0;  // z schedule holds offsets / 16 in 32 bits
+    // LDS split: A ranges are smaller; never more than the prefetch registers hold
+    const int64_t reg_cap = 16LL * 16 * kRelaxThreads;
+    const int64_t room = LDS_MAX - (int64_t)pair_relax_lds(0, 0, c->max_len);
+    int64_t cap_a = std::min({max_a, reg_cap, room / 3}) & ~(int64_t)15;
+    int64_t cap_b = std::min({max_b, reg_cap, room - cap_a}) & ~(int64_t)15;
     std::vector<char> big(c->n, 0);
     for (int64_t p = 0; p < c->P; p++) {
       const int64_t nz = c->ent_off[p + 1] - c->ent_off[p];
-      if (nz >= 65536 || img_off[2 * p + 2] - img_off[2 * p + 1] > img_cap ||
-          img_off[2 * p + 1] - img_off[2 * p] > img_cap)
-        big[c->pa[p]] = big[c->pb[p]] = 1;
+      bool b = nz >= 65536;
+      for (int o = 0; o < 2; o++) b = b || rng_a[2 * p + o] > cap_a || rng_b[2 * p + o] > cap_b;
+      if (b) big[c->pa[p]] = big[c->pb[p]] = 1;
     }
     std::vector<int64_t> fast, tp;
     std::vector<int32_t> tr;
+    int64_t max_tasks = 0;
     for (int64_t p = r0; p < r1; p++) {
       const int64_t nz = c->ent_off[p + 1] - c->ent_off[p];
       if (nz == 0) continue;  // empty mask: the filter writes an empty block
-      if (!tasks_only && img_cap > 0 && !big[c->pa[p]] && !big[c->pb[p]] && nz <= acc_cap) {
+      // tasks = sum over rows of ceil(cells / kRelaxCells) <= nz / kRelaxCells + rows
+      const int La = c->lens[c->pa[p]];
+      const int64_t tasks_bound = nz / kRelaxCells + La;
+      if (!tasks_only && cap_a > 0 && cap_b > 0 && !big[c->pa[p]] && !big[c->pb[p]] &&
+          pair_relax_slots(tasks_bound)) {
         fast.push_back(p);
+        max_tasks = std::max(max_tasks, tasks_bound);
         continue;
       }
-      const int La = c->lens[c->pa[p]];
       for (int g = 1; g <= La; g += 64) {
         tp.push_back(p);
         tr.push_back(g);
@@ -1255,7 +1266,6 @@ int mlp_relax(mlp_ctx* c, int iters) {
       pk.img_off = (const int64_t*)c->r_imgoff.p;
       pk.img = (uint8_t*)c->r_img.p;
       pk.nimg = 2 * c->P;
-      pk.threads = threads;
       Timer t(c, KTRANS, total);
       HIPCHK(c, launch_pack(pk, c->stream));
     }
@@ -1299,12 +1309,12 @@ int mlp_relax(mlp_ctx* c, int iters) {
     pr.pairs = (const int64_t*)c->r_fast.p;
     pr.npairs = (int64_t)fast.size();
     pr.out = (float*)c->r_raw.p;
-    pr.img_cap = (int)img_cap;
-    pr.mask_words = mask_words;
-    pr.acc_cap = (int)acc_cap;
+    pr.cap_a = (int)cap_a;
+    pr.cap_b = (int)cap_b;
+    pr.max_len = c->max_len;
     {
       Timer t(c, KRELAX, c->ent_off[r1] - c->ent_off[r0]);
-      HIPCHK(c, launch_relax_pairs(pr, threads, c->stream));
+      HIPCHK(c, launch_relax_pairs(pr, pair_relax_slots(max_tasks), c->stream));
       HIPCHK(c, launch_relax_tasks(ra, c->stream));
     }
     // filter: count, host scan, write

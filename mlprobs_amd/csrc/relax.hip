@@ -19,6 +19,8 @@
 #include "mlp_kernels.h"
 #include "mlp_numerics.h"
 
+#include <algorithm>
+
 namespace mlp {
 
 __device__ __forceinline__ int64_t pair_index(int n, int a, int b) {  // a < b
@@ -216,8 +218,9 @@ __global__ __launch_bounds__(256) void k_filter(FilterArgs A) {
 }
 
 // ------------------------------------------------------------ block images
-// One wave per image: copy the block (or its transpose) into the packed
-// layout of mlp_kernels.h (img_ent_off / img_bytes).
+// One wave per image: the block (or its transpose) in the layout of
+// mlp_kernels.h (img_layout): CSR for the left-factor role, row bitmaps with
+// per-word entry bases for the right-factor role.
 __global__ __launch_bounds__(256) void k_pack(PackArgs A) {
   const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (q >= A.nimg) return;
@@ -230,170 +233,273 @@ __global__ __launch_bounds__(256) void k_pack(PackArgs A) {
   while (r >= n - 1 - a) { r -= n - 1 - a; ++a; }
   const int b = a + 1 + (int)r;
   const int rows = tr ? A.lens[b] : A.lens[a];
+  const int ncol = tr ? A.lens[a] : A.lens[b];
+  const int W = (ncol >> 5) + 1;
   const int64_t e0 = A.ent_off[p];
   const int64_t nnz = A.ent_off[p + 1] - e0;
   const int32_t* rp = tr ? A.trowptr + A.trp_off[p] : A.rowptr + A.rp_off[p];
   const uint16_t* cols = (tr ? A.tcols : A.cols) + e0;
   const float* vals = (tr ? A.tvals : A.vals) + e0;
+  const ImgLayout L = img_layout(rows, ncol, nnz);
   uint8_t* dst = A.img + A.img_off[q];
-  uint16_t* drp = (uint16_t*)dst;
-  uint2* dent = (uint2*)(dst + img_ent_off(rows));
-  const uint32_t wstride = (uint32_t)A.threads * 8;
+  uint16_t* dcols = (uint16_t*)dst;
+  uint16_t* drp = (uint16_t*)(dst + L.rp);
+  float* dvals = (float*)(dst + L.vals);
+  uint2* dbits = (uint2*)(dst + L.bits);
   for (int k = lane; k < rows + 2; k += 64) drp[k] = (uint16_t)rp[k];
   for (int64_t e = lane; e < nnz; e += 64) {
-    const uint32_t c = cols[e];
-    dent[e] = make_uint2(c | (((c >> 5) * wstride) << 10), __float_as_uint(vals[e]));
+    dcols[e] = cols[e];
+    dvals[e] = vals[e];
+  }
+  // row bitmaps: lane per row, words in column order
+  for (int k = lane + 1; k <= rows; k += 64) {
+    int e = rp[k];
+    const int re = rp[k + 1];
+    for (int w = 0; w < W; ++w) {
+      uint32_t bits = 0;
+      const int base = e;
+      while (e < re && (cols[e] >> 5) == w) {
+        bits |= 1u << (cols[e] & 31);
+        ++e;
+      }
+      dbits[(int64_t)(k - 1) * W + w] = make_uint2(bits, (uint32_t)base);
+    }
   }
 }
 
 // ------------------------------------------------- pair-resident relaxation
-// One workgroup per output pair (x, y), one thread per row i of x.  For each
-// z (ascending) the workgroup stages A_z = P(x, z) and B_z = P(z, y) as block
-// images in LDS (the next z's images are prefetched into registers while the
-// current z is computed), and thread i walks A_z row i (k ascending) and each
-// B_z row k, adding a * b into the accumulator of output cell (i, j) when
-// (i, j) is in the mask (the pattern of P_xy, CPNP/MSA.cpp:1237-1261).  The
-// per-cell order is therefore z ascending, then k ascending -- the order of
-// Relax / Relax1 (CPNP/MSA.cpp:1276-1350) -- and every sum is bit-identical
-// (the adds are ds_add_f32, IEEE round-to-nearest like the host's float +=;
-// one lane's LDS operations complete in issue order).
-//
-// The mask of row i is a bitmap over j, one 64-bit element per 32 columns:
-// low half the bits, high half the accumulator slot of the word's first set
-// bit; word-major (word w of thread t at w * threads + t), so a wave's mask
-// reads never share a bank.  A hit's slot is that base plus the popcount of
-// the lower bits.  Accumulators are the pair's entry slots, in LDS.
+// One workgroup per output pair (x, y).  The output cells (the mask: the
+// pattern of P_xy, CPNP/MSA.cpp:1237-1261) are cut into tasks of up to four
+// cells of one row i; a thread owns a few tasks, their accumulators live in
+// registers.  For each z (ascending) the workgroup stages A_z = P(x, z) (CSR)
+// and B_z = P(z, y) (row bitmaps) in LDS -- the next z's ranges are
+// prefetched into registers while the current z is computed -- and a task
+// walks A_z row i (k ascending), looking its cells' columns j up in the
+// bitmap of B_z row k.  Each cell's sum therefore runs z ascending, then k
+// ascending: the order of Relax / Relax1 (CPNP/MSA.cpp:1276-1350), so every
+// float sum is bit-identical to the reference's.
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));  // plain vector: stays in VGPRs
-
-size_t pair_relax_lds(int threads, int img_cap, int mask_words, int acc_cap) {
-  return 2 * (size_t)img_cap + (size_t)mask_words * threads * 8 + 4 * (size_t)acc_cap;
+constexpr int kRelaxZChunk = 256;  // z schedule entries per LDS fill
+static __host__ __device__ inline size_t relax_tp_bytes(int max_len) {
+  return (4 * (size_t)(max_len + 2) + 15) & ~(size_t)15;
 }
 
-int pair_relax_prefetch(int threads, int img_cap) {
-  const int chunks = (img_cap / 16 + threads - 1) / threads;
+size_t pair_relax_lds(int cap_a, int cap_b, int max_len) {
+  return (size_t)cap_a + (size_t)cap_b + relax_tp_bytes(max_len) + 16 * kRelaxZChunk;
+}
+
+int pair_relax_prefetch(int cap) {
+  const int chunks = (cap / 16 + kRelaxThreads - 1) / kRelaxThreads;
   for (int kp : {1, 2, 4, 8, 16})
     if (chunks <= kp) return kp;
   return 0;
 }
 
-template <int KP>
-__global__ __launch_bounds__(1024) void k_relax_pair(PairRelaxArgs A) {
+int pair_relax_slots(int64_t tasks) {
+  const int64_t per = (tasks + kRelaxThreads - 1) / kRelaxThreads;
+  for (int sl : {1, 2, 4, 8})
+    if (per <= sl) return sl;
+  return 0;
+}
+
+template <int KP, int SL>
+__global__ __launch_bounds__(kRelaxThreads) void k_relax_pair(PairRelaxArgs A) {
   extern __shared__ __align__(16) uint8_t lds[];
-  const int nt = blockDim.x;
+  constexpr int nt = kRelaxThreads;
+  constexpr int NC = kRelaxCells;
   const int tid = threadIdx.x;
   const int64_t p = A.pairs[blockIdx.x];
   const int n = A.n;
   const int64_t exy = A.ent_off[p];
-  const int64_t nxy = A.ent_off[p + 1] - exy;
-  if (nxy == 0) return;  // empty mask: nothing survives
+  if (A.ent_off[p + 1] == exy) return;  // empty mask: nothing survives
   int x = 0;
   int64_t q = p;
   while (q >= n - 1 - x) { q -= n - 1 - x; ++x; }
   const int y = x + 1 + (int)q;
-  const int Lx = A.lens[x];
-  const int mw = A.mask_words;
+  const int Lx = A.lens[x], Ly = A.lens[y];
+  const int W = (Ly >> 5) + 1;
   uint8_t* sA = lds;
-  uint8_t* sB = lds + A.img_cap;
-  uint2* mask = (uint2*)(lds + 2 * A.img_cap);
-  float* acc = (float*)(mask + (size_t)mw * nt);
+  uint8_t* sB = lds + A.cap_a;
+  int32_t* tp = (int32_t*)(lds + A.cap_a + A.cap_b);  // tasks before row i
 
-  // mask bitmap, slot bases and the z = x, z = y term (CPNP/MSA.cpp:1211-1213)
-  const int i = tid + 1;
+  // tasks: row i contributes ceil(m_i / NC); prefix by wave 0
   const int32_t* rpxy = A.rowptr + A.rp_off[p];
-  int mb = 0, me = 0;
-  if (i <= Lx) { mb = rpxy[i]; me = rpxy[i + 1]; }
-  for (int w = 0; w < mw; ++w) mask[w * nt + tid].x = 0;
-  for (int e = mb; e < me; ++e) {
-    const int j = A.cols[exy + e];
-    mask[(j >> 5) * nt + tid].x |= 1u << (j & 31);
-    const float v = A.vals[exy + e];
-    acc[e] = v + v;
-  }
-  {
-    int run = mb;
-    for (int w = 0; w < mw; ++w) {
-      mask[w * nt + tid].y = (uint32_t)run;
-      run += __popc(mask[w * nt + tid].x);
+  if (tid < 64) {
+    int run = 0;
+    if (tid == 0) tp[1] = 0;
+    for (int r0 = 1; r0 <= Lx; r0 += 64) {
+      const int i = r0 + tid;
+      const int c = i <= Lx ? (rpxy[i + 1] - rpxy[i] + NC - 1) / NC : 0;
+      int xs = c;
+      for (int off = 1; off < 64; off <<= 1) {
+        const int v = __shfl_up(xs, off);
+        if (tid >= off) xs += v;
+      }
+      if (i <= Lx) tp[i + 1] = run + xs;
+      run += __shfl(xs, 63);
     }
   }
-  const bool active = me > mb;
-  const uint8_t* mbase = (const uint8_t*)mask + tid * 8;
-
-  // images of A_z = P(x, z) and B_z = P(z, y); false when either is empty
-  auto images = [&](int z, int64_t& qa, int64_t& qb) -> bool {
-    int64_t pa, pb;
-    if (z > x) { pa = pair_index(n, x, z); qa = 2 * pa; } else { pa = pair_index(n, z, x); qa = 2 * pa + 1; }
-    if (z < y) { pb = pair_index(n, z, y); qb = 2 * pb; } else { pb = pair_index(n, y, z); qb = 2 * pb + 1; }
-    return A.ent_off[pa + 1] > A.ent_off[pa] && A.ent_off[pb + 1] > A.ent_off[pb];
-  };
-  auto next_z = [&](int z, int64_t& qa, int64_t& qb) -> int {
-    for (++z; z < n; ++z)
-      if (z != x && z != y && images(z, qa, qb)) return z;
-    return n;
-  };
-  // register prefetch of the next z's images (written out, not in lambdas:
-  // arrays captured by reference end up in scratch)
-  u32x4 ra[KP], rb[KP];
-  int na = 0, nb = 0;  // 16-byte chunks of the prefetched images
-  int64_t qa, qb;
-  int z = next_z(-1, qa, qb);
-  int Lz_next = z < n ? A.lens[z] : 0;
-#define MLP_ISSUE()                                                          \
-  {                                                                          \
-    const u32x4* ga = (const u32x4*)(A.img + A.img_off[qa]);                 \
-    const u32x4* gb = (const u32x4*)(A.img + A.img_off[qb]);                 \
-    na = (int)((A.img_off[qa + 1] - A.img_off[qa]) >> 4);                    \
-    nb = (int)((A.img_off[qb + 1] - A.img_off[qb]) >> 4);                    \
-    _Pragma("unroll") for (int m = 0; m < KP; ++m) {                         \
-      const int c = tid + m * nt;                                            \
-      ra[m] = ga[min(c, na - 1)];                                            \
-      rb[m] = gb[min(c, nb - 1)];                                            \
-    }                                                                        \
+  __syncthreads();
+  const int ntask = tp[Lx + 1];
+  int ti[SL];           // row of each task (0 = no task)
+  uint32_t wo[SL][NC];  // byte offset of the cell's word in a bitmap row
+  uint32_t bm[SL][NC];  // the cell's bit (0 = no cell: never hits)
+  float acc[SL][NC];
+#pragma unroll
+  for (int s = 0; s < SL; ++s) {
+    const int g = tid + s * nt;
+    ti[s] = 0;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) { wo[s][c] = 0; bm[s][c] = 0; acc[s][c] = 0.f; }
+    if (g < ntask) {
+      int lo = 1, hi = Lx;  // last row with tp[row] <= g
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (tp[mid] <= g) lo = mid; else hi = mid - 1;
+      }
+      ti[s] = lo;
+      const int e0 = rpxy[lo] + NC * (g - tp[lo]), e1 = rpxy[lo + 1];
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+        if (e0 + c < e1) {
+          const uint32_t j = A.cols[exy + e0 + c];
+          wo[s][c] = (j >> 5) * 8;
+          bm[s][c] = 1u << (j & 31);
+          const float v = A.vals[exy + e0 + c];
+          acc[s][c] = v + v;  // z = x and z = y (CPNP/MSA.cpp:1211-1213)
+        }
+    }
   }
-  if (z < n) MLP_ISSUE();
-  while (z < n) {
+  if (tid == 0) tp[0] = 0;  // tp[0] (unused by the scan) doubles as a 0.0f for misses
+  const float* zero = (const float*)tp;
+
+  // The z schedule, ZC values of z at a time, in LDS: per z the 16-byte
+  // offsets of the A_z range (P(x, z)) and the B_z range (P(z, y)), both
+  // blocks' entry counts and L_z; nnz 0 marks a z to skip (z = x, z = y or
+  // an empty block).  Filling it costs one memory round trip per ZC values
+  // of z instead of one per z.
+  uint4* ztab = (uint4*)(lds + A.cap_a + A.cap_b + relax_tp_bytes(A.max_len));
+  int zbase = 0, zpos = -1;
+  auto fill = [&]() {
+    __syncthreads();  // every wave is done reading the previous chunk
+    if (tid < kRelaxZChunk) {
+      const int z = zbase + tid;
+      uint4 e = make_uint4(0, 0, 0, 0);
+      if (z < n && z != x && z != y) {
+        int64_t pa, pb, qa, qb;
+        if (z > x) { pa = pair_index(n, x, z); qa = 2 * pa; } else { pa = pair_index(n, z, x); qa = 2 * pa + 1; }
+        if (z < y) { pb = pair_index(n, z, y); qb = 2 * pb; } else { pb = pair_index(n, y, z); qb = 2 * pb + 1; }
+        const int na = (int)(A.ent_off[pa + 1] - A.ent_off[pa]);
+        const int nb = (int)(A.ent_off[pb + 1] - A.ent_off[pb]);
+        if (na > 0 && nb > 0) {
+          const int Lz = A.lens[z];
+          const ImgLayout lb = img_layout(Lz, Ly, nb);
+          e = make_uint4((uint32_t)(A.img_off[qa] >> 4), (uint32_t)((A.img_off[qb] + lb.vals) >> 4),
+                         (uint32_t)na | ((uint32_t)nb << 16), (uint32_t)Lz);
+        }
+      }
+      ztab[tid] = e;
+    }
+    __syncthreads();
+  };
+  // next scheduled z (uniform across the workgroup); .z == 0 when done
+  auto next = [&]() -> uint4 {
+    for (;;) {
+      if (++zpos == kRelaxZChunk) {
+        zbase += kRelaxZChunk;
+        if (zbase >= n) return make_uint4(0, 0, 0, 0);
+        zpos = 0;
+        fill();
+      }
+      if (zbase + zpos >= n) return make_uint4(0, 0, 0, 0);
+      const uint4 e = ztab[zpos];
+      if (e.z) return e;
+    }
+  };
+  // register prefetch of the next z's ranges (written out: arrays captured
+  // by reference in a lambda end up in scratch)
+  u32x4 ra[KP], rb[KP];
+  int ca = 0, cb = 0;  // 16-byte chunks of the prefetched ranges
+  fill();
+  uint4 en = next();
+#define MLP_ISSUE()                                                                    \
+  {                                                                                    \
+    const int Lz_ = (int)en.w, na_ = (int)(en.z & 0xffff), nb_ = (int)(en.z >> 16);   \
+    const ImgLayout la = img_layout(Lx, Lz_, na_), lb = img_layout(Lz_, Ly, nb_);      \
+    const u32x4* ga = (const u32x4*)(A.img + ((int64_t)en.x << 4));                    \
+    const u32x4* gb = (const u32x4*)(A.img + ((int64_t)en.y << 4));                    \
+    ca = (int)(la.bits >> 4);                                                          \
+    cb = (int)((lb.end - lb.vals + 15) >> 4);                                          \
+    _Pragma("unroll") for (int m = 0; m < KP; ++m) {                                   \
+      const int c = tid + m * nt;                                                      \
+      ra[m] = ga[min(c, ca - 1)];                                                      \
+      rb[m] = gb[min(c, cb - 1)];                                                      \
+    }                                                                                  \
+  }
+  if (en.z) MLP_ISSUE();
+#ifdef MLP_RELAX_NOSTAGE
+  const uint4 e0 = en;
+#endif
+  while (en.z) {
 #pragma unroll
     for (int m = 0; m < KP; ++m) {
       const int c = tid + m * nt;
-      if (c < na) ((u32x4*)sA)[c] = ra[m];
-      if (c < nb) ((u32x4*)sB)[c] = rb[m];
+      if (c < ca) ((u32x4*)sA)[c] = ra[m];
+      if (c < cb) ((u32x4*)sB)[c] = rb[m];
     }
     __syncthreads();
-    const int Lz = Lz_next;
-    z = next_z(z, qa, qb);
-    Lz_next = z < n ? A.lens[z] : 0;
-    if (z < n) MLP_ISSUE();
-#ifdef MLP_RELAX_NOCOMPUTE
-    if (false) {
+#ifdef MLP_RELAX_NOSTAGE  // timing experiment: every z computes on the first z's images
+    const int Lz = (int)e0.w, nzA = (int)(e0.z & 0xffff), nzB = (int)(e0.z >> 16);
+    en = next();
+    ca = cb = 0;
 #else
-    if (active) {
+    const int Lz = (int)en.w, nzA = (int)(en.z & 0xffff), nzB = (int)(en.z >> 16);
+    en = next();
+    if (en.z) MLP_ISSUE();
 #endif
-      const uint16_t* Arp = (const uint16_t*)sA;
-      const uint2* Aent = (const uint2*)(sA + img_ent_off(Lx));
-      const uint16_t* Brp = (const uint16_t*)sB;
-      const uint2* Bent = (const uint2*)(sB + img_ent_off(Lz));
-      const int a0 = Arp[i], a1 = Arp[i + 1];
-      for (int t = a0; t < a1; ++t) {
-        const uint2 ea = Aent[t];
-        const int k = ea.x & 1023;
-        const float av = __uint_as_float(ea.y);
-        const int b0 = Brp[k], b1 = Brp[k + 1];
-        // four entries of B_z row k at a time: distinct columns, so their
-        // updates are independent; the groups stay in k order
-        for (int u = b0; u < b1; u += 4) {
-          uint2 eb[4], mk[4];
+    {
+      const ImgLayout la = img_layout(Lx, Lz, nzA), lb = img_layout(Lz, Ly, nzB);
+      const uint16_t* Acols = (const uint16_t*)sA;
+      const uint16_t* Arp = (const uint16_t*)(sA + la.rp);
+      const float* Avals = (const float*)(sA + la.vals);
+      const float* Bvals = (const float*)sB;
+      const uint8_t* Bbits = sB + (lb.bits - lb.vals) - 8 * W;  // row k at k * W words
+      const uint32_t W8 = 8 * W;
 #pragma unroll
-          for (int g = 0; g < 4; ++g) eb[g] = Bent[min(u + g, b1 - 1)];
+      for (int s = 0; s < SL; ++s) {
+#ifdef MLP_RELAX_NOCOMPUTE
+        continue;
+#endif
+        if (ti[s] == 0) continue;
+        const int a0 = Arp[ti[s]], a1 = Arp[ti[s] + 1];
+        // two A entries per iteration (the second a zero-weight copy of the
+        // first past the row end: + 0.0f leaves a positive sum unchanged)
+        for (int t = a0; t < a1; t += 2) {
+          const bool two = t + 1 < a1;
+          const int k0 = Acols[t], k1 = Acols[two ? t + 1 : t];
+          const float av0 = Avals[t];
+          const float av1 = two ? Avals[t + 1] : 0.f;
+          const uint8_t* r0 = Bbits + __umul24(k0, W8);
+          const uint8_t* r1 = Bbits + __umul24(k1, W8);
+          uint2 w0[NC], w1[NC];
 #pragma unroll
-          for (int g = 0; g < 4; ++g) mk[g] = *(const uint2*)(mbase + (eb[g].x >> 10));
+          for (int c = 0; c < NC; ++c) {
+            w0[c] = *(const uint2*)(r0 + wo[s][c]);
+            w1[c] = *(const uint2*)(r1 + wo[s][c]);
+          }
+          float b0[NC], b1[NC];
 #pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const uint32_t sh = eb[g].x & 31;
-            if (u + g < b1 && ((mk[g].x >> sh) & 1u)) {
-              const uint32_t slot = mk[g].y + __popc(mk[g].x & ((1u << sh) - 1u));
-              __hip_atomic_fetch_add(acc + slot, av * __uint_as_float(eb[g].y), __ATOMIC_RELAXED,
-                                     __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
+          for (int c = 0; c < NC; ++c) {
+            const uint32_t below = bm[s][c] - 1u;
+            const uint32_t i0 = w0[c].y + __popc(w0[c].x & below);
+            const uint32_t i1 = w1[c].y + __popc(w1[c].x & below);
+            b0[c] = *((w0[c].x & bm[s][c]) ? Bvals + i0 : zero);
+            b1[c] = *((w1[c].x & bm[s][c]) ? Bvals + i1 : zero);
+          }
+#pragma unroll
+          for (int c = 0; c < NC; ++c) {
+            acc[s][c] += av0 * b0[c];  // a miss adds av * 0 = +0: no change
+            acc[s][c] += av1 * b1[c];
           }
         }
       }
@@ -401,8 +507,16 @@ __global__ __launch_bounds__(1024) void k_relax_pair(PairRelaxArgs A) {
     __syncthreads();
   }
 #undef MLP_ISSUE
-  const float fn = (float)n;
-  for (int e = mb; e < me; ++e) A.out[exy + e] = acc[e] / fn;  // CPNP/MSA.cpp:1233-1235
+  const float fn = (float)n;  // CPNP/MSA.cpp:1233-1235
+#pragma unroll
+  for (int s = 0; s < SL; ++s) {
+    const int g = tid + s * nt;
+    if (ti[s] == 0) continue;
+    const int e0 = rpxy[ti[s]] + NC * (g - tp[ti[s]]);
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+      if (bm[s][c]) A.out[exy + e0 + c] = acc[s][c] / fn;
+  }
 }
 
 hipError_t launch_pack(const PackArgs& a, hipStream_t st) {
@@ -411,28 +525,38 @@ hipError_t launch_pack(const PackArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
-hipError_t launch_relax_pairs(const PairRelaxArgs& a, int threads, hipStream_t st) {
-  if (a.npairs <= 0) return hipSuccess;
-  const size_t lds = pair_relax_lds(threads, a.img_cap, a.mask_words, a.acc_cap);
-  const int kp = pair_relax_prefetch(threads, a.img_cap);
-  const dim3 grid((unsigned)a.npairs), block((unsigned)threads);
-  switch (kp) {
-#define MLP_RELAX_CASE(K)                                                                    \
-  case K:                                                                                    \
-    hipFuncSetAttribute((const void*)k_relax_pair<K>, hipFuncAttributeMaxDynamicSharedMemorySize, \
-                        (int)lds);                                                           \
-    hipLaunchKernelGGL(k_relax_pair<K>, grid, block, lds, st, a);                            \
+template <int KP>
+static hipError_t launch_relax_kp(const PairRelaxArgs& a, int slots, size_t lds, hipStream_t st) {
+  const dim3 grid((unsigned)a.npairs), block(kRelaxThreads);
+  switch (slots) {
+#define MLP_RELAX_CASE(SL)                                                                  \
+  case SL:                                                                                  \
+    hipFuncSetAttribute((const void*)k_relax_pair<KP, SL>,                                  \
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);              \
+    hipLaunchKernelGGL((k_relax_pair<KP, SL>), grid, block, lds, st, a);                    \
     break;
     MLP_RELAX_CASE(1)
     MLP_RELAX_CASE(2)
     MLP_RELAX_CASE(4)
     MLP_RELAX_CASE(8)
-    MLP_RELAX_CASE(16)
 #undef MLP_RELAX_CASE
     default:
       return hipErrorInvalidValue;
   }
   return hipGetLastError();
+}
+
+hipError_t launch_relax_pairs(const PairRelaxArgs& a, int slots, hipStream_t st) {
+  if (a.npairs <= 0) return hipSuccess;
+  const size_t lds = pair_relax_lds(a.cap_a, a.cap_b, a.max_len);
+  switch (pair_relax_prefetch(std::max(a.cap_a, a.cap_b))) {
+    case 1: return launch_relax_kp<1>(a, slots, lds, st);
+    case 2: return launch_relax_kp<2>(a, slots, lds, st);
+    case 4: return launch_relax_kp<4>(a, slots, lds, st);
+    case 8: return launch_relax_kp<8>(a, slots, lds, st);
+    case 16: return launch_relax_kp<16>(a, slots, lds, st);
+    default: return hipErrorInvalidValue;
+  }
 }
 
 hipError_t launch_transpose(const TransposeArgs& a, hipStream_t st) {
