@@ -207,10 +207,14 @@ std::vector<float> build_posterior(const Profile& A, const Profile& B, const Spa
   if (weights)
     for (const Row& x : A)
       for (const Row& y : B) total += weights[x.label] * weights[y.label];
+  std::vector<std::vector<int>> m2s;
+  m2s.reserve(B.size());
+  for (const Row& y : B) m2s.push_back(mapping(y));
   for (const Row& x : A) {
     const std::vector<int> m1 = mapping(x);
-    for (const Row& y : B) {
-      const std::vector<int> m2 = mapping(y);
+    for (size_t yb = 0; yb < B.size(); yb++) {
+      const Row& y = B[yb];
+      const std::vector<int>& m2 = m2s[yb];
       const int first = x.label, second = y.label;
       const float w = weights ? (float)(weights[first] * weights[second]) / total : 1.f;
       const int lo = std::min(first, second), hi = std::max(first, second);
@@ -219,19 +223,27 @@ std::vector<float> build_posterior(const Profile& A, const Profile& B, const Spa
       const uint16_t* cols = sp.cols.data() + sp.ent_off[p];
       const float* vals = sp.vals.data() + sp.ent_off[p];
       const int rows = sp.lens[lo], ncols = sp.lens[hi];
+      // the reference subtracts the cutoff from every cell of the pair
+      // (ProbabilisticModel.h:1229-1283); x - 0.0f == x for every value the
+      // sums take (no -0.0: they start at +0 and add non-negative terms), so
+      // with the default cutoff 0 that O(L1 L2) sweep is skipped exactly
+      const float sub = weights ? w * cutoff : cutoff;
+      const bool do_sub = sub != 0.f;
       if (first < second) {
         for (int ii = 1; ii <= rows; ii++) {
           const int64_t base = (int64_t)m1[ii] * W2;
           for (int32_t e = rp[ii]; e < rp[ii + 1]; e++)
             post[base + m2[cols[e]]] += weights ? w * vals[e] : vals[e];
-          for (int jj = 0; jj < ncols; jj++) post[base + m2[jj]] -= weights ? w * cutoff : cutoff;
+          if (do_sub)
+            for (int jj = 0; jj < ncols; jj++) post[base + m2[jj]] -= sub;
         }
       } else {
         for (int jj = 1; jj <= rows; jj++) {
           const int64_t base = m2[jj];
           for (int32_t e = rp[jj]; e < rp[jj + 1]; e++)
             post[base + (int64_t)m1[cols[e]] * W2] += weights ? w * vals[e] : vals[e];
-          for (int ii = 0; ii < ncols; ii++) post[base + (int64_t)m1[ii] * W2] -= weights ? w * cutoff : cutoff;
+          if (do_sub)
+            for (int ii = 0; ii < ncols; ii++) post[base + (int64_t)m1[ii] * W2] -= sub;
         }
       }
     }

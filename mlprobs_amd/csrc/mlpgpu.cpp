@@ -83,7 +83,7 @@ struct mlp_ctx {
   size_t scratch_budget = 0;
   // relaxation buffers
   DevBuf r_trowptr, r_tcols, r_tvals, r_raw, r_newrp, r_newcols, r_newvals, r_tasks_p, r_tasks_r,
-      r_pairs, r_nnz, r_newoff, r_img, r_imgoff, r_fast;
+      r_pairs, r_nnz, r_newoff, r_img, r_imgoff, r_tiles, r_nwords;
   // comm
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
@@ -247,6 +247,10 @@ static void build_tables(Tables& T, ModelScalars& ms, float delta) {
   ms.vit_init[2] = logf(0.1959836632f);
 }
 
+static inline int64_t pair_index_host(int n, int a, int b) {  // a < b, row-major
+  return (int64_t)a * n - (int64_t)a * (a + 1) / 2 + (b - a - 1);
+}
+
 static int pair_cost_cells(const mlp_ctx* c, int64_t p) {
   return (c->lens[c->pa[p]] + 1) * (c->lens[c->pb[p]] + 1);
 }
@@ -294,7 +298,7 @@ void mlp_ctx_destroy(mlp_ctx* c) {
     if (p) hipFree(p);
   DevBuf* bufs[] = {&c->scratch, &c->r_trowptr, &c->r_tcols, &c->r_tvals, &c->r_raw, &c->r_newrp,
                     &c->r_newcols, &c->r_newvals, &c->r_tasks_p, &c->r_tasks_r, &c->r_pairs,
-                    &c->r_nnz, &c->r_newoff, &c->r_img, &c->r_imgoff, &c->r_fast};
+                    &c->r_nnz, &c->r_newoff, &c->r_img, &c->r_imgoff, &c->r_tiles, &c->r_nwords};
   for (DevBuf* b : bufs)
     if (b->p) hipFree(b->p);
   if (c->comm) ncclCommDestroy(c->comm);
@@ -1188,84 +1192,128 @@ int mlp_relax(mlp_ctx* c, int iters) {
       Timer t(c, KTRANS, total);
       HIPCHK(c, launch_transpose(ta, c->stream));
     }
-    // Pair-resident path (k_relax_pair) for every output pair whose blocks fit
-    // the LDS ranges; the row-task kernel for the rest (MLP_RELAX=tasks: all).
+    // Tiled path (k_relax_tile) for every output pair whose blocks fit the
+    // LDS tile; the row-task kernel for the rest (MLP_RELAX=tasks: all).
     const int64_t LDS_MAX = 160 * 1024;
     const char* mode = getenv("MLP_RELAX");
-    const bool tasks_only = (mode && !strcmp(mode, "tasks")) || c->max_len > 65000;
-    std::vector<int64_t> img_off(2 * c->P + 1, 0), rng_a(2 * c->P), rng_b(2 * c->P);
-    int64_t max_a = 0, max_b = 0;
-    for (int64_t p = 0; p < c->P; p++) {
-      const int64_t nz = c->ent_off[p + 1] - c->ent_off[p];
-      const int La = c->lens[c->pa[p]], Lb = c->lens[c->pb[p]];
-      const ImgLayout l0 = img_layout(La, Lb, nz), l1 = img_layout(Lb, La, nz);
-      img_off[2 * p + 1] = img_off[2 * p] + mlp_align16(l0.end);
-      img_off[2 * p + 2] = img_off[2 * p + 1] + mlp_align16(l1.end);
-      rng_a[2 * p] = l0.bits;
-      rng_a[2 * p + 1] = l1.bits;
-      rng_b[2 * p] = mlp_align16(l0.end - l0.vals);
-      rng_b[2 * p + 1] = mlp_align16(l1.end - l1.vals);
-      if (nz < 65536) {
-        max_a = std::max(max_a, std::max(rng_a[2 * p], rng_a[2 * p + 1]));
-        max_b = std::max(max_b, std::max(rng_b[2 * p], rng_b[2 * p + 1]));
+    const char* tenv = getenv("MLP_RELAX_TILE");  // test hook: outputs per tile, 1..kTileMax
+    const int tmax = tenv ? std::max(1, std::min(kTileMax, atoi(tenv))) : kTileMax;
+    bool tasks_only = (mode && !strcmp(mode, "tasks")) || c->max_len > 8000 || c->P >= (1LL << 31);
+    std::vector<int32_t> nwords(2 * c->P, 0);
+    if ((rc = ensure(c, c->r_nwords, sizeof(int32_t) * std::max<int64_t>(2 * c->P, 1)))) return rc;
+    PackArgs pk;
+    pk.n = c->n;
+    pk.lens = c->d_len;
+    pk.rp_off = c->d_rp_off;
+    pk.rowptr = c->d_rowptr;
+    pk.ent_off = c->d_ent_off;
+    pk.cols = c->d_cols;
+    pk.vals = c->d_vals;
+    pk.trp_off = c->d_trp_off;
+    pk.trowptr = (const int32_t*)c->r_trowptr.p;
+    pk.tcols = (const uint16_t*)c->r_tcols.p;
+    pk.tvals = (const float*)c->r_tvals.p;
+    pk.img_off = nullptr;
+    pk.nwords = (int32_t*)c->r_nwords.p;
+    pk.img = nullptr;
+    pk.nimg = 2 * c->P;
+    pk.count = 1;
+    if (!tasks_only) {
+      {
+        Timer t(c, KTRANS, total);
+        HIPCHK(c, launch_pack(pk, c->stream));
       }
+      HIPCHK(c, hipMemcpyAsync(nwords.data(), c->r_nwords.p, sizeof(int32_t) * 2 * c->P, hipMemcpyDeviceToHost,
+                               c->stream));
+      HIPCHK(c, hipStreamSynchronize(c->stream));
     }
-    if (img_off[2 * c->P] >= (1LL << 36)) max_a = max_b = 0;  // z schedule holds offsets / 16 in 32 bits
-    // LDS split: A ranges are smaller; never more than the prefetch registers hold
-    const int64_t reg_cap = 16LL * 16 * kRelaxThreads;
-    const int64_t room = LDS_MAX - (int64_t)pair_relax_lds(0, 0, c->max_len);
-    int64_t cap_a = std::min({max_a, reg_cap, room / 3}) & ~(int64_t)15;
-    int64_t cap_b = std::min({max_b, reg_cap, room - cap_a}) & ~(int64_t)15;
+    // record offsets; per sequence the largest A range (as the left factor
+    // P(x, .)) and B range (as the right factor P(., y)) over its partners
+    std::vector<int64_t> img_off(2 * c->P + 1, 0), maxA(c->n, 0), maxB(c->n, 0);
     std::vector<char> big(c->n, 0);
-    for (int64_t p = 0; p < c->P; p++) {
+    for (int64_t p = 0; p < c->P && !tasks_only; p++) {
       const int64_t nz = c->ent_off[p + 1] - c->ent_off[p];
-      bool b = nz >= 65536;
-      for (int o = 0; o < 2; o++) b = b || rng_a[2 * p + o] > cap_a || rng_b[2 * p + o] > cap_b;
-      if (b) big[c->pa[p]] = big[c->pb[p]] = 1;
-    }
-    std::vector<int64_t> fast, tp;
-    std::vector<int32_t> tr;
-    int64_t max_tasks = 0;
-    for (int64_t p = r0; p < r1; p++) {
-      const int64_t nz = c->ent_off[p + 1] - c->ent_off[p];
-      if (nz == 0) continue;  // empty mask: the filter writes an empty block
-      // tasks = sum over rows of ceil(cells / kRelaxCells) <= nz / kRelaxCells + rows
-      const int La = c->lens[c->pa[p]];
-      const int64_t tasks_bound = nz / kRelaxCells + La;
-      if (!tasks_only && cap_a > 0 && cap_b > 0 && !big[c->pa[p]] && !big[c->pb[p]] &&
-          pair_relax_slots(tasks_bound)) {
-        fast.push_back(p);
-        max_tasks = std::max(max_tasks, tasks_bound);
-        continue;
+      const int a = c->pa[p], b = c->pb[p];
+      for (int o = 0; o < 2; o++) {
+        const int64_t q = 2 * p + o;
+        const int rows = c->lens[o ? b : a];
+        const int xr = o ? b : a, yc = o ? a : b;
+        img_off[q + 1] = img_off[q] + mlp_align16(img_layout(rows, nz, nwords[q]).end);
+        if (nz >= 65536 || nwords[q] >= 65536) big[a] = big[b] = 1;
+        maxA[xr] = std::max(maxA[xr], img_a_bytes(rows, nz));
+        maxB[yc] = std::max(maxB[yc], img_b_bytes(rows, nz, nwords[q]));
       }
-      for (int g = 1; g <= La; g += 64) {
+    }
+    if (img_off[2 * c->P] >= (1LL << 36)) tasks_only = true;  // z schedule holds offsets / 16 in 32 bits
+    const int64_t budget =
+        std::min<int64_t>(LDS_MAX - (int64_t)tile_relax_lds(0, c->max_len), tile_relax_max_cap()) & ~(int64_t)15;
+    // tiles: per y, consecutive x's (ascending) while the LDS bound and the
+    // task slots allow; ordered by (first x, y) for the XCD-aware grid order
+    struct TileRec { int x0, y; int64_t first; };
+    std::vector<int32_t> tiles_raw;
+    std::vector<TileRec> order;
+    std::vector<int64_t> tp;
+    std::vector<int32_t> tr;
+    int64_t cap = 0, max_tasks = 0;
+    auto row_tasks = [&](int64_t p) {
+      for (int g = 1; g <= c->lens[c->pa[p]]; g += 64) {
         tp.push_back(p);
         tr.push_back(g);
       }
+    };
+    for (int yy = 1; yy < c->n; yy++) {
+      int32_t cur_p[kTileMax], cur_x[kTileMax];
+      int cnt = 0;
+      int64_t sumA = 0, ntask = 0;
+      auto flush = [&]() {
+        if (!cnt) return;
+        order.push_back({cur_x[0], yy, (int64_t)tiles_raw.size()});
+        for (int t = 0; t < kTileMax; t++) tiles_raw.push_back(t < cnt ? cur_p[t] : -1);
+        for (int t = 0; t < kTileMax; t++) tiles_raw.push_back(t < cnt ? cur_x[t] : 0);
+        tiles_raw.push_back(yy);
+        cap = std::max(cap, sumA + maxB[yy]);
+        max_tasks = std::max(max_tasks, ntask);
+        cnt = 0;
+        sumA = ntask = 0;
+      };
+      for (int x = 0; x < yy; x++) {
+        const int64_t p = pair_index_host(c->n, x, yy);
+        if (p < r0 || p >= r1) continue;
+        const int64_t nz = c->ent_off[p + 1] - c->ent_off[p];
+        if (nz == 0) continue;  // empty mask: the filter writes an empty block
+        // tasks = sum over rows of ceil(cells / kRelaxCells) <= nz / kRelaxCells + rows
+        const int64_t tasks = nz / kRelaxCells + c->lens[x];
+        if (tasks_only || big[x] || big[yy] || maxA[x] + maxB[yy] > budget || !tile_relax_slots(tasks)) {
+          row_tasks(p);
+          continue;
+        }
+        if (cnt == tmax || sumA + maxA[x] + maxB[yy] > budget || !tile_relax_slots(ntask + tasks)) flush();
+        cur_p[cnt] = (int32_t)p;
+        cur_x[cnt] = x;
+        cnt++;
+        sumA += maxA[x];
+        ntask += tasks;
+      }
+      flush();
     }
-    if (!fast.empty()) {
+    std::stable_sort(order.begin(), order.end(),
+                     [](const TileRec& u, const TileRec& v) { return u.x0 != v.x0 ? u.x0 < v.x0 : u.y < v.y; });
+    std::vector<int32_t> tiles;
+    tiles.reserve(tiles_raw.size());
+    for (const TileRec& r : order)
+      tiles.insert(tiles.end(), tiles_raw.begin() + r.first, tiles_raw.begin() + r.first + kTileInts);
+    const int64_t ntiles = (int64_t)order.size();
+    if (ntiles) {
       if ((rc = ensure(c, c->r_img, std::max<int64_t>(img_off[2 * c->P], 16)))) return rc;
       if ((rc = ensure(c, c->r_imgoff, sizeof(int64_t) * (2 * c->P + 1)))) return rc;
-      if ((rc = ensure(c, c->r_fast, sizeof(int64_t) * fast.size()))) return rc;
+      if ((rc = ensure(c, c->r_tiles, sizeof(int32_t) * tiles.size()))) return rc;
       HIPCHK(c, hipMemcpyAsync(c->r_imgoff.p, img_off.data(), sizeof(int64_t) * (2 * c->P + 1),
                                hipMemcpyHostToDevice, c->stream));
-      HIPCHK(c, hipMemcpyAsync(c->r_fast.p, fast.data(), sizeof(int64_t) * fast.size(), hipMemcpyHostToDevice,
+      HIPCHK(c, hipMemcpyAsync(c->r_tiles.p, tiles.data(), sizeof(int32_t) * tiles.size(), hipMemcpyHostToDevice,
                                c->stream));
-      PackArgs pk;
-      pk.n = c->n;
-      pk.lens = c->d_len;
-      pk.rp_off = c->d_rp_off;
-      pk.rowptr = c->d_rowptr;
-      pk.ent_off = c->d_ent_off;
-      pk.cols = c->d_cols;
-      pk.vals = c->d_vals;
-      pk.trp_off = c->d_trp_off;
-      pk.trowptr = (const int32_t*)c->r_trowptr.p;
-      pk.tcols = (const uint16_t*)c->r_tcols.p;
-      pk.tvals = (const float*)c->r_tvals.p;
       pk.img_off = (const int64_t*)c->r_imgoff.p;
       pk.img = (uint8_t*)c->r_img.p;
-      pk.nimg = 2 * c->P;
+      pk.count = 0;
       Timer t(c, KTRANS, total);
       HIPCHK(c, launch_pack(pk, c->stream));
     }
@@ -1296,7 +1344,7 @@ int mlp_relax(mlp_ctx* c, int iters) {
     ra.task_row0 = (const int32_t*)c->r_tasks_r.p;
     ra.ntasks = nt;
     ra.out = (float*)c->r_raw.p;
-    PairRelaxArgs pr;
+    TileRelaxArgs pr;
     pr.n = c->n;
     pr.lens = c->d_len;
     pr.rp_off = c->d_rp_off;
@@ -1305,16 +1353,17 @@ int mlp_relax(mlp_ctx* c, int iters) {
     pr.cols = c->d_cols;
     pr.vals = c->d_vals;
     pr.img_off = (const int64_t*)c->r_imgoff.p;
+    pr.nwords = (const int32_t*)c->r_nwords.p;
     pr.img = (const uint8_t*)c->r_img.p;
-    pr.pairs = (const int64_t*)c->r_fast.p;
-    pr.npairs = (int64_t)fast.size();
+    pr.img_chunks = img_off[2 * c->P] / 16;
+    pr.tiles = (const int32_t*)c->r_tiles.p;
+    pr.ntiles = ntiles;
     pr.out = (float*)c->r_raw.p;
-    pr.cap_a = (int)cap_a;
-    pr.cap_b = (int)cap_b;
+    pr.cap = (int)mlp_align16(cap);
     pr.max_len = c->max_len;
     {
       Timer t(c, KRELAX, c->ent_off[r1] - c->ent_off[r0]);
-      HIPCHK(c, launch_relax_pairs(pr, pair_relax_slots(max_tasks), c->stream));
+      HIPCHK(c, launch_relax_tiles(pr, tile_relax_slots(max_tasks), c->stream));
       HIPCHK(c, launch_relax_tasks(ra, c->stream));
     }
     // filter: count, host scan, write

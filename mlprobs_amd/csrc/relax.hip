@@ -218,9 +218,8 @@ __global__ __launch_bounds__(256) void k_filter(FilterArgs A) {
 }
 
 // ------------------------------------------------------------ block images
-// One wave per image: the block (or its transpose) in the layout of
-// mlp_kernels.h (img_layout): CSR for the left-factor role, row bitmaps with
-// per-word entry bases for the right-factor role.
+// One wave per image.  Count pass: bitmap words of the image (host sizes the
+// records from them); write pass: the record of mlp_kernels.h (img_layout).
 __global__ __launch_bounds__(256) void k_pack(PackArgs A) {
   const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (q >= A.nimg) return;
@@ -233,245 +232,390 @@ __global__ __launch_bounds__(256) void k_pack(PackArgs A) {
   while (r >= n - 1 - a) { r -= n - 1 - a; ++a; }
   const int b = a + 1 + (int)r;
   const int rows = tr ? A.lens[b] : A.lens[a];
-  const int ncol = tr ? A.lens[a] : A.lens[b];
-  const int W = (ncol >> 5) + 1;
   const int64_t e0 = A.ent_off[p];
   const int64_t nnz = A.ent_off[p + 1] - e0;
   const int32_t* rp = tr ? A.trowptr + A.trp_off[p] : A.rowptr + A.rp_off[p];
   const uint16_t* cols = (tr ? A.tcols : A.cols) + e0;
   const float* vals = (tr ? A.tvals : A.vals) + e0;
-  const ImgLayout L = img_layout(rows, ncol, nnz);
+  // words spanned by row k: first .. last entry's 32-column word
+  auto row_words = [&](int k) -> int {
+    const int rb = rp[k], re = rp[k + 1];
+    return rb < re ? (cols[re - 1] >> 5) - (cols[rb] >> 5) + 1 : 0;
+  };
+  if (A.count) {
+    int s = 0;
+    for (int k = lane + 1; k <= rows; k += 64) s += row_words(k);
+    for (int off = 32; off; off >>= 1) s += __shfl_xor(s, off);
+    if (lane == 0) A.nwords[q] = s;
+    return;
+  }
+  const ImgLayout L = img_layout(rows, nnz, A.nwords[q]);
   uint8_t* dst = A.img + A.img_off[q];
   uint16_t* dcols = (uint16_t*)dst;
   uint16_t* drp = (uint16_t*)(dst + L.rp);
   float* dvals = (float*)(dst + L.vals);
-  uint2* dbits = (uint2*)(dst + L.bits);
+  uint32_t* dhdr = (uint32_t*)(dst + L.hdr);
+  uint2* dwords = (uint2*)(dst + L.words);
   for (int k = lane; k < rows + 2; k += 64) drp[k] = (uint16_t)rp[k];
   for (int64_t e = lane; e < nnz; e += 64) {
     dcols[e] = cols[e];
     dvals[e] = vals[e];
   }
-  // row bitmaps: lane per row, words in column order
-  for (int k = lane + 1; k <= rows; k += 64) {
-    int e = rp[k];
-    const int re = rp[k + 1];
-    for (int w = 0; w < W; ++w) {
-      uint32_t bits = 0;
-      const int base = e;
-      while (e < re && (cols[e] >> 5) == w) {
-        bits |= 1u << (cols[e] & 31);
-        ++e;
-      }
-      dbits[(int64_t)(k - 1) * W + w] = make_uint2(bits, (uint32_t)base);
+  if (lane == 0) dhdr[0] = 0;
+  int run = 0;  // words before this 64-row chunk
+  for (int k0 = 1; k0 <= rows; k0 += 64) {
+    const int k = k0 + lane;
+    const int nw = k <= rows ? row_words(k) : 0;
+    int xs = nw;
+    for (int off = 1; off < 64; off <<= 1) {
+      const int v = __shfl_up(xs, off);
+      if (lane >= off) xs += v;
     }
+    if (k <= rows) {
+      const int woff = run + xs - nw;
+      int e = rp[k];
+      const int re = rp[k + 1];
+      const int c0w = nw ? cols[e] >> 5 : 0;
+      dhdr[k] = (uint32_t)woff | (uint32_t)c0w << 16 | (uint32_t)nw << 24;
+      for (int w = 0; w < nw; ++w) {
+        uint32_t bits = 0;
+        const int base = e;
+        while (e < re && (cols[e] >> 5) == c0w + w) {
+          bits |= 1u << (cols[e] & 31);
+          ++e;
+        }
+        dwords[woff + w] = make_uint2(bits, (uint32_t)base);
+      }
+    }
+    run += __shfl(xs, 63);
   }
 }
 
-// ------------------------------------------------- pair-resident relaxation
-// One workgroup per output pair (x, y).  The output cells (the mask: the
-// pattern of P_xy, CPNP/MSA.cpp:1237-1261) are cut into tasks of up to four
-// cells of one row i; a thread owns a few tasks, their accumulators live in
-// registers.  For each z (ascending) the workgroup stages A_z = P(x, z) (CSR)
-// and B_z = P(z, y) (row bitmaps) in LDS -- the next z's ranges are
-// prefetched into registers while the current z is computed -- and a task
-// walks A_z row i (k ascending), looking its cells' columns j up in the
-// bitmap of B_z row k.  Each cell's sum therefore runs z ascending, then k
-// ascending: the order of Relax / Relax1 (CPNP/MSA.cpp:1276-1350), so every
-// float sum is bit-identical to the reference's.
+// ------------------------------------------------------------ tiled relaxation
+// One workgroup per tile of up to kTileMax output pairs (x_t, y) sharing y.
+// The output cells (the mask: the pattern of P_{x_t y}, CPNP/MSA.cpp:1237-1261)
+// are cut into tasks of up to four cells of one row i; a thread owns a few
+// tasks, their accumulators live in registers.  For each z (ascending) the
+// workgroup stages the A_t = P(x_t, z) blocks (CSR) and the one shared
+// B = P(z, y) block (row bitmaps over each row's column span) in LDS -- the
+// next z's ranges are prefetched into registers while the current z is
+// computed -- and a task walks A_t row i (k ascending), looking its cells'
+// columns j up in the bitmap of B row k.  Each cell's sum therefore runs
+// z ascending, then k ascending: the order of Relax / Relax1
+// (CPNP/MSA.cpp:1276-1350), so every float sum is bit-identical to the
+// reference's.  Sharing B across the tile halves (T = 2) to quarters (T = 4)
+// the B traffic per output pair; the XCD-aware tile order lets tiles with the
+// same x group run on one XCD, so their A blocks meet in that XCD's L2.
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));  // plain vector: stays in VGPRs
-constexpr int kRelaxZChunk = 256;  // z schedule entries per LDS fill
+#ifdef MLP_RELAX_NOLOAD  // timing experiment: no global loads for the staging
+#define MLP_PF_LOAD(dst, src) (dst) = u32x4{(uint32_t)c, 0u, 0u, 0u}
+#else
+#define MLP_PF_LOAD(dst, src) (dst) = (src)
+#endif
+#ifdef MLP_RELAX_SEQADDR  // timing experiment: each workgroup streams consecutive memory over z
+#define MLP_PF_SRC ((uint32_t)((((uint64_t)tile * 7919 + (uint64_t)zcount) * (uint64_t)tot_) % (uint64_t)(A.img_chunks - tot_)) + (uint32_t)c)
+#else
+#define MLP_PF_SRC ((uint32_t)(c + d))
+#endif
+constexpr int kRelaxZChunk = 128;  // z schedule entries per LDS fill (48 B each)
+constexpr int kRelaxGuard = 2048;  // LDS bytes after the tile: unchecked bitmap-word reads stay inside
 static __host__ __device__ inline size_t relax_tp_bytes(int max_len) {
-  return (4 * (size_t)(max_len + 2) + 15) & ~(size_t)15;
+  return (4 * (size_t)kTileMax * (max_len + 2) + 15) & ~(size_t)15;
 }
-
-size_t pair_relax_lds(int cap_a, int cap_b, int max_len) {
-  return (size_t)cap_a + (size_t)cap_b + relax_tp_bytes(max_len) + 16 * kRelaxZChunk;
+// LDS: [z schedule][task prefixes][per-output A bases][zero][tile][guard];
+// the schedule (6 KB) in front keeps unchecked reads below the tile inside too
+static __host__ __device__ inline size_t relax_tile_off(int max_len) {
+  return 48 * (size_t)kRelaxZChunk + relax_tp_bytes(max_len) + 32 * kTileMax + 16;
 }
+size_t tile_relax_lds(int cap, int max_len) { return relax_tile_off(max_len) + (size_t)cap + kRelaxGuard; }
 
-int pair_relax_prefetch(int cap) {
+int tile_relax_prefetch(int cap) {
   const int chunks = (cap / 16 + kRelaxThreads - 1) / kRelaxThreads;
-  for (int kp : {1, 2, 4, 8, 16})
+  for (int kp : {6, 12})
     if (chunks <= kp) return kp;
   return 0;
 }
 
-int pair_relax_slots(int64_t tasks) {
+int tile_relax_max_cap() { return 12 * kRelaxThreads * 16; }
+
+int tile_relax_slots(int64_t tasks) {
   const int64_t per = (tasks + kRelaxThreads - 1) / kRelaxThreads;
-  for (int sl : {1, 2, 4, 8})
+  for (int sl : {2, 4})
     if (per <= sl) return sl;
   return 0;
 }
 
+
+// workgroup-uniform values read from LDS: keep them in SGPRs
+__device__ __forceinline__ uint4 rfl(uint4 v) {
+  return make_uint4(__builtin_amdgcn_readfirstlane(v.x), __builtin_amdgcn_readfirstlane(v.y),
+                    __builtin_amdgcn_readfirstlane(v.z), __builtin_amdgcn_readfirstlane(v.w));
+}
+
 template <int KP, int SL>
-__global__ __launch_bounds__(kRelaxThreads) void k_relax_pair(PairRelaxArgs A) {
+__global__ __launch_bounds__(kRelaxThreads) void k_relax_tile(TileRelaxArgs A) {
   extern __shared__ __align__(16) uint8_t lds[];
   constexpr int nt = kRelaxThreads;
   constexpr int NC = kRelaxCells;
+  constexpr int TM = kTileMax;
   const int tid = threadIdx.x;
-  const int64_t p = A.pairs[blockIdx.x];
+  // blocks b, b + 8, ... share an XCD: give each XCD a contiguous run of tiles
+  const int64_t nb = gridDim.x, bid = blockIdx.x;
+  const int64_t xcd = bid & 7, per = nb >> 3, rem = nb & 7;
+  const int64_t tile = xcd * per + (xcd < rem ? xcd : rem) + (bid >> 3);
+  const int32_t* td = A.tiles + tile * kTileInts;
   const int n = A.n;
-  const int64_t exy = A.ent_off[p];
-  if (A.ent_off[p + 1] == exy) return;  // empty mask: nothing survives
-  int x = 0;
-  int64_t q = p;
-  while (q >= n - 1 - x) { q -= n - 1 - x; ++x; }
-  const int y = x + 1 + (int)q;
-  const int Lx = A.lens[x], Ly = A.lens[y];
-  const int W = (Ly >> 5) + 1;
-  uint8_t* sA = lds;
-  uint8_t* sB = lds + A.cap_a;
-  int32_t* tp = (int32_t*)(lds + A.cap_a + A.cap_b);  // tasks before row i
+  int pt[TM], xt[TM], Lxt[TM];
+  int T = 0;
+#pragma unroll
+  for (int t = 0; t < TM; ++t) {
+    pt[t] = td[t];
+    xt[t] = td[TM + t];
+    T = pt[t] >= 0 ? t + 1 : T;
+    Lxt[t] = pt[t] >= 0 ? A.lens[xt[t]] : 0;
+  }
+  const int y = td[2 * TM];
+  const int tps = A.max_len + 2;
+  uint4* ztab = (uint4*)lds;
+  int32_t* tp = (int32_t*)(lds + 48 * kRelaxZChunk);  // per output: tasks before row i
+  int4* zb = (int4*)(lds + 48 * kRelaxZChunk + relax_tp_bytes(A.max_len));  // per output: A bases this z
+  int4* oinf = zb + TM;  // per output: {pair, L_x, tasks before it, -} (per-lane lookups by output)
+  float* zero = (float*)(oinf + TM);
+  uint8_t* tileb = lds + relax_tile_off(A.max_len);
 
-  // tasks: row i contributes ceil(m_i / NC); prefix by wave 0
-  const int32_t* rpxy = A.rowptr + A.rp_off[p];
-  if (tid < 64) {
-    int run = 0;
-    if (tid == 0) tp[1] = 0;
-    for (int r0 = 1; r0 <= Lx; r0 += 64) {
-      const int i = r0 + tid;
-      const int c = i <= Lx ? (rpxy[i + 1] - rpxy[i] + NC - 1) / NC : 0;
-      int xs = c;
-      for (int off = 1; off < 64; off <<= 1) {
-        const int v = __shfl_up(xs, off);
-        if (tid >= off) xs += v;
+  // task prefixes: wave t scans output t (row i contributes ceil(m_i / NC))
+  {
+    const int wv = tid >> 6, ln = tid & 63;
+    if (wv < T) {
+      const int64_t p = td[wv];
+      const int Lx = A.lens[td[TM + wv]];
+      const int32_t* rpxy = A.rowptr + A.rp_off[p];
+      int32_t* tw = tp + wv * tps;
+      int run = 0;
+      if (ln == 0) tw[1] = 0;
+      for (int r0 = 1; r0 <= Lx; r0 += 64) {
+        const int i = r0 + ln;
+        const int c = i <= Lx ? (rpxy[i + 1] - rpxy[i] + NC - 1) / NC : 0;
+        int xs = c;
+        for (int off = 1; off < 64; off <<= 1) {
+          const int v = __shfl_up(xs, off);
+          if (ln >= off) xs += v;
+        }
+        if (i <= Lx) tw[i + 1] = run + xs;
+        run += __shfl(xs, 63);
       }
-      if (i <= Lx) tp[i + 1] = run + xs;
-      run += __shfl(xs, 63);
     }
+    if (tid == 0) *zero = 0.f;
   }
   __syncthreads();
-  const int ntask = tp[Lx + 1];
-  int ti[SL];           // row of each task (0 = no task)
-  uint32_t wo[SL][NC];  // byte offset of the cell's word in a bitmap row
+  int tb[TM + 1];
+  tb[0] = 0;
+#pragma unroll
+  for (int t = 0; t < TM; ++t)
+    tb[t + 1] = tb[t] + (t < T ? __builtin_amdgcn_readfirstlane(tp[t * tps + Lxt[t] + 1]) : 0);
+  if (tid < TM) {
+    int4 o = make_int4(-1, 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < TM; ++t)
+      if (tid == t) o = make_int4(pt[t], Lxt[t], tb[t], 0);
+    oinf[tid] = o;
+  }
+  __syncthreads();
+
+  uint32_t tio[SL];     // row i (0 = no task) | output t << 16 of each task
+  uint32_t jw[SL][NC];  // the cell's 32-column word index j >> 5
   uint32_t bm[SL][NC];  // the cell's bit (0 = no cell: never hits)
   float acc[SL][NC];
 #pragma unroll
   for (int s = 0; s < SL; ++s) {
     const int g = tid + s * nt;
-    ti[s] = 0;
+    tio[s] = 0;
 #pragma unroll
-    for (int c = 0; c < NC; ++c) { wo[s][c] = 0; bm[s][c] = 0; acc[s][c] = 0.f; }
-    if (g < ntask) {
-      int lo = 1, hi = Lx;  // last row with tp[row] <= g
+    for (int c = 0; c < NC; ++c) { jw[s][c] = 0; bm[s][c] = 0; acc[s][c] = 0.f; }
+    if (g < tb[TM]) {
+      int t = 0;
+#pragma unroll
+      for (int u = 1; u < TM; ++u) t += g >= tb[u] ? 1 : 0;
+      const int4 o = oinf[t];
+      const int gl = g - o.z;
+      const int32_t* tt = tp + t * tps;
+      int lo = 1, hi = o.y;  // last row with tt[row] <= gl
       while (lo < hi) {
         const int mid = (lo + hi + 1) >> 1;
-        if (tp[mid] <= g) lo = mid; else hi = mid - 1;
+        if (tt[mid] <= gl) lo = mid; else hi = mid - 1;
       }
-      ti[s] = lo;
-      const int e0 = rpxy[lo] + NC * (g - tp[lo]), e1 = rpxy[lo + 1];
+      const int64_t p = o.x;
+      const int64_t exy = A.ent_off[p];
+      const int32_t* rpxy = A.rowptr + A.rp_off[p];
+      tio[s] = (uint32_t)lo | (uint32_t)t << 16;
+      const int e0 = rpxy[lo] + NC * (gl - tt[lo]), e1 = rpxy[lo + 1];
 #pragma unroll
       for (int c = 0; c < NC; ++c)
         if (e0 + c < e1) {
           const uint32_t j = A.cols[exy + e0 + c];
-          wo[s][c] = (j >> 5) * 8;
+          jw[s][c] = j >> 5;
           bm[s][c] = 1u << (j & 31);
           const float v = A.vals[exy + e0 + c];
           acc[s][c] = v + v;  // z = x and z = y (CPNP/MSA.cpp:1211-1213)
         }
     }
   }
-  if (tid == 0) tp[0] = 0;  // tp[0] (unused by the scan) doubles as a 0.0f for misses
-  const float* zero = (const float*)tp;
 
-  // The z schedule, ZC values of z at a time, in LDS: per z the 16-byte
-  // offsets of the A_z range (P(x, z)) and the B_z range (P(z, y)), both
-  // blocks' entry counts and L_z; nnz 0 marks a z to skip (z = x, z = y or
-  // an empty block).  Filling it costs one memory round trip per ZC values
-  // of z instead of one per z.
-  uint4* ztab = (uint4*)(lds + A.cap_a + A.cap_b + relax_tp_bytes(A.max_len));
+  // The z schedule, kRelaxZChunk values of z at a time, in LDS (3 uint4 per
+  // z): {B range start / 16, nnz(B) | L_z << 16 (0: skip z), B chunks, -},
+  // {A_t range start / 16}, {nnz(A_t) (0: output t skips z)}.  z = y, an
+  // empty B or no live A_t skip the whole z.
   int zbase = 0, zpos = -1;
   auto fill = [&]() {
     __syncthreads();  // every wave is done reading the previous chunk
     if (tid < kRelaxZChunk) {
       const int z = zbase + tid;
-      uint4 e = make_uint4(0, 0, 0, 0);
-      if (z < n && z != x && z != y) {
-        int64_t pa, pb, qa, qb;
-        if (z > x) { pa = pair_index(n, x, z); qa = 2 * pa; } else { pa = pair_index(n, z, x); qa = 2 * pa + 1; }
+      uint4 e0 = make_uint4(0, 0, 0, 0), e1 = e0, e2 = e0;
+      if (z < n && z != y) {
+        int64_t pb, qb;
         if (z < y) { pb = pair_index(n, z, y); qb = 2 * pb; } else { pb = pair_index(n, y, z); qb = 2 * pb + 1; }
-        const int na = (int)(A.ent_off[pa + 1] - A.ent_off[pa]);
-        const int nb = (int)(A.ent_off[pb + 1] - A.ent_off[pb]);
-        if (na > 0 && nb > 0) {
-          const int Lz = A.lens[z];
-          const ImgLayout lb = img_layout(Lz, Ly, nb);
-          e = make_uint4((uint32_t)(A.img_off[qa] >> 4), (uint32_t)((A.img_off[qb] + lb.vals) >> 4),
-                         (uint32_t)na | ((uint32_t)nb << 16), (uint32_t)Lz);
+        const int nbz = (int)(A.ent_off[pb + 1] - A.ent_off[pb]);
+        if (nbz > 0) {
+          uint32_t ao[TM], na[TM];
+          bool any = false;
+#pragma unroll
+          for (int t = 0; t < TM; ++t) {
+            ao[t] = 0;
+            na[t] = 0;
+            const int xx = td[TM + t];  // (not xt[]: arrays captured by a lambda end up in scratch)
+            if (td[t] >= 0 && z != xx) {
+              int64_t pa, qa;
+              if (xx < z) { pa = pair_index(n, xx, z); qa = 2 * pa; } else { pa = pair_index(n, z, xx); qa = 2 * pa + 1; }
+              const int nza = (int)(A.ent_off[pa + 1] - A.ent_off[pa]);
+              if (nza > 0) {
+                ao[t] = (uint32_t)(A.img_off[qa] >> 4);
+                na[t] = (uint32_t)nza;
+                any = true;
+              }
+            }
+          }
+          if (any) {
+            const int Lz = A.lens[z];
+            const int nw = A.nwords[qb];
+            const ImgLayout lb = img_layout(Lz, nbz, nw);
+            e0 = make_uint4((uint32_t)((A.img_off[qb] + lb.vals) >> 4), (uint32_t)nbz | ((uint32_t)Lz << 16),
+                            (uint32_t)(img_b_bytes(Lz, nbz, nw) >> 4), 0);
+            e1 = make_uint4(ao[0], ao[1], ao[2], ao[3]);
+            e2 = make_uint4(na[0], na[1], na[2], na[3]);
+          }
         }
       }
-      ztab[tid] = e;
+      ztab[3 * tid] = e0;
+      ztab[3 * tid + 1] = e1;
+      ztab[3 * tid + 2] = e2;
     }
     __syncthreads();
   };
-  // next scheduled z (uniform across the workgroup); .z == 0 when done
-  auto next = [&]() -> uint4 {
+  // next scheduled z (uniform across the workgroup); returns false when done
+  uint4 nB, nAo, nNa;  // the staged-next z's entry
+  auto next = [&]() -> bool {
     for (;;) {
       if (++zpos == kRelaxZChunk) {
         zbase += kRelaxZChunk;
-        if (zbase >= n) return make_uint4(0, 0, 0, 0);
+        if (zbase >= n) return false;
         zpos = 0;
         fill();
       }
-      if (zbase + zpos >= n) return make_uint4(0, 0, 0, 0);
-      const uint4 e = ztab[zpos];
-      if (e.z) return e;
+      if (zbase + zpos >= n) return false;
+      nB = rfl(ztab[3 * zpos]);
+      if (nB.y) {
+        nAo = rfl(ztab[3 * zpos + 1]);
+        nNa = rfl(ztab[3 * zpos + 2]);
+        return true;
+      }
     }
   };
-  // register prefetch of the next z's ranges (written out: arrays captured
-  // by reference in a lambda end up in scratch)
-  u32x4 ra[KP], rb[KP];
-  int ca = 0, cb = 0;  // 16-byte chunks of the prefetched ranges
-  fill();
-  uint4 en = next();
-#define MLP_ISSUE()                                                                    \
-  {                                                                                    \
-    const int Lz_ = (int)en.w, na_ = (int)(en.z & 0xffff), nb_ = (int)(en.z >> 16);   \
-    const ImgLayout la = img_layout(Lx, Lz_, na_), lb = img_layout(Lz_, Ly, nb_);      \
-    const u32x4* ga = (const u32x4*)(A.img + ((int64_t)en.x << 4));                    \
-    const u32x4* gb = (const u32x4*)(A.img + ((int64_t)en.y << 4));                    \
-    ca = (int)(la.bits >> 4);                                                          \
-    cb = (int)((lb.end - lb.vals + 15) >> 4);                                          \
-    _Pragma("unroll") for (int m = 0; m < KP; ++m) {                                   \
-      const int c = tid + m * nt;                                                      \
-      ra[m] = ga[min(c, ca - 1)];                                                      \
-      rb[m] = gb[min(c, cb - 1)];                                                      \
-    }                                                                                  \
+  // register prefetch of the next z's tile: segments A_0 .. A_{TM-1}, B,
+  // contiguous in LDS (written out: arrays captured by a lambda end up in scratch)
+  u32x4 pf[KP];
+  int sg[TM + 1];  // segment starts (16-byte chunks) of the prefetched tile
+  const u32x4* g16 = (const u32x4*)A.img;
+#define MLP_ISSUE()                                                                      \
+  {                                                                                      \
+    const uint32_t ao_[TM] = {nAo.x, nAo.y, nAo.z, nAo.w};                               \
+    const uint32_t na_[TM] = {nNa.x, nNa.y, nNa.z, nNa.w};                               \
+    int dl_[TM];                                                                         \
+    sg[0] = 0;                                                                           \
+    _Pragma("unroll") for (int t = 0; t < TM; ++t) {                                     \
+      const int ca_ = na_[t] ? (int)(img_a_bytes(Lxt[t], na_[t]) >> 4) : 0;              \
+      dl_[t] = (int)ao_[t] - sg[t];                                                      \
+      sg[t + 1] = sg[t] + ca_;                                                           \
+    }                                                                                    \
+    const int tot_ = sg[TM] + (int)nB.z;                                                 \
+    const int dB_ = (int)nB.x - sg[TM];                                                  \
+    _Pragma("unroll") for (int m = 0; m < KP; ++m) {                                     \
+      const int c = tid + m * nt;                                                        \
+      if (c < tot_) {                                                                    \
+        int d = dB_;                                                                     \
+        _Pragma("unroll") for (int t = TM - 1; t >= 0; --t) d = c < sg[t + 1] ? dl_[t] : d; \
+        MLP_PF_LOAD(pf[m], g16[MLP_PF_SRC]);                                             \
+      }                                                                                  \
+    }                                                                                    \
   }
-  if (en.z) MLP_ISSUE();
-#ifdef MLP_RELAX_NOSTAGE
-  const uint4 e0 = en;
+  fill();
+  int zcount = 0;
+  (void)zcount;
+  bool more = next();
+  if (more) MLP_ISSUE();
+#ifdef MLP_RELAX_SAMEADDR  // timing experiment: every z loads the first z's tile again
+  const uint4 fB = nB, fAo = nAo, fNa = nNa;
 #endif
-  while (en.z) {
+#ifdef MLP_RELAX_NOSTAGE  // timing experiment: every z computes on the first z's tile
+  const uint4 fB = nB, fAo = nAo, fNa = nNa;
+#endif
+  while (more) {
+    // stage the prefetched tile; outputs' A bases (+ validity) into zb
+    const int tot = sg[TM] + (int)nB.z;
 #pragma unroll
     for (int m = 0; m < KP; ++m) {
       const int c = tid + m * nt;
-      if (c < ca) ((u32x4*)sA)[c] = ra[m];
-      if (c < cb) ((u32x4*)sB)[c] = rb[m];
+      if (c < tot) ((u32x4*)tileb)[c] = pf[m];
+    }
+    const int Lz = (int)(nB.y >> 16), nzB = (int)(nB.y & 0xffff);
+    const uint32_t boff = (uint32_t)(relax_tile_off(A.max_len) + 16 * (size_t)sg[TM]);
+    if (tid == 0) {
+      const uint32_t na_[TM] = {nNa.x, nNa.y, nNa.z, nNa.w};
+#pragma unroll
+      for (int t = 0; t < TM; ++t) {
+        const uint32_t ab = (uint32_t)(relax_tile_off(A.max_len) + 16 * (size_t)sg[t]);
+        const uint32_t rpo = ab + (uint32_t)mlp_align16(2 * (int64_t)na_[t]);
+        zb[t] = make_int4((int)ab, (int)rpo, (int)(rpo + (uint32_t)mlp_align16(2 * (int64_t)(Lxt[t] + 2))),
+                          (int)na_[t]);
+      }
     }
     __syncthreads();
-#ifdef MLP_RELAX_NOSTAGE  // timing experiment: every z computes on the first z's images
-    const int Lz = (int)e0.w, nzA = (int)(e0.z & 0xffff), nzB = (int)(e0.z >> 16);
-    en = next();
-    ca = cb = 0;
+    more = next();
+    ++zcount;
+#ifdef MLP_RELAX_NOSTAGE
+    nB = fB; nAo = fAo; nNa = fNa;
 #else
-    const int Lz = (int)en.w, nzA = (int)(en.z & 0xffff), nzB = (int)(en.z >> 16);
-    en = next();
-    if (en.z) MLP_ISSUE();
+#ifdef MLP_RELAX_SAMEADDR
+    nB = fB; nAo = fAo; nNa = fNa;
+#endif
+    if (more) MLP_ISSUE();
 #endif
     {
-      const ImgLayout la = img_layout(Lx, Lz, nzA), lb = img_layout(Lz, Ly, nzB);
-      const uint16_t* Acols = (const uint16_t*)sA;
-      const uint16_t* Arp = (const uint16_t*)(sA + la.rp);
-      const float* Avals = (const float*)(sA + la.vals);
-      const float* Bvals = (const float*)sB;
-      const uint8_t* Bbits = sB + (lb.bits - lb.vals) - 8 * W;  // row k at k * W words
-      const uint32_t W8 = 8 * W;
+      const float* Bvals = (const float*)(lds + boff);
+      const uint32_t* Bhdr = (const uint32_t*)(lds + boff + (uint32_t)mlp_align16(4 * (int64_t)nzB));
+      const uint2* Bwords = (const uint2*)((const uint8_t*)Bhdr + (uint32_t)mlp_align16(4 * (int64_t)(Lz + 1)));
 #pragma unroll
       for (int s = 0; s < SL; ++s) {
-#ifdef MLP_RELAX_NOCOMPUTE
+        const int ti = (int)(tio[s] & 0xffff);
+#ifdef MLP_RELAX_NOCOMPUTE  // timing experiment: staging only
         continue;
 #endif
-        if (ti[s] == 0) continue;
-        const int a0 = Arp[ti[s]], a1 = Arp[ti[s] + 1];
+        if (ti == 0) continue;
+        const int4 z4 = zb[tio[s] >> 16];
+        if (z4.w == 0) continue;
+        const uint16_t* Acols = (const uint16_t*)(lds + z4.x);
+        const uint16_t* Arp = (const uint16_t*)(lds + z4.y);
+        const float* Avals = (const float*)(lds + z4.z);
+        const int a0 = Arp[ti], a1 = Arp[ti + 1];
         // two A entries per iteration (the second a zero-weight copy of the
         // first past the row end: + 0.0f leaves a positive sum unchanged)
         for (int t = a0; t < a1; t += 2) {
@@ -479,22 +623,28 @@ __global__ __launch_bounds__(kRelaxThreads) void k_relax_pair(PairRelaxArgs A) {
           const int k0 = Acols[t], k1 = Acols[two ? t + 1 : t];
           const float av0 = Avals[t];
           const float av1 = two ? Avals[t + 1] : 0.f;
-          const uint8_t* r0 = Bbits + __umul24(k0, W8);
-          const uint8_t* r1 = Bbits + __umul24(k1, W8);
+          const uint32_t h0 = Bhdr[k0], h1 = Bhdr[k1];
+          // word of column word jw in row k: woff + (jw - c0w), valid iff jw - c0w < nw
+          const int o0 = (int)(h0 & 0xffff) - (int)((h0 >> 16) & 0xff);
+          const int o1 = (int)(h1 & 0xffff) - (int)((h1 >> 16) & 0xff);
+          const uint32_t c00 = (h0 >> 16) & 0xff, c01 = (h1 >> 16) & 0xff;
+          const uint32_t nw0 = h0 >> 24, nw1 = h1 >> 24;
           uint2 w0[NC], w1[NC];
 #pragma unroll
-          for (int c = 0; c < NC; ++c) {
-            w0[c] = *(const uint2*)(r0 + wo[s][c]);
-            w1[c] = *(const uint2*)(r1 + wo[s][c]);
+          for (int c = 0; c < NC; ++c) {  // unchecked: |jw - c0w| < 256 words stays in LDS
+            w0[c] = Bwords[o0 + (int)jw[s][c]];
+            w1[c] = Bwords[o1 + (int)jw[s][c]];
           }
           float b0[NC], b1[NC];
 #pragma unroll
           for (int c = 0; c < NC; ++c) {
             const uint32_t below = bm[s][c] - 1u;
+            const bool h0c = (jw[s][c] - c00 < nw0) && (w0[c].x & bm[s][c]);
+            const bool h1c = (jw[s][c] - c01 < nw1) && (w1[c].x & bm[s][c]);
             const uint32_t i0 = w0[c].y + __popc(w0[c].x & below);
             const uint32_t i1 = w1[c].y + __popc(w1[c].x & below);
-            b0[c] = *((w0[c].x & bm[s][c]) ? Bvals + i0 : zero);
-            b1[c] = *((w1[c].x & bm[s][c]) ? Bvals + i1 : zero);
+            b0[c] = *(h0c ? Bvals + i0 : zero);
+            b1[c] = *(h1c ? Bvals + i1 : zero);
           }
 #pragma unroll
           for (int c = 0; c < NC; ++c) {
@@ -510,9 +660,13 @@ __global__ __launch_bounds__(kRelaxThreads) void k_relax_pair(PairRelaxArgs A) {
   const float fn = (float)n;  // CPNP/MSA.cpp:1233-1235
 #pragma unroll
   for (int s = 0; s < SL; ++s) {
+    const int ti = (int)(tio[s] & 0xffff);
+    if (ti == 0) continue;
     const int g = tid + s * nt;
-    if (ti[s] == 0) continue;
-    const int e0 = rpxy[ti[s]] + NC * (g - tp[ti[s]]);
+    const int t = (int)(tio[s] >> 16);
+    const int4 o = oinf[t];
+    const int64_t exy = A.ent_off[o.x];
+    const int e0 = A.rowptr[A.rp_off[o.x] + ti] + NC * (g - o.z - tp[t * tps + ti]);
 #pragma unroll
     for (int c = 0; c < NC; ++c)
       if (bm[s][c]) A.out[exy + e0 + c] = acc[s][c] / fn;
@@ -526,19 +680,17 @@ hipError_t launch_pack(const PackArgs& a, hipStream_t st) {
 }
 
 template <int KP>
-static hipError_t launch_relax_kp(const PairRelaxArgs& a, int slots, size_t lds, hipStream_t st) {
-  const dim3 grid((unsigned)a.npairs), block(kRelaxThreads);
+static hipError_t launch_tiles_kp(const TileRelaxArgs& a, int slots, size_t lds, hipStream_t st) {
+  const dim3 grid((unsigned)a.ntiles), block(kRelaxThreads);
   switch (slots) {
 #define MLP_RELAX_CASE(SL)                                                                  \
   case SL:                                                                                  \
-    hipFuncSetAttribute((const void*)k_relax_pair<KP, SL>,                                  \
+    hipFuncSetAttribute((const void*)k_relax_tile<KP, SL>,                                  \
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);              \
-    hipLaunchKernelGGL((k_relax_pair<KP, SL>), grid, block, lds, st, a);                    \
+    hipLaunchKernelGGL((k_relax_tile<KP, SL>), grid, block, lds, st, a);                    \
     break;
-    MLP_RELAX_CASE(1)
     MLP_RELAX_CASE(2)
     MLP_RELAX_CASE(4)
-    MLP_RELAX_CASE(8)
 #undef MLP_RELAX_CASE
     default:
       return hipErrorInvalidValue;
@@ -546,15 +698,13 @@ static hipError_t launch_relax_kp(const PairRelaxArgs& a, int slots, size_t lds,
   return hipGetLastError();
 }
 
-hipError_t launch_relax_pairs(const PairRelaxArgs& a, int slots, hipStream_t st) {
-  if (a.npairs <= 0) return hipSuccess;
-  const size_t lds = pair_relax_lds(a.cap_a, a.cap_b, a.max_len);
-  switch (pair_relax_prefetch(std::max(a.cap_a, a.cap_b))) {
-    case 1: return launch_relax_kp<1>(a, slots, lds, st);
-    case 2: return launch_relax_kp<2>(a, slots, lds, st);
-    case 4: return launch_relax_kp<4>(a, slots, lds, st);
-    case 8: return launch_relax_kp<8>(a, slots, lds, st);
-    case 16: return launch_relax_kp<16>(a, slots, lds, st);
+hipError_t launch_relax_tiles(const TileRelaxArgs& a, int slots, hipStream_t st) {
+  if (a.ntiles <= 0) return hipSuccess;
+  const size_t lds = tile_relax_lds(a.cap, a.max_len);
+  const char* kp = getenv("MLP_RELAX_KP");  // test hook: force the large-prefetch variant
+  switch (kp ? atoi(kp) : tile_relax_prefetch(a.cap)) {
+    case 6: return launch_tiles_kp<6>(a, slots, lds, st);
+    case 12: return launch_tiles_kp<12>(a, slots, lds, st);
     default: return hipErrorInvalidValue;
   }
 }

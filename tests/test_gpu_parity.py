@@ -222,7 +222,7 @@ def test_family_features_cli_golden(name):
 
 
 def _relax_both_paths(seqs, pid, iters, tag):
-    """Pair-resident and row-task relaxation vs the oracle, bit-exact, `iters` rounds."""
+    """Tiled and row-task relaxation vs the oracle, bit-exact, `iters` rounds."""
     n = len(seqs)
     fam = Family(seqs)
     fam.posteriors(pid, 0.132548)
@@ -234,16 +234,21 @@ def _relax_both_paths(seqs, pid, iters, tag):
     for _ in range(iters):
         cur = orc.relax(lens, cur)
         refs.append(cur)
-    for mode in ('pairs', 'tasks'):
-        os.environ['MLP_RELAX'] = mode
+    # tiled kernel with up to 4 outputs per tile, one output per tile, the
+    # large-prefetch instantiation, and the row-task kernel
+    modes = [{'MLP_RELAX': 'pairs'}, {'MLP_RELAX': 'pairs', 'MLP_RELAX_TILE': '1'},
+             {'MLP_RELAX': 'pairs', 'MLP_RELAX_KP': '12'}, {'MLP_RELAX': 'tasks'}]
+    for env in modes:
+        os.environ.update(env)
         try:
             fam.import_csr(rp, eo, cols, vals)
             for it in range(iters):
                 fam.relax(1)
                 for k in range(len(refs[it])):
-                    csr_equal(refs[it][k], fam.sparse(k), f'{tag} {mode} it{it + 1} p{k}')
+                    csr_equal(refs[it][k], fam.sparse(k), f'{tag} {env} it{it + 1} p{k}')
         finally:
-            del os.environ['MLP_RELAX']
+            for key in env:
+                del os.environ[key]
     fam.close()
 
 

@@ -13,5 +13,5 @@ synth.write_fasta('$F.fa', synth.family($N, $L, 0.7, seed=11))
 t0=$(date +%s.%N)
 MLP_CLI_TIMES=1 ./mlprobs_amd/cli/c_p_np_aln -p 0 "$@" $F.fa > $F.mfa 2> $F.err
 t1=$(date +%s.%N)
-echo "N=$N L=$L wall $(echo "$t1 - $t0" | bc) s" | tee $F.time
+echo "N=$N L=$L wall $(awk "BEGIN{print $t1 - $t0}") s" | tee $F.time
 cat $F.err >> $F.time

@@ -16,7 +16,7 @@ def main():
     modes = sys.argv[3].split(',') if len(sys.argv) > 3 else ['default']
     seqs = [s for _, s in synth.family(n, L, 0.7, seed=11)]
     fam = engine.Family(seqs)
-    fam.posteriors(0, 0.0)
+    fam.posteriors(0, float(os.environ.get("MLP_DELTA", "0.132548")))
     csr = [a.copy() for a in fam.export()]
     print(f'n={n} L={L} nnz={len(csr[2])}', flush=True)
     for mode in modes:
