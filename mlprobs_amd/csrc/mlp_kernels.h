@@ -204,41 +204,30 @@ struct FilterArgs {
   int64_t npairs;
   int write;
 };
-// Block images for the tiled relaxation (relax.hip).  Every block P(a, b)
-// and its transpose is packed once per round as one record, in two
-// overlapping 16-byte aligned ranges that a workgroup stages into LDS:
-//   cols  u16[nnz]                             \
-//   rp    u16[R + 2]  (row_ptr, relative)       | A range: the block as the
-//   vals  f32[nnz]              \              /  left factor (CSR)
-//   hdr   u32[R + 1]             | B range: the block as the right factor
-//   words {u32 bits, u32 base}[NW] /  (row bitmaps over its column span)
-// R = rows of that orientation.  Row k's bitmap covers only the 32-column
-// words between its first and last entry: hdr[k] = woff | c0w << 16 | nw << 24
+// Row-bitmap images for the relaxation (relax.hip).  Every block P(a, b)
+// and its transpose is packed once per round as one 16-byte aligned record:
+//   vals  f32[nnz]
+//   hdr   u32[R + 1]
+//   words {u32 bits, u32 base}[NW]
+// R = rows of that orientation.  Row r's bitmap covers only the 32-column
+// words between its first and last entry: hdr[r] = woff | c0w << 16 | nw << 24
 // (first word index in `words`, first word's column / 32, word count; hdr[0]
 // is an empty row), words[woff + w] covers columns 32 (c0w + w) .. + 31 and
 // base is the entry index of its first set bit.  Divergent posteriors spread
 // ~10 entries of a row over ~100 columns, so this is ~3.5 words per row
-// instead of C / 32 + 1.  Image 2p is P(a, b) of pair p, image 2p + 1 its
-// transpose.  Needs C <= 8191 (c0w, nw fit 8 bits) and nnz < 65536.
+// instead of C / 32 + 1.  Image 2p is P(a, b) of pair p (rows a), image
+// 2p + 1 its transpose (rows b).  Needs C <= 8000 (c0w, nw fit 8 bits) and
+// nnz, NW < 65536.
 struct ImgLayout {
-  int64_t rp, vals, hdr, words, end;  // byte offsets (cols at 0)
+  int64_t hdr, words, end;  // byte offsets (vals at 0)
 };
 __host__ __device__ inline int64_t mlp_align16(int64_t v) { return (v + 15) & ~(int64_t)15; }
 __host__ __device__ inline ImgLayout img_layout(int rows, int64_t nnz, int64_t nwords) {
   ImgLayout l;
-  l.rp = mlp_align16(2 * nnz);
-  l.vals = mlp_align16(l.rp + 2 * (int64_t)(rows + 2));
-  l.hdr = mlp_align16(l.vals + 4 * nnz);
-  l.words = mlp_align16(l.hdr + 4 * (int64_t)(rows + 1));
-  l.end = l.words + 8 * nwords;
+  l.hdr = mlp_align16(4 * nnz);
+  l.words = l.hdr + mlp_align16(4 * (int64_t)(rows + 1));
+  l.end = mlp_align16(l.words + 8 * nwords);
   return l;
-}
-// A range bytes (= l.hdr) and B range bytes (= l.end - l.vals, rounded to 16)
-__host__ __device__ inline int64_t img_a_bytes(int rows, int64_t nnz) {
-  return mlp_align16(mlp_align16(mlp_align16(2 * nnz) + 2 * (int64_t)(rows + 2)) + 4 * nnz);
-}
-__host__ __device__ inline int64_t img_b_bytes(int rows, int64_t nnz, int64_t nwords) {
-  return mlp_align16(mlp_align16(4 * nnz) + mlp_align16(4 * (int64_t)(rows + 1)) + 8 * nwords);
 }
 struct PackArgs {
   int n;
@@ -275,14 +264,12 @@ struct TileRelaxArgs {
   int64_t ntiles;
   float* out;                // raw relaxed values at the input entry slots
   int cap;                   // LDS bytes for one staged tile (multiple of 16)
-  int max_len;               // longest sequence (task-prefix scratch)
 };
 constexpr int kTileInts = 2 * kTileMax + 1;
 constexpr int kRelaxThreads = 768;   // workgroup of the tiled relaxation (12 waves, 168 VGPRs)
-constexpr int kRelaxCells = 4;       // mask cells of one row per task
-size_t tile_relax_lds(int cap, int max_len);
+size_t tile_relax_lds(int cap);
 int tile_relax_prefetch(int cap);              // 16-byte chunks per thread, 0 = too large
-int tile_relax_slots(int64_t tasks);           // tasks per thread, 0 = too many
+int tile_relax_slots(int64_t cells);           // cells per thread, 0 = too many
 int tile_relax_max_cap();                      // largest tile the prefetch registers hold
 hipError_t launch_pack(const PackArgs& a, hipStream_t st);
 hipError_t launch_relax_tiles(const TileRelaxArgs& a, int slots, hipStream_t st);

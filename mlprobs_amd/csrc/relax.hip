@@ -251,16 +251,10 @@ __global__ __launch_bounds__(256) void k_pack(PackArgs A) {
   }
   const ImgLayout L = img_layout(rows, nnz, A.nwords[q]);
   uint8_t* dst = A.img + A.img_off[q];
-  uint16_t* dcols = (uint16_t*)dst;
-  uint16_t* drp = (uint16_t*)(dst + L.rp);
-  float* dvals = (float*)(dst + L.vals);
+  float* dvals = (float*)dst;
   uint32_t* dhdr = (uint32_t*)(dst + L.hdr);
   uint2* dwords = (uint2*)(dst + L.words);
-  for (int k = lane; k < rows + 2; k += 64) drp[k] = (uint16_t)rp[k];
-  for (int64_t e = lane; e < nnz; e += 64) {
-    dcols[e] = cols[e];
-    dvals[e] = vals[e];
-  }
+  for (int64_t e = lane; e < nnz; e += 64) dvals[e] = vals[e];
   if (lane == 0) dhdr[0] = 0;
   int run = 0;  // words before this 64-row chunk
   for (int k0 = 1; k0 <= rows; k0 += 64) {
@@ -292,42 +286,33 @@ __global__ __launch_bounds__(256) void k_pack(PackArgs A) {
 }
 
 // ------------------------------------------------------------ tiled relaxation
-// One workgroup per tile of up to kTileMax output pairs (x_t, y) sharing y.
-// The output cells (the mask: the pattern of P_{x_t y}, CPNP/MSA.cpp:1237-1261)
-// are cut into tasks of up to four cells of one row i; a thread owns a few
-// tasks, their accumulators live in registers.  For each z (ascending) the
-// workgroup stages the A_t = P(x_t, z) blocks (CSR) and the one shared
-// B = P(z, y) block (row bitmaps over each row's column span) in LDS -- the
-// next z's ranges are prefetched into registers while the current z is
-// computed -- and a task walks A_t row i (k ascending), looking its cells'
-// columns j up in the bitmap of B row k.  Each cell's sum therefore runs
-// z ascending, then k ascending: the order of Relax / Relax1
-// (CPNP/MSA.cpp:1276-1350), so every float sum is bit-identical to the
-// reference's.  Sharing B across the tile halves (T = 2) to quarters (T = 4)
-// the B traffic per output pair; the XCD-aware tile order lets tiles with the
-// same x group run on one XCD, so their A blocks meet in that XCD's L2.
+// One workgroup per tile of up to kTileMax output pairs (x_t, y) sharing y;
+// one thread slot per output cell (i, j) of the masks (the patterns of
+// P_{x_t y}, CPNP/MSA.cpp:1237-1261), its accumulator in a register.  For
+// each z (ascending) the workgroup stages the row bitmaps of A_t = P(x_t, z)
+// (rows i) and of the one shared C = P(y, z) (rows j, i.e. P(z, y)
+// transposed) in LDS -- the next z's images are prefetched into registers
+// while the current z is computed -- and a cell intersects A_t row i with
+// C row j word by word: each common column k contributes
+// P_{x_t z}(i, k) * P_{z y}(k, j).  Set bits are taken lowest first, so each
+// cell's sum runs z ascending, then k ascending: the order of Relax / Relax1
+// (CPNP/MSA.cpp:1276-1350), and every float sum is bit-identical to the
+// reference's.  A divergent C3 cell meets ~1.2 common columns per z over
+// ~1.8 overlapping words, where a lookup per A entry costs ~11 probes.
+// Sharing C across the tile divides its traffic per output pair by T; the
+// XCD-aware tile order lets tiles of one x group run on one XCD, so their A
+// blocks meet in that XCD's L2.
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));  // plain vector: stays in VGPRs
 #ifdef MLP_RELAX_NOLOAD  // timing experiment: no global loads for the staging
 #define MLP_PF_LOAD(dst, src) (dst) = u32x4{(uint32_t)c, 0u, 0u, 0u}
 #else
 #define MLP_PF_LOAD(dst, src) (dst) = (src)
 #endif
-#ifdef MLP_RELAX_SEQADDR  // timing experiment: each workgroup streams consecutive memory over z
-#define MLP_PF_SRC ((uint32_t)((((uint64_t)tile * 7919 + (uint64_t)zcount) * (uint64_t)tot_) % (uint64_t)(A.img_chunks - tot_)) + (uint32_t)c)
-#else
-#define MLP_PF_SRC ((uint32_t)(c + d))
-#endif
-constexpr int kRelaxZChunk = 128;  // z schedule entries per LDS fill (48 B each)
-constexpr int kRelaxGuard = 2048;  // LDS bytes after the tile: unchecked bitmap-word reads stay inside
-static __host__ __device__ inline size_t relax_tp_bytes(int max_len) {
-  return (4 * (size_t)kTileMax * (max_len + 2) + 15) & ~(size_t)15;
-}
-// LDS: [z schedule][task prefixes][per-output A bases][zero][tile][guard];
-// the schedule (6 KB) in front keeps unchecked reads below the tile inside too
-static __host__ __device__ inline size_t relax_tile_off(int max_len) {
-  return 48 * (size_t)kRelaxZChunk + relax_tp_bytes(max_len) + 32 * kTileMax + 16;
-}
-size_t tile_relax_lds(int cap, int max_len) { return relax_tile_off(max_len) + (size_t)cap + kRelaxGuard; }
+constexpr int kRelaxZChunk = 128;  // z schedule entries per LDS fill (64 B each)
+constexpr int kZEntBytes = 64;
+// LDS: [z schedule][per-output A bases][tile]
+static __host__ __device__ inline size_t relax_tile_off() { return (size_t)kZEntBytes * kRelaxZChunk + 16 * kTileMax; }
+size_t tile_relax_lds(int cap) { return relax_tile_off() + (size_t)cap + 16; }  // + a word pair read past the last row
 
 int tile_relax_prefetch(int cap) {
   const int chunks = (cap / 16 + kRelaxThreads - 1) / kRelaxThreads;
@@ -338,13 +323,12 @@ int tile_relax_prefetch(int cap) {
 
 int tile_relax_max_cap() { return 12 * kRelaxThreads * 16; }
 
-int tile_relax_slots(int64_t tasks) {
-  const int64_t per = (tasks + kRelaxThreads - 1) / kRelaxThreads;
-  for (int sl : {2, 4})
+int tile_relax_slots(int64_t cells) {
+  const int64_t per = (cells + kRelaxThreads - 1) / kRelaxThreads;
+  for (int sl : {4, 8, 12, 16})
     if (per <= sl) return sl;
   return 0;
 }
-
 
 // workgroup-uniform values read from LDS: keep them in SGPRs
 __device__ __forceinline__ uint4 rfl(uint4 v) {
@@ -356,7 +340,6 @@ template <int KP, int SL>
 __global__ __launch_bounds__(kRelaxThreads) void k_relax_tile(TileRelaxArgs A) {
   extern __shared__ __align__(16) uint8_t lds[];
   constexpr int nt = kRelaxThreads;
-  constexpr int NC = kRelaxCells;
   constexpr int TM = kTileMax;
   const int tid = threadIdx.x;
   // blocks b, b + 8, ... share an XCD: give each XCD a contiguous run of tiles
@@ -366,6 +349,7 @@ __global__ __launch_bounds__(kRelaxThreads) void k_relax_tile(TileRelaxArgs A) {
   const int32_t* td = A.tiles + tile * kTileInts;
   const int n = A.n;
   int pt[TM], xt[TM], Lxt[TM];
+  int64_t eo[TM];
   int T = 0;
 #pragma unroll
   for (int t = 0; t < TM; ++t) {
@@ -373,115 +357,69 @@ __global__ __launch_bounds__(kRelaxThreads) void k_relax_tile(TileRelaxArgs A) {
     xt[t] = td[TM + t];
     T = pt[t] >= 0 ? t + 1 : T;
     Lxt[t] = pt[t] >= 0 ? A.lens[xt[t]] : 0;
+    eo[t] = pt[t] >= 0 ? A.ent_off[pt[t]] : 0;
   }
   const int y = td[2 * TM];
-  const int tps = A.max_len + 2;
+  const int Ly = A.lens[y];
   uint4* ztab = (uint4*)lds;
-  int32_t* tp = (int32_t*)(lds + 48 * kRelaxZChunk);  // per output: tasks before row i
-  int4* zb = (int4*)(lds + 48 * kRelaxZChunk + relax_tp_bytes(A.max_len));  // per output: A bases this z
-  int4* oinf = zb + TM;  // per output: {pair, L_x, tasks before it, -} (per-lane lookups by output)
-  float* zero = (float*)(oinf + TM);
-  uint8_t* tileb = lds + relax_tile_off(A.max_len);
-
-  // task prefixes: wave t scans output t (row i contributes ceil(m_i / NC))
-  {
-    const int wv = tid >> 6, ln = tid & 63;
-    if (wv < T) {
-      const int64_t p = td[wv];
-      const int Lx = A.lens[td[TM + wv]];
-      const int32_t* rpxy = A.rowptr + A.rp_off[p];
-      int32_t* tw = tp + wv * tps;
-      int run = 0;
-      if (ln == 0) tw[1] = 0;
-      for (int r0 = 1; r0 <= Lx; r0 += 64) {
-        const int i = r0 + ln;
-        const int c = i <= Lx ? (rpxy[i + 1] - rpxy[i] + NC - 1) / NC : 0;
-        int xs = c;
-        for (int off = 1; off < 64; off <<= 1) {
-          const int v = __shfl_up(xs, off);
-          if (ln >= off) xs += v;
-        }
-        if (i <= Lx) tw[i + 1] = run + xs;
-        run += __shfl(xs, 63);
-      }
-    }
-    if (tid == 0) *zero = 0.f;
-  }
-  __syncthreads();
-  int tb[TM + 1];
-  tb[0] = 0;
+  int4* zb = (int4*)(lds + kZEntBytes * kRelaxZChunk);  // per output: A_t image bases this z
+  uint8_t* tileb = lds + relax_tile_off();
+  // cells before output t (the masks' entries, in CSR order)
+  int cb[TM + 1];
+  cb[0] = 0;
 #pragma unroll
-  for (int t = 0; t < TM; ++t)
-    tb[t + 1] = tb[t] + (t < T ? __builtin_amdgcn_readfirstlane(tp[t * tps + Lxt[t] + 1]) : 0);
-  if (tid < TM) {
-    int4 o = make_int4(-1, 0, 0, 0);
-#pragma unroll
-    for (int t = 0; t < TM; ++t)
-      if (tid == t) o = make_int4(pt[t], Lxt[t], tb[t], 0);
-    oinf[tid] = o;
-  }
-  __syncthreads();
+  for (int t = 0; t < TM; ++t) cb[t + 1] = cb[t] + (t < T ? (int)(A.ent_off[pt[t] + 1] - eo[t]) : 0);
 
-  uint32_t tio[SL];     // row i (0 = no task) | output t << 16 of each task
-  uint32_t jw[SL][NC];  // the cell's 32-column word index j >> 5
-  uint32_t bm[SL][NC];  // the cell's bit (0 = no cell: never hits)
-  float acc[SL][NC];
+  // slot s of this thread: cell g = tid + s * nt: i | j << 13 | t << 26 (0 = none)
+  uint32_t cel[SL];
+  float acc[SL];
 #pragma unroll
   for (int s = 0; s < SL; ++s) {
     const int g = tid + s * nt;
-    tio[s] = 0;
-#pragma unroll
-    for (int c = 0; c < NC; ++c) { jw[s][c] = 0; bm[s][c] = 0; acc[s][c] = 0.f; }
-    if (g < tb[TM]) {
+    cel[s] = 0;
+    acc[s] = 0.f;
+    if (g < cb[TM]) {
       int t = 0;
 #pragma unroll
-      for (int u = 1; u < TM; ++u) t += g >= tb[u] ? 1 : 0;
-      const int4 o = oinf[t];
-      const int gl = g - o.z;
-      const int32_t* tt = tp + t * tps;
-      int lo = 1, hi = o.y;  // last row with tt[row] <= gl
+      for (int u = 1; u < TM; ++u) t += g >= cb[u] ? 1 : 0;
+      int e = g, Lx = Lxt[0], p = pt[0];
+      int64_t ex = eo[0];
+#pragma unroll
+      for (int u = 1; u < TM; ++u)
+        if (t == u) { e = g - cb[u]; Lx = Lxt[u]; p = pt[u]; ex = eo[u]; }
+      const int32_t* rp = A.rowptr + A.rp_off[p];
+      int lo = 1, hi = Lx;  // row i: last row with rp[i] <= e
       while (lo < hi) {
         const int mid = (lo + hi + 1) >> 1;
-        if (tt[mid] <= gl) lo = mid; else hi = mid - 1;
+        if (rp[mid] <= e) lo = mid; else hi = mid - 1;
       }
-      const int64_t p = o.x;
-      const int64_t exy = A.ent_off[p];
-      const int32_t* rpxy = A.rowptr + A.rp_off[p];
-      tio[s] = (uint32_t)lo | (uint32_t)t << 16;
-      const int e0 = rpxy[lo] + NC * (gl - tt[lo]), e1 = rpxy[lo + 1];
-#pragma unroll
-      for (int c = 0; c < NC; ++c)
-        if (e0 + c < e1) {
-          const uint32_t j = A.cols[exy + e0 + c];
-          jw[s][c] = j >> 5;
-          bm[s][c] = 1u << (j & 31);
-          const float v = A.vals[exy + e0 + c];
-          acc[s][c] = v + v;  // z = x and z = y (CPNP/MSA.cpp:1211-1213)
-        }
+      const uint32_t j = A.cols[ex + e];
+      cel[s] = (uint32_t)lo | j << 13 | (uint32_t)t << 26;
+      const float v = A.vals[ex + e];
+      acc[s] = v + v;  // z = x and z = y (CPNP/MSA.cpp:1211-1213)
     }
   }
 
-  // The z schedule, kRelaxZChunk values of z at a time, in LDS (3 uint4 per
-  // z): {B range start / 16, nnz(B) | L_z << 16 (0: skip z), B chunks, -},
-  // {A_t range start / 16}, {nnz(A_t) (0: output t skips z)}.  z = y, an
-  // empty B or no live A_t skip the whole z.
+  // The z schedule, kRelaxZChunk values of z at a time, in LDS (4 uint4 per
+  // z): {C start / 16, nnz(C) (0: skip z), C chunks, L_z}, {A_t start / 16},
+  // {nnz(A_t) (0: output t skips z)}, {A_t chunks}.  z = y, an empty C or no
+  // live A_t skip the whole z.
   int zbase = 0, zpos = -1;
   auto fill = [&]() {
     __syncthreads();  // every wave is done reading the previous chunk
     if (tid < kRelaxZChunk) {
       const int z = zbase + tid;
-      uint4 e0 = make_uint4(0, 0, 0, 0), e1 = e0, e2 = e0;
+      uint4 e0 = make_uint4(0, 0, 0, 0), e1 = e0, e2 = e0, e3 = e0;
       if (z < n && z != y) {
-        int64_t pb, qb;
-        if (z < y) { pb = pair_index(n, z, y); qb = 2 * pb; } else { pb = pair_index(n, y, z); qb = 2 * pb + 1; }
-        const int nbz = (int)(A.ent_off[pb + 1] - A.ent_off[pb]);
-        if (nbz > 0) {
-          uint32_t ao[TM], na[TM];
+        int64_t pc, qc;
+        if (y < z) { pc = pair_index(n, y, z); qc = 2 * pc; } else { pc = pair_index(n, z, y); qc = 2 * pc + 1; }
+        const int nzc = (int)(A.ent_off[pc + 1] - A.ent_off[pc]);
+        if (nzc > 0) {
+          uint32_t ao[TM], na[TM], ac[TM];
           bool any = false;
 #pragma unroll
           for (int t = 0; t < TM; ++t) {
-            ao[t] = 0;
-            na[t] = 0;
+            ao[t] = na[t] = ac[t] = 0;
             const int xx = td[TM + t];  // (not xt[]: arrays captured by a lambda end up in scratch)
             if (td[t] >= 0 && z != xx) {
               int64_t pa, qa;
@@ -490,29 +428,29 @@ __global__ __launch_bounds__(kRelaxThreads) void k_relax_tile(TileRelaxArgs A) {
               if (nza > 0) {
                 ao[t] = (uint32_t)(A.img_off[qa] >> 4);
                 na[t] = (uint32_t)nza;
+                ac[t] = (uint32_t)((A.img_off[qa + 1] - A.img_off[qa]) >> 4);
                 any = true;
               }
             }
           }
           if (any) {
-            const int Lz = A.lens[z];
-            const int nw = A.nwords[qb];
-            const ImgLayout lb = img_layout(Lz, nbz, nw);
-            e0 = make_uint4((uint32_t)((A.img_off[qb] + lb.vals) >> 4), (uint32_t)nbz | ((uint32_t)Lz << 16),
-                            (uint32_t)(img_b_bytes(Lz, nbz, nw) >> 4), 0);
+            e0 = make_uint4((uint32_t)(A.img_off[qc] >> 4), (uint32_t)nzc,
+                            (uint32_t)((A.img_off[qc + 1] - A.img_off[qc]) >> 4), (uint32_t)A.lens[z]);
             e1 = make_uint4(ao[0], ao[1], ao[2], ao[3]);
             e2 = make_uint4(na[0], na[1], na[2], na[3]);
+            e3 = make_uint4(ac[0], ac[1], ac[2], ac[3]);
           }
         }
       }
-      ztab[3 * tid] = e0;
-      ztab[3 * tid + 1] = e1;
-      ztab[3 * tid + 2] = e2;
+      ztab[4 * tid] = e0;
+      ztab[4 * tid + 1] = e1;
+      ztab[4 * tid + 2] = e2;
+      ztab[4 * tid + 3] = e3;
     }
     __syncthreads();
   };
   // next scheduled z (uniform across the workgroup); returns false when done
-  uint4 nB, nAo, nNa;  // the staged-next z's entry
+  uint4 nC, nAo, nNa, nAc;  // the staged-next z's entry
   auto next = [&]() -> bool {
     for (;;) {
       if (++zpos == kRelaxZChunk) {
@@ -522,15 +460,16 @@ __global__ __launch_bounds__(kRelaxThreads) void k_relax_tile(TileRelaxArgs A) {
         fill();
       }
       if (zbase + zpos >= n) return false;
-      nB = rfl(ztab[3 * zpos]);
-      if (nB.y) {
-        nAo = rfl(ztab[3 * zpos + 1]);
-        nNa = rfl(ztab[3 * zpos + 2]);
+      nC = rfl(ztab[4 * zpos]);
+      if (nC.y) {
+        nAo = rfl(ztab[4 * zpos + 1]);
+        nNa = rfl(ztab[4 * zpos + 2]);
+        nAc = rfl(ztab[4 * zpos + 3]);
         return true;
       }
     }
   };
-  // register prefetch of the next z's tile: segments A_0 .. A_{TM-1}, B,
+  // register prefetch of the next z's tile: segments A_0 .. A_{TM-1}, C,
   // contiguous in LDS (written out: arrays captured by a lambda end up in scratch)
   u32x4 pf[KP];
   int sg[TM + 1];  // segment starts (16-byte chunks) of the prefetched tile
@@ -538,138 +477,135 @@ __global__ __launch_bounds__(kRelaxThreads) void k_relax_tile(TileRelaxArgs A) {
 #define MLP_ISSUE()                                                                      \
   {                                                                                      \
     const uint32_t ao_[TM] = {nAo.x, nAo.y, nAo.z, nAo.w};                               \
-    const uint32_t na_[TM] = {nNa.x, nNa.y, nNa.z, nNa.w};                               \
+    const uint32_t ac_[TM] = {nAc.x, nAc.y, nAc.z, nAc.w};                               \
     int dl_[TM];                                                                         \
     sg[0] = 0;                                                                           \
     _Pragma("unroll") for (int t = 0; t < TM; ++t) {                                     \
-      const int ca_ = na_[t] ? (int)(img_a_bytes(Lxt[t], na_[t]) >> 4) : 0;              \
       dl_[t] = (int)ao_[t] - sg[t];                                                      \
-      sg[t + 1] = sg[t] + ca_;                                                           \
+      sg[t + 1] = sg[t] + (int)ac_[t];                                                   \
     }                                                                                    \
-    const int tot_ = sg[TM] + (int)nB.z;                                                 \
-    const int dB_ = (int)nB.x - sg[TM];                                                  \
+    const int tot_ = sg[TM] + (int)nC.z;                                                 \
+    const int dC_ = (int)nC.x - sg[TM];                                                  \
     _Pragma("unroll") for (int m = 0; m < KP; ++m) {                                     \
       const int c = tid + m * nt;                                                        \
       if (c < tot_) {                                                                    \
-        int d = dB_;                                                                     \
+        int d = dC_;                                                                     \
         _Pragma("unroll") for (int t = TM - 1; t >= 0; --t) d = c < sg[t + 1] ? dl_[t] : d; \
-        MLP_PF_LOAD(pf[m], g16[MLP_PF_SRC]);                                             \
+        MLP_PF_LOAD(pf[m], g16[(uint32_t)(c + d)]);                                      \
       }                                                                                  \
     }                                                                                    \
   }
   fill();
-  int zcount = 0;
-  (void)zcount;
   bool more = next();
   if (more) MLP_ISSUE();
-#ifdef MLP_RELAX_SAMEADDR  // timing experiment: every z loads the first z's tile again
-  const uint4 fB = nB, fAo = nAo, fNa = nNa;
-#endif
-#ifdef MLP_RELAX_NOSTAGE  // timing experiment: every z computes on the first z's tile
-  const uint4 fB = nB, fAo = nAo, fNa = nNa;
+#ifdef MLP_RELAX_NOSTAGE
+  const uint4 fC = nC, fAo = nAo, fNa = nNa, fAc = nAc;
 #endif
   while (more) {
     // stage the prefetched tile; outputs' A bases (+ validity) into zb
-    const int tot = sg[TM] + (int)nB.z;
+    const int tot = sg[TM] + (int)nC.z;
 #pragma unroll
     for (int m = 0; m < KP; ++m) {
       const int c = tid + m * nt;
       if (c < tot) ((u32x4*)tileb)[c] = pf[m];
     }
-    const int Lz = (int)(nB.y >> 16), nzB = (int)(nB.y & 0xffff);
-    const uint32_t boff = (uint32_t)(relax_tile_off(A.max_len) + 16 * (size_t)sg[TM]);
+    const uint32_t cbase = (uint32_t)(relax_tile_off() + 16 * (size_t)sg[TM]);
+    const int nzC = (int)nC.y;
     if (tid == 0) {
       const uint32_t na_[TM] = {nNa.x, nNa.y, nNa.z, nNa.w};
 #pragma unroll
       for (int t = 0; t < TM; ++t) {
-        const uint32_t ab = (uint32_t)(relax_tile_off(A.max_len) + 16 * (size_t)sg[t]);
-        const uint32_t rpo = ab + (uint32_t)mlp_align16(2 * (int64_t)na_[t]);
-        zb[t] = make_int4((int)ab, (int)rpo, (int)(rpo + (uint32_t)mlp_align16(2 * (int64_t)(Lxt[t] + 2))),
+        const uint32_t ab = (uint32_t)(relax_tile_off() + 16 * (size_t)sg[t]);
+        const uint32_t ho = ab + (uint32_t)mlp_align16(4 * (int64_t)na_[t]);
+        zb[t] = make_int4((int)ab, (int)ho, (int)(ho + (uint32_t)mlp_align16(4 * (int64_t)(Lxt[t] + 1))),
                           (int)na_[t]);
       }
     }
     __syncthreads();
     more = next();
-    ++zcount;
-#ifdef MLP_RELAX_NOSTAGE
-    nB = fB; nAo = fAo; nNa = fNa;
+#ifdef MLP_RELAX_NOSTAGE  // timing experiment: every z computes on the first z's tile
+    nC = fC; nAo = fAo; nNa = fNa; nAc = fAc;
 #else
-#ifdef MLP_RELAX_SAMEADDR
-    nB = fB; nAo = fAo; nNa = fNa;
-#endif
     if (more) MLP_ISSUE();
 #endif
+#ifndef MLP_RELAX_NOCOMPUTE  // (timing experiment: staging only)
     {
-      const float* Bvals = (const float*)(lds + boff);
-      const uint32_t* Bhdr = (const uint32_t*)(lds + boff + (uint32_t)mlp_align16(4 * (int64_t)nzB));
-      const uint2* Bwords = (const uint2*)((const uint8_t*)Bhdr + (uint32_t)mlp_align16(4 * (int64_t)(Lz + 1)));
+      const float* Cvals = (const float*)(lds + cbase);
+      const uint32_t* Chdr = (const uint32_t*)(lds + cbase + (uint32_t)mlp_align16(4 * (int64_t)nzC));
+      const uint2* Cwords = (const uint2*)((const uint8_t*)Chdr + (uint32_t)mlp_align16(4 * (int64_t)(Ly + 1)));
+      // row headers of slot s + 1 are read while slot s intersects
+      auto headers = [&](uint32_t cl, int4& z4, uint32_t& ha, uint32_t& hc) {
+        z4 = zb[cl >> 26];
+        ha = z4.w ? ((const uint32_t*)(lds + z4.y))[cl & 0x1fff] : 0u;  // nw 0: no words
+        hc = Chdr[(cl >> 13) & 0x1fff];
+      };
+      uint32_t cl = cel[0];
+      asm volatile("" : "+v"(cl));
+      int4 z4;
+      uint32_t ha, hc;
+      headers(cl, z4, ha, hc);
 #pragma unroll
       for (int s = 0; s < SL; ++s) {
-        const int ti = (int)(tio[s] & 0xffff);
-#ifdef MLP_RELAX_NOCOMPUTE  // timing experiment: staging only
-        continue;
-#endif
-        if (ti == 0) continue;
-        const int4 z4 = zb[tio[s] >> 16];
-        if (z4.w == 0) continue;
-        const uint16_t* Acols = (const uint16_t*)(lds + z4.x);
-        const uint16_t* Arp = (const uint16_t*)(lds + z4.y);
-        const float* Avals = (const float*)(lds + z4.z);
-        const int a0 = Arp[ti], a1 = Arp[ti + 1];
-        // two A entries per iteration (the second a zero-weight copy of the
-        // first past the row end: + 0.0f leaves a positive sum unchanged)
-        for (int t = a0; t < a1; t += 2) {
-          const bool two = t + 1 < a1;
-          const int k0 = Acols[t], k1 = Acols[two ? t + 1 : t];
-          const float av0 = Avals[t];
-          const float av1 = two ? Avals[t + 1] : 0.f;
-          const uint32_t h0 = Bhdr[k0], h1 = Bhdr[k1];
-          // word of column word jw in row k: woff + (jw - c0w), valid iff jw - c0w < nw
-          const int o0 = (int)(h0 & 0xffff) - (int)((h0 >> 16) & 0xff);
-          const int o1 = (int)(h1 & 0xffff) - (int)((h1 >> 16) & 0xff);
-          const uint32_t c00 = (h0 >> 16) & 0xff, c01 = (h1 >> 16) & 0xff;
-          const uint32_t nw0 = h0 >> 24, nw1 = h1 >> 24;
-          uint2 w0[NC], w1[NC];
-#pragma unroll
-          for (int c = 0; c < NC; ++c) {  // unchecked: |jw - c0w| < 256 words stays in LDS
-            w0[c] = Bwords[o0 + (int)jw[s][c]];
-            w1[c] = Bwords[o1 + (int)jw[s][c]];
-          }
-          float b0[NC], b1[NC];
-#pragma unroll
-          for (int c = 0; c < NC; ++c) {
-            const uint32_t below = bm[s][c] - 1u;
-            const bool h0c = (jw[s][c] - c00 < nw0) && (w0[c].x & bm[s][c]);
-            const bool h1c = (jw[s][c] - c01 < nw1) && (w1[c].x & bm[s][c]);
-            const uint32_t i0 = w0[c].y + __popc(w0[c].x & below);
-            const uint32_t i1 = w1[c].y + __popc(w1[c].x & below);
-            b0[c] = *(h0c ? Bvals + i0 : zero);
-            b1[c] = *(h1c ? Bvals + i1 : zero);
-          }
-#pragma unroll
-          for (int c = 0; c < NC; ++c) {
-            acc[s][c] += av0 * b0[c];  // a miss adds av * 0 = +0: no change
-            acc[s][c] += av1 * b1[c];
-          }
+        uint32_t cl1 = 0, ha1 = 0, hc1 = 0;
+        int4 z41 = make_int4(0, 0, 0, 0);
+        if (s + 1 < SL) {
+          cl1 = cel[s + 1];
+          // re-derive the cells' offsets every z: hoisting them out of the z
+          // loop would hold ~4 more registers per slot
+          asm volatile("" : "+v"(cl1));
+          headers(cl1, z41, ha1, hc1);
         }
+        if (cl != 0) {
+          const int a0 = (int)((ha >> 16) & 0xff), c0 = (int)((hc >> 16) & 0xff);
+          const int we = min(a0 + (int)(ha >> 24), c0 + (int)(hc >> 24));
+          const uint2* pa = (const uint2*)(lds + z4.z) + ((int)(ha & 0xffff) - a0);
+          const uint2* pc = Cwords + ((int)(hc & 0xffff) - c0);
+          const float* Avals = (const float*)(lds + z4.x);
+          float ac = acc[s];
+          // two words per step (the second masked off past the overlap)
+          for (int w = max(a0, c0); w < we; w += 2) {
+            const uint2 xa0 = pa[w], xa1 = pa[w + 1], xc0 = pc[w], xc1 = pc[w + 1];
+            uint32_t m0 = xa0.x & xc0.x;
+            uint32_t m1 = w + 1 < we ? xa1.x & xc1.x : 0u;
+            while (m0) {  // common columns k, ascending
+              const uint32_t bit = 1u << __builtin_ctz(m0);
+              m0 ^= bit;
+              const float va = Avals[xa0.y + __popc(xa0.x & (bit - 1u))];
+              const float vc = Cvals[xc0.y + __popc(xc0.x & (bit - 1u))];
+              ac += va * vc;
+            }
+            while (m1) {
+              const uint32_t bit = 1u << __builtin_ctz(m1);
+              m1 ^= bit;
+              const float va = Avals[xa1.y + __popc(xa1.x & (bit - 1u))];
+              const float vc = Cvals[xc1.y + __popc(xc1.x & (bit - 1u))];
+              ac += va * vc;
+            }
+          }
+          acc[s] = ac;
+        }
+        cl = cl1;
+        z4 = z41;
+        ha = ha1;
+        hc = hc1;
       }
     }
+#endif
     __syncthreads();
   }
 #undef MLP_ISSUE
   const float fn = (float)n;  // CPNP/MSA.cpp:1233-1235
 #pragma unroll
   for (int s = 0; s < SL; ++s) {
-    const int ti = (int)(tio[s] & 0xffff);
-    if (ti == 0) continue;
+    if (cel[s] == 0) continue;
     const int g = tid + s * nt;
-    const int t = (int)(tio[s] >> 16);
-    const int4 o = oinf[t];
-    const int64_t exy = A.ent_off[o.x];
-    const int e0 = A.rowptr[A.rp_off[o.x] + ti] + NC * (g - o.z - tp[t * tps + ti]);
+    const int t = (int)(cel[s] >> 26);
+    int e = g;
+    int64_t ex = eo[0];
 #pragma unroll
-    for (int c = 0; c < NC; ++c)
-      if (bm[s][c]) A.out[exy + e0 + c] = acc[s][c] / fn;
+    for (int u = 1; u < TM; ++u)
+      if (t == u) { e = g - cb[u]; ex = eo[u]; }
+    A.out[ex + e] = acc[s] / fn;
   }
 }
 
@@ -689,8 +625,10 @@ static hipError_t launch_tiles_kp(const TileRelaxArgs& a, int slots, size_t lds,
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);              \
     hipLaunchKernelGGL((k_relax_tile<KP, SL>), grid, block, lds, st, a);                    \
     break;
-    MLP_RELAX_CASE(2)
     MLP_RELAX_CASE(4)
+    MLP_RELAX_CASE(8)
+    MLP_RELAX_CASE(12)
+    MLP_RELAX_CASE(16)
 #undef MLP_RELAX_CASE
     default:
       return hipErrorInvalidValue;
@@ -700,7 +638,7 @@ static hipError_t launch_tiles_kp(const TileRelaxArgs& a, int slots, size_t lds,
 
 hipError_t launch_relax_tiles(const TileRelaxArgs& a, int slots, hipStream_t st) {
   if (a.ntiles <= 0) return hipSuccess;
-  const size_t lds = tile_relax_lds(a.cap, a.max_len);
+  const size_t lds = tile_relax_lds(a.cap);
   const char* kp = getenv("MLP_RELAX_KP");  // test hook: force the large-prefetch variant
   switch (kp ? atoi(kp) : tile_relax_prefetch(a.cap)) {
     case 6: return launch_tiles_kp<6>(a, slots, lds, st);

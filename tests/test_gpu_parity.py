@@ -166,6 +166,13 @@ def test_batches_of_one(monkeypatch):
     _check_family_vs_oracle([x for _, x in synth.family(5, 70, 0.6, seed=44)], 2, 'batch1')
 
 
+def test_pipelined_batches(monkeypatch):
+    """Several batches alternating over the two posterior streams (all three
+    models): compaction order, store growth and records stay pair-ordered."""
+    monkeypatch.setenv('MLP_SCRATCH_GB', '0.004')
+    _check_family_vs_oracle(_ragged_family(14, 60, 220, 45), 0, 'pipe')
+
+
 # ---- family test: Viterbi alignments (CPNP/MSA.cpp:646-882)
 @pytest.mark.parametrize('name', family_names())
 def test_model_adjustment_golden(name):
