@@ -266,7 +266,7 @@ struct TileRelaxArgs {
   int cap;                   // LDS bytes for one staged tile (multiple of 16)
 };
 constexpr int kTileInts = 2 * kTileMax + 1;
-constexpr int kRelaxThreads = 768;   // workgroup of the tiled relaxation (12 waves, 168 VGPRs)
+constexpr int kRelaxThreads = 1024;  // workgroup of the tiled relaxation (16 waves, 128 VGPRs)
 size_t tile_relax_lds(int cap);
 int tile_relax_prefetch(int cap);              // 16-byte chunks per thread, 0 = too large
 int tile_relax_slots(int64_t cells);           // cells per thread, 0 = too many

@@ -316,16 +316,16 @@ size_t tile_relax_lds(int cap) { return relax_tile_off() + (size_t)cap + 16; }  
 
 int tile_relax_prefetch(int cap) {
   const int chunks = (cap / 16 + kRelaxThreads - 1) / kRelaxThreads;
-  for (int kp : {6, 12})
+  for (int kp : {5, 9})
     if (chunks <= kp) return kp;
   return 0;
 }
 
-int tile_relax_max_cap() { return 12 * kRelaxThreads * 16; }
+int tile_relax_max_cap() { return 9 * kRelaxThreads * 16; }
 
 int tile_relax_slots(int64_t cells) {
   const int64_t per = (cells + kRelaxThreads - 1) / kRelaxThreads;
-  for (int sl : {4, 8, 12, 16})
+  for (int sl : {4, 8, 12})
     if (per <= sl) return sl;
   return 0;
 }
@@ -628,7 +628,6 @@ static hipError_t launch_tiles_kp(const TileRelaxArgs& a, int slots, size_t lds,
     MLP_RELAX_CASE(4)
     MLP_RELAX_CASE(8)
     MLP_RELAX_CASE(12)
-    MLP_RELAX_CASE(16)
 #undef MLP_RELAX_CASE
     default:
       return hipErrorInvalidValue;
@@ -641,8 +640,8 @@ hipError_t launch_relax_tiles(const TileRelaxArgs& a, int slots, hipStream_t st)
   const size_t lds = tile_relax_lds(a.cap);
   const char* kp = getenv("MLP_RELAX_KP");  // test hook: force the large-prefetch variant
   switch (kp ? atoi(kp) : tile_relax_prefetch(a.cap)) {
-    case 6: return launch_tiles_kp<6>(a, slots, lds, st);
-    case 12: return launch_tiles_kp<12>(a, slots, lds, st);
+    case 5: return launch_tiles_kp<5>(a, slots, lds, st);
+    case 9: return launch_tiles_kp<9>(a, slots, lds, st);
     default: return hipErrorInvalidValue;
   }
 }

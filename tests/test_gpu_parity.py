@@ -244,7 +244,7 @@ def _relax_both_paths(seqs, pid, iters, tag):
     # tiled kernel with up to 4 outputs per tile, one output per tile, the
     # large-prefetch instantiation, and the row-task kernel
     modes = [{'MLP_RELAX': 'pairs'}, {'MLP_RELAX': 'pairs', 'MLP_RELAX_TILE': '1'},
-             {'MLP_RELAX': 'pairs', 'MLP_RELAX_KP': '12'}, {'MLP_RELAX': 'tasks'}]
+             {'MLP_RELAX': 'pairs', 'MLP_RELAX_KP': '9'}, {'MLP_RELAX': 'tasks'}]
     for env in modes:
         os.environ.update(env)
         try:
