@@ -49,7 +49,8 @@ def parse():
     ap.add_argument('--cpu-pairs', type=int, default=6144, help='reference CPU baseline sample (pairs)')
     ap.add_argument('--cpu-threads', type=int, default=16)
     ap.add_argument('--no-cpu', action='store_true')
-    ap.add_argument('--relax', type=int, default=0, help='also time N relaxation rounds (reported separately)')
+    ap.add_argument('--relax', type=int, default=1, help='also time N relaxation rounds (reported separately)')
+    ap.add_argument('--no-e2e', action='store_true', help='skip the end-to-end c_p_np_aln family timings')
     return ap.parse_args()
 
 
@@ -81,6 +82,33 @@ def cpu_baseline(fasta, pid, pairs, threads, cells_per_pair):
             'sample': f'first {pairs} pairs, {dt:.1f} s, oracle port'}
 
 
+def e2e_families(args):
+    """End-to-end seconds per family of the c_p_np_aln drop-in (-p 0: family
+    test, posteriors, guide tree, 2 consistency rounds, progressive alignment,
+    refinement), one fresh process per family, wall clock around the process;
+    stage times from MLP_CLI_TIMES."""
+    from mlprobs_amd import synth
+    cli = os.path.join(ROOT, 'mlprobs_amd', 'cli', 'c_p_np_aln')
+    if not os.path.exists(cli):
+        return None
+    res = {}
+    for tag, n, L in (('C2 128x256', 128, 256), (f'C3 {args.n}x{args.len}', args.n, args.len)):
+        with tempfile.TemporaryDirectory() as td:
+            fa = os.path.join(td, 'fam.fa')
+            synth.write_fasta(fa, synth.family(n, L, args.s, seed=args.seed))
+            t0 = time.perf_counter()
+            r = subprocess.run([cli, '-p', '0', fa], capture_output=True, text=True, timeout=600,
+                               env=dict(os.environ, MLP_CLI_TIMES='1'))
+            dt = time.perf_counter() - t0
+        stages = {}
+        for line in r.stderr.splitlines():
+            if line.startswith('[stage] '):
+                name, sec = line[8:].rsplit(' ', 2)[0], line.rsplit(' ', 2)[1]
+                stages[name] = float(sec)
+        res[tag] = {'seconds': dt, 'exit': r.returncode, 'stages_s': stages}
+    return res
+
+
 def main():
     args = parse()
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -95,6 +123,9 @@ def main():
     from mlprobs_amd import synth
     from mlprobs_amd.engine import Family
 
+    # end-to-end family timings first, on an idle device (a process that
+    # follows a large release waits for the driver to clear that memory)
+    e2e = e2e_families(args) if (not args.no_e2e and world == 1) else None
     fam_in = synth.family(args.n, args.len, args.s, seed=args.seed)
     seqs = [s for _, s in fam_in]
     lens = np.array([len(s) for s in seqs], np.int64)
@@ -137,6 +168,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     kt = fam.kernel_times()
+    _, _, nnz = fam.results()  # posterior-stage sparse set (before any relaxation)
     relax_info = None
     if args.relax > 0:
         fam.profile(True)
@@ -144,9 +176,10 @@ def main():
         tr = time.perf_counter()
         fam.relax(args.relax)
         barrier()
+        rk = fam.kernel_times()
         relax_info = {'rounds': args.relax, 'seconds': time.perf_counter() - tr,
-                      'kernels': fam.kernel_times()}
-    _, _, nnz = fam.results()
+                      'kernels_ms': {k: v['ms'] for k, v in rk.items() if v['launches']},
+                      'nnz_out': int(fam.results()[2].sum())}
     value = total_cells * args.steps / dt
     # roofline of the dominant kernel (largest accumulated device time)
     dom = max(ALGO_BYTES, key=lambda k: kt[k]['ms'])
@@ -211,6 +244,8 @@ def main():
             out['speedup_vs_cpu'] = value / cpu['value']
         if relax_info:
             out['relax'] = relax_info
+        if e2e is not None:
+            out['e2e'] = e2e
         print(json.dumps(out))
     fam.close()
     if world > 1:

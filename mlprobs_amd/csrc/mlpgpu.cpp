@@ -313,7 +313,10 @@ int mlp_ctx_create(int device, mlp_ctx** out) {
   // half of the free HBM for per-batch scratch (the rest: CSR store, relaxation
   // buffers): larger batches keep every SIMD busy through the serial
   // local-total chains and shorten the per-batch tails
-  c->scratch_budget = freeb / 2;
+  // (free memory may read low for a while after another process released a
+  // large allocation -- the driver clears it lazily -- so plan with at least
+  // 45% of the device; an allocation that really fails halves the budget)
+  c->scratch_budget = std::max<size_t>(freeb, total / 10 * 9) / 2;
   if (const char* s = getenv("MLP_SCRATCH_GB")) c->scratch_budget = (size_t)(atof(s) * (1ull << 30));
   *out = c;
   return MLP_OK;
@@ -660,7 +663,7 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
   // kernels run, and finishes batch b (entry offsets from its pair records,
   // compaction into the store) before batch b + 1 reuses the scratch.
   const bool two = false;
-  const size_t batch_target = batch_target_for(c, p0, p1, pair_bytes);
+  size_t batch_target = batch_target_for(c, p0, p1, pair_bytes);
   hipStream_t streams[2] = {c->stream, c->stream2};
   DevBuf* scr[2] = {&c->scratch, &c->scratch2};
   if (two) {  // stream2 must not run ahead of the tables upload on stream
@@ -749,7 +752,12 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
                  o_ev = cv.take(P.ell_rows * kEll * 4), o_en = cv.take(P.ell_rows * 4),
                  o_entb = cv.take(np * 8), o_rpb = cv.take(np * 8), o_rec = cv.take(np * sizeof(PairRec));
     const PlanDev pd = carve_plan(cv, P);
-    if ((rc = ensure(c, *scr[slot], cv.off))) return rc;
+    if ((rc = ensure(c, *scr[slot], cv.off))) {
+      if (rc != MLP_ERR_MEMORY || c->scratch_budget < (64u << 20)) return rc;
+      c->scratch_budget /= 2;  // the device is shared: plan smaller batches and retry
+      batch_target = batch_target_for(c, p, p1, pair_bytes);
+      continue;
+    }
     char* base = (char*)scr[slot]->p;
     Scratch sc{};
     sc.f5 = (float*)(base + o_f5);
