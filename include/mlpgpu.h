@@ -47,6 +47,12 @@ typedef struct mlp_ctx mlp_ctx;
 int mlp_ctx_create(int device, mlp_ctx **out);
 void mlp_ctx_destroy(mlp_ctx *ctx);
 const char *mlp_last_error(const mlp_ctx *ctx);
+/* Device bytes the posterior stage may hold as batch scratch (default: 45%
+ * of the device; larger batches shorten the per-batch kernel tails).  A
+ * one-shot process (the c_p_np_aln drop-in) asks for less: a fresh process's
+ * large allocation waits while the driver clears memory another process just
+ * released.  No reference counterpart (the reference allocates per pair). */
+int mlp_set_scratch(mlp_ctx *ctx, uint64_t bytes);
 
 /* Upload a family (replaces the sequence side of MultiSequence, CPNP/MultiSequence.h:267-315).
  * residues: concatenated uppercase letters; offsets[n+1] delimit sequence k. */

@@ -345,6 +345,12 @@ void mlp_ctx_destroy(mlp_ctx* c) {
 
 const char* mlp_last_error(const mlp_ctx* c) { return c ? c->err.c_str() : "null context"; }
 
+int mlp_set_scratch(mlp_ctx* c, uint64_t bytes) {
+  if (!c || bytes < (64u << 20)) return MLP_ERR_ARG;
+  c->scratch_budget = (size_t)bytes;
+  return MLP_OK;
+}
+
 int mlp_family_load(mlp_ctx* c, int n, const char* residues, const int64_t* offsets) {
   if (!c || n < 1 || !residues || !offsets) return MLP_ERR_ARG;
   hipSetDevice(c->device);

@@ -57,6 +57,7 @@ def lib():
         L.mlp_ctx_destroy.restype = None
         L.mlp_last_error.argtypes = [P]
         L.mlp_last_error.restype = C.c_char_p
+        L.mlp_set_scratch.argtypes = [P, C.c_uint64]
         L.mlp_family_load.argtypes = [P, C.c_int, C.c_char_p, I64P]
         L.mlp_family_npairs.argtypes = [P]
         L.mlp_family_npairs.restype = I64
@@ -85,7 +86,7 @@ def lib():
     return _LIB
 
 
-EXPORTED = ['mlp_ctx_create', 'mlp_ctx_destroy', 'mlp_last_error', 'mlp_family_load',
+EXPORTED = ['mlp_ctx_create', 'mlp_ctx_destroy', 'mlp_last_error', 'mlp_set_scratch', 'mlp_family_load',
             'mlp_family_npairs', 'mlp_posteriors', 'mlp_pair_results', 'mlp_csr_total',
             'mlp_csr_export', 'mlp_csr_import', 'mlp_relax', 'mlp_viterbi', 'mlp_viterbi_results',
             'mlp_viterbi_path', 'mlp_model_adjustment', 'mlp_family_features', 'mlp_comm_unique_id', 'mlp_comm_init',
