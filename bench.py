@@ -49,7 +49,8 @@ def parse():
     ap.add_argument('--cpu-pairs', type=int, default=6144, help='reference CPU baseline sample (pairs)')
     ap.add_argument('--cpu-threads', type=int, default=16)
     ap.add_argument('--no-cpu', action='store_true')
-    ap.add_argument('--relax', type=int, default=1, help='also time N relaxation rounds (reported separately)')
+    ap.add_argument('--relax', type=int, default=-1,
+                    help='also time N relaxation rounds (reported separately; default 1 on one GPU, 0 on several)')
     ap.add_argument('--no-e2e', action='store_true', help='skip the end-to-end c_p_np_aln family timings')
     return ap.parse_args()
 
@@ -126,6 +127,8 @@ def main():
     # end-to-end family timings first, on an idle device (a process that
     # follows a large release waits for the driver to clear that memory)
     e2e = e2e_families(args) if (not args.no_e2e and world == 1) else None
+    if args.relax < 0:
+        args.relax = 1 if world == 1 else 0
     fam_in = synth.family(args.n, args.len, args.s, seed=args.seed)
     seqs = [s for _, s in fam_in]
     lens = np.array([len(s) for s in seqs], np.int64)
