@@ -66,7 +66,14 @@ int64_t mlp_family_npairs(const mlp_ctx *ctx);
  * partition function only (pid >= 3); the MEA distance
  * 1 - score / min(L_a, L_b); and the sparse matrix (>= 0.01).
  * delta = initDistrib[2] after ModelAdjustmentTest (CPNP/MSA.cpp:861-870).
+ * pid = MLP_PID_QP runs QuickProbs' posterior stage instead (the realigner
+ * MLProbs calls, PosteriorStage::computePairwise + combineMatrices,
+ * QP/Alignment/Multiple/PosteriorStage.cpp:123-196): the same 5-state pair-HMM
+ * and QuickProbs' double-precision VTML200 partition function, merged as
+ * sqrt((a^2 + b^2) / 2), MEA distance, entries >= 0.01 stored as QuickProbs'
+ * 16-bit fixed point q read back as q / 65535 (delta is ignored).
  * Results stay in device memory in the context's canonical CSR store. */
+#define MLP_PID_QP 16
 int mlp_posteriors(mlp_ctx *ctx, int pid, float delta, int64_t p_begin, int64_t p_end);
 
 /* Per-pair scalars of pairs [p_begin, p_end) (host arrays, may be NULL):

@@ -16,7 +16,7 @@ CSRC = os.path.join(HERE, 'csrc')
 LIBDIR = os.path.join(HERE, 'lib')
 LIB = os.path.join(LIBDIR, 'libmlpgpu.so')
 SOURCES = ['posterior.hip', 'totals.hip', 'viterbi.hip', 'relax.hip', 'mlpgpu.cpp']
-HEADERS = ['mlp_kernels.h', 'mlp_numerics.h', 'mlp_chain.h', 'mlp_params_default.inc']
+HEADERS = ['mlp_kernels.h', 'mlp_numerics.h', 'mlp_chain.h', 'mlp_params_default.inc', 'mlp_params_qp.inc']
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 FLAGS = ['--offload-arch=gfx950', '-O3', '-ffp-contract=off', '-fno-fast-math', '-fPIC',
          '-std=c++17', '-Wno-unused-result', '-Wno-unused-value']

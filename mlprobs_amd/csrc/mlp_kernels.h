@@ -124,9 +124,15 @@ struct VitOut {
   int32_t* state;          // best terminating state (k_viterbi -> k_vit_trace)
 };
 
-enum ModelSet : int { kHmm5 = 1, kLocal = 2, kPF = 4 };
+// kQP: QuickProbs' posterior stage (QP/Alignment/Multiple/PosteriorStage.cpp:
+// 123-196): its partition function runs in the transposed orientation of
+// C_P_NP_Aln's (so the three-term sums add in the other order) and keeps only
+// posteriors in [0.001, 1]; the merge is the RMS of two models.
+enum ModelSet : int { kHmm5 = 1, kLocal = 2, kPF = 4, kQP = 8 };
+constexpr int kPidQP = 16;  // pid code of the QuickProbs posterior stage (include/mlpgpu.h MLP_PID_QP)
 
 inline int model_set_for_pid(int pid) {
+  if (pid == kPidQP) return kHmm5 | kPF | kQP;
   if (pid == 2) return kLocal;
   if (pid >= 3) return kPF;
   return kHmm5 | kLocal | kPF;

@@ -25,6 +25,7 @@
 
 #include "mlp_kernels.h"
 #include "mlp_params_default.inc"
+#include "mlp_params_qp.inc"
 
 using namespace mlp;
 
@@ -190,7 +191,7 @@ static void flush_timers(mlp_ctx* c) {
 }
 
 // Parameter tables exactly as the reference builds them.
-static void build_tables(Tables& T, ModelScalars& ms, float delta) {
+static void build_tables(Tables& T, ModelScalars& ms, float delta, bool qp = false) {
   static float emitPairs[256][256];
   static float emitSingle[256];
   for (int i = 0; i < 256; i++) {
@@ -270,6 +271,12 @@ static void build_tables(Tables& T, ModelScalars& ms, float delta) {
   const double beta_d = beta;
   ms.pf_open = exp(beta_d * -22.0);
   ms.pf_ext = exp(beta_d * -1.0);
+  if (qp) {  // QuickProbs' partition function: VTML200 (mlp_params_qp.inc); its pair-HMM is this one
+    for (int r = 0; r < 26; r++)
+      for (int c = 0; c < 26; c++) T.sub[r * 26 + c] = mlp_qp_pf_sub[c * 26 + r];  // [seq2][seq1]
+    ms.pf_open = mlp_qp_pf_open;
+    ms.pf_ext = mlp_qp_pf_extend;
+  }
   // CPNP/ProbabilisticModel.h:1068-1070: LOG(0.6080327034), LOG(0.1959836632) x 2
   ms.vit_init[0] = logf(0.6080327034f);
   ms.vit_init[1] = logf(0.1959836632f);
@@ -650,7 +657,7 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
     c->store_total = 0;
   }
   ModelScalars ms;
-  build_tables(c->h_tables, ms, delta);
+  build_tables(c->h_tables, ms, delta, pid == kPidQP);
   HIPCHK(c, hipMemcpyAsync(c->d_tables, &c->h_tables, sizeof(Tables), hipMemcpyHostToDevice, c->stream));
   const int models = model_set_for_pid(pid);
   SeqSet seqs{c->d_res, c->d_off, c->d_len};

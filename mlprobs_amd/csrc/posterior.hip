@@ -230,14 +230,15 @@ __global__ __launch_bounds__(256) void k_forward(ModelScalars ms, const Tables* 
             const double o1 = (i == L1) ? 1.0 : pfo, e1 = (i == L1) ? 1.0 : pfe;
             Ze = UZm * o0 + UZe * e0;
             Zf = LZm * o1 + LZf * e1;
-            Zm = (DZm + DZe + DZf) * score;
+            // QuickProbs' Ze/Zf are ours transposed (QP/PartitionFunction.cpp:128-130)
+            Zm = ((M & kQP) != 0 ? (DZm + DZf) + DZe : (DZm + DZe) + DZf) * score;
             pf_rescale(Zm, Ze, Zf, E);
           }
           sc.zm[idx] = mlp_pf_pack(Zm, E);
           if (act) {
             if (E > 250) atomicOr(&rec[c.slot].flags, 1);
-            if (i == L1 && j == L2) {  // CPNP/MSAPartProbs.cpp:591,612
-              rec[c.slot].zmant = (Zm + Ze) + Zf;
+            if (i == L1 && j == L2) {  // CPNP/MSAPartProbs.cpp:591,612; QP/PartitionFunction.cpp:132,155
+              rec[c.slot].zmant = (M & kQP) != 0 ? (Zm + Zf) + Ze : (Zm + Ze) + Zf;
               rec[c.slot].zexp = E;
             }
           }
@@ -459,13 +460,15 @@ __global__ __launch_bounds__(256) void k_backward(ModelScalars ms, const Tables*
             E = pf_align(nZm, nZe, nZf, ne, rZm, rZe, rZf, re, gZm, gZe, gZf, ge);
             Zf = rZm * o1 + rZf * e1;
             Ze = nZm * o0 + nZe * e0;
-            Zm = (gZm + gZf + gZe) * score;
+            Zm = ((M & kQP) != 0 ? (gZm + gZe) + gZf : (gZm + gZf) + gZe) * score;  // QP/PartitionFunction.cpp:260
             pf_rescale(Zm, Ze, Zf, E);
             if (act) {
               int ef;
               const double zf = mlp_pf_unpack(zmv, &ef);
               const double qv = (zf * Zm) / (score * c.zmant);
               post = (float)ldexp(qv, MLP_PF_STEP * (ef + E - c.zexp));
+              // QuickProbs stores only probabilities in [0.001, 1] (QP/PartitionFunction.cpp:266-272)
+              if constexpr ((M & kQP) != 0) post = (post <= 1.0f && post >= 0.001f) ? post : 0.0f;
             }
           }
           sc.pg[idx] = post;
@@ -552,6 +555,12 @@ __global__ __launch_bounds__(256) void k_merge(ModelScalars ms, SeqSet sq, PairM
         if (act) {
           if constexpr (PID == 2) {
             P = mlp_post_from_sum_t(flv, c.TL, ex);
+          } else if constexpr (PID == kPidQP) {
+            // QP/ParallelProbabilisticModel.cpp:246-248 (a zero total reads as 1) and
+            // PosteriorStage::combineMatrices (QP/PosteriorStage.cpp:176-178)
+            const float v1 = mlp_post_from_sum_t(f5v, c.T5 == 0.f ? 1.0f : c.T5, ex);
+            const float v2 = pgv;
+            P = sqrtf((v1 * v1 + v2 * v2) * 0.5f);
           } else if constexpr (PID >= 3) {
             P = pgv;
           } else {
@@ -570,7 +579,10 @@ __global__ __launch_bounds__(256) void k_merge(ModelScalars ms, SeqSet sq, PairM
           if (P >= 0.01f) {  // POSTERIOR_CUTOFF (CPNP/SparseMatrix.h:14)
             if (cnt < kEll) {
               sc.ell_col[erow * kEll + cnt] = (uint16_t)j;
-              sc.ell_val[erow * kEll + cnt] = P;
+              // QuickProbs keeps 16-bit fixed point: (uint16)(P * 65535), read back
+              // as q / 65535 (QP/DataStructures/SparseEntry.h:31-32)
+              sc.ell_val[erow * kEll + cnt] =
+                  PID == kPidQP ? (float)(uint32_t)(uint16_t)(P * 65535.0f) / 65535.0f : P;
             } else {
               atomicOr(&rec[c.slot].flags, 2);
             }
@@ -631,6 +643,10 @@ static hipError_t launch_sweep(int models, const ModelScalars& ms, const Tables*
     case kLocal: go(std::integral_constant<int, kLocal>{}); break;
     case kPF: go(std::integral_constant<int, kPF>{}); break;
     case kHmm5: go(std::integral_constant<int, kHmm5>{}); break;
+    case kHmm5 | kPF | kQP:  // QuickProbs: the same fp32 pair-HMM sweep, its own partition function
+      go(std::integral_constant<int, kHmm5>{});
+      go(std::integral_constant<int, kPF | kQP>{});
+      break;
     default: return hipErrorInvalidValue;
   }
   return hipSuccess;
@@ -663,7 +679,9 @@ hipError_t launch_merge(int models, int pid, const ModelScalars& ms, SeqSet seqs
                         hipStream_t st) {
   if (nchains <= 0) return hipSuccess;
   const ChainLaunch l = chain_launch(nchains, lds_seq);
-  if (pid == 2)
+  if (pid == kPidQP)
+    hipLaunchKernelGGL((k_merge<kHmm5 | kPF | kQP, kPidQP>), l.grid, l.block, l.lds, st, ms, seqs, pm, cm, rec, sc, nchains, lds_seq);
+  else if (pid == 2)
     hipLaunchKernelGGL((k_merge<kLocal, 2>), l.grid, l.block, l.lds, st, ms, seqs, pm, cm, rec, sc, nchains, lds_seq);
   else if (pid >= 3)
     hipLaunchKernelGGL((k_merge<kPF, 3>), l.grid, l.block, l.lds, st, ms, seqs, pm, cm, rec, sc, nchains, lds_seq);

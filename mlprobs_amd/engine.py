@@ -26,6 +26,7 @@ I32P = np.ctypeslib.ndpointer(np.int32, flags='C_CONTIGUOUS')
 I64P = np.ctypeslib.ndpointer(np.int64, flags='C_CONTIGUOUS')
 U16P = np.ctypeslib.ndpointer(np.uint16, flags='C_CONTIGUOUS')
 
+PID_QP = 16  # include/mlpgpu.h MLP_PID_QP: QuickProbs' posterior stage
 ERRORS = {1: 'bad argument', 2: 'HIP error', 3: 'partition function overflow', 4: 'state error',
           5: 'RCCL error', 6: 'device memory'}
 KERNELS = ['forward', 'backward', 'local_totals', 'merge_mea_sparsify', 'compact', 'relax',

@@ -16,6 +16,7 @@
 #endif
 
 #include "../mlprobs_amd/csrc/mlp_params_default.inc"
+#include "../mlprobs_amd/csrc/mlp_params_qp.inc"
 
 #define LOG_ZERO (-2e20f)
 #define LOG_ONE (0.0f)
@@ -841,4 +842,134 @@ int64_t orc_pair_loop(const orc_model *m, int N, const char *const *seqs, const 
     free(post);
   }
   return total;
+}
+
+/* ------------------------------------------------------------ QuickProbs
+ * QuickProbs' posterior stage (QP/Alignment/Multiple/PosteriorStage.cpp:
+ * 123-196): the 5-state pair-HMM above with the default tables (QuickProbs'
+ * ProteinHmm5 tables are the same; tools/gen_params.py --qp checks it) and
+ * its own partition function in double over exp(beta * VTML200)
+ * (mlp_params_qp.inc, QP/Alignment/Multiple/PartitionFunction.cpp:71-291,
+ * restated below with its two-row buffers).  s1, s2 are '@'-prefixed. */
+static double qp_sub(char a, char b) { return mlp_qp_pf_sub[(a - 'A') * 26 + (b - 'A')]; }
+
+void orc_qp_pf_posterior(const char *s1, int L1, const char *s2, int L2, float *post) {
+  const int lda = L2 + 1;
+  const size_t cells = (size_t)(L1 + 1) * lda;
+  const double go = mlp_qp_pf_open, ge = mlp_qp_pf_extend, tgo = 1.0, tge = 1.0;  /* exp(beta * 0) */
+  double *Zm = calloc(cells, sizeof(double));
+  double *buf = calloc(4 * (size_t)lda, sizeof(double));
+  double *Ze = buf, *Zf = buf + 2 * lda, zz = 0;
+  /* forward, PartitionFunction.cpp:85-156 */
+  Zm[0] = 1.0;
+  Zf[0] = Ze[0] = 0;
+  Zf[lda + 0] = Zm[0] * tgo;
+  Ze[1] = Zm[0] * tgo;
+  for (int j = 2; j <= L2; j++) Ze[j] = Ze[j - 1] * tge;
+  for (int i = 1; i <= L1; i++) {
+    for (int j = 1; j <= L2; j++) {
+      const double score = qp_sub(s1[i], s2[j]);
+      double open0 = go, extend0 = ge, open1 = go, extend1 = ge;
+      if (i == L1) { open0 = tgo; extend0 = tge; }
+      if (j == L2) { open1 = tgo; extend1 = tge; }
+      Ze[lda + j] = Zm[(size_t)i * lda + j - 1] * open0 + Ze[lda + j - 1] * extend0;
+      Zf[lda + j] = Zm[(size_t)(i - 1) * lda + j] * open1 + Zf[j] * extend1;
+      Zm[(size_t)i * lda + j] = (Zm[(size_t)(i - 1) * lda + j - 1] + Ze[j - 1] + Zf[j - 1]) * score;
+      zz = Zm[(size_t)i * lda + j] + Ze[lda + j] + Zf[lda + j];
+    }
+    for (int t = 0; t <= L2; t++) {
+      Ze[t] = Ze[lda + t]; Ze[lda + t] = 0;
+      Zf[t] = Zf[lda + t]; Zf[lda + t] = 0;
+    }
+    Zf[lda + 0] = 1;
+  }
+  Zm[0] = zz;
+  /* reverse, PartitionFunction.cpp:185-289 */
+  double *rb = calloc(6 * (size_t)lda, sizeof(double));
+  double *Rm = rb, *Re = rb + 2 * lda, *Rf = rb + 4 * lda;
+  for (size_t c = 0; c < cells; c++) post[c] = 0.0f;
+  Rm[lda + L2] = 1;
+  Re[L2] = Rf[L2] = 0;
+  Rf[lda + L2] = Rm[lda + L2] * tgo;
+  Re[L2 - 1] = Rm[lda + L2] * tgo;
+  for (int j = L2 - 2; j >= 0; j--) Re[j] = Re[j + 1] * tge;
+  for (int i = L1 - 1; i >= 0; i--) {
+    for (int j = L2 - 1; j >= 0; j--) {
+      const double scorez = qp_sub(s1[i + 1], s2[j + 1]);
+      double open0 = go, extend0 = ge, open1 = go, extend1 = ge;
+      if (i == 0) { open0 = tgo; extend0 = tge; }
+      if (j == 0) { open1 = tgo; extend1 = tge; }
+      Rf[lda + j] = Rm[lda + j] * open1 + Rf[j] * extend1;
+      Re[lda + j] = Rm[j + 1] * open0 + Re[lda + j + 1] * extend0;
+      Rm[j] = (Rm[lda + j + 1] + Rf[j + 1] + Re[j + 1]) * scorez;
+      double tempvar = Zm[(size_t)(i + 1) * lda + j + 1] * Rm[j];
+      tempvar /= (scorez * Zm[0]);
+      const float probability = (float)tempvar;
+      if (probability <= 1 && probability >= 0.001) post[(size_t)(i + 1) * lda + j + 1] = probability;
+    }
+    for (int t = 0; t <= L2; t++) {
+      Re[t] = Re[lda + t]; Re[lda + t] = 0;
+      Rf[t] = Rf[lda + t]; Rf[lda + t] = 0;
+      Rm[lda + t] = Rm[t]; Rm[t] = 0;
+    }
+    Rf[L2] = 1;
+  }
+  post[0] = 0;
+  free(Zm); free(buf); free(rb);
+}
+
+/* PosteriorStage::computePairwise + combineMatrices: HMM posterior (post_hmm),
+ * partition-function posterior (post_pf), their RMS (post); returns the
+ * distance 1 - MEA / min(L1, L2). */
+float orc_qp_pair(const orc_model *m, const char *s1, int L1, const char *s2, int L2,
+                  float *post_hmm, float *post_pf, float *post) {
+  const size_t cells = (size_t)(L1 + 1) * (L2 + 1);
+  orc_qp_pf_posterior(s1, L1, s2, L2, post_pf);
+  float *F = malloc(sizeof(float) * 5 * cells), *B = malloc(sizeof(float) * 5 * cells);
+  orc_forward(m, s1, L1, s2, L2, 1, F);
+  orc_backward(m, s1, L1, s2, L2, 1, B);
+  orc_posterior(m, s1, L1, s2, L2, F, B, 1, post_hmm);
+  free(F); free(B);
+  /* combineMatrices, PosteriorStage.cpp:160-196 */
+  const int W = L2 + 1;
+  float *oldRow = calloc(W, sizeof(float)), *newRow = calloc(W, sizeof(float));
+  for (int i = 0; i <= L1; i++) {
+    for (int j = 0; j <= L2; j++) {
+      const size_t c = (size_t)i * W + j;
+      if (i == 0 || j == 0) {
+        post[c] = 0;
+        newRow[j] = 0;
+      } else {
+        const float v1 = post_hmm[c], v2 = post_pf[c];
+        post[c] = sqrtf((v1 * v1 + v2 * v2) * 0.5f);
+        float a = post[c] + oldRow[j - 1], b = newRow[j - 1], d = oldRow[j];
+        newRow[j] = a >= b ? (a >= d ? a : d) : (b >= d ? b : d);
+      }
+    }
+    float *t = oldRow; oldRow = newRow; newRow = t;
+  }
+  const float total = oldRow[L2];
+  free(oldRow); free(newRow);
+  return 1.0f - total / (float)(L1 < L2 ? L1 : L2);
+}
+
+/* FilteredSparseMatrix(L1, L2, post, cutoff) with 16-bit fixed-point values
+ * (QP/DataStructures/PackedSparseMatrix.cpp:40-80, SparseEntry.h:31-32).
+ * Returns the entry count; cols / q may be NULL to count. */
+int64_t orc_qp_sparsify(int L1, int L2, const float *post, int32_t *rowptr, int32_t *cols, uint16_t *q) {
+  const int W = L2 + 1;
+  int64_t n = 0;
+  rowptr[0] = rowptr[1] = 0;
+  for (int i = 1; i <= L1; i++) {
+    for (int j = 1; j <= L2; j++) {
+      const float v = post[(size_t)i * W + j];
+      if (v >= mlp_qp_cutoff) {
+        if (cols) cols[n] = j;
+        if (q) q[n] = (uint16_t)(v * 65535.0f);
+        n++;
+      }
+    }
+    rowptr[i + 1] = (int32_t)n;
+  }
+  return n;
 }

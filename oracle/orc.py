@@ -62,6 +62,10 @@ def lib():
         L.orc_pair_loop.argtypes = [C.POINTER(Model), C.c_int, C.POINTER(C.c_char_p), I32P, C.c_int,
                                     C.c_int64, C.c_int, F32P, I64P]
         L.orc_pair_loop.restype = C.c_int64
+        L.orc_qp_pair.argtypes = [C.POINTER(Model), C.c_char_p, C.c_int, C.c_char_p, C.c_int, F32P, F32P, F32P]
+        L.orc_qp_pair.restype = C.c_float
+        L.orc_qp_sparsify.argtypes = [C.c_int, C.c_int, F32P, I32P, C.c_void_p, C.c_void_p]
+        L.orc_qp_sparsify.restype = C.c_int64
         _LIB = L
     return _LIB
 
@@ -196,3 +200,23 @@ def relax(lens, csrs):
         n = rp[-1]
         res.append((rp, out_c[o:o + n].copy(), out_v[o:o + n].copy()))
     return res
+
+
+# ---- QuickProbs posterior stage (QP/Alignment/Multiple/PosteriorStage.cpp:123-196)
+def qp_pair(m, s1, s2):
+    """(hmm posterior, partition-function posterior, combined, distance)."""
+    n = (len(s1) + 1) * (len(s2) + 1)
+    h, g, p = (np.empty(n, np.float32) for _ in range(3))
+    d = lib().orc_qp_pair(C.byref(m), _s(s1), len(s1), _s(s2), len(s2), h, g, p)
+    return h, g, p, np.float32(d)
+
+
+def qp_sparsify(L1, L2, post):
+    """(row_ptr, cols, 16-bit fixed-point values) of entries >= 0.01."""
+    post = np.ascontiguousarray(post, np.float32)
+    rp = np.zeros(L1 + 2, np.int32)
+    n = lib().orc_qp_sparsify(L1, L2, post, rp, None, None)
+    cols = np.empty(max(n, 1), np.int32)
+    q = np.empty(max(n, 1), np.uint16)
+    lib().orc_qp_sparsify(L1, L2, post, rp, cols.ctypes.data, q.ctypes.data)
+    return rp, cols[:n], q[:n]

@@ -1,0 +1,137 @@
+// qp_probe.cpp -- TEST INFRASTRUCTURE ONLY (oracle side).
+//
+// A harness that links the *reference's own* QuickProbs sources
+// (realign/QuickProbs/src, compiled in place by `make -C oracle qp` into
+// oracle/_ref/qpobj/) and calls its posterior stage on given inputs, dumping
+// the outputs as the tagged binary records of ref_probe.cpp.  It is used to
+//   (1) dump QuickProbs' constant tables (pair-HMM logs, the exp-space
+//       partition function parameters from VTML200) for the GPU build
+//       (tools/gen_params.py --qp),
+//   (2) generate golden vectors of PosteriorStage::computePairwise
+//       (QP/Alignment/Multiple/PosteriorStage.cpp:123-196) under tests/golden/
+//       (tests/golden/gen_golden.py).
+// Nothing in the product (mlprobs_amd/, include/) links or calls this.
+//
+//   qp_probe params            -> tables
+//   qp_probe pair SEQ1 SEQ2    -> posteriors, distance, sparse matrix
+// (records written to $REF_PROBE_OUT)
+
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+// Compiled with -fno-access-control: the model tables are protected members.
+#include "Alignment/DataStructures/Sequence.h"
+#include "Alignment/DataStructures/SparseMatrixType.h"
+#include "Alignment/Multiple/BufferSet.h"
+#include "Alignment/Multiple/Configuration.h"
+#include "Alignment/Multiple/ExpPartitionFunctionParams.h"
+#include "Alignment/Multiple/ParallelProbabilisticModel.h"
+#include "Alignment/Multiple/PartitionFunction.h"
+#include "Alignment/Multiple/PosteriorStage.h"
+
+using namespace quickprobs;
+
+static FILE *g_out = nullptr;
+
+static void rec(const char *name, char dtype, const void *data, uint64_t count) {
+  uint32_t n = (uint32_t)strlen(name);
+  fwrite(&n, 4, 1, g_out);
+  fwrite(name, 1, n, g_out);
+  fwrite(&dtype, 1, 1, g_out);
+  fwrite(&count, 8, 1, g_out);
+  size_t es = (dtype == 'f' || dtype == 'i') ? 4 : (dtype == 'd' || dtype == 'q') ? 8 : (dtype == 'h') ? 2 : 1;
+  fwrite(data, es, count, g_out);
+}
+
+// The protein configuration QuickProbs runs MLProbs' families with
+// (Configuration::setType, QP/Alignment/Multiple/Configuration.cpp:306-330).
+static std::shared_ptr<Configuration> protein_config() {
+  auto cfg = std::make_shared<Configuration>();
+  cfg->hardware.numThreads = 1;
+  cfg->setType(AlignmentType::PROTEIN);
+  return cfg;
+}
+
+static Sequence *make_seq(const std::string &s, int label) {
+  auto *v = new std::vector<char>();
+  v->push_back('@');
+  for (char c : s) v->push_back(c);
+  return new Sequence(v, "s", (int)s.size(), label, label);
+}
+
+static int cmd_params() {
+  auto cfg = protein_config();
+  PosteriorStage stage(cfg);
+  const ProbabilisticModel &m = *stage.getModel();
+  rec("initial", 'f', m.initialDistribution, 5);
+  rec("trans", 'f', &m.transProb[0][0], 25);
+  rec("match", 'f', &m.matchProb[0][0], 256 * 256);
+  rec("ins", 'f', &m.insProb[0][0], 256 * 5);
+  const auto &raw = dynamic_cast<const ExpPartitionFunctionParams<double> &>(*stage.function->params).raw;
+  rec("pf_term_open", 'd', &raw.termGapOpen, 1);
+  rec("pf_term_extend", 'd', &raw.termGapExtend, 1);
+  rec("pf_open", 'd', &raw.gapOpen, 1);
+  rec("pf_extend", 'd', &raw.gapExt, 1);
+  rec("pf_sub", 'd', raw.subMatrix, 26 * 26);
+  const float cutoff = cfg->algorithm.posteriorCutoff;
+  rec("cutoff", 'f', &cutoff, 1);
+  return 0;
+}
+
+static int cmd_pair(const char *a, const char *b) {
+  auto cfg = protein_config();
+  PosteriorStage stage(cfg);
+  std::unique_ptr<Sequence> s1(make_seq(a, 0)), s2(make_seq(b, 1));
+  const int L1 = s1->GetLength(), L2 = s2->GetLength();
+  const size_t layer = (size_t)(L1 + 1) * (L2 + 1);
+  BufferSet buf(layer);
+  float dist = 0;
+  // computePairwise leaves: f2 = partition-function posterior, f1 = pair-HMM
+  // posterior, f0 = their combination (PosteriorStage.cpp:123-158)
+  stage.computePairwise(*s1, *s2, buf, dist);
+  rec("dist", 'f', &dist, 1);
+  rec("post_hmm", 'f', buf.f1(), layer);
+  rec("post_pf", 'f', buf.f2(), layer);
+  rec("post", 'f', buf.f0(), layer);
+  // the sparse form the posterior stage keeps (PosteriorStage.cpp:104-106)
+  SparseMatrixType sm(L1, L2, buf.f0(), cfg->algorithm.posteriorCutoff);
+  std::vector<int32_t> rp(L1 + 2, 0);
+  std::vector<uint16_t> cols, q;
+  for (int i = 1; i <= L1; i++) {
+    const auto *row = sm.getRowPtr(i);
+    for (int k = 0; k < sm.getRowSize(i); k++) {
+      cols.push_back((uint16_t)row[k].getColumn());
+      q.push_back(row[k].second);  // the stored fixed-point value (SparseEntry.h:31-32)
+    }
+    rp[i + 1] = (int32_t)cols.size();
+  }
+  rec("row_ptr", 'i', rp.data(), rp.size());
+  rec("cols", 'h', cols.data(), cols.size());
+  rec("qvals", 'h', q.data(), q.size());
+  return 0;
+}
+
+int main(int argc, char **argv) {
+  if (argc < 2) {
+    fprintf(stderr, "usage: qp_probe params | pair SEQ1 SEQ2\n");
+    return 2;
+  }
+  const char *outp = getenv("REF_PROBE_OUT");
+  if (!outp) {
+    fprintf(stderr, "set REF_PROBE_OUT\n");
+    return 2;
+  }
+  g_out = fopen(outp, "wb");
+  if (!g_out) return 3;
+  const std::string cmd = argv[1];
+  int rc = 2;
+  if (cmd == "params") rc = cmd_params();
+  else if (cmd == "pair" && argc == 4) rc = cmd_pair(argv[2], argv[3]);
+  fclose(g_out);
+  return rc;
+}

@@ -148,7 +148,51 @@ def gen_cli(td):
     return man
 
 
+QPPROBE = os.path.join(ROOT, 'oracle', '_ref', 'qp_probe')
+
+
+def gen_qp(td):
+    """QuickProbs posterior-stage vectors (oracle/_ref/qp_probe, the reference
+    QuickProbs sources compiled in place by `make -C oracle qp`)."""
+    cases = [
+        ('tiny', 'A', 'W'),
+        ('xbz', 'MKVXLBAZGHWJ', 'MKVLLDAEGHWQOU'),
+        ('short', 'MKVLAAGIVGLLLAQ', 'MKVLGAGIVLLAQW'),
+    ]
+    f = synth.family(4, 60, 0.7, seed=21)
+    cases.append(('div60', f[0][1], f[2][1]))
+    f = synth.family(4, 120, 0.45, seed=22)
+    cases.append(('mid120', f[1][1], f[3][1]))
+    f = synth.family(3, 200, 0.15, seed=23)
+    cases.append(('sim200', f[0][1], f[1][1]))
+    g = synth.family(2, 25, 0.4, seed=24)
+    h = synth.family(2, 300, 0.4, seed=25)
+    cases.append(('ragged', g[0][1], h[1][1]))
+    cases.append(('ragged_t', h[1][1], g[0][1]))
+    manifest = []
+    for name, s1, s2 in cases:
+        out = os.path.join(td, 'q.bin')
+        subprocess.check_call([QPPROBE, 'pair', s1, s2], env=dict(os.environ, REF_PROBE_OUT=out))
+        d = refdump.read(out)
+        d['s1'] = np.frombuffer(s1.encode(), np.uint8)
+        d['s2'] = np.frombuffer(s2.encode(), np.uint8)
+        np.savez_compressed(os.path.join(HERE, f'qp_pair_{name}.npz'), **d)
+        manifest.append({'name': name, 'L1': len(s1), 'L2': len(s2)})
+    return manifest
+
+
 def main():
+    if '--qp' in sys.argv:  # QuickProbs vectors only (merged into the manifest)
+        with tempfile.TemporaryDirectory() as td:
+            qp = gen_qp(td)
+        path = os.path.join(HERE, 'manifest.json')
+        with open(path) as fh:
+            man = json.load(fh)
+        man['qp_pairs'] = qp
+        man['qp_reference'] = '/root/reference realign/QuickProbs/src, oracle/Makefile `make qp`'
+        with open(path, 'w') as fh:
+            json.dump(man, fh, indent=1)
+        return
     with tempfile.TemporaryDirectory() as td:
         gen_params(td)
         pairs = gen_pairs(td)
@@ -164,11 +208,13 @@ def main():
         bali = synth.read_fasta(BALI)
         fams.append(gen_family(td, 'bb11028', bali, 2))
         cli = gen_cli(td)
+        qp = gen_qp(td)
     with open(os.path.join(HERE, 'manifest.json'), 'w') as fh:
         json.dump({'generator': 'tests/golden/gen_golden.py',
                    'reference': '/root/reference (kuangmeng/MLProbs v1), baseMSA/C_P_NP_Aln',
                    'build': 'oracle/Makefile `make ref` (CPNP/Makefile flags)',
-                   'pairs': pairs, 'families': fams, 'cli': cli}, fh, indent=1)
+                   'pairs': pairs, 'families': fams, 'cli': cli, 'qp_pairs': qp,
+                   'qp_reference': '/root/reference realign/QuickProbs/src, oracle/Makefile `make qp`'}, fh, indent=1)
 
 
 if __name__ == '__main__':

@@ -54,3 +54,15 @@ def family_csrs(d, it):
 
 def pairs_of(n):
     return [(a, b) for a in range(n) for b in range(a + 1, n)]
+
+
+def qp_pair_names():
+    return sorted(os.path.basename(p)[8:-4] for p in glob.glob(os.path.join(GOLDEN, 'qp_pair_*.npz')))
+
+
+def load_qp_pair(name):
+    """QuickProbs posterior-stage vectors (tests/golden/gen_golden.py gen_qp)."""
+    d = dict(np.load(os.path.join(GOLDEN, f'qp_pair_{name}.npz')))
+    d['s1'] = bytes(d['s1']).decode()
+    d['s2'] = bytes(d['s2']).decode()
+    return d

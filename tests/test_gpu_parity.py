@@ -7,9 +7,10 @@ import numpy as np
 import pytest
 
 import orc
-from goldens import GOLDEN, family_csrs, family_names, load_family, load_pair, pair_names
+from goldens import (GOLDEN, family_csrs, family_names, load_family, load_pair, load_qp_pair, pair_names,
+                     qp_pair_names)
 from mlprobs_amd import synth
-from mlprobs_amd.engine import Family
+from mlprobs_amd.engine import PID_QP, Family
 from parity import close_scalar, csr_close, csr_equal
 
 pytestmark = pytest.mark.gpu
@@ -273,3 +274,49 @@ def test_relax_pair_path_ragged():
 def test_relax_pair_path_similar():
     seqs = [x for _, x in synth.family(30, 200, 0.2, seed=43)]
     _relax_both_paths(seqs, 3, 3, 'similar')
+
+
+# ---- QuickProbs posterior stage (QP/Alignment/Multiple/PosteriorStage.cpp:123-196)
+def _qp_expected(seqs, a, b):
+    """Oracle CSR (values as QuickProbs reads its 16-bit entries) and distance."""
+    h, g, p, dist = orc.qp_pair(orc.model(-1.0), seqs[a], seqs[b])
+    rp, cols, q = orc.qp_sparsify(len(seqs[a]), len(seqs[b]), p)
+    return (rp, cols, q.astype(np.float32) / np.float32(65535)), dist
+
+
+def _check_qp_family(seqs, tag):
+    n = len(seqs)
+    fam = Family(seqs)
+    fam.posteriors(PID_QP, 0.0)
+    D = fam.distances()
+    k = 0
+    for a in range(n):
+        for b in range(a + 1, n):
+            ref, dist = _qp_expected(seqs, a, b)
+            csr_equal(ref, fam.sparse(k), f'{tag} qp p{k}')
+            assert D[a, b] == dist, (tag, k, D[a, b], dist)
+            k += 1
+    fam.close()
+
+
+@pytest.mark.parametrize('name', qp_pair_names())
+def test_qp_golden(name):
+    """Bit-exact against the reference QuickProbs build: the sparse rows, the
+    16-bit values and the distance of every golden pair."""
+    d = load_qp_pair(name)
+    fam = Family([d['s1'], d['s2']])
+    fam.posteriors(PID_QP, 0.0)
+    ref = (d['row_ptr'], d['cols'], d['qvals'].astype(np.float32) / np.float32(65535))
+    csr_equal(ref, fam.sparse(0), f'qp {name}')
+    assert fam.distances()[0, 1] == d['dist'][0]
+    fam.close()
+
+
+@pytest.mark.parametrize('s,L,n,seed', [(0.7, 150, 6, 61), (0.4, 220, 5, 62), (0.15, 180, 4, 63)])
+def test_qp_vs_oracle(s, L, n, seed):
+    _check_qp_family([x for _, x in synth.family(n, L, s, seed=seed)], f'qp{seed}')
+
+
+def test_qp_ragged_chains():
+    """Many short ragged pairs stacked into chains, lengths 1..260."""
+    _check_qp_family(_ragged_family(12, 1, 260, 64), 'qp_ragged')

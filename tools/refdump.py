@@ -2,7 +2,7 @@
 import struct
 import numpy as np
 
-_DT = {b'f': np.float32, b'i': np.int32, b'd': np.float64, b'q': np.int64, b'c': np.uint8}
+_DT = {b'f': np.float32, b'i': np.int32, b'd': np.float64, b'q': np.int64, b'c': np.uint8, b'h': np.uint16}
 
 
 def read(path):
