@@ -578,22 +578,24 @@ typedef struct {
 } csr_view;
 
 /* MSA::Relax (CPNP/MSA.cpp:1290-1322): XZ rows x, ZY rows z. */
-static void relax_xz_zy(csr_view xz, csr_view zy, float *post, int Wy) {
+/* w: QuickProbs' weight (ConsistencyStage::relax, QP/.../ConsistencyStage.cpp:
+ * 264-292: weight * XZ * ZY); 1 for C_P_NP_Aln, where (1 * a) * b == a * b. */
+static void relax_xz_zy(csr_view xz, csr_view zy, float *post, int Wy, float w) {
   for (int i = 1; i <= xz.L1; i++) {
     float *base = post + (size_t)i * Wy;
     for (int a = xz.rp[i]; a < xz.rp[i + 1]; a++) {
       int z = xz.cols[a];
-      float v = xz.vals[a];
+      float v = w * xz.vals[a];
       for (int b = zy.rp[z]; b < zy.rp[z + 1]; b++) base[zy.cols[b]] += v * zy.vals[b];
     }
   }
 }
 
 /* MSA::Relax1 (CPNP/MSA.cpp:1331-1360): ZX rows z, ZY rows z. */
-static void relax_zx_zy(csr_view zx, csr_view zy, float *post, int Wy) {
+static void relax_zx_zy(csr_view zx, csr_view zy, float *post, int Wy, float w) {
   for (int k = 1; k <= zx.L1; k++) {
     for (int a = zx.rp[k]; a < zx.rp[k + 1]; a++) {
-      float v = zx.vals[a];
+      float v = w * zx.vals[a];
       float *base = post + (size_t)zx.cols[a] * Wy;
       for (int b = zy.rp[k]; b < zy.rp[k + 1]; b++) base[zy.cols[b]] += v * zy.vals[b];
     }
@@ -621,10 +623,59 @@ static int pair_index(int N, int a, int b) { /* a < b, row-major */
   return a * N - a * (a + 1) / 2 + (b - a - 1);
 }
 
+/* qp: QuickProbs' ConsistencyStage::doRelaxation with its defaults
+ * (QP/Alignment/Multiple/ConsistencyStage.cpp:133-258): the deterministic
+ * selectivity filter with selectivity 200 accepts every z (distances <= 1,
+ * the Park-Miller draw < 1.003 < 2), so P' = (P + sum_z w_z / W_xy P_xz P_zy)
+ * / (1 + sum_z w_z / W_xy), W_xy = (1 + (s - 1)(N - 2) / 200)(w_x + w_y),
+ * re-sparsified at `cutoff` into 16-bit fixed point (values out as q / 65535). */
+static int64_t relax_impl(int qp, const float *weights, float selfweight, float cutoff,
+                          int N, const int32_t *lens, const int64_t *row_off, const int64_t *ent_off,
+                          const int32_t *in_rp, const int32_t *in_cols, const float *in_vals,
+                          int32_t *out_rp, int64_t *out_ent_off, int32_t *out_cols, float *out_vals,
+                          int64_t max_out);
+
 int64_t orc_relax(int N, const int32_t *lens, const int64_t *row_off, const int64_t *ent_off,
                   const int32_t *in_rp, const int32_t *in_cols, const float *in_vals,
                   int32_t *out_rp, int64_t *out_ent_off, int32_t *out_cols, float *out_vals,
                   int64_t max_out) {
+  return relax_impl(0, NULL, 0, 0, N, lens, row_off, ent_off, in_rp, in_cols, in_vals, out_rp, out_ent_off,
+                    out_cols, out_vals, max_out);
+}
+
+int64_t orc_qp_relax(const float *weights, float selfweight, float cutoff,
+                     int N, const int32_t *lens, const int64_t *row_off, const int64_t *ent_off,
+                     const int32_t *in_rp, const int32_t *in_cols, const float *in_vals,
+                     int32_t *out_rp, int64_t *out_ent_off, int32_t *out_cols, float *out_vals,
+                     int64_t max_out) {
+  return relax_impl(1, weights, selfweight, cutoff, N, lens, row_off, ent_off, in_rp, in_cols, in_vals, out_rp,
+                    out_ent_off, out_cols, out_vals, max_out);
+}
+
+static int64_t qp_sparsify_vals(int L1, int L2, const float *post, float cutoff, int32_t *rowptr, int32_t *cols,
+                                float *vals) {
+  const int W = L2 + 1;
+  int64_t n = 0;
+  rowptr[0] = rowptr[1] = 0;
+  for (int i = 1; i <= L1; i++) {
+    for (int j = 1; j <= L2; j++) {
+      const float v = post[(size_t)i * W + j];
+      if (v >= cutoff) {
+        if (cols) cols[n] = j;
+        if (vals) vals[n] = (float)(uint16_t)(v * 65535.0f) / 65535.0f;
+        n++;
+      }
+    }
+    rowptr[i + 1] = (int32_t)n;
+  }
+  return n;
+}
+
+static int64_t relax_impl(int qp, const float *weights, float selfweight, float cutoff,
+                          int N, const int32_t *lens, const int64_t *row_off, const int64_t *ent_off,
+                          const int32_t *in_rp, const int32_t *in_cols, const float *in_vals,
+                          int32_t *out_rp, int64_t *out_ent_off, int32_t *out_cols, float *out_vals,
+                          int64_t max_out) {
   const int P = N * (N - 1) / 2;
   int64_t *cnt = calloc(P > 0 ? P : 1, sizeof(int64_t));
   float **dense = calloc(P > 0 ? P : 1, sizeof(float *));
@@ -641,7 +692,13 @@ int64_t orc_relax(int N, const int32_t *lens, const int64_t *row_off, const int6
     csr_view xy = VIEW(i, j);
     for (int x = 1; x <= L1; x++)
       for (int a = xy.rp[x]; a < xy.rp[x + 1]; a++) post[(size_t)x * W + xy.cols[a]] = xy.vals[a];
-    for (size_t k = 0; k < (size_t)(L1 + 1) * W; k++) post[k] += post[k];
+    if (!qp)  /* z = x and z = y (CPNP/MSA.cpp:1211-1213) */
+      for (size_t k = 0; k < (size_t)(L1 + 1) * W; k++) post[k] += post[k];
+    float wxy = 0, sumW = 1.0f;
+    if (qp) {  /* ConsistencyStage.cpp:199-203 */
+      wxy = 1.0f + (selfweight - 1.0f) * (float)(N - 2) / 200.0f;
+      wxy *= weights[i] + weights[j];
+    }
     int maxL = 0;
     for (int k = 0; k < N; k++) if (lens[k] > maxL) maxL = lens[k];
     int32_t *trp = malloc(sizeof(int32_t) * (maxL + 2));
@@ -651,10 +708,15 @@ int64_t orc_relax(int N, const int32_t *lens, const int64_t *row_off, const int6
     int64_t tcap = 0;
     for (int k = 0; k < N; k++) {
       if (k == i || k == j) continue;
+      float w = 1.0f;
+      if (qp) {
+        w = weights[k] / wxy;
+        sumW += w;
+      }
       if (k < i) {
-        relax_zx_zy(VIEW(k, i), VIEW(k, j), post, W);
+        relax_zx_zy(VIEW(k, i), VIEW(k, j), post, W, w);
       } else if (k < j) {
-        relax_xz_zy(VIEW(i, k), VIEW(k, j), post, W);
+        relax_xz_zy(VIEW(i, k), VIEW(k, j), post, W, w);
       } else {
         csr_view jk = VIEW(j, k);
         int64_t nnz = jk.rp[jk.L1 + 1];
@@ -665,11 +727,11 @@ int64_t orc_relax(int N, const int32_t *lens, const int64_t *row_off, const int6
         }
         transpose(jk, trp, tcur, tcols, tvals);
         csr_view t = {jk.L2, jk.L1, trp, tcols, tvals};
-        relax_xz_zy(VIEW(i, k), t, post, W);
+        relax_xz_zy(VIEW(i, k), t, post, W, w);
       }
     }
     free(trp); free(tcur); free(tcols); free(tvals);
-    for (size_t k = 0; k < (size_t)(L1 + 1) * W; k++) post[k] /= N;
+    for (size_t k = 0; k < (size_t)(L1 + 1) * W; k++) post[k] /= qp ? sumW : (float)N;
     /* mask (CPNP/MSA.cpp:1237-1261) */
     for (int y = 0; y <= L2; y++) post[y] = 0;
     for (int x = 1; x <= L1; x++) {
@@ -682,7 +744,7 @@ int64_t orc_relax(int N, const int32_t *lens, const int64_t *row_off, const int6
       while (curr <= L2) base[curr++] = 0;
     }
     int32_t *rp = out_rp + row_off[p];
-    cnt[p] = orc_sparsify(L1, L2, post, rp, NULL, NULL);
+    cnt[p] = qp ? qp_sparsify_vals(L1, L2, post, cutoff, rp, NULL, NULL) : orc_sparsify(L1, L2, post, rp, NULL, NULL);
     dense[p] = post;
   }
 #undef VIEW
@@ -698,8 +760,12 @@ int64_t orc_relax(int N, const int32_t *lens, const int64_t *row_off, const int6
     int i = 0, q = p;
     while (q >= N - 1 - i) { q -= N - 1 - i; i++; }
     int j = i + 1 + q;
-    orc_sparsify(lens[i], lens[j], dense[p], out_rp + row_off[p], out_cols + out_ent_off[p],
-                 out_vals + out_ent_off[p]);
+    if (qp)
+      qp_sparsify_vals(lens[i], lens[j], dense[p], cutoff, out_rp + row_off[p], out_cols + out_ent_off[p],
+                       out_vals + out_ent_off[p]);
+    else
+      orc_sparsify(lens[i], lens[j], dense[p], out_rp + row_off[p], out_cols + out_ent_off[p],
+                   out_vals + out_ent_off[p]);
     free(dense[p]);
   }
   free(dense); free(cnt);

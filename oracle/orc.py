@@ -66,6 +66,8 @@ def lib():
         L.orc_qp_pair.restype = C.c_float
         L.orc_qp_sparsify.argtypes = [C.c_int, C.c_int, F32P, I32P, C.c_void_p, C.c_void_p]
         L.orc_qp_sparsify.restype = C.c_int64
+        L.orc_qp_relax.argtypes = [F32P, C.c_float, C.c_float] + L.orc_relax.argtypes
+        L.orc_qp_relax.restype = C.c_int64
         _LIB = L
     return _LIB
 
@@ -170,8 +172,9 @@ def pair_loop(m, seqs, pid, max_pairs=-1, threads=0):
     return dist[:P], nnz[:P], tot
 
 
-def relax(lens, csrs):
-    """csrs: list over pairs (a<b row-major) of (rowptr[L_a+2], cols, vals)."""
+def relax(lens, csrs, qp=None):
+    """csrs: list over pairs (a<b row-major) of (rowptr[L_a+2], cols, vals).
+    qp = (weights, selfweight, cutoff): QuickProbs' consistency round instead."""
     N = len(lens)
     lens = np.asarray(lens, np.int32)
     row_off = np.zeros(len(csrs), np.int64)
@@ -190,7 +193,12 @@ def relax(lens, csrs):
     cap = max(e, 1)
     out_c = np.zeros(cap, np.int32)
     out_v = np.zeros(cap, np.float32)
-    tot = lib().orc_relax(N, lens, row_off, ent_off, in_rp, in_c, in_v, out_rp, out_off, out_c, out_v, cap)
+    if qp is None:
+        tot = lib().orc_relax(N, lens, row_off, ent_off, in_rp, in_c, in_v, out_rp, out_off, out_c, out_v, cap)
+    else:
+        w = np.ascontiguousarray(qp[0], np.float32)
+        tot = lib().orc_qp_relax(w, float(qp[1]), float(qp[2]), N, lens, row_off, ent_off, in_rp, in_c, in_v,
+                                 out_rp, out_off, out_c, out_v, cap)
     assert tot >= 0
     res = []
     for p in range(len(csrs)):

@@ -14,6 +14,8 @@
 //
 //   qp_probe params            -> tables
 //   qp_probe pair SEQ1 SEQ2    -> posteriors, distance, sparse matrix
+//   qp_probe relax FILE ITERS  -> posterior stage + ITERS consistency rounds
+//                                 (FILE: lines "weight sequence")
 // (records written to $REF_PROBE_OUT)
 
 #include <cstdint>
@@ -33,6 +35,11 @@
 #include "Alignment/Multiple/ParallelProbabilisticModel.h"
 #include "Alignment/Multiple/PartitionFunction.h"
 #include "Alignment/Multiple/PosteriorStage.h"
+#include "Alignment/Multiple/ConsistencyStage.h"
+#include "Alignment/DataStructures/MultiSequence.h"
+
+#include <fstream>
+#include <sstream>
 
 using namespace quickprobs;
 
@@ -116,6 +123,80 @@ static int cmd_pair(const char *a, const char *b) {
   return 0;
 }
 
+// Sparse set of all pairs (a < b) as one CSR: row_ptr per pair (L_a + 2,
+// relative), 16-bit values.
+static void dump_set(const char *tag, int n, Array<SparseMatrixType *> &mats) {
+  std::vector<int32_t> rp;
+  std::vector<uint16_t> cols, q;
+  std::vector<int64_t> eo(1, 0);
+  for (int a = 0; a < n; a++)
+    for (int b = a + 1; b < n; b++) {
+      SparseMatrixType *m = mats[a][b];
+      const int L1 = m->getSeq1Length();
+      const size_t base = cols.size();
+      rp.push_back(0);
+      rp.push_back(0);
+      for (int i = 1; i <= L1; i++) {
+        const auto *row = m->getRowPtr(i);
+        for (int k = 0; k < m->getRowSize(i); k++) {
+          cols.push_back((uint16_t)row[k].getColumn());
+          q.push_back(row[k].second);
+        }
+        rp.push_back((int32_t)(cols.size() - base));
+      }
+      eo.push_back((int64_t)cols.size());
+    }
+  std::string t(tag);
+  rec((t + ".row_ptr").c_str(), 'i', rp.data(), rp.size());
+  rec((t + ".ent_off").c_str(), 'q', eo.data(), eo.size());
+  rec((t + ".cols").c_str(), 'h', cols.data(), cols.size());
+  rec((t + ".qvals").c_str(), 'h', q.data(), q.size());
+}
+
+// PosteriorStage::run's pair loop, then ConsistencyStage::run with the
+// default configuration (QP/Alignment/Multiple/ConsistencyStage.cpp:90-128):
+// the last round keeps entries >= 1e-5 instead of the 0.01 cutoff.
+static int cmd_relax(const char *path, int iters) {
+  auto cfg = protein_config();
+  std::ifstream in(path);
+  std::vector<float> w;
+  MultiSequence set;
+  std::string line;
+  while (std::getline(in, line)) {
+    std::istringstream ls(line);
+    float wt;
+    std::string s;
+    if (!(ls >> wt >> s)) continue;
+    set.AddSequence(make_seq(s, (int)w.size()));
+    w.push_back(wt);
+  }
+  const int n = (int)w.size();
+  Array<float> dist(n);
+  Array<SparseMatrixType *> mats(n);
+  PosteriorStage post(cfg);
+  post(set, dist, mats);
+  std::vector<float> d;
+  for (int a = 0; a < n; a++)
+    for (int b = a + 1; b < n; b++) d.push_back(dist[a][b]);
+  rec("dist", 'f', d.data(), d.size());
+  dump_set("it0", n, mats);
+  ConsistencyStage cons(cfg);
+  cons.selfweight = n > cfg->algorithm.consistency.selfweightThreshold ? cfg->algorithm.consistency.largeSelfweight
+                                                                       : cfg->algorithm.consistency.smallSelfweight;
+  for (int it = 0; it < iters; it++) {
+    const bool filter = it != iters - 1;  // numFilterings < 0 (Configuration.cpp:105)
+    Array<SparseMatrixType *> nm = cons.doRelaxation(w.data(), &set, dist, mats, filter);
+    for (int a = 0; a < n; a++)
+      for (int b = 0; b < n; b++)
+        if (a != b) {
+          delete mats[a][b];
+          mats[a][b] = nm[a][b];
+        }
+    dump_set(("it" + std::to_string(it + 1)).c_str(), n, mats);
+  }
+  return 0;
+}
+
 int main(int argc, char **argv) {
   if (argc < 2) {
     fprintf(stderr, "usage: qp_probe params | pair SEQ1 SEQ2\n");
@@ -132,6 +213,7 @@ int main(int argc, char **argv) {
   int rc = 2;
   if (cmd == "params") rc = cmd_params();
   else if (cmd == "pair" && argc == 4) rc = cmd_pair(argv[2], argv[3]);
+  else if (cmd == "relax" && argc == 4) rc = cmd_relax(argv[2], atoi(argv[3]));
   fclose(g_out);
   return rc;
 }

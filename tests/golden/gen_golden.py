@@ -181,14 +181,45 @@ def gen_qp(td):
     return manifest
 
 
+def gen_qp_relax(td):
+    """QuickProbs' posterior stage + consistency rounds on small families
+    (qp_probe relax: PosteriorStage, then ConsistencyStage::doRelaxation with
+    the default configuration, the last round unfiltered)."""
+    rng = np.random.default_rng(31)
+    fams = [
+        ('mid6', synth.family(6, 60, 0.5, seed=31), 2),
+        ('div8', synth.family(8, 80, 0.7, seed=32), 2),
+        ('ragged7', [(h, s[: 12 + 11 * i]) for i, (h, s) in enumerate(synth.family(7, 90, 0.4, seed=33))], 1),
+    ]
+    manifest = []
+    for name, fam, iters in fams:
+        seqs = [s for _, s in fam]
+        w = rng.uniform(0.5, 20.0, len(seqs)).astype(np.float32)
+        path = os.path.join(td, 'r.txt')
+        with open(path, 'w') as fh:
+            for wt, sq in zip(w, seqs):
+                fh.write(f'{float(wt)!r} {sq}\n')
+        out = os.path.join(td, 'r.bin')
+        subprocess.check_call([QPPROBE, 'relax', path, str(iters)], env=dict(os.environ, REF_PROBE_OUT=out))
+        d = refdump.read(out)
+        d['seqs'] = np.array(seqs)
+        d['weights'] = w
+        d['iters'] = np.int32(iters)
+        np.savez_compressed(os.path.join(HERE, f'qp_family_{name}.npz'), **d)
+        manifest.append({'name': name, 'n': len(seqs), 'iters': iters})
+    return manifest
+
+
 def main():
     if '--qp' in sys.argv:  # QuickProbs vectors only (merged into the manifest)
         with tempfile.TemporaryDirectory() as td:
             qp = gen_qp(td)
+            qpf = gen_qp_relax(td)
         path = os.path.join(HERE, 'manifest.json')
         with open(path) as fh:
             man = json.load(fh)
         man['qp_pairs'] = qp
+        man['qp_families'] = qpf
         man['qp_reference'] = '/root/reference realign/QuickProbs/src, oracle/Makefile `make qp`'
         with open(path, 'w') as fh:
             json.dump(man, fh, indent=1)
@@ -209,11 +240,12 @@ def main():
         fams.append(gen_family(td, 'bb11028', bali, 2))
         cli = gen_cli(td)
         qp = gen_qp(td)
+        qpf = gen_qp_relax(td)
     with open(os.path.join(HERE, 'manifest.json'), 'w') as fh:
         json.dump({'generator': 'tests/golden/gen_golden.py',
                    'reference': '/root/reference (kuangmeng/MLProbs v1), baseMSA/C_P_NP_Aln',
                    'build': 'oracle/Makefile `make ref` (CPNP/Makefile flags)',
-                   'pairs': pairs, 'families': fams, 'cli': cli, 'qp_pairs': qp,
+                   'pairs': pairs, 'families': fams, 'cli': cli, 'qp_pairs': qp, 'qp_families': qpf,
                    'qp_reference': '/root/reference realign/QuickProbs/src, oracle/Makefile `make qp`'}, fh, indent=1)
 
 

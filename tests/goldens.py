@@ -66,3 +66,31 @@ def load_qp_pair(name):
     d['s1'] = bytes(d['s1']).decode()
     d['s2'] = bytes(d['s2']).decode()
     return d
+
+
+def qp_family_names():
+    return sorted(os.path.basename(p)[10:-4] for p in glob.glob(os.path.join(GOLDEN, 'qp_family_*.npz')))
+
+
+def load_qp_family(name):
+    d = dict(np.load(os.path.join(GOLDEN, f'qp_family_{name}.npz')))
+    d['seqs'] = [str(s) for s in d['seqs']]
+    d['iters'] = int(np.asarray(d['iters']).reshape(-1)[0])
+    return d
+
+
+def qp_family_csrs(d, it):
+    """Per-pair (rowptr, cols, q / 65535) of round `it` (0 = posterior stage)."""
+    lens = [len(s) for s in d['seqs']]
+    n = len(lens)
+    rp, eo = d[f'it{it}.row_ptr'], d[f'it{it}.ent_off']
+    cols, q = d[f'it{it}.cols'], d[f'it{it}.qvals']
+    out, ro, p = [], 0, 0
+    for a in range(n):
+        for b in range(a + 1, n):
+            r = rp[ro:ro + lens[a] + 2].astype(np.int32)
+            ro += lens[a] + 2
+            out.append((r, cols[eo[p]:eo[p + 1]].astype(np.int32),
+                        q[eo[p]:eo[p + 1]].astype(np.float32) / np.float32(65535)))
+            p += 1
+    return out

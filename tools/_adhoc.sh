@@ -1,8 +1,3 @@
 set -e -o pipefail
-O=gpurun_out/r01t; mkdir -p $O
-for i in 1 2 3; do timeout -k 10 120 tools/probe/alloc_probe 140 >> $O/alloc.log 2>&1; done
-sleep 15
-timeout -k 10 120 tools/probe/alloc_probe 140 >> $O/alloc.log 2>&1
-timeout -k 10 120 tools/probe/alloc_probe 24 >> $O/alloc.log 2>&1
-timeout -k 10 120 tools/probe/alloc_probe 24 >> $O/alloc.log 2>&1
-timeout -k 10 120 tools/probe/alloc_probe 140 >> $O/alloc.log 2>&1
+O=gpurun_out/r01u; mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/pytest.log 2>&1
