@@ -115,6 +115,14 @@ int mlp_csr_import(mlp_ctx *ctx, const int32_t *row_ptr, const int64_t *ent_off,
  * [p_begin, p_end) of its shard (mlp_shard_range) and the new store is
  * all-gathered after every round. */
 int mlp_relax(mlp_ctx *ctx, int iters);
+/* QuickProbs' consistency stage instead (ConsistencyStage::run / doRelaxation,
+ * QP/Alignment/Multiple/ConsistencyStage.cpp:90-258), on a sparse set from
+ * mlp_posteriors(MLP_PID_QP): default configuration (every z accepted by the
+ * deterministic selectivity filter, self-weight 3), z weighted by
+ * seq_weights[z] / W_xy, normalised by the weight sum; rounds re-sparsify at
+ * 0.01 except the last (1e-5) into 16-bit fixed point.  iters < 0: QuickProbs'
+ * default (2 rounds up to 50 sequences, else 1). */
+int mlp_relax_qp(mlp_ctx *ctx, int iters, const float *seq_weights);
 
 /* Multi-GPU (one process per GPU): RCCL over xGMI. */
 int mlp_comm_unique_id(unsigned char id[128]);

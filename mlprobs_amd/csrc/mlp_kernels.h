@@ -160,6 +160,15 @@ hipError_t launch_compact(SeqSet seqs, PairMeta pm, PairRec* rec, Scratch sc,
                           uint16_t* out_cols, float* out_vals, int64_t npairs, hipStream_t st);
 
 // relaxation (relax.hip)
+// QuickProbs' consistency round (ConsistencyStage::doRelaxation, QP/Alignment/
+// Multiple/ConsistencyStage.cpp:133-258) instead of C_P_NP_Aln's: every z is
+// weighted by w_z / W_xy, W_xy = (1 + (s - 1)(N - 2) / 200)(w_x + w_y), the
+// sum starts from P_xy (not 2 P_xy) and is divided by 1 + sum_z w_z / W_xy.
+struct QpRelax {
+  int on;                    // 0: C_P_NP_Aln's round
+  const float* weights;      // per sequence (device)
+  float selfweight;
+};
 struct RelaxArgs {
   int n;                     // sequences in the family
   const int32_t* lens;
@@ -176,6 +185,7 @@ struct RelaxArgs {
   const int32_t* task_row0;
   int64_t ntasks;
   float* out;                // raw relaxed values at the input entry slots
+  QpRelax qp;
 };
 struct TransposeArgs {
   int n;
@@ -209,6 +219,8 @@ struct FilterArgs {
   const int64_t* pairs;      // output pairs handled
   int64_t npairs;
   int write;
+  float cutoff;              // keep values >= cutoff (0.01; QuickProbs' last round 1e-5)
+  int fixed16;               // QuickProbs: store (uint16)(v * 65535) / 65535
 };
 // Row-bitmap images for the relaxation (relax.hip).  Every block P(a, b)
 // and its transpose is packed once per round as one 16-byte aligned record:
@@ -270,6 +282,7 @@ struct TileRelaxArgs {
   int64_t ntiles;
   float* out;                // raw relaxed values at the input entry slots
   int cap;                   // LDS bytes for one staged tile (multiple of 16)
+  QpRelax qp;
 };
 constexpr int kTileInts = 2 * kTileMax + 1;
 constexpr int kRelaxThreads = 1024;  // workgroup of the tiled relaxation (16 waves, 128 VGPRs)

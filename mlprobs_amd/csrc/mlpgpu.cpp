@@ -85,7 +85,7 @@ struct mlp_ctx {
   size_t scratch_budget = 0;
   // relaxation buffers
   DevBuf r_trowptr, r_tcols, r_tvals, r_raw, r_newrp, r_newcols, r_newvals, r_tasks_p, r_tasks_r,
-      r_pairs, r_nnz, r_newoff, r_img, r_imgoff, r_tiles, r_nwords;
+      r_pairs, r_nnz, r_newoff, r_img, r_imgoff, r_tiles, r_nwords, r_weights;
   // comm
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
@@ -340,7 +340,7 @@ void mlp_ctx_destroy(mlp_ctx* c) {
     if (p) hipFree(p);
   DevBuf* bufs[] = {&c->scratch, &c->scratch2, &c->r_trowptr, &c->r_tcols, &c->r_tvals, &c->r_raw, &c->r_newrp,
                     &c->r_newcols, &c->r_newvals, &c->r_tasks_p, &c->r_tasks_r, &c->r_pairs,
-                    &c->r_nnz, &c->r_newoff, &c->r_img, &c->r_imgoff, &c->r_tiles, &c->r_nwords};
+                    &c->r_nnz, &c->r_newoff, &c->r_img, &c->r_imgoff, &c->r_tiles, &c->r_nwords, &c->r_weights};
   for (DevBuf* b : bufs)
     if (b->p) hipFree(b->p);
   if (c->comm) ncclCommDestroy(c->comm);
@@ -1262,8 +1262,28 @@ int mlp_allgather(mlp_ctx* c) {
 }
 
 // ------------------------------------------------------------------ relax
+static int relax_rounds(mlp_ctx* c, int iters, const QpRelax& qp);
+
 int mlp_relax(mlp_ctx* c, int iters) {
   if (!c || iters < 0) return MLP_ERR_ARG;
+  return relax_rounds(c, iters, QpRelax{0, nullptr, 0.f});
+}
+
+// QuickProbs' consistency stage (ConsistencyStage::operator() / run,
+// QP/Alignment/Multiple/ConsistencyStage.cpp:62-128) with its default
+// configuration: 2 rounds up to 50 sequences, 1 above (iters < 0), self-weight
+// 3, every round but the last re-sparsified at 0.01, the last at 1e-5.
+int mlp_relax_qp(mlp_ctx* c, int iters, const float* seq_weights) {
+  if (!c || !seq_weights) return MLP_ERR_ARG;
+  if (c->n < 2) return MLP_ERR_STATE;
+  if (iters < 0) iters = c->n > 50 ? 1 : 2;
+  int rc;
+  if ((rc = ensure(c, c->r_weights, sizeof(float) * c->n))) return rc;
+  HIPCHK(c, hipMemcpyAsync(c->r_weights.p, seq_weights, sizeof(float) * c->n, hipMemcpyHostToDevice, c->stream));
+  return relax_rounds(c, iters, QpRelax{1, (const float*)c->r_weights.p, 3.0f});
+}
+
+static int relax_rounds(mlp_ctx* c, int iters, const QpRelax& qp) {
   if (c->n < 2) return MLP_ERR_STATE;
   if (c->store_p0 != 0 || c->store_p1 != c->P) {
     c->err = "relaxation needs every pair (all-gather first)";
@@ -1456,6 +1476,7 @@ int mlp_relax(mlp_ctx* c, int iters) {
     ra.task_row0 = (const int32_t*)c->r_tasks_r.p;
     ra.ntasks = nt;
     ra.out = (float*)c->r_raw.p;
+    ra.qp = qp;
     TileRelaxArgs pr;
     pr.n = c->n;
     pr.lens = c->d_len;
@@ -1472,6 +1493,7 @@ int mlp_relax(mlp_ctx* c, int iters) {
     pr.ntiles = ntiles;
     pr.out = (float*)c->r_raw.p;
     pr.cap = (int)mlp_align16(cap);
+    pr.qp = qp;
     {
       Timer t(c, KRELAX, c->ent_off[r1] - c->ent_off[r0]);
       HIPCHK(c, launch_relax_tiles(pr, tile_relax_slots(max_cells), c->stream));
@@ -1497,6 +1519,8 @@ int mlp_relax(mlp_ctx* c, int iters) {
     fa.pairs = (const int64_t*)c->r_pairs.p;
     fa.npairs = nout;
     fa.write = 0;
+    fa.cutoff = qp.on && it == iters - 1 ? 1e-5f : 0.01f;
+    fa.fixed16 = qp.on;
     {
       Timer t(c, KFILTER, 0);
       HIPCHK(c, launch_filter(fa, c->stream));

@@ -52,10 +52,21 @@ __global__ __launch_bounds__(256) void k_relax(RelaxArgs A) {
   float* acc = A.out + exy;
   for (int e = mb; e < me; ++e) {
     const float v = A.vals[exy + e];
-    acc[e] = v + v;  // contribution of z = x and z = y (CPNP/MSA.cpp:1211-1213)
+    // z = x and z = y (CPNP/MSA.cpp:1211-1213); QuickProbs starts from P_xy
+    acc[e] = A.qp.on ? v : v + v;
+  }
+  float wxy = 0.f, sumw = 1.0f;  // QuickProbs' weights (ConsistencyStage.cpp:199-203)
+  if (A.qp.on) {
+    wxy = 1.0f + (A.qp.selfweight - 1.0f) * (float)(n - 2) / 200.0f;
+    wxy *= A.qp.weights[x] + A.qp.weights[y];
   }
   for (int z = 0; z < n; ++z) {
     if (z == x || z == y) continue;
+    float wk = 1.0f;  // (1 * a) * b == a * b: C_P_NP_Aln's unweighted terms
+    if (A.qp.on) {
+      wk = A.qp.weights[z] / wxy;
+      sumw += wk;
+    }
     // A_z row i
     const uint16_t* acol;
     const float* aval;
@@ -91,7 +102,7 @@ __global__ __launch_bounds__(256) void k_relax(RelaxArgs A) {
     }
     for (int u = ab; u < ae; ++u) {
       const int k = acol[u];
-      const float av = aval[u];
+      const float av = wk * aval[u];
       int bb = brp[k];
       const int be = brp[k + 1];
       int s = mb;
@@ -108,8 +119,8 @@ __global__ __launch_bounds__(256) void k_relax(RelaxArgs A) {
       }
     }
   }
-  const float fn = (float)n;
-  for (int e = mb; e < me; ++e) acc[e] = acc[e] / fn;  // CPNP/MSA.cpp:1233-1235
+  const float fn = A.qp.on ? sumw : (float)n;
+  for (int e = mb; e < me; ++e) acc[e] = acc[e] / fn;  // CPNP/MSA.cpp:1233-1235; ConsistencyStage.cpp:224-226
 }
 
 // Stable CSR transpose of one block per wave (rows processed in order, the
@@ -193,7 +204,7 @@ __global__ __launch_bounds__(256) void k_filter(FilterArgs A) {
     int rb = 0, re = 0;
     if (i <= La) {
       rb = rp[i]; re = rp[i + 1];
-      for (int e = rb; e < re; ++e) c += (A.raw[eo + e] >= 0.01f) ? 1 : 0;
+      for (int e = rb; e < re; ++e) c += (A.raw[eo + e] >= A.cutoff) ? 1 : 0;
     }
     int xs = c;
     for (int off = 1; off < 64; off <<= 1) {
@@ -205,9 +216,10 @@ __global__ __launch_bounds__(256) void k_filter(FilterArgs A) {
       nrp[i + 1] = pos + c;
       for (int e = rb; e < re; ++e) {
         const float v = A.raw[eo + e];
-        if (v >= 0.01f) {
+        if (v >= A.cutoff) {
           A.new_cols[neo + pos] = A.cols[eo + e];
-          A.new_vals[neo + pos] = v;
+          // QuickProbs' 16-bit entries (SparseEntry.h:31-32)
+          A.new_vals[neo + pos] = A.fixed16 ? (float)(uint32_t)(uint16_t)(v * 65535.0f) / 65535.0f : v;
           ++pos;
         }
       }
@@ -310,8 +322,10 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));  // plain vector: st
 #endif
 constexpr int kRelaxZChunk = 128;  // z schedule entries per LDS fill (64 B each)
 constexpr int kZEntBytes = 64;
-// LDS: [z schedule][per-output A bases][tile]
-static __host__ __device__ inline size_t relax_tile_off() { return (size_t)kZEntBytes * kRelaxZChunk + 16 * kTileMax; }
+// LDS: [z schedule][QuickProbs z weights][per-output A bases, weights, weight sums][tile]
+static __host__ __device__ inline size_t relax_tile_off() {
+  return (size_t)kZEntBytes * kRelaxZChunk + 16 * kRelaxZChunk + 16 * kTileMax + 16 + 16 + 16;
+}
 size_t tile_relax_lds(int cap) { return relax_tile_off() + (size_t)cap + 16; }  // + a word pair read past the last row
 
 int tile_relax_prefetch(int cap) {
@@ -336,7 +350,7 @@ __device__ __forceinline__ uint4 rfl(uint4 v) {
                     __builtin_amdgcn_readfirstlane(v.z), __builtin_amdgcn_readfirstlane(v.w));
 }
 
-template <int KP, int SL>
+template <int KP, int SL, bool QP>
 __global__ __launch_bounds__(kRelaxThreads) void k_relax_tile(TileRelaxArgs A) {
   extern __shared__ __align__(16) uint8_t lds[];
   constexpr int nt = kRelaxThreads;
@@ -362,8 +376,24 @@ __global__ __launch_bounds__(kRelaxThreads) void k_relax_tile(TileRelaxArgs A) {
   const int y = td[2 * TM];
   const int Ly = A.lens[y];
   uint4* ztab = (uint4*)lds;
-  int4* zb = (int4*)(lds + kZEntBytes * kRelaxZChunk);  // per output: A_t image bases this z
+  float4* wtab = (float4*)(lds + kZEntBytes * kRelaxZChunk);  // QuickProbs: w_z / W_{x_t y} per z of the chunk
+  int4* zb = (int4*)(lds + kZEntBytes * kRelaxZChunk + 16 * kRelaxZChunk);  // per output: A_t image bases this z
+  float* zw = (float*)(zb + TM);  // per output: this z's weight
+  float* zsum = zw + 4;           // per output: 1 + sum of the weights so far (z ascending)
+  float* wxy = zsum + 4;          // per output: QuickProbs' W_{x_t y} (ConsistencyStage.cpp:199-203)
   uint8_t* tileb = lds + relax_tile_off();
+  if (tid < TM) {
+    zsum[tid] = 1.0f;
+    float w = 1.0f;
+    if constexpr (QP) {
+      const int xx = td[TM + tid];
+      if (td[tid] >= 0) {
+        w = 1.0f + (A.qp.selfweight - 1.0f) * (float)(n - 2) / 200.0f;
+        w *= A.qp.weights[xx] + A.qp.weights[y];
+      }
+    }
+    wxy[tid] = w;
+  }
   // cells before output t (the masks' entries, in CSR order)
   int cb[TM + 1];
   cb[0] = 0;
@@ -396,7 +426,7 @@ __global__ __launch_bounds__(kRelaxThreads) void k_relax_tile(TileRelaxArgs A) {
       const uint32_t j = A.cols[ex + e];
       cel[s] = (uint32_t)lo | j << 13 | (uint32_t)t << 26;
       const float v = A.vals[ex + e];
-      acc[s] = v + v;  // z = x and z = y (CPNP/MSA.cpp:1211-1213)
+      acc[s] = QP ? v : v + v;  // z = x and z = y (CPNP/MSA.cpp:1211-1213); QuickProbs starts from P_xy
     }
   }
 
@@ -446,11 +476,29 @@ __global__ __launch_bounds__(kRelaxThreads) void k_relax_tile(TileRelaxArgs A) {
       ztab[4 * tid + 1] = e1;
       ztab[4 * tid + 2] = e2;
       ztab[4 * tid + 3] = e3;
+      if constexpr (QP) {  // every z != x_t, y counts in the weight sum, scheduled or not
+        float wz[TM];
+#pragma unroll
+        for (int t = 0; t < TM; ++t)
+          wz[t] = (z < n && z != y && td[t] >= 0 && z != td[TM + t]) ? A.qp.weights[z] / wxy[t] : 0.f;
+        wtab[tid] = make_float4(wz[0], wz[1], wz[2], wz[3]);
+      }
     }
     __syncthreads();
+    if constexpr (QP) {  // weight sums in z order (ConsistencyStage.cpp:205-217); + 0 leaves them unchanged
+      if (tid < TM) {
+        float sw = zsum[tid];
+        for (int k = 0; k < kRelaxZChunk && zbase + k < n; ++k) {
+          const float4 w4 = wtab[k];
+          sw += tid == 0 ? w4.x : tid == 1 ? w4.y : tid == 2 ? w4.z : w4.w;
+        }
+        zsum[tid] = sw;
+      }
+    }
   };
   // next scheduled z (uniform across the workgroup); returns false when done
   uint4 nC, nAo, nNa, nAc;  // the staged-next z's entry
+  float4 nW = make_float4(1.f, 1.f, 1.f, 1.f);  // its QuickProbs weights
   auto next = [&]() -> bool {
     for (;;) {
       if (++zpos == kRelaxZChunk) {
@@ -465,6 +513,12 @@ __global__ __launch_bounds__(kRelaxThreads) void k_relax_tile(TileRelaxArgs A) {
         nAo = rfl(ztab[4 * zpos + 1]);
         nNa = rfl(ztab[4 * zpos + 2]);
         nAc = rfl(ztab[4 * zpos + 3]);
+        if constexpr (QP) {
+          const float4 w4 = wtab[zpos];
+          const uint4 u = rfl(make_uint4(__float_as_uint(w4.x), __float_as_uint(w4.y), __float_as_uint(w4.z),
+                                         __float_as_uint(w4.w)));  // (readfirstlane is an int builtin)
+          nW = make_float4(__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w));
+        }
         return true;
       }
     }
@@ -500,6 +554,7 @@ __global__ __launch_bounds__(kRelaxThreads) void k_relax_tile(TileRelaxArgs A) {
   if (more) MLP_ISSUE();
 #ifdef MLP_RELAX_NOSTAGE
   const uint4 fC = nC, fAo = nAo, fNa = nNa, fAc = nAc;
+  const float4 fW = nW;
 #endif
   while (more) {
     // stage the prefetched tile; outputs' A bases (+ validity) into zb
@@ -512,6 +567,7 @@ __global__ __launch_bounds__(kRelaxThreads) void k_relax_tile(TileRelaxArgs A) {
     const uint32_t cbase = (uint32_t)(relax_tile_off() + 16 * (size_t)sg[TM]);
     const int nzC = (int)nC.y;
     if (tid == 0) {
+      zw[0] = nW.x; zw[1] = nW.y; zw[2] = nW.z; zw[3] = nW.w;
       const uint32_t na_[TM] = {nNa.x, nNa.y, nNa.z, nNa.w};
 #pragma unroll
       for (int t = 0; t < TM; ++t) {
@@ -524,7 +580,7 @@ __global__ __launch_bounds__(kRelaxThreads) void k_relax_tile(TileRelaxArgs A) {
     __syncthreads();
     more = next();
 #ifdef MLP_RELAX_NOSTAGE  // timing experiment: every z computes on the first z's tile
-    nC = fC; nAo = fAo; nNa = fNa; nAc = fAc;
+    nC = fC; nAo = fAo; nNa = fNa; nAc = fAc; nW = fW;
 #else
     if (more) MLP_ISSUE();
 #endif
@@ -561,6 +617,7 @@ __global__ __launch_bounds__(kRelaxThreads) void k_relax_tile(TileRelaxArgs A) {
           const uint2* pa = (const uint2*)(lds + z4.z) + ((int)(ha & 0xffff) - a0);
           const uint2* pc = Cwords + ((int)(hc & 0xffff) - c0);
           const float* Avals = (const float*)(lds + z4.x);
+          const float wk = QP ? zw[cl >> 26] : 1.0f;  // weight * XZ * ZY (ConsistencyStage.cpp:284)
           float ac = acc[s];
           // two words per step (the second masked off past the overlap)
           for (int w = max(a0, c0); w < we; w += 2) {
@@ -570,14 +627,16 @@ __global__ __launch_bounds__(kRelaxThreads) void k_relax_tile(TileRelaxArgs A) {
             while (m0) {  // common columns k, ascending
               const uint32_t bit = 1u << __builtin_ctz(m0);
               m0 ^= bit;
-              const float va = Avals[xa0.y + __popc(xa0.x & (bit - 1u))];
+              const float va = QP ? wk * Avals[xa0.y + __popc(xa0.x & (bit - 1u))]
+                                  : Avals[xa0.y + __popc(xa0.x & (bit - 1u))];
               const float vc = Cvals[xc0.y + __popc(xc0.x & (bit - 1u))];
               ac += va * vc;
             }
             while (m1) {
               const uint32_t bit = 1u << __builtin_ctz(m1);
               m1 ^= bit;
-              const float va = Avals[xa1.y + __popc(xa1.x & (bit - 1u))];
+              const float va = QP ? wk * Avals[xa1.y + __popc(xa1.x & (bit - 1u))]
+                                  : Avals[xa1.y + __popc(xa1.x & (bit - 1u))];
               const float vc = Cvals[xc1.y + __popc(xc1.x & (bit - 1u))];
               ac += va * vc;
             }
@@ -594,7 +653,8 @@ __global__ __launch_bounds__(kRelaxThreads) void k_relax_tile(TileRelaxArgs A) {
     __syncthreads();
   }
 #undef MLP_ISSUE
-  const float fn = (float)n;  // CPNP/MSA.cpp:1233-1235
+  __syncthreads();  // the weight sums of the last chunk
+  const float fn = (float)n;  // CPNP/MSA.cpp:1233-1235; QuickProbs: / the weight sum
 #pragma unroll
   for (int s = 0; s < SL; ++s) {
     if (cel[s] == 0) continue;
@@ -605,7 +665,7 @@ __global__ __launch_bounds__(kRelaxThreads) void k_relax_tile(TileRelaxArgs A) {
 #pragma unroll
     for (int u = 1; u < TM; ++u)
       if (t == u) { e = g - cb[u]; ex = eo[u]; }
-    A.out[ex + e] = acc[s] / fn;
+    A.out[ex + e] = acc[s] / (QP ? zsum[t] : fn);
   }
 }
 
@@ -615,15 +675,15 @@ hipError_t launch_pack(const PackArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
-template <int KP>
+template <int KP, bool QP>
 static hipError_t launch_tiles_kp(const TileRelaxArgs& a, int slots, size_t lds, hipStream_t st) {
   const dim3 grid((unsigned)a.ntiles), block(kRelaxThreads);
   switch (slots) {
 #define MLP_RELAX_CASE(SL)                                                                  \
   case SL:                                                                                  \
-    hipFuncSetAttribute((const void*)k_relax_tile<KP, SL>,                                  \
+    hipFuncSetAttribute((const void*)k_relax_tile<KP, SL, QP>,                              \
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);              \
-    hipLaunchKernelGGL((k_relax_tile<KP, SL>), grid, block, lds, st, a);                    \
+    hipLaunchKernelGGL((k_relax_tile<KP, SL, QP>), grid, block, lds, st, a);                \
     break;
     MLP_RELAX_CASE(4)
     MLP_RELAX_CASE(8)
@@ -640,8 +700,8 @@ hipError_t launch_relax_tiles(const TileRelaxArgs& a, int slots, hipStream_t st)
   const size_t lds = tile_relax_lds(a.cap);
   const char* kp = getenv("MLP_RELAX_KP");  // test hook: force the large-prefetch variant
   switch (kp ? atoi(kp) : tile_relax_prefetch(a.cap)) {
-    case 5: return launch_tiles_kp<5>(a, slots, lds, st);
-    case 9: return launch_tiles_kp<9>(a, slots, lds, st);
+    case 5: return a.qp.on ? launch_tiles_kp<5, true>(a, slots, lds, st) : launch_tiles_kp<5, false>(a, slots, lds, st);
+    case 9: return a.qp.on ? launch_tiles_kp<9, true>(a, slots, lds, st) : launch_tiles_kp<9, false>(a, slots, lds, st);
     default: return hipErrorInvalidValue;
   }
 }

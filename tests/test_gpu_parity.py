@@ -7,8 +7,8 @@ import numpy as np
 import pytest
 
 import orc
-from goldens import (GOLDEN, family_csrs, family_names, load_family, load_pair, load_qp_pair, pair_names,
-                     qp_pair_names)
+from goldens import (GOLDEN, family_csrs, family_names, load_family, load_pair, load_qp_family, load_qp_pair,
+                     pair_names, qp_family_csrs, qp_family_names, qp_pair_names)
 from mlprobs_amd import synth
 from mlprobs_amd.engine import PID_QP, Family
 from parity import close_scalar, csr_close, csr_equal
@@ -320,3 +320,56 @@ def test_qp_vs_oracle(s, L, n, seed):
 def test_qp_ragged_chains():
     """Many short ragged pairs stacked into chains, lengths 1..260."""
     _check_qp_family(_ragged_family(12, 1, 260, 64), 'qp_ragged')
+
+
+# ---- QuickProbs consistency (QP/Alignment/Multiple/ConsistencyStage.cpp:90-258)
+_RELAX_MODES = [{'MLP_RELAX': 'pairs'}, {'MLP_RELAX': 'pairs', 'MLP_RELAX_TILE': '1'},
+                {'MLP_RELAX': 'pairs', 'MLP_RELAX_KP': '9'}, {'MLP_RELAX': 'tasks'}]
+
+
+def _import(fam, csrs):
+    rp = np.concatenate([c[0] for c in csrs]).astype(np.int32)
+    eo = np.zeros(len(csrs) + 1, np.int64)
+    eo[1:] = np.cumsum([len(c[1]) for c in csrs])
+    cols = np.concatenate([c[1] for c in csrs] + [np.zeros(0, np.int32)]).astype(np.uint16)
+    vals = np.concatenate([c[2] for c in csrs] + [np.zeros(0, np.float32)]).astype(np.float32)
+    fam.import_csr(rp, eo, cols, vals)
+
+
+@pytest.mark.parametrize('name', qp_family_names())
+def test_qp_relax_golden(name):
+    """QuickProbs' consistency rounds from the reference's own posterior-stage
+    set, bit-exact against the reference build, on every relaxation path."""
+    d = load_qp_family(name)
+    ref = qp_family_csrs(d, d['iters'])
+    fam = Family(d['seqs'])
+    for env in _RELAX_MODES:
+        os.environ.update(env)
+        try:
+            _import(fam, qp_family_csrs(d, 0))
+            fam.relax_qp(d['iters'], d['weights'])
+            for k in range(len(ref)):
+                csr_equal(ref[k], fam.sparse(k), f'{name} {env} p{k}')
+        finally:
+            for key in env:
+                del os.environ[key]
+    fam.close()
+
+
+@pytest.mark.parametrize('n,L,s,iters,seed', [(9, 140, 0.6, 2, 71), (7, 200, 0.3, 1, 72), (12, 90, 0.7, 3, 73)])
+def test_qp_stage_vs_oracle(n, L, s, iters, seed):
+    """QuickProbs posterior stage then consistency, all on the GPU, against the
+    oracle's restatement of both stages."""
+    seqs = [x for _, x in synth.family(n, L, s, seed=seed)]
+    w = np.random.default_rng(seed).uniform(1, 30, n).astype(np.float32)
+    fam = Family(seqs)
+    fam.posteriors(PID_QP, 0.0)
+    cur = [_qp_expected(seqs, a, b)[0] for a in range(n) for b in range(a + 1, n)]
+    cur = [(r.astype(np.int32), c.astype(np.int32), v) for r, c, v in cur]
+    lens = [len(x) for x in seqs]
+    for it in range(1, iters + 1):
+        cur = orc.relax(lens, cur, qp=(w, 3.0, 1e-5 if it == iters else 0.01))
+    fam.relax_qp(iters, w)
+    for k in range(len(cur)):
+        csr_equal(cur[k], fam.sparse(k), f'qp stage p{k}')
+    fam.close()
