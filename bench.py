@@ -52,6 +52,7 @@ def parse():
     ap.add_argument('--relax', type=int, default=-1,
                     help='also time N relaxation rounds (reported separately; default 1 on one GPU, 0 on several)')
     ap.add_argument('--no-e2e', action='store_true', help='skip the end-to-end c_p_np_aln family timings')
+    ap.add_argument('--no-qp', action='store_true', help='skip the QuickProbs posterior/consistency timings')
     return ap.parse_args()
 
 
@@ -107,6 +108,43 @@ def e2e_families(args):
                 name, sec = line[8:].rsplit(' ', 2)[0], line.rsplit(' ', 2)[1]
                 stages[name] = float(sec)
         res[tag] = {'seconds': dt, 'exit': r.returncode, 'stages_s': stages}
+    return res
+
+
+def quickprobs_stage(fam, fam_in, total_cells, args):
+    """QuickProbs' posterior stage (MLP_PID_QP) and one consistency round
+    (its default for N > 50) on the same family, resident in HBM; the
+    reference QuickProbs posterior stage (oracle/_ref/qp_probe, compiled from
+    the reference sources) timed on a bounded sample as its CPU baseline."""
+    from mlprobs_amd.engine import PID_QP
+    fam.profile(False)
+    fam.posteriors(PID_QP, 0.0)  # warm-up
+    fam.synchronize()
+    t0 = time.perf_counter()
+    fam.posteriors(PID_QP, 0.0)
+    fam.synchronize()
+    dt = time.perf_counter() - t0
+    tr = time.perf_counter()
+    fam.relax_qp(1, np.ones(fam.n, np.float32))
+    fam.synchronize()
+    dr = time.perf_counter() - tr
+    res = {'posterior_pair_cells_per_s': total_cells / dt, 'posterior_ms': dt * 1e3,
+           'consistency_round_s': dr, 'nnz_out': int(fam.results()[2].sum())}
+    probe = os.path.join(ROOT, 'oracle', '_ref', 'qp_probe')
+    if os.path.exists(probe) and not args.no_cpu:
+        with tempfile.TemporaryDirectory() as td:
+            path = os.path.join(td, 'fam.txt')
+            with open(path, 'w') as fh:
+                fh.write('\n'.join(sq for _, sq in fam_in))
+            out = subprocess.run([probe, 'bench', path, str(args.cpu_pairs // 2), str(args.cpu_threads)],
+                                 capture_output=True, text=True, timeout=600)
+        if out.returncode == 0:
+            r = json.loads(out.stdout.strip().splitlines()[-1])
+            res['cpu_baseline'] = {'value': r['pair_cells_per_s'], 'unit': 'pair-cells/s',
+                                   'cores': args.cpu_threads, 'kind': 'reference',
+                                   'sample': f"first {r['pairs']} pairs, {r['seconds']:.1f} s, reference "
+                                             "QuickProbs PosteriorStage::computePairwise"}
+            res['speedup_vs_cpu'] = res['posterior_pair_cells_per_s'] / r['pair_cells_per_s']
     return res
 
 
@@ -172,6 +210,7 @@ def main():
         dt = float(t.item())
     kt = fam.kernel_times()
     _, _, nnz = fam.results()  # posterior-stage sparse set (before any relaxation)
+    nnz = nnz.copy()
     relax_info = None
     if args.relax > 0:
         fam.profile(True)
@@ -205,6 +244,7 @@ def main():
             valu = {'achieved': issued, 'peak': VALU_PEAK_WAVE_INSTS, 'unit': 'wave-instr/s',
                     'frac': issued / VALU_PEAK_WAVE_INSTS,
                     'insts_per_cell': g['valu_insts_per_cell']}
+    qp_info = quickprobs_stage(fam, fam_in, total_cells, args) if (world == 1 and not args.no_qp) else None
     out = None
     if rank == 0:
         cpu = None
@@ -249,6 +289,8 @@ def main():
             out['relax'] = relax_info
         if e2e is not None:
             out['e2e'] = e2e
+        if qp_info is not None:
+            out['quickprobs'] = qp_info
         print(json.dumps(out))
     fam.close()
     if world > 1:

@@ -14,6 +14,7 @@
 //
 //   qp_probe params            -> tables
 //   qp_probe pair SEQ1 SEQ2    -> posteriors, distance, sparse matrix
+//   qp_probe bench FILE PAIRS THREADS -> reference CPU posterior-stage timing
 //   qp_probe relax FILE ITERS  -> posterior stage + ITERS consistency rounds
 //                                 (FILE: lines "weight sequence")
 // (records written to $REF_PROBE_OUT)
@@ -38,7 +39,9 @@
 #include "Alignment/Multiple/ConsistencyStage.h"
 #include "Alignment/DataStructures/MultiSequence.h"
 
+#include <algorithm>
 #include <fstream>
+#include <omp.h>
 #include <sstream>
 
 using namespace quickprobs;
@@ -197,11 +200,52 @@ static int cmd_relax(const char *path, int iters) {
   return 0;
 }
 
+// Reference CPU baseline for the QuickProbs posterior stage: PosteriorStage::
+// computePairwise over the first `pairs` pairs of a family file (one sequence
+// per line), OpenMP over pairs like PosteriorStage::run; prints one JSON line.
+static int cmd_bench(const char *path, int pairs, int threads) {
+  auto cfg = protein_config();
+  std::ifstream in(path);
+  std::vector<std::string> seqs;
+  std::string line;
+  while (std::getline(in, line))
+    if (!line.empty()) seqs.push_back(line);
+  const int n = (int)seqs.size();
+  std::vector<std::pair<int, int>> pl;
+  for (int a = 0; a < n && (int)pl.size() < pairs; a++)
+    for (int b = a + 1; b < n && (int)pl.size() < pairs; b++) pl.push_back({a, b});
+  std::vector<std::unique_ptr<Sequence>> sq;
+  size_t maxL = 0;
+  for (int k = 0; k < n; k++) {
+    sq.emplace_back(make_seq(seqs[k], k));
+    maxL = std::max(maxL, seqs[k].size());
+  }
+  PosteriorStage stage(cfg);
+  omp_set_num_threads(threads);
+  double cells = 0;
+  for (auto &p : pl) cells += (double)(seqs[p.first].size() + 1) * (seqs[p.second].size() + 1);
+  const double t0 = omp_get_wtime();
+#pragma omp parallel
+  {
+    BufferSet buf((maxL + 1) * (maxL + 1));
+#pragma omp for schedule(dynamic)
+    for (int k = 0; k < (int)pl.size(); k++) {
+      float d;
+      stage.computePairwise(*sq[pl[k].first], *sq[pl[k].second], buf, d);
+    }
+  }
+  const double dt = omp_get_wtime() - t0;
+  printf("{\"pairs\": %d, \"seconds\": %.3f, \"pair_cells_per_s\": %.1f, \"threads\": %d}\n", (int)pl.size(), dt,
+         cells / dt, threads);
+  return 0;
+}
+
 int main(int argc, char **argv) {
   if (argc < 2) {
     fprintf(stderr, "usage: qp_probe params | pair SEQ1 SEQ2\n");
     return 2;
   }
+  if (std::string(argv[1]) == "bench" && argc == 5) return cmd_bench(argv[2], atoi(argv[3]), atoi(argv[4]));
   const char *outp = getenv("REF_PROBE_OUT");
   if (!outp) {
     fprintf(stderr, "set REF_PROBE_OUT\n");
