@@ -123,6 +123,15 @@ int mlp_relax(mlp_ctx *ctx, int iters);
  * 0.01 except the last (1e-5) into 16-bit fixed point.  iters < 0: QuickProbs'
  * default (2 rounds up to 50 sequences, else 1). */
 int mlp_relax_qp(mlp_ctx *ctx, int iters, const float *seq_weights);
+/* The same with QuickProbs' selectivity (ConsistencyStage.cpp:35-47, 171-205;
+ * ExtendedMSA::doAlign, QP/Alignment/Multiple/ExtendedMSA.cpp:96-176): z is
+ * accepted for (x, y) iff max(sel_dist[x][z], sel_dist[y][z]) <= selectivity
+ * (the Deterministic filter), W_xy counts the accepted z only
+ * (1 + (s - 1) A_xy / selectivity).  sel_dist: N x N host matrix, row-major
+ * (QuickProbs passes the guide tree's subtree sizes with selectivity 200);
+ * NULL accepts every z (= mlp_relax_qp). */
+int mlp_relax_qp_selective(mlp_ctx *ctx, int iters, const float *seq_weights, const float *sel_dist,
+                           float selectivity);
 
 /* Multi-GPU (one process per GPU): RCCL over xGMI. */
 int mlp_comm_unique_id(unsigned char id[128]);

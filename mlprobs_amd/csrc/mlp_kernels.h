@@ -161,14 +161,24 @@ hipError_t launch_compact(SeqSet seqs, PairMeta pm, PairRec* rec, Scratch sc,
 
 // relaxation (relax.hip)
 // QuickProbs' consistency round (ConsistencyStage::doRelaxation, QP/Alignment/
-// Multiple/ConsistencyStage.cpp:133-258) instead of C_P_NP_Aln's: every z is
-// weighted by w_z / W_xy, W_xy = (1 + (s - 1)(N - 2) / 200)(w_x + w_y), the
-// sum starts from P_xy (not 2 P_xy) and is divided by 1 + sum_z w_z / W_xy.
+// Multiple/ConsistencyStage.cpp:133-258) instead of C_P_NP_Aln's: an accepted
+// z is weighted by w_z / W_xy, W_xy = (1 + (s - 1) A_xy / a)(w_x + w_y) with
+// A_xy the number of accepted z, the sum starts from P_xy (not 2 P_xy) and is
+// divided by 1 + sum_z w_z / W_xy.  Selectivity (the Deterministic filter,
+// ConsistencyStage.cpp:35-47, 171-186): z is accepted for (x, y) iff
+// max(D[x][z], D[y][z]) <= a; without D every z is.
 struct QpRelax {
   int on;                    // 0: C_P_NP_Aln's round
   const float* weights;      // per sequence (device)
   float selfweight;
+  const float* seldist;      // N x N selectivity distances (device) or null
+  float selectivity;         // a (the filter threshold and the A_xy divisor)
 };
+__device__ __forceinline__ bool qp_accept(const QpRelax& q, int n, int x, int y, int z) {
+  if (!q.seldist) return true;
+  const float dx = q.seldist[(int64_t)x * n + z], dy = q.seldist[(int64_t)y * n + z];
+  return (dx > dy ? dx : dy) <= q.selectivity;  // std::max(x, y), then x <= a
+}
 struct RelaxArgs {
   int n;                     // sequences in the family
   const int32_t* lens;

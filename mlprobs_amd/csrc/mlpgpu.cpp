@@ -85,7 +85,7 @@ struct mlp_ctx {
   size_t scratch_budget = 0;
   // relaxation buffers
   DevBuf r_trowptr, r_tcols, r_tvals, r_raw, r_newrp, r_newcols, r_newvals, r_tasks_p, r_tasks_r,
-      r_pairs, r_nnz, r_newoff, r_img, r_imgoff, r_tiles, r_nwords, r_weights;
+      r_pairs, r_nnz, r_newoff, r_img, r_imgoff, r_tiles, r_nwords, r_weights, r_seldist;
   // comm
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
@@ -340,7 +340,8 @@ void mlp_ctx_destroy(mlp_ctx* c) {
     if (p) hipFree(p);
   DevBuf* bufs[] = {&c->scratch, &c->scratch2, &c->r_trowptr, &c->r_tcols, &c->r_tvals, &c->r_raw, &c->r_newrp,
                     &c->r_newcols, &c->r_newvals, &c->r_tasks_p, &c->r_tasks_r, &c->r_pairs,
-                    &c->r_nnz, &c->r_newoff, &c->r_img, &c->r_imgoff, &c->r_tiles, &c->r_nwords, &c->r_weights};
+                    &c->r_nnz, &c->r_newoff, &c->r_img, &c->r_imgoff, &c->r_tiles, &c->r_nwords, &c->r_weights,
+                    &c->r_seldist};
   for (DevBuf* b : bufs)
     if (b->p) hipFree(b->p);
   if (c->comm) ncclCommDestroy(c->comm);
@@ -1266,7 +1267,7 @@ static int relax_rounds(mlp_ctx* c, int iters, const QpRelax& qp);
 
 int mlp_relax(mlp_ctx* c, int iters) {
   if (!c || iters < 0) return MLP_ERR_ARG;
-  return relax_rounds(c, iters, QpRelax{0, nullptr, 0.f});
+  return relax_rounds(c, iters, QpRelax{0, nullptr, 0.f, nullptr, 200.f});
 }
 
 // QuickProbs' consistency stage (ConsistencyStage::operator() / run,
@@ -1274,13 +1275,26 @@ int mlp_relax(mlp_ctx* c, int iters) {
 // configuration: 2 rounds up to 50 sequences, 1 above (iters < 0), self-weight
 // 3, every round but the last re-sparsified at 0.01, the last at 1e-5.
 int mlp_relax_qp(mlp_ctx* c, int iters, const float* seq_weights) {
-  if (!c || !seq_weights) return MLP_ERR_ARG;
+  return mlp_relax_qp_selective(c, iters, seq_weights, nullptr, 200.f);
+}
+
+int mlp_relax_qp_selective(mlp_ctx* c, int iters, const float* seq_weights, const float* sel_dist,
+                           float selectivity) {
+  if (!c || !seq_weights || !(selectivity > 0)) return MLP_ERR_ARG;
   if (c->n < 2) return MLP_ERR_STATE;
   if (iters < 0) iters = c->n > 50 ? 1 : 2;
   int rc;
   if ((rc = ensure(c, c->r_weights, sizeof(float) * c->n))) return rc;
   HIPCHK(c, hipMemcpyAsync(c->r_weights.p, seq_weights, sizeof(float) * c->n, hipMemcpyHostToDevice, c->stream));
-  return relax_rounds(c, iters, QpRelax{1, (const float*)c->r_weights.p, 3.0f});
+  const float* dsel = nullptr;
+  if (sel_dist) {
+    const size_t bytes = sizeof(float) * (size_t)c->n * c->n;
+    if ((rc = ensure(c, c->r_seldist, bytes))) return rc;
+    HIPCHK(c, hipMemcpyAsync(c->r_seldist.p, sel_dist, bytes, hipMemcpyHostToDevice, c->stream));
+    dsel = (const float*)c->r_seldist.p;
+  }
+  HIPCHK(c, hipStreamSynchronize(c->stream));  // the caller's buffers may go away
+  return relax_rounds(c, iters, QpRelax{1, (const float*)c->r_weights.p, 3.0f, dsel, selectivity});
 }
 
 static int relax_rounds(mlp_ctx* c, int iters, const QpRelax& qp) {

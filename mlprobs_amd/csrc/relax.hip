@@ -57,11 +57,14 @@ __global__ __launch_bounds__(256) void k_relax(RelaxArgs A) {
   }
   float wxy = 0.f, sumw = 1.0f;  // QuickProbs' weights (ConsistencyStage.cpp:199-203)
   if (A.qp.on) {
-    wxy = 1.0f + (A.qp.selfweight - 1.0f) * (float)(n - 2) / 200.0f;
+    int accepted = 0;
+    for (int z = 0; z < n; ++z) accepted += z != x && z != y && qp_accept(A.qp, n, x, y, z);
+    wxy = 1.0f + (A.qp.selfweight - 1.0f) * (float)accepted / A.qp.selectivity;
     wxy *= A.qp.weights[x] + A.qp.weights[y];
   }
   for (int z = 0; z < n; ++z) {
     if (z == x || z == y) continue;
+    if (A.qp.on && !qp_accept(A.qp, n, x, y, z)) continue;
     float wk = 1.0f;  // (1 * a) * b == a * b: C_P_NP_Aln's unweighted terms
     if (A.qp.on) {
       wk = A.qp.weights[z] / wxy;
@@ -382,13 +385,32 @@ __global__ __launch_bounds__(kRelaxThreads) void k_relax_tile(TileRelaxArgs A) {
   float* zsum = zw + 4;           // per output: 1 + sum of the weights so far (z ascending)
   float* wxy = zsum + 4;          // per output: QuickProbs' W_{x_t y} (ConsistencyStage.cpp:199-203)
   uint8_t* tileb = lds + relax_tile_off();
+  if constexpr (QP) {  // accepted z per output (A_xy)
+    int* nacc = (int*)wxy;
+    if (tid < TM) nacc[tid] = 0;
+    __syncthreads();
+    if (A.qp.seldist) {
+      int c[TM];
+#pragma unroll
+      for (int t = 0; t < TM; ++t) c[t] = 0;
+      for (int z = tid; z < n; z += nt)
+#pragma unroll
+        for (int t = 0; t < TM; ++t)
+          c[t] += td[t] >= 0 && z != y && z != td[TM + t] && qp_accept(A.qp, n, td[TM + t], y, z);
+#pragma unroll
+      for (int t = 0; t < TM; ++t)
+        if (c[t]) atomicAdd(&nacc[t], c[t]);
+    }
+    __syncthreads();
+  }
   if (tid < TM) {
     zsum[tid] = 1.0f;
     float w = 1.0f;
     if constexpr (QP) {
       const int xx = td[TM + tid];
       if (td[tid] >= 0) {
-        w = 1.0f + (A.qp.selfweight - 1.0f) * (float)(n - 2) / 200.0f;
+        const int accepted = A.qp.seldist ? ((const int*)wxy)[tid] : n - 2;
+        w = 1.0f + (A.qp.selfweight - 1.0f) * (float)accepted / A.qp.selectivity;
         w *= A.qp.weights[xx] + A.qp.weights[y];
       }
     }
@@ -451,7 +473,7 @@ __global__ __launch_bounds__(kRelaxThreads) void k_relax_tile(TileRelaxArgs A) {
           for (int t = 0; t < TM; ++t) {
             ao[t] = na[t] = ac[t] = 0;
             const int xx = td[TM + t];  // (not xt[]: arrays captured by a lambda end up in scratch)
-            if (td[t] >= 0 && z != xx) {
+            if (td[t] >= 0 && z != xx && (!QP || qp_accept(A.qp, n, xx, y, z))) {
               int64_t pa, qa;
               if (xx < z) { pa = pair_index(n, xx, z); qa = 2 * pa; } else { pa = pair_index(n, z, xx); qa = 2 * pa + 1; }
               const int nza = (int)(A.ent_off[pa + 1] - A.ent_off[pa]);
@@ -476,11 +498,13 @@ __global__ __launch_bounds__(kRelaxThreads) void k_relax_tile(TileRelaxArgs A) {
       ztab[4 * tid + 1] = e1;
       ztab[4 * tid + 2] = e2;
       ztab[4 * tid + 3] = e3;
-      if constexpr (QP) {  // every z != x_t, y counts in the weight sum, scheduled or not
+      if constexpr (QP) {  // every accepted z != x_t, y counts in the weight sum, scheduled or not
         float wz[TM];
 #pragma unroll
         for (int t = 0; t < TM; ++t)
-          wz[t] = (z < n && z != y && td[t] >= 0 && z != td[TM + t]) ? A.qp.weights[z] / wxy[t] : 0.f;
+          wz[t] = (z < n && z != y && td[t] >= 0 && z != td[TM + t] && qp_accept(A.qp, n, td[TM + t], y, z))
+                      ? A.qp.weights[z] / wxy[t]
+                      : 0.f;
         wtab[tid] = make_float4(wz[0], wz[1], wz[2], wz[3]);
       }
     }

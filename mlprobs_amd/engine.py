@@ -69,6 +69,7 @@ def lib():
         L.mlp_csr_import.argtypes = [P, I32P, I64P, U16P, F32P]
         L.mlp_relax.argtypes = [P, C.c_int]
         L.mlp_relax_qp.argtypes = [P, C.c_int, F32P]
+        L.mlp_relax_qp_selective.argtypes = [P, C.c_int, F32P, C.c_void_p, C.c_float]
         L.mlp_viterbi.argtypes = [P, I64, I64, C.c_int]
         L.mlp_viterbi_results.argtypes = [P, I64, I64, C.c_void_p, C.c_void_p]
         L.mlp_viterbi_path.argtypes = [P, I64, C.c_void_p, C.c_void_p]
@@ -90,7 +91,8 @@ def lib():
 
 EXPORTED = ['mlp_ctx_create', 'mlp_ctx_destroy', 'mlp_last_error', 'mlp_set_scratch', 'mlp_family_load',
             'mlp_family_npairs', 'mlp_posteriors', 'mlp_pair_results', 'mlp_csr_total',
-            'mlp_csr_export', 'mlp_csr_import', 'mlp_relax', 'mlp_relax_qp', 'mlp_viterbi', 'mlp_viterbi_results',
+            'mlp_csr_export', 'mlp_csr_import', 'mlp_relax', 'mlp_relax_qp',
+            'mlp_relax_qp_selective', 'mlp_viterbi', 'mlp_viterbi_results',
             'mlp_viterbi_path', 'mlp_model_adjustment', 'mlp_family_features', 'mlp_comm_unique_id', 'mlp_comm_init',
             'mlp_shard_range', 'mlp_shard_plan', 'mlp_gather_layout', 'mlp_allgather', 'mlp_synchronize', 'mlp_profile',
             'mlp_kernel_times', 'mlp_profile_reset']
@@ -220,11 +222,18 @@ class Family:
         return r, cols[e0:e1].astype(np.int32), vals[e0:e1]
 
     # ---- consistency
-    def relax_qp(self, iters, weights):
-        """QuickProbs' consistency rounds (include/mlpgpu.h mlp_relax_qp)."""
+    def relax_qp(self, iters, weights, sel_dist=None, selectivity=200.0):
+        """QuickProbs' consistency rounds (include/mlpgpu.h mlp_relax_qp,
+        mlp_relax_qp_selective with an N x N selectivity distance matrix)."""
         w = np.ascontiguousarray(weights, np.float32)
         assert len(w) == self.n
-        self._chk(self._L.mlp_relax_qp(self._ctx, int(iters), w))
+        self._csr = None
+        if sel_dist is None:
+            self._chk(self._L.mlp_relax_qp(self._ctx, int(iters), w))
+            return
+        d = np.ascontiguousarray(sel_dist, np.float32)
+        assert d.shape == (self.n, self.n)
+        self._chk(self._L.mlp_relax_qp_selective(self._ctx, int(iters), w, d.ctypes.data, float(selectivity)))
 
     def relax(self, iters):
         self._csr = None

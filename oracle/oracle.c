@@ -623,13 +623,15 @@ static int pair_index(int N, int a, int b) { /* a < b, row-major */
   return a * N - a * (a + 1) / 2 + (b - a - 1);
 }
 
-/* qp: QuickProbs' ConsistencyStage::doRelaxation with its defaults
- * (QP/Alignment/Multiple/ConsistencyStage.cpp:133-258): the deterministic
- * selectivity filter with selectivity 200 accepts every z (distances <= 1,
- * the Park-Miller draw < 1.003 < 2), so P' = (P + sum_z w_z / W_xy P_xz P_zy)
- * / (1 + sum_z w_z / W_xy), W_xy = (1 + (s - 1)(N - 2) / 200)(w_x + w_y),
- * re-sparsified at `cutoff` into 16-bit fixed point (values out as q / 65535). */
+/* qp: QuickProbs' ConsistencyStage::doRelaxation (QP/Alignment/Multiple/
+ * ConsistencyStage.cpp:133-258) with the Deterministic selectivity filter
+ * (qp_accept below; without seldist every z is accepted): P' = (P + sum_z
+ * w_z / W_xy P_xz P_zy) / (1 + sum_z w_z / W_xy) over the accepted z,
+ * W_xy = (1 + (s - 1) A_xy / a)(w_x + w_y), re-sparsified at `cutoff` into
+ * 16-bit fixed point (values out as q / 65535). */
+static int qp_accept(const float *seldist, float a, int N, int i, int j, int k);
 static int64_t relax_impl(int qp, const float *weights, float selfweight, float cutoff,
+                          const float *seldist, float selectivity,
                           int N, const int32_t *lens, const int64_t *row_off, const int64_t *ent_off,
                           const int32_t *in_rp, const int32_t *in_cols, const float *in_vals,
                           int32_t *out_rp, int64_t *out_ent_off, int32_t *out_cols, float *out_vals,
@@ -639,7 +641,7 @@ int64_t orc_relax(int N, const int32_t *lens, const int64_t *row_off, const int6
                   const int32_t *in_rp, const int32_t *in_cols, const float *in_vals,
                   int32_t *out_rp, int64_t *out_ent_off, int32_t *out_cols, float *out_vals,
                   int64_t max_out) {
-  return relax_impl(0, NULL, 0, 0, N, lens, row_off, ent_off, in_rp, in_cols, in_vals, out_rp, out_ent_off,
+  return relax_impl(0, NULL, 0, 0, NULL, 200.0f, N, lens, row_off, ent_off, in_rp, in_cols, in_vals, out_rp, out_ent_off,
                     out_cols, out_vals, max_out);
 }
 
@@ -648,8 +650,27 @@ int64_t orc_qp_relax(const float *weights, float selfweight, float cutoff,
                      const int32_t *in_rp, const int32_t *in_cols, const float *in_vals,
                      int32_t *out_rp, int64_t *out_ent_off, int32_t *out_cols, float *out_vals,
                      int64_t max_out) {
-  return relax_impl(1, weights, selfweight, cutoff, N, lens, row_off, ent_off, in_rp, in_cols, in_vals, out_rp,
-                    out_ent_off, out_cols, out_vals, max_out);
+  return relax_impl(1, weights, selfweight, cutoff, NULL, 200.0f, N, lens, row_off, ent_off, in_rp, in_cols, in_vals,
+                    out_rp, out_ent_off, out_cols, out_vals, max_out);
+}
+
+int64_t orc_qp_relax_sel(const float *weights, float selfweight, float cutoff, const float *seldist,
+                         float selectivity, int N, const int32_t *lens, const int64_t *row_off,
+                         const int64_t *ent_off, const int32_t *in_rp, const int32_t *in_cols,
+                         const float *in_vals, int32_t *out_rp, int64_t *out_ent_off, int32_t *out_cols,
+                         float *out_vals, int64_t max_out) {
+  return relax_impl(1, weights, selfweight, cutoff, seldist, selectivity, N, lens, row_off, ent_off, in_rp, in_cols,
+                    in_vals, out_rp, out_ent_off, out_cols, out_vals, max_out);
+}
+
+/* The Deterministic selectivity filter (ConsistencyStage.cpp:35-47, 171-186):
+ * x = max(D[i][k], D[j][k]); filter = x <= a ? 2 : 0; the Park-Miller draw
+ * seed * RND_MAX_INV lies in [0, 1.0026], so z is accepted iff x <= a (a draw
+ * of exactly 0 with filter 0 gives w = 0, not < 0: rejected as well). */
+static int qp_accept(const float *seldist, float a, int N, int i, int j, int k) {
+  if (!seldist) return 1;
+  const float di = seldist[(size_t)i * N + k], dj = seldist[(size_t)j * N + k];
+  return (di > dj ? di : dj) <= a;
 }
 
 static int64_t qp_sparsify_vals(int L1, int L2, const float *post, float cutoff, int32_t *rowptr, int32_t *cols,
@@ -672,6 +693,7 @@ static int64_t qp_sparsify_vals(int L1, int L2, const float *post, float cutoff,
 }
 
 static int64_t relax_impl(int qp, const float *weights, float selfweight, float cutoff,
+                          const float *seldist, float selectivity,
                           int N, const int32_t *lens, const int64_t *row_off, const int64_t *ent_off,
                           const int32_t *in_rp, const int32_t *in_cols, const float *in_vals,
                           int32_t *out_rp, int64_t *out_ent_off, int32_t *out_cols, float *out_vals,
@@ -695,8 +717,11 @@ static int64_t relax_impl(int qp, const float *weights, float selfweight, float 
     if (!qp)  /* z = x and z = y (CPNP/MSA.cpp:1211-1213) */
       for (size_t k = 0; k < (size_t)(L1 + 1) * W; k++) post[k] += post[k];
     float wxy = 0, sumW = 1.0f;
-    if (qp) {  /* ConsistencyStage.cpp:199-203 */
-      wxy = 1.0f + (selfweight - 1.0f) * (float)(N - 2) / 200.0f;
+    if (qp) {  /* ConsistencyStage.cpp:165-203 */
+      int accepted = 0;
+      for (int k = 0; k < N; k++)
+        if (k != i && k != j && qp_accept(seldist, selectivity, N, i, j, k)) accepted++;
+      wxy = 1.0f + (selfweight - 1.0f) * (float)accepted / selectivity;
       wxy *= weights[i] + weights[j];
     }
     int maxL = 0;
@@ -708,6 +733,7 @@ static int64_t relax_impl(int qp, const float *weights, float selfweight, float 
     int64_t tcap = 0;
     for (int k = 0; k < N; k++) {
       if (k == i || k == j) continue;
+      if (qp && !qp_accept(seldist, selectivity, N, i, j, k)) continue;
       float w = 1.0f;
       if (qp) {
         w = weights[k] / wxy;

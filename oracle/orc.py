@@ -68,6 +68,8 @@ def lib():
         L.orc_qp_sparsify.restype = C.c_int64
         L.orc_qp_relax.argtypes = [F32P, C.c_float, C.c_float] + L.orc_relax.argtypes
         L.orc_qp_relax.restype = C.c_int64
+        L.orc_qp_relax_sel.argtypes = [F32P, C.c_float, C.c_float, F32P, C.c_float] + L.orc_relax.argtypes
+        L.orc_qp_relax_sel.restype = C.c_int64
         _LIB = L
     return _LIB
 
@@ -174,7 +176,8 @@ def pair_loop(m, seqs, pid, max_pairs=-1, threads=0):
 
 def relax(lens, csrs, qp=None):
     """csrs: list over pairs (a<b row-major) of (rowptr[L_a+2], cols, vals).
-    qp = (weights, selfweight, cutoff): QuickProbs' consistency round instead."""
+    qp = (weights, selfweight, cutoff[, seldist, selectivity]): QuickProbs'
+    consistency round instead (with its selectivity filter when seldist is given)."""
     N = len(lens)
     lens = np.asarray(lens, np.int32)
     row_off = np.zeros(len(csrs), np.int64)
@@ -197,8 +200,13 @@ def relax(lens, csrs, qp=None):
         tot = lib().orc_relax(N, lens, row_off, ent_off, in_rp, in_c, in_v, out_rp, out_off, out_c, out_v, cap)
     else:
         w = np.ascontiguousarray(qp[0], np.float32)
-        tot = lib().orc_qp_relax(w, float(qp[1]), float(qp[2]), N, lens, row_off, ent_off, in_rp, in_c, in_v,
-                                 out_rp, out_off, out_c, out_v, cap)
+        if len(qp) > 3 and qp[3] is not None:
+            d = np.ascontiguousarray(qp[3], np.float32)
+            tot = lib().orc_qp_relax_sel(w, float(qp[1]), float(qp[2]), d, float(qp[4]), N, lens, row_off, ent_off,
+                                         in_rp, in_c, in_v, out_rp, out_off, out_c, out_v, cap)
+        else:
+            tot = lib().orc_qp_relax(w, float(qp[1]), float(qp[2]), N, lens, row_off, ent_off, in_rp, in_c, in_v,
+                                     out_rp, out_off, out_c, out_v, cap)
     assert tot >= 0
     res = []
     for p in range(len(csrs)):

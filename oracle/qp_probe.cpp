@@ -15,8 +15,9 @@
 //   qp_probe params            -> tables
 //   qp_probe pair SEQ1 SEQ2    -> posteriors, distance, sparse matrix
 //   qp_probe bench FILE PAIRS THREADS -> reference CPU posterior-stage timing
-//   qp_probe relax FILE ITERS  -> posterior stage + ITERS consistency rounds
-//                                 (FILE: lines "weight sequence")
+//   qp_probe relax FILE ITERS [SEL] -> posterior stage + ITERS consistency
+//                                 rounds (FILE: lines "weight sequence"; SEL: the
+//                                 selectivity threshold over posterior distances)
 // (records written to $REF_PROBE_OUT)
 
 #include <cstdint>
@@ -159,8 +160,12 @@ static void dump_set(const char *tag, int n, Array<SparseMatrixType *> &mats) {
 // PosteriorStage::run's pair loop, then ConsistencyStage::run with the
 // default configuration (QP/Alignment/Multiple/ConsistencyStage.cpp:90-128):
 // the last round keeps entries >= 1e-5 instead of the 0.01 cutoff.
-static int cmd_relax(const char *path, int iters) {
+static int cmd_relax(const char *path, int iters, float selectivity) {
   auto cfg = protein_config();
+  // selectivity > 0: the Deterministic filter's threshold (default 200, which
+  // accepts every z for posterior distances <= 1); the stage reads it at
+  // construction (ConsistencyStage.cpp:44-47)
+  if (selectivity > 0) cfg->algorithm.consistency.selectivity = selectivity;
   std::ifstream in(path);
   std::vector<float> w;
   MultiSequence set;
@@ -182,6 +187,12 @@ static int cmd_relax(const char *path, int iters) {
   for (int a = 0; a < n; a++)
     for (int b = a + 1; b < n; b++) d.push_back(dist[a][b]);
   rec("dist", 'f', d.data(), d.size());
+  std::vector<float> full((size_t)n * n);  // the N x N matrix the stage's filter reads
+  for (int a = 0; a < n; a++)
+    for (int b = 0; b < n; b++) full[(size_t)a * n + b] = dist[a][b];
+  rec("seldist", 'f', full.data(), full.size());
+  const float sel = cfg->algorithm.consistency.selectivity;
+  rec("selectivity", 'f', &sel, 1);
   dump_set("it0", n, mats);
   ConsistencyStage cons(cfg);
   cons.selfweight = n > cfg->algorithm.consistency.selfweightThreshold ? cfg->algorithm.consistency.largeSelfweight
@@ -257,7 +268,7 @@ int main(int argc, char **argv) {
   int rc = 2;
   if (cmd == "params") rc = cmd_params();
   else if (cmd == "pair" && argc == 4) rc = cmd_pair(argv[2], argv[3]);
-  else if (cmd == "relax" && argc == 4) rc = cmd_relax(argv[2], atoi(argv[3]));
+  else if (cmd == "relax" && (argc == 4 || argc == 5)) rc = cmd_relax(argv[2], atoi(argv[3]), argc == 5 ? atof(argv[4]) : 0);
   fclose(g_out);
   return rc;
 }

@@ -149,6 +149,29 @@ def gen_cli(td):
 
 
 QPPROBE = os.path.join(ROOT, 'oracle', '_ref', 'qp_probe')
+QPCLI = os.path.join(ROOT, 'oracle', '_ref', 'quickprobs')
+
+
+def gen_qp_cli():
+    """Reference QuickProbs CLI outputs (oracle/_ref/quickprobs: QP/Console/
+    main.cpp built from the reference sources by `make -C oracle qp`; its
+    output does not depend on the thread count)."""
+    outdir = os.path.join(HERE, 'cli')
+    extra = {'qp_div60.fa': synth.family(60, 50, 0.6, seed=41),     # > 50 sequences: 1 consistency round
+             'qp_big210.fa': synth.family(210, 30, 0.5, seed=42)}   # > 200: selectivity rejects z, 200 passes
+    for fname, fam in extra.items():
+        synth.write_fasta(os.path.join(outdir, fname), fam)
+    cases = [('bb11028.fa', []), ('bb11028.fa', ['-c', '0']), ('bb11028.fa', ['-c', '1', '-r', '5']),
+             ('div12.fa', []), ('div12.fa', ['-c', '0']), ('sim8.fa', []), ('sim8.fa', ['-c', '3', '-r', '50']),
+             ('qp_div60.fa', []), ('qp_big210.fa', [])]
+    man = []
+    for fname, args in cases:
+        r = subprocess.run([QPCLI] + args + [os.path.join(outdir, fname)], capture_output=True, text=True)
+        tag = 'qp_' + fname[:-3].replace('qp_', '') + ''.join('_' + a.strip('-') for a in args)
+        with open(os.path.join(outdir, tag + '.out'), 'w') as fh:
+            fh.write(r.stdout)
+        man.append({'input': fname, 'args': args, 'out': tag + '.out', 'rc': r.returncode, 'stderr': r.stderr})
+    return man
 
 
 def gen_qp(td):
@@ -187,12 +210,15 @@ def gen_qp_relax(td):
     the default configuration, the last round unfiltered)."""
     rng = np.random.default_rng(31)
     fams = [
-        ('mid6', synth.family(6, 60, 0.5, seed=31), 2),
-        ('div8', synth.family(8, 80, 0.7, seed=32), 2),
-        ('ragged7', [(h, s[: 12 + 11 * i]) for i, (h, s) in enumerate(synth.family(7, 90, 0.4, seed=33))], 1),
+        ('mid6', synth.family(6, 60, 0.5, seed=31), 2, None),
+        ('div8', synth.family(8, 80, 0.7, seed=32), 2, None),
+        ('ragged7', [(h, s[: 12 + 11 * i]) for i, (h, s) in enumerate(synth.family(7, 90, 0.4, seed=33))], 1, None),
+        # the selectivity filter rejecting z: threshold = the median posterior
+        # distance (ConsistencyStage.cpp:171-205)
+        ('sel9', synth.family(9, 70, 0.5, seed=34), 2, 'median'),
     ]
     manifest = []
-    for name, fam, iters in fams:
+    for name, fam, iters, sel in fams:
         seqs = [s for _, s in fam]
         w = rng.uniform(0.5, 20.0, len(seqs)).astype(np.float32)
         path = os.path.join(td, 'r.txt')
@@ -200,17 +226,30 @@ def gen_qp_relax(td):
             for wt, sq in zip(w, seqs):
                 fh.write(f'{float(wt)!r} {sq}\n')
         out = os.path.join(td, 'r.bin')
-        subprocess.check_call([QPPROBE, 'relax', path, str(iters)], env=dict(os.environ, REF_PROBE_OUT=out))
+        args = [QPPROBE, 'relax', path, str(iters)]
+        if sel == 'median':
+            subprocess.check_call(args, env=dict(os.environ, REF_PROBE_OUT=out))
+            args.append(repr(float(np.median(refdump.read(out)['dist']))))
+        subprocess.check_call(args, env=dict(os.environ, REF_PROBE_OUT=out))
         d = refdump.read(out)
         d['seqs'] = np.array(seqs)
         d['weights'] = w
         d['iters'] = np.int32(iters)
         np.savez_compressed(os.path.join(HERE, f'qp_family_{name}.npz'), **d)
-        manifest.append({'name': name, 'n': len(seqs), 'iters': iters})
+        manifest.append({'name': name, 'n': len(seqs), 'iters': iters,
+                         'selectivity': float(d['selectivity'][0])})
     return manifest
 
 
 def main():
+    if '--qpcli' in sys.argv:  # QuickProbs CLI outputs only (merged into the manifest)
+        path = os.path.join(HERE, 'manifest.json')
+        with open(path) as fh:
+            man = json.load(fh)
+        man['qp_cli'] = gen_qp_cli()
+        with open(path, 'w') as fh:
+            json.dump(man, fh, indent=1)
+        return
     if '--qp' in sys.argv:  # QuickProbs vectors only (merged into the manifest)
         with tempfile.TemporaryDirectory() as td:
             qp = gen_qp(td)

@@ -40,3 +40,33 @@ def test_cli_errors():
     assert _run('-p', '2', 'x.fa').returncode == 1
     r = _run('-p', '1', os.path.join(GOLDEN, 'cli', 'sim8.fa'))
     assert r.returncode != 0
+
+
+# ---- the quickprobs drop-in (QuickProbs 2 realigner) against the reference
+# QuickProbs CLI built from its sources (tests/golden/cli/qp_*.out)
+QP_BIN = os.path.join(ROOT, 'mlprobs_amd', 'cli', 'quickprobs')
+
+
+@pytest.mark.parametrize('name,args', [('bb11028', []), ('bb11028', ['-c', '0']), ('bb11028', ['-c', '1', '-r', '5']),
+                                       ('div12', []), ('div12', ['-c', '0']), ('sim8', []),
+                                       ('sim8', ['-c', '3', '-r', '50']), ('qp_div60', []), ('qp_big210', [])])
+def test_quickprobs_cli(name, args):
+    r = subprocess.run([QP_BIN, *args, os.path.join(GOLDEN, 'cli', f'{name}.fa')], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0 and r.stderr == '', r.stderr
+    tag = 'qp_' + name.replace('qp_', '') + ''.join('_' + a.strip('-') for a in args)
+    with open(os.path.join(GOLDEN, 'cli', f'{tag}.out')) as fh:
+        assert r.stdout == fh.read()
+
+
+def test_quickprobs_cli_edges(tmp_path):
+    r = subprocess.run([QP_BIN], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and r.stdout.startswith('Usage:')        # no input: usage (main.cpp:31-37)
+    bad = tmp_path / 'bad.fa'
+    bad.write_text('>a\nMK1V\n>b\nMKV\n')
+    r = subprocess.run([QP_BIN, str(bad)], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 255 and 'illegal sequence character:1' in r.stdout
+    one = tmp_path / 'one.fa'
+    one.write_text('>only one\nmkvlaa\nGG\n')
+    r = subprocess.run([QP_BIN, '-o', str(tmp_path / 'o.fa'), str(one)], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and (tmp_path / 'o.fa').read_text() == '>only one\nMKVLAAGG\n'

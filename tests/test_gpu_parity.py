@@ -347,7 +347,8 @@ def test_qp_relax_golden(name):
         os.environ.update(env)
         try:
             _import(fam, qp_family_csrs(d, 0))
-            fam.relax_qp(d['iters'], d['weights'])
+            n = len(d['seqs'])
+            fam.relax_qp(d['iters'], d['weights'], d['seldist'].reshape(n, n), float(d['selectivity'][0]))
             for k in range(len(ref)):
                 csr_equal(ref[k], fam.sparse(k), f'{name} {env} p{k}')
         finally:
@@ -356,20 +357,29 @@ def test_qp_relax_golden(name):
     fam.close()
 
 
-@pytest.mark.parametrize('n,L,s,iters,seed', [(9, 140, 0.6, 2, 71), (7, 200, 0.3, 1, 72), (12, 90, 0.7, 3, 73)])
-def test_qp_stage_vs_oracle(n, L, s, iters, seed):
+@pytest.mark.parametrize('n,L,s,iters,seed,sel', [(9, 140, 0.6, 2, 71, False), (7, 200, 0.3, 1, 72, False),
+                                                  (12, 90, 0.7, 3, 73, False), (14, 120, 0.6, 2, 74, True),
+                                                  (10, 260, 0.5, 1, 75, True)])
+def test_qp_stage_vs_oracle(n, L, s, iters, seed, sel):
     """QuickProbs posterior stage then consistency, all on the GPU, against the
-    oracle's restatement of both stages."""
+    oracle's restatement of both stages; `sel`: with a subtree-size-like
+    selectivity matrix that rejects z (ExtendedMSA.cpp:96-100, threshold 6)."""
     seqs = [x for _, x in synth.family(n, L, s, seed=seed)]
-    w = np.random.default_rng(seed).uniform(1, 30, n).astype(np.float32)
+    rng = np.random.default_rng(seed)
+    w = rng.uniform(1, 30, n).astype(np.float32)
+    seld = None
+    if sel:
+        seld = rng.integers(2, n + 1, (n, n)).astype(np.float32)
+        seld = np.minimum(seld, seld.T)
+        np.fill_diagonal(seld, 0)
     fam = Family(seqs)
     fam.posteriors(PID_QP, 0.0)
     cur = [_qp_expected(seqs, a, b)[0] for a in range(n) for b in range(a + 1, n)]
     cur = [(r.astype(np.int32), c.astype(np.int32), v) for r, c, v in cur]
     lens = [len(x) for x in seqs]
     for it in range(1, iters + 1):
-        cur = orc.relax(lens, cur, qp=(w, 3.0, 1e-5 if it == iters else 0.01))
-    fam.relax_qp(iters, w)
+        cur = orc.relax(lens, cur, qp=(w, 3.0, 1e-5 if it == iters else 0.01, seld, 6.0))
+    fam.relax_qp(iters, w, seld, 6.0)
     for k in range(len(cur)):
         csr_equal(cur[k], fam.sparse(k), f'qp stage p{k}')
     fam.close()
