@@ -155,10 +155,11 @@ int main(int argc, char** argv) {
 
   mlp_ctx* ctx = nullptr;
   check(nullptr, mlp_ctx_create(0, &ctx), "device");
-  // one family per process: a moderate batch scratch (64 GB, C3 posteriors
-  // 0.84 s warm vs 0.75 s at 130 GB) fits in memory the driver has already
-  // cleared, where a larger one can wait seconds behind the previous process
-  if (!getenv("MLP_SCRATCH_GB")) check(ctx, mlp_set_scratch(ctx, 64ull << 30), "device");
+  // one family per process: a moderate batch scratch.  A fresh process's
+  // allocation waits for the driver to clear memory the previous process
+  // released; back to back at C3 (512 x 400) the posterior stage took 1.09 s
+  // at 32 GB, 1.39 s at 16 GB, 7.4-10.5 s at 64 GB
+  if (!getenv("MLP_SCRATCH_GB")) check(ctx, mlp_set_scratch(ctx, 32ull << 30), "device");
   std::string res;
   std::vector<int64_t> off(1, 0);
   for (const Row& r : seqs) {

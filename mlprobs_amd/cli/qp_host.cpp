@@ -4,6 +4,7 @@
 #include <math.h>
 #include <omp.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -330,12 +331,22 @@ Seq add_gaps(const Seq& s, const std::string& path, char id) {
   return r;
 }
 
+// time split of the host stages (MLP_CLI_TIMES)
+double g_t_post = 0, g_t_mea = 0;
+int64_t g_n_terms = 0;
+double now() { return omp_get_wtime(); }
+
 // ConstructionStage::alignAlignments (ConstructionStage.cpp:86-126)
 Profile align_alignments(const std::vector<float>& w, const Profile& A, const Profile& B, const Sparse& sp,
                          std::vector<float>& post, int threads) {
+  const double t0 = now();
   build_posterior(w, A, B, sp, post, threads);
+  const double t1 = now();
   float score;
   const std::string path = cpnp::mea_path(A[0].length(), B[0].length(), post, &score);
+  g_t_post += t1 - t0;
+  g_t_mea += now() - t1;
+  g_n_terms += (int64_t)A.size() * (int64_t)B.size();
   Profile r;
   r.reserve(A.size() + B.size());
   for (const Seq& s : A) r.push_back(add_gaps(s, path, 'X'));
@@ -452,6 +463,9 @@ Profile construct_and_refine(const std::vector<Seq>& seqs, const Sparse& sp, con
     Profile cand = align_alignments(w, p1, p2, sp, post, threads);
     if (aln[0].length() >= cand[0].length()) aln = std::move(cand);  // checkAcceptance (length)
   }
+  if (getenv("MLP_CLI_TIMES"))
+    fprintf(stderr, "[host] profile posteriors %.3f s (%lld sequence pairs), MEA %.3f s, %d refinement passes\n",
+            g_t_post, (long long)g_n_terms, g_t_mea, iters);
   return aln;
 }
 
