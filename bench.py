@@ -51,7 +51,8 @@ def parse():
     ap.add_argument('--no-cpu', action='store_true')
     ap.add_argument('--relax', type=int, default=-1,
                     help='also time N relaxation rounds (reported separately; default 1 on one GPU, 0 on several)')
-    ap.add_argument('--no-e2e', action='store_true', help='skip the end-to-end c_p_np_aln family timings')
+    ap.add_argument('--no-e2e', action='store_true',
+                    help='skip the end-to-end c_p_np_aln / quickprobs family timings')
     ap.add_argument('--no-qp', action='store_true', help='skip the QuickProbs posterior/consistency timings')
     return ap.parse_args()
 
@@ -108,6 +109,33 @@ def e2e_families(args):
                 name, sec = line[8:].rsplit(' ', 2)[0], line.rsplit(' ', 2)[1]
                 stages[name] = float(sec)
         res[tag] = {'seconds': dt, 'exit': r.returncode, 'stages_s': stages}
+    qp = os.path.join(ROOT, 'mlprobs_amd', 'cli', 'quickprobs')
+    ref = os.path.join(ROOT, 'oracle', '_ref', 'quickprobs')
+    if os.path.exists(qp):
+        # the quickprobs drop-in (QuickProbs 2 realigner): GPU posteriors and
+        # selective consistency, host tree / construction / 30-200 refinement
+        # passes; at C2 also the reference QuickProbs CLI (built from its
+        # sources, 16 threads) on the same input, outputs compared byte for byte
+        for tag, n, L in (('quickprobs C2 128x256', 128, 256), (f'quickprobs C3 {args.n}x{args.len}', args.n, args.len)):
+            with tempfile.TemporaryDirectory() as td:
+                fa = os.path.join(td, 'fam.fa')
+                synth.write_fasta(fa, synth.family(n, L, args.s, seed=args.seed))
+                t0 = time.perf_counter()
+                r = subprocess.run([qp, fa], capture_output=True, text=True, timeout=600,
+                                   env=dict(os.environ, MLP_CLI_TIMES='1'))
+                dt = time.perf_counter() - t0
+                stages = {}
+                for line in r.stderr.splitlines():
+                    if line.startswith('[stage] '):
+                        name, sec = line[8:].rsplit(' ', 2)[0], line.rsplit(' ', 2)[1]
+                        stages[name] = float(sec)
+                res[tag] = {'seconds': dt, 'exit': r.returncode, 'stages_s': stages}
+                if n <= 128 and os.path.exists(ref) and not args.no_cpu:
+                    t0 = time.perf_counter()
+                    rr = subprocess.run([ref, '-t', str(args.cpu_threads), fa], capture_output=True, text=True,
+                                        timeout=600)
+                    res[tag]['reference_cpu'] = {'seconds': time.perf_counter() - t0, 'threads': args.cpu_threads,
+                                                 'exit': rr.returncode, 'identical_output': rr.stdout == r.stdout}
     return res
 
 

@@ -277,7 +277,8 @@ void mapping(const Seq& s, std::vector<int>& m) {
 void build_posterior(const std::vector<float>& w, const Profile& A, const Profile& B, const Sparse& sp,
                      std::vector<float>& post, int threads) {
   const int L1 = A[0].length(), L2 = B[0].length(), W2 = L2 + 1;
-  post.assign((size_t)(L1 + 1) * W2, 0.f);
+  if (post.size() < (size_t)(L1 + 1) * W2) post.resize((size_t)(L1 + 1) * W2);
+  std::fill(post.begin(), post.begin() + W2, 0.f);  // row 0 (the threads zero rows 1..L1)
   double total = 0;
   for (const Seq& a : A) {
     const double w1 = w[a.label];
@@ -291,6 +292,7 @@ void build_posterior(const std::vector<float>& w, const Profile& A, const Profil
   {
     const int t = omp_get_thread_num(), T = omp_get_num_threads();
     const int r0 = 1 + (int)((int64_t)L1 * t / T), r1 = 1 + (int)((int64_t)L1 * (t + 1) / T);  // dense rows [r0, r1)
+    std::fill(post.begin() + (size_t)r0 * W2, post.begin() + (size_t)r1 * W2, 0.f);
     for (size_t i = 0; i < A.size(); i++) {
       const int first = A[i].label;
       const std::vector<int>& map1 = m1[i];
@@ -321,13 +323,12 @@ Seq add_gaps(const Seq& s, const std::string& path, char id) {
   r.header = s.header;
   r.sort_label = s.sort_label;
   r.label = s.label;
-  r.data.reserve(path.size() + 1);
-  r.data = "@";
-  size_t k = 1;
-  for (char c : path) {
-    if (c == 'B' || c == id) r.data += s.data[k++];
-    else r.data += '-';
-  }
+  r.data.assign(path.size() + 1, '-');
+  r.data[0] = '@';
+  const char* src = s.data.data() + 1;
+  char* dst = &r.data[1];
+  for (size_t c = 0; c < path.size(); c++)
+    if (path[c] == 'B' || path[c] == id) dst[c] = *src++;
   return r;
 }
 
@@ -370,21 +371,24 @@ Profile process_tree(const Tree& T, int node, const std::vector<Seq>& seqs, cons
 Profile extract_subset(const Profile& aln, const std::set<int>& idx) {
   const int L = aln[*idx.begin()].length();
   std::vector<char> keep(L + 1, 0);
+  for (int i : idx) {
+    const char* d = aln[i].data.data();
+    for (int c = 1; c <= L; c++) keep[c] |= d[c] != '-';
+  }
+  std::vector<int> cols;  // columns not gapped in every selected row
   for (int c = 1; c <= L; c++)
-    for (int i : idx)
-      if (aln[i].data[c] != '-') {
-        keep[c] = 1;
-        break;
-      }
+    if (keep[c]) cols.push_back(c);
   Profile r;
+  r.reserve(idx.size());
   for (int i : idx) {
     Seq s;
     s.header = aln[i].header;
     s.sort_label = aln[i].sort_label;
     s.label = aln[i].label;
-    s.data = "@";
-    for (int c = 1; c <= L; c++)
-      if (keep[c]) s.data += aln[i].data[c];
+    s.data.resize(cols.size() + 1);
+    s.data[0] = '@';
+    const char* d = aln[i].data.data();
+    for (size_t k = 0; k < cols.size(); k++) s.data[k + 1] = d[cols[k]];
     r.push_back(std::move(s));
   }
   return r;
@@ -415,10 +419,16 @@ struct ColumnRefiner {
   void update(const Profile& aln) {
     const int n = (int)aln.size(), L = aln[0].length();
     scores.resize(L, std::pair<int, float>(0, 0));
+    // gap counts per column; adding them at once equals adding 1.0f per gap
+    // (integers below 2^24 are exact in float)
+    std::vector<int> gaps(L, 0);
+    for (int i = 0; i < n; i++) {
+      const char* d = aln[i].data.data() + 1;
+      for (int c = 0; c < L; c++) gaps[c] += d[c] == '-';
+    }
     for (int c = 0; c < (int)scores.size(); c++) {
       scores[c].first = c;
-      for (int i = 0; i < n; i++)
-        if (aln[i].data[c + 1] == '-') scores[c].second += 1.0f;
+      scores[c].second += (float)gaps[c];
     }
     std::stable_sort(scores.begin(), scores.end(), [n](const std::pair<int, float>& a, const std::pair<int, float>& b) {
       return fabsf((float)n / 2 - a.second) > fabsf((float)n / 2 - b.second);
