@@ -353,6 +353,9 @@ __device__ __forceinline__ uint4 rfl(uint4 v) {
                     __builtin_amdgcn_readfirstlane(v.z), __builtin_amdgcn_readfirstlane(v.w));
 }
 
+#ifdef MLP_RELAX_TIMING  // measurement variant: per-z compute imbalance across the 16 waves
+__device__ unsigned long long g_rtime[8];
+#endif
 template <int KP, int SL, bool QP>
 __global__ __launch_bounds__(kRelaxThreads) void k_relax_tile(TileRelaxArgs A) {
   extern __shared__ __align__(16) uint8_t lds[];
@@ -564,15 +567,19 @@ __global__ __launch_bounds__(kRelaxThreads) void k_relax_tile(TileRelaxArgs A) {
     }                                                                                    \
     const int tot_ = sg[TM] + (int)nC.z;                                                 \
     const int dC_ = (int)nC.x - sg[TM];                                                  \
+    /* unconditional loads (past the tile: its first chunk again), so the */            \
+    /* KP loads issue back to back with no wait between them */                          \
     _Pragma("unroll") for (int m = 0; m < KP; ++m) {                                     \
-      const int c = tid + m * nt;                                                        \
-      if (c < tot_) {                                                                    \
-        int d = dC_;                                                                     \
-        _Pragma("unroll") for (int t = TM - 1; t >= 0; --t) d = c < sg[t + 1] ? dl_[t] : d; \
-        MLP_PF_LOAD(pf[m], g16[(uint32_t)(c + d)]);                                      \
-      }                                                                                  \
+      const int c = tid + m * nt < tot_ ? tid + m * nt : 0;                              \
+      int d = dC_;                                                                       \
+      _Pragma("unroll") for (int t = TM - 1; t >= 0; --t) d = c < sg[t + 1] ? dl_[t] : d; \
+      MLP_PF_LOAD(pf[m], g16[(uint32_t)(c + d)]);                                        \
     }                                                                                    \
   }
+#ifdef MLP_RELAX_TIMING
+  unsigned long long t_max = 0, t_mean = 0, t_step = 0, t_steps = 0, t_seg[4] = {0, 0, 0, 0};
+  uint64_t t_last = clock64();
+#endif
   fill();
   bool more = next();
   if (more) MLP_ISSUE();
@@ -581,6 +588,9 @@ __global__ __launch_bounds__(kRelaxThreads) void k_relax_tile(TileRelaxArgs A) {
   const float4 fW = nW;
 #endif
   while (more) {
+#ifdef MLP_RELAX_TIMING
+    const uint64_t ts0 = clock64();
+#endif
     // stage the prefetched tile; outputs' A bases (+ validity) into zb
     const int tot = sg[TM] + (int)nC.z;
 #pragma unroll
@@ -601,12 +611,24 @@ __global__ __launch_bounds__(kRelaxThreads) void k_relax_tile(TileRelaxArgs A) {
                           (int)na_[t]);
       }
     }
+#ifdef MLP_RELAX_TIMING
+    const uint64_t ts1 = clock64();  // stage writes issued (after the loads landed)
+#endif
     __syncthreads();
+#ifdef MLP_RELAX_TIMING
+    const uint64_t ts2 = clock64();
+#endif
     more = next();
+#ifdef MLP_RELAX_TIMING
+    const uint64_t ts3 = clock64();
+#endif
 #ifdef MLP_RELAX_NOSTAGE  // timing experiment: every z computes on the first z's tile
     nC = fC; nAo = fAo; nNa = fNa; nAc = fAc; nW = fW;
 #else
     if (more) MLP_ISSUE();
+#endif
+#ifdef MLP_RELAX_TIMING
+    const uint64_t tc0 = clock64();
 #endif
 #ifndef MLP_RELAX_NOCOMPUTE  // (timing experiment: staging only)
     {
@@ -674,8 +696,38 @@ __global__ __launch_bounds__(kRelaxThreads) void k_relax_tile(TileRelaxArgs A) {
       }
     }
 #endif
+#ifdef MLP_RELAX_TIMING
+    {
+      __shared__ uint32_t wct[16];
+      const uint64_t tc1 = clock64();
+      if ((tid & 63) == 0) wct[tid >> 6] = (uint32_t)(tc1 - tc0);
+      __syncthreads();
+      if (tid == 0) {
+        uint32_t mx = 0, sm = 0;
+        for (int w = 0; w < nt / 64; ++w) { mx = max(mx, wct[w]); sm += wct[w]; }
+        t_max += mx;
+        t_mean += sm / (nt / 64);
+        t_steps += 1;
+        t_step += clock64() - t_last;
+        t_last = clock64();
+        t_seg[0] += ts1 - ts0;
+        t_seg[1] += ts2 - ts1;
+        t_seg[2] += ts3 - ts2;
+        t_seg[3] += tc0 - ts3;
+      }
+    }
+#endif
     __syncthreads();
   }
+#ifdef MLP_RELAX_TIMING
+  if (tid == 0) {
+    atomicAdd(&g_rtime[0], t_max);
+    atomicAdd(&g_rtime[1], t_mean);
+    atomicAdd(&g_rtime[2], t_step);
+    atomicAdd(&g_rtime[3], t_steps);
+    for (int q = 0; q < 4; ++q) atomicAdd(&g_rtime[4 + q], t_seg[q]);
+  }
+#endif
 #undef MLP_ISSUE
   __syncthreads();  // the weight sums of the last chunk
   const float fn = (float)n;  // CPNP/MSA.cpp:1233-1235; QuickProbs: / the weight sum
@@ -723,11 +775,25 @@ hipError_t launch_relax_tiles(const TileRelaxArgs& a, int slots, hipStream_t st)
   if (a.ntiles <= 0) return hipSuccess;
   const size_t lds = tile_relax_lds(a.cap);
   const char* kp = getenv("MLP_RELAX_KP");  // test hook: force the large-prefetch variant
+  hipError_t e;
   switch (kp ? atoi(kp) : tile_relax_prefetch(a.cap)) {
-    case 5: return a.qp.on ? launch_tiles_kp<5, true>(a, slots, lds, st) : launch_tiles_kp<5, false>(a, slots, lds, st);
-    case 9: return a.qp.on ? launch_tiles_kp<9, true>(a, slots, lds, st) : launch_tiles_kp<9, false>(a, slots, lds, st);
+    case 5: e = a.qp.on ? launch_tiles_kp<5, true>(a, slots, lds, st) : launch_tiles_kp<5, false>(a, slots, lds, st); break;
+    case 9: e = a.qp.on ? launch_tiles_kp<9, true>(a, slots, lds, st) : launch_tiles_kp<9, false>(a, slots, lds, st); break;
     default: return hipErrorInvalidValue;
   }
+#ifdef MLP_RELAX_TIMING
+  unsigned long long h[8];
+  hipStreamSynchronize(st);
+  hipMemcpyFromSymbol(h, HIP_SYMBOL(g_rtime), sizeof h);
+  fprintf(stderr,
+          "relax timing: z-steps %llu, cycles per step %.0f, wave compute mean %.0f max %.0f | wave0: stage-write %.0f "
+          "barrier %.0f next %.0f issue %.0f\n",
+          h[3], (double)h[2] / h[3], (double)h[1] / h[3], (double)h[0] / h[3], (double)h[4] / h[3],
+          (double)h[5] / h[3], (double)h[6] / h[3], (double)h[7] / h[3]);
+  for (auto& v : h) v = 0;
+  hipMemcpyToSymbol(HIP_SYMBOL(g_rtime), h, sizeof h);
+#endif
+  return e;
 }
 
 hipError_t launch_transpose(const TransposeArgs& a, hipStream_t st) {
