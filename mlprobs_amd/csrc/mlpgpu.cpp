@@ -1011,17 +1011,25 @@ int mlp_family_features(mlp_ctx* c, float theta, float* f, int32_t* ints) {
   if (!(c->vit_done && c->vit_paths) && (rc = mlp_viterbi(c, 0, c->P, 1))) return rc;
   // CPNP/MSA.cpp:646-772 (Alter_ModelAdjustmentTest), serial in pair order.
   // BLOSUM62 is indexed through alphabetDefault.find(); a letter outside the
-  // 20-letter alphabet gives index -1, i.e. a read just before the row / the
-  // table.  The reference build lays emitPairsDefault[20][20] out directly
-  // before BLOSUM62 (CPNP/Defaults.h:36-104), so those reads return
-  // emitPairsDefault entries; `mem` reproduces that layout (pinned by the
-  // BB11028 `-G` golden line, whose sequences contain X).
+  // 20-letter alphabet (X, B, Z, ...) gives index npos = -1, i.e. a read of
+  // the 84 bytes before the table: reference UB whose values depend on the
+  // binary's data layout.  Pinned here to the reference built from its
+  // sources (oracle/Makefile `make ref`, g++ -O3): there the 80 bytes before
+  // BLOSUM62 hold MSA.cpp's globals MATRIXTYPE = 160, TEMPERATURE = 5.0f,
+  // matrixtype = "gonnet_160", allscores, numIterativeRefinementReps,
+  // numConsistencyReps and two bools (MSA.cpp:59-79), at 4-byte slots
+  // 4, 5, 8-10, 13-16 of that row (`nm`/`objdump` of oracle/_ref/c_p_np_aln);
+  // X against Q thus adds 5.0, X against H reads a huge value and adds
+  // nothing.  Pinned by the `-G` golden lines of the real families in
+  // tests/golden/real (BB11036 holds X opposite Q).
   int idx[26];
   for (int k = 0; k < 26; k++) idx[k] = -1;
   for (int k = 0; k < 20; k++) idx[MLP_ALPHABET[k] - 'A'] = k;
   float mem[800] = {0};
-  for (int i = 0, t = 0; i < 20; i++)
-    for (int j = 0; j <= i; j++) mem[i * 20 + j] = mlp_emit_pairs_lower[t++];
+  static const uint32_t kBefore[20] = {0, 0, 0, 0, 0x000000a0u, 0x40a00000u, 0, 0, 0x6e6e6f67u, 0x315f7465u,
+                                       0x00003036u, 0, 0, 0x00000001u, 0x00000064u, 0x00000002u, 0x00000101u,
+                                       0, 0, 0};
+  for (int k = 0; k < 20; k++) memcpy(&mem[380 + k], &kBefore[k], 4);  // mem[379] (byte -84) = 0
   for (int k = 0; k < 400; k++) mem[400 + k] = (float)mlp_blosum62[k];
   const int P = (int)c->P;
   std::vector<float> finals(10000, 0.f);   // MAX_ARR (CPNP/MSA.cpp:17)

@@ -225,13 +225,16 @@ __global__ __launch_bounds__(256) void k_forward(ModelScalars ms, const Tables* 
           } else if (j == 0) {
             Zm = 0.0; Ze = 1.0; Zf = 0.0; E = 0;
           } else {
-            E = pf_align(UZm, UZe, UZf, Ue, DZm, DZe, DZf, De, LZm, LZe, LZf, Le);
+            // align copies: U becomes the next column's D with its own frame
+            double uZm = UZm, uZe = UZe, uZf = UZf, dZm = DZm, dZe = DZe, dZf = DZf;
+            double lZm = LZm, lZe = LZe, lZf = LZf;
+            E = pf_align(uZm, uZe, uZf, Ue, dZm, dZe, dZf, De, lZm, lZe, lZf, Le);
             const double o0 = (j == L2) ? 1.0 : pfo, e0 = (j == L2) ? 1.0 : pfe;
             const double o1 = (i == L1) ? 1.0 : pfo, e1 = (i == L1) ? 1.0 : pfe;
-            Ze = UZm * o0 + UZe * e0;
-            Zf = LZm * o1 + LZf * e1;
+            Ze = uZm * o0 + uZe * e0;
+            Zf = lZm * o1 + lZf * e1;
             // QuickProbs' Ze/Zf are ours transposed (QP/PartitionFunction.cpp:128-130)
-            Zm = ((M & kQP) != 0 ? (DZm + DZf) + DZe : (DZm + DZe) + DZf) * score;
+            Zm = ((M & kQP) != 0 ? (dZm + dZf) + dZe : (dZm + dZe) + dZf) * score;
             pf_rescale(Zm, Ze, Zf, E);
           }
           sc.zm[idx] = mlp_pf_pack(Zm, E);

@@ -70,3 +70,20 @@ def test_quickprobs_cli_edges(tmp_path):
     one.write_text('>only one\nmkvlaa\nGG\n')
     r = subprocess.run([QP_BIN, '-o', str(tmp_path / 'o.fa'), str(one)], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0 and (tmp_path / 'o.fa').read_text() == '>only one\nMKVLAAGG\n'
+
+
+# ---- both drop-ins on real benchmark families (the reference's own TEST
+# inputs, tests/golden/real, made by tests/golden/gen_real.py from the
+# reference CLIs built from source)
+REAL = os.path.join(GOLDEN, 'real')
+_REAL = sorted(f[:-3] for f in os.listdir(REAL) if f.endswith('.fa')) if os.path.isdir(REAL) else []
+
+
+@pytest.mark.parametrize('name', _REAL)
+def test_real_families(name):
+    fa = os.path.join(REAL, f'{name}.fa')
+    for tag, cmd in (('G', [BIN, '-G', fa]), ('p_0', [BIN, '-p', '0', fa]), ('qp', [QP_BIN, fa])):
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0 and r.stderr == '', (tag, r.stderr)
+        with open(os.path.join(REAL, f'{name}.{tag}.out')) as fh:
+            assert r.stdout == fh.read(), (name, tag)

@@ -161,6 +161,18 @@ def test_chains_mixed_widths():
     _check_family_vs_oracle(seqs, 2, 'mixed')
 
 
+@pytest.mark.parametrize('pid', [3, 0])
+def test_pf_frames(pid):
+    """Partition functions beyond fp64's range of one frame (2^200): runs of
+    W (high self-score), near-identical long pairs (the real family
+    oxx____8t2 that exposed a frame-label bug) and lengths that wrap several
+    64-row strips; values must stay within the PF tolerance of the long-double
+    oracle."""
+    real = [x for _, x in synth.read_fasta(os.path.join(GOLDEN, 'real', 'oxx____8t2.fa'))]
+    seqs = ['W' * 50, 'W' * 70, 'W' * 110, 'C' * 130, real[0], real[4], real[11], real[16]]
+    _check_family_vs_oracle(seqs, pid, f'pf frames pid{pid}')
+
+
 def test_batches_of_one(monkeypatch):
     """A scratch budget below one pair: every batch holds a single pair."""
     monkeypatch.setenv('MLP_SCRATCH_GB', '0.0001')

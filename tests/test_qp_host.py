@@ -59,9 +59,13 @@ def _posteriors(seqs):
     return D, csrs
 
 
-@pytest.mark.parametrize('name,args', CASES)
+REAL = ['bali3_BB11001', 'bali3_BB12005', 'ox_581s18', 'oxx_588s27', 'oxx____397', 'sabre_sup_062']
+
+
+@pytest.mark.parametrize('name,args', CASES + [('real/' + r, []) for r in REAL])
 def test_quickprobs_host_vs_reference_cli(qdriver, tmp_path, name, args):
-    fam = synth.read_fasta(os.path.join(GOLDEN, 'cli', f'{name}.fa'))
+    """`real/...`: the reference's own benchmark families (tests/golden/real)."""
+    fam = synth.read_fasta(os.path.join(GOLDEN, 'cli' if not name.startswith('real/') else '', f'{name}.fa'))
     headers = [h for h, _ in fam]
     seqs = [s for _, s in fam]
     n = len(seqs)
@@ -97,6 +101,8 @@ def test_quickprobs_host_vs_reference_cli(qdriver, tmp_path, name, args):
         fh.write(np.concatenate([c for _, c, _ in csrs] + [np.zeros(0, np.int32)]).astype('<u2').tobytes())
         fh.write(np.concatenate([v for _, _, v in csrs] + [np.zeros(0, np.float32)]).astype('<f4').tobytes())
     got = subprocess.run([qdriver, 'align', inp], capture_output=True, check=True).stdout.decode()
-    with open(os.path.join(GOLDEN, 'cli', golden_name(name, args))) as fh:
+    ref_out = (os.path.join(GOLDEN, name + '.qp.out') if name.startswith('real/')
+               else os.path.join(GOLDEN, 'cli', golden_name(name, args)))
+    with open(ref_out) as fh:
         ref = fh.read()
     assert got == ref
