@@ -11,6 +11,7 @@ stays short).  For each family:
   quickprobs               oracle/_ref/quickprobs (the reference QuickProbs
                            sources, `make -C oracle qp`); exit status kept,
                            QuickProbs rejects '-' in its input.
+plus 8 larger oxx families (60-420 sequences) for quickprobs only.
 Usage: python tests/golden/gen_real.py
 """
 import json
@@ -67,6 +68,28 @@ def main():
                 ent[tag] = {'rc': r.returncode, 'stderr': r.stderr[-200:]}
             man.append(ent)
             print(name, ent['n'], ent['pair_cells'], {t: ent[t]['rc'] for t in ('G', 'p_0', 'qp')}, flush=True)
+    # larger families for the quickprobs drop-in only (its output does not
+    # depend on the thread count): > 50 sequences (1 consistency round), > 200
+    # (selectivity rejects z, 200 refinement passes)
+    files = sorted(os.listdir(os.path.join(TEST, 'oxx', 'in')))
+    picked = 0
+    for k, f in enumerate(files):
+        src = os.path.join(TEST, 'oxx', 'in', f)
+        s = seqs_of(src)
+        if picked >= 8 or k % 5 != 0 or not (60 <= len(s) <= 420) or pair_cells(s) > 2e9:
+            continue
+        picked += 1
+        name = f'oxxL_{f}'
+        dst = os.path.join(OUT, name + '.fa')
+        with open(src, 'rb') as fi, open(dst, 'wb') as fo:
+            fo.write(fi.read())
+        r = subprocess.run([QPCLI, '-t', '8', dst], capture_output=True, text=True, timeout=1800)
+        with open(os.path.join(OUT, f'{name}.qp.out'), 'w') as fh:
+            fh.write(r.stdout)
+        ent = {'family': name, 'n': len(s), 'pair_cells': pair_cells(s), 'qp': {'rc': r.returncode,
+                                                                                'stderr': r.stderr[-200:]}}
+        man.append(ent)
+        print(name, ent['n'], ent['pair_cells'], r.returncode, flush=True)
     with open(os.path.join(OUT, 'manifest.json'), 'w') as fh:
         json.dump(man, fh, indent=1)
 

@@ -83,6 +83,8 @@ _REAL = sorted(f[:-3] for f in os.listdir(REAL) if f.endswith('.fa')) if os.path
 def test_real_families(name):
     fa = os.path.join(REAL, f'{name}.fa')
     for tag, cmd in (('G', [BIN, '-G', fa]), ('p_0', [BIN, '-p', '0', fa]), ('qp', [QP_BIN, fa])):
+        if not os.path.exists(os.path.join(REAL, f'{name}.{tag}.out')):
+            continue  # the larger oxxL_ families are quickprobs-only
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
         assert r.returncode == 0 and r.stderr == '', (tag, r.stderr)
         with open(os.path.join(REAL, f'{name}.{tag}.out')) as fh:
