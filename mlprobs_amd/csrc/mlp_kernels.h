@@ -295,7 +295,13 @@ struct TileRelaxArgs {
   QpRelax qp;
 };
 constexpr int kTileInts = 2 * kTileMax + 1;
-constexpr int kRelaxThreads = 1024;  // workgroup of the tiled relaxation (16 waves, 128 VGPRs)
+#ifndef MLP_RELAX_THREADS
+#define MLP_RELAX_THREADS 1024
+#endif
+// workgroup of the tiled relaxation: 1024 threads (16 waves, 128 VGPRs, one
+// per CU), or 512 with two workgroups sharing a CU's LDS and SIMDs
+constexpr int kRelaxThreads = MLP_RELAX_THREADS;
+constexpr int kRelaxGroupsPerCU = 1024 / kRelaxThreads;
 size_t tile_relax_lds(int cap);
 int tile_relax_prefetch(int cap);              // 16-byte chunks per thread, 0 = too large
 int tile_relax_slots(int64_t cells);           // cells per thread, 0 = too many

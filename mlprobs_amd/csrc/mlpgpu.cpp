@@ -1351,7 +1351,7 @@ static int relax_rounds(mlp_ctx* c, int iters, const QpRelax& qp) {
     }
     // Tiled path (k_relax_tile) for every output pair whose blocks fit the
     // LDS tile; the row-task kernel for the rest (MLP_RELAX=tasks: all).
-    const int64_t LDS_MAX = 160 * 1024;
+    const int64_t LDS_MAX = 160 * 1024 / kRelaxGroupsPerCU;
     const char* mode = getenv("MLP_RELAX");
     const char* tenv = getenv("MLP_RELAX_TILE");  // test hook: outputs per tile, 1..kTileMax
     const int tmax = tenv ? std::max(1, std::min(kTileMax, atoi(tenv))) : kTileMax;

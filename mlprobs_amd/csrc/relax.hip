@@ -344,6 +344,7 @@ int tile_relax_slots(int64_t cells) {
   const int64_t per = (cells + kRelaxThreads - 1) / kRelaxThreads;
   for (int sl : {4, 8, 12})
     if (per <= sl) return sl;
+  if (kRelaxThreads < 1024 && per <= 16) return 16;
   return 0;
 }
 
@@ -357,7 +358,7 @@ __device__ __forceinline__ uint4 rfl(uint4 v) {
 __device__ unsigned long long g_rtime[8];
 #endif
 template <int KP, int SL, bool QP>
-__global__ __launch_bounds__(kRelaxThreads) void k_relax_tile(TileRelaxArgs A) {
+__global__ __launch_bounds__(kRelaxThreads, 4) void k_relax_tile(TileRelaxArgs A) {
   extern __shared__ __align__(16) uint8_t lds[];
   constexpr int nt = kRelaxThreads;
   constexpr int TM = kTileMax;
@@ -764,6 +765,9 @@ static hipError_t launch_tiles_kp(const TileRelaxArgs& a, int slots, size_t lds,
     MLP_RELAX_CASE(4)
     MLP_RELAX_CASE(8)
     MLP_RELAX_CASE(12)
+#if MLP_RELAX_THREADS < 1024
+    MLP_RELAX_CASE(16)
+#endif
 #undef MLP_RELAX_CASE
     default:
       return hipErrorInvalidValue;
