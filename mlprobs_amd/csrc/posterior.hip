@@ -36,6 +36,20 @@ namespace mlp {
 // Depth of the software-pipelined loads of the backward step loop.
 constexpr int kPrefetch = 4;
 
+// Waves per SIMD the sweeps are compiled for (launch bounds: 6 waves <=> at
+// most 80 VGPRs, 5 <=> 96): the chains of a batch keep ~8 waves per SIMD
+// queued, and the extra resident waves hide the DP's dependency stalls.  The
+// PF backward holds more fp64 state and stays at 5 (6 would spill); the
+// all-in-one M = 7 build keeps the compiler's choice.
+#ifndef MLP_SWEEP_WAVES
+#define MLP_SWEEP_WAVES 6
+#endif
+template <int M>
+struct SweepWaves {
+  static constexpr int fwd = M == 7 ? 1 : MLP_SWEEP_WAVES;
+  static constexpr int bwd = M == 7 ? 1 : ((M & 4) != 0 && MLP_SWEEP_WAVES > 5 ? 5 : MLP_SWEEP_WAVES);
+};
+
 // Bring three scaled-fp64 frames to their common maximum (exact: powers of two).
 __device__ __forceinline__ int pf_align(double& a0, double& a1, double& a2, int ea,
                                         double& b0, double& b1, double& b2, int eb,
@@ -59,7 +73,7 @@ __device__ __forceinline__ void pf_rescale(double& m, double& e, double& f, int&
 // Forward sweep: 5-state forward, local forward, PF forward Zm.
 // =====================================================================
 template <int M>
-__global__ __launch_bounds__(256) void k_forward(ModelScalars ms, const Tables* __restrict__ tab,
+__global__ __launch_bounds__(256, SweepWaves<M>::fwd) void k_forward(ModelScalars ms, const Tables* __restrict__ tab,
                                                  SeqSet sq, PairMeta pm, ChainMeta cm,
                                                  PairRec* __restrict__ rec, Scratch sc,
                                                  int64_t nchains, int lds_seq) {
@@ -264,7 +278,7 @@ __global__ __launch_bounds__(256) void k_forward(ModelScalars ms, const Tables* 
 // and chain, PF posterior.
 // =====================================================================
 template <int M>
-__global__ __launch_bounds__(256) void k_backward(ModelScalars ms, const Tables* __restrict__ tab,
+__global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScalars ms, const Tables* __restrict__ tab,
                                                   SeqSet sq, PairMeta pm, ChainMeta cm,
                                                   PairRec* __restrict__ rec, Scratch sc,
                                                   int64_t nchains, int lds_seq) {
