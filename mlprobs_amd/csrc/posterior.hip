@@ -513,7 +513,10 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
 // Merge + MEA + sparsify: forward-order sweep over the merged posterior.
 // =====================================================================
 template <int M, int PID>
-__global__ __launch_bounds__(256) void k_merge(ModelScalars ms, SeqSet sq, PairMeta pm, ChainMeta cm,
+#ifndef MLP_MERGE_WAVES
+#define MLP_MERGE_WAVES 6
+#endif
+__global__ __launch_bounds__(256, MLP_MERGE_WAVES) void k_merge(ModelScalars ms, SeqSet sq, PairMeta pm, ChainMeta cm,
                                                PairRec* __restrict__ rec, Scratch sc, int64_t nchains,
                                                int lds_seq) {
   __shared__ double ex[7 * 6];
