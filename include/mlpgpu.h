@@ -133,6 +133,20 @@ int mlp_relax_qp(mlp_ctx *ctx, int iters, const float *seq_weights);
 int mlp_relax_qp_selective(mlp_ctx *ctx, int iters, const float *seq_weights, const float *sel_dist,
                            float selectivity);
 
+/* The weighted profile-profile posterior of QuickProbs' progressive
+ * construction and refinement (ParallelProbabilisticModel::buildPosterior,
+ * QP/Alignment/Multiple/ParallelProbabilisticModel.cpp:301-430) from the
+ * device-resident sparse set (every pair; after mlp_relax_qp*): profile A
+ * holds sequences labels1[0..n1) over L1 columns, B labels2[0..n2) over L2.
+ * map1 / map2: per sequence of the profile, in order, its Sequence::getMapping
+ * array (len + 1 entries: 0, then the column of each residue).  out receives
+ * the dense (L1 + 1) x (L2 + 1) matrix, bit-identical to the reference's
+ * (weights w_i w_j / sum in double, cast to float; terms in the reference's
+ * order).  MLP_ERR_STATE when a row of L2 + 1 floats does not fit in LDS. */
+int mlp_profile_posterior(mlp_ctx *ctx, const float *seq_weights, int n1, const int32_t *labels1, int L1,
+                          const int32_t *map1, int n2, const int32_t *labels2, int L2, const int32_t *map2,
+                          float *out);
+
 /* Multi-GPU (one process per GPU): RCCL over xGMI. */
 int mlp_comm_unique_id(unsigned char id[128]);
 int mlp_comm_init(mlp_ctx *ctx, const unsigned char id[128], int nranks, int rank);

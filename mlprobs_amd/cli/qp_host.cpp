@@ -338,10 +338,10 @@ int64_t g_n_terms = 0;
 double now() { return omp_get_wtime(); }
 
 // ConstructionStage::alignAlignments (ConstructionStage.cpp:86-126)
-Profile align_alignments(const std::vector<float>& w, const Profile& A, const Profile& B, const Sparse& sp,
+Profile align_alignments(const std::vector<float>& w, const Profile& A, const Profile& B, const PosteriorBackend& be,
                          std::vector<float>& post, int threads) {
   const double t0 = now();
-  build_posterior(w, A, B, sp, post, threads);
+  if (!(be.device && be.device(w, A, B, post))) build_posterior(w, A, B, be.host_sparse(), post, threads);
   const double t1 = now();
   float score;
   const std::string path = cpnp::mea_path(A[0].length(), B[0].length(), post, &score);
@@ -359,12 +359,12 @@ Profile align_alignments(const std::vector<float>& w, const Profile& A, const Pr
 
 // ConstructionStage::processTree (ConstructionStage.cpp:52-84)
 Profile process_tree(const Tree& T, int node, const std::vector<Seq>& seqs, const std::vector<float>& w,
-                     const Sparse& sp, std::vector<float>& post, int threads) {
+                     const PosteriorBackend& be, std::vector<float>& post, int threads) {
   const Tree::Node& nd = T.nodes[node];
   if (nd.leaf) return Profile{seqs[node]};
-  const Profile l = process_tree(T, nd.left, seqs, w, sp, post, threads);
-  const Profile r = process_tree(T, nd.right, seqs, w, sp, post, threads);
-  return align_alignments(w, l, r, sp, post, threads);
+  const Profile l = process_tree(T, nd.left, seqs, w, be, post, threads);
+  const Profile r = process_tree(T, nd.right, seqs, w, be, post, threads);
+  return align_alignments(w, l, r, be, post, threads);
 }
 
 // MultiSequence::extractSubset (QP/Alignment/DataStructures/MultiSequence.cpp:407-464)
@@ -445,14 +445,26 @@ struct ColumnRefiner {
 
 }  // namespace
 
-Profile construct_and_refine(const std::vector<Seq>& seqs, const Sparse& sp, const Tree& tree, const Options& opt,
-                             int threads) {
+std::vector<int32_t> profile_maps(const Profile& p) {
+  std::vector<int32_t> out;
+  std::vector<int> m;
+  for (const Seq& s : p) {
+    mapping(s, m);
+    int n = 0;
+    for (int i = 1; i <= s.length(); i++) n += s.data[i] != '-';
+    out.insert(out.end(), m.begin(), m.begin() + n + 1);
+  }
+  return out;
+}
+
+Profile construct_and_refine(const std::vector<Seq>& seqs, const PosteriorBackend& be, const Tree& tree,
+                             const Options& opt, int threads) {
   const int n = (int)seqs.size();
   // ExtendedMSA::doAlign (ExtendedMSA.cpp:178-186): weights saturated at 1e-6
   std::vector<float> w = tree.weights;
   for (float& x : w) x = std::max(x, 1e-6f);
   std::vector<float> post;
-  Profile aln = process_tree(tree, tree.root, seqs, w, sp, post, threads);
+  Profile aln = process_tree(tree, tree.root, seqs, w, be, post, threads);
   // RefinementBase::operator() (RefinementBase.cpp:13-49)
   const int iters = opt.refinement > 0 ? opt.refinement : (n > 200 ? 200 : 30);
   ColumnRefiner cr;
@@ -470,7 +482,7 @@ Profile construct_and_refine(const std::vector<Seq>& seqs, const Sparse& sp, con
     for (int i = 0; i < n; i++) (aln[i].data[col + 1] == '-' ? g1 : g2).insert(i);
     if (g1.empty() || g2.empty()) continue;
     const Profile p1 = extract_subset(aln, g1), p2 = extract_subset(aln, g2);
-    Profile cand = align_alignments(w, p1, p2, sp, post, threads);
+    Profile cand = align_alignments(w, p1, p2, be, post, threads);
     if (aln[0].length() >= cand[0].length()) aln = std::move(cand);  // checkAcceptance (length)
   }
   if (getenv("MLP_CLI_TIMES"))

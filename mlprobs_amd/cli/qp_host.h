@@ -9,6 +9,7 @@
 #pragma once
 #include <stdint.h>
 
+#include <functional>
 #include <random>
 #include <string>
 #include <utility>
@@ -78,9 +79,22 @@ struct Options {
   int refinement = -1;   // -r (<= 0 -> 30 passes up to 200 sequences, else 200)
 };
 
+// Where the weighted profile posteriors come from: `device` (libmlpgpu's
+// mlp_profile_posterior over the device-resident sparse set) when set and it
+// succeeds, else the host restatement over `host_sparse()` (built on first
+// use).
+struct PosteriorBackend {
+  std::function<bool(const std::vector<float>& w, const Profile& A, const Profile& B, std::vector<float>& post)>
+      device;
+  std::function<const Sparse&()> host_sparse;
+};
+
 // ConstructionStage::processTree + ColumnRefinement (QP/Alignment/Multiple/
 // ConstructionStage.cpp, RefinementBase.cpp, ColumnRefinement.cpp).
-Profile construct_and_refine(const std::vector<Seq>& seqs, const Sparse& sp, const Tree& tree, const Options& opt,
-                             int threads);
+Profile construct_and_refine(const std::vector<Seq>& seqs, const PosteriorBackend& be, const Tree& tree,
+                             const Options& opt, int threads);
+
+// Sequence::getMapping arrays of a profile, concatenated (len + 1 per row).
+std::vector<int32_t> profile_maps(const Profile& p);
 
 }  // namespace qph

@@ -23,6 +23,7 @@
 #include <algorithm>
 #include <chrono>
 #include <iostream>
+#include <memory>
 #include <string>
 #include <thread>
 #include <vector>
@@ -162,26 +163,49 @@ int main(int argc, char** argv) {
         check(ctx, mlp_relax_qp_selective(ctx, opt.consistency, wc.data(), seld.data(), 200.f), "consistency");
       check(ctx, mlp_synchronize(ctx), "consistency");
       stage("consistency");
-      qph::Sparse sp;
-      sp.n = n;
-      sp.lens.resize(n);
-      for (int k = 0; k < n; k++) sp.lens[k] = seqs[k].length();
-      sp.rp_off.assign(P + 1, 0);
-      for (int a = 0, p = 0; a < n; a++)
-        for (int b = a + 1; b < n; b++, p++) sp.rp_off[p + 1] = sp.rp_off[p] + sp.lens[a] + 2;
-      int64_t total = 0;
-      check(ctx, mlp_csr_total(ctx, &total), "sparse set");
-      sp.row_ptr.resize(sp.rp_off[P]);
-      sp.ent_off.resize(P + 1);
-      sp.cols.resize(std::max<int64_t>(total, 1));
-      sp.vals.resize(std::max<int64_t>(total, 1));
-      check(ctx, mlp_csr_export(ctx, sp.row_ptr.data(), sp.ent_off.data(), sp.cols.data(), sp.vals.data()),
-            "sparse set");
+      // construction + refinement: profile posteriors on the GPU from the
+      // device-resident sparse set; the host copy of the set is fetched only
+      // if a profile is too wide for the kernel's LDS row
+      std::unique_ptr<qph::Sparse> host_sp;
+      qph::PosteriorBackend be;
+      be.device = [&](const std::vector<float>& w, const qph::Profile& A, const qph::Profile& B,
+                      std::vector<float>& post) {
+        const int L1 = A[0].length(), L2 = B[0].length();
+        std::vector<int32_t> l1, l2;
+        for (const qph::Seq& q : A) l1.push_back(q.label);
+        for (const qph::Seq& q : B) l2.push_back(q.label);
+        const std::vector<int32_t> m1 = qph::profile_maps(A), m2 = qph::profile_maps(B);
+        if (post.size() < (size_t)(L1 + 1) * (L2 + 1)) post.resize((size_t)(L1 + 1) * (L2 + 1));
+        const int rc = mlp_profile_posterior(ctx, w.data(), (int)A.size(), l1.data(), L1, m1.data(), (int)B.size(),
+                                             l2.data(), L2, m2.data(), post.data());
+        if (rc == MLP_ERR_STATE) return false;  // too wide: the host restatement
+        check(ctx, rc, "profile posterior");
+        return true;
+      };
+      be.host_sparse = [&]() -> const qph::Sparse& {
+        if (!host_sp) {
+          host_sp.reset(new qph::Sparse());
+          qph::Sparse& sp = *host_sp;
+          sp.n = n;
+          sp.lens.resize(n);
+          for (int k = 0; k < n; k++) sp.lens[k] = seqs[k].length();
+          sp.rp_off.assign(P + 1, 0);
+          for (int a = 0, p = 0; a < n; a++)
+            for (int b = a + 1; b < n; b++, p++) sp.rp_off[p + 1] = sp.rp_off[p] + sp.lens[a] + 2;
+          int64_t total = 0;
+          check(ctx, mlp_csr_total(ctx, &total), "sparse set");
+          sp.row_ptr.resize(sp.rp_off[P]);
+          sp.ent_off.resize(P + 1);
+          sp.cols.resize(std::max<int64_t>(total, 1));
+          sp.vals.resize(std::max<int64_t>(total, 1));
+          check(ctx, mlp_csr_export(ctx, sp.row_ptr.data(), sp.ent_off.data(), sp.cols.data(), sp.vals.data()),
+                "sparse set");
+          sp.build_views();
+        }
+        return *host_sp;
+      };
+      aln = qph::construct_and_refine(seqs, be, tree, opt, threads);
       mlp_ctx_destroy(ctx);
-      stage("sparse set to host");
-      sp.build_views();
-      stage("transposes");
-      aln = qph::construct_and_refine(seqs, sp, tree, opt, threads);
       stage("construction + refinement");
     }
   } catch (const std::runtime_error& e) {

@@ -308,6 +308,26 @@ int tile_relax_slots(int64_t cells);           // cells per thread, 0 = too many
 int tile_relax_max_cap();                      // largest tile the prefetch registers hold
 hipError_t launch_pack(const PackArgs& a, hipStream_t st);
 hipError_t launch_relax_tiles(const TileRelaxArgs& a, int slots, hipStream_t st);
+// profile posterior (profile.hip)
+struct ProfileArgs {
+  int n;                     // family size
+  const int32_t* rowptr;     // the sparse set (pairs a < b) and its transposes
+  const uint16_t* cols;
+  const float* vals;
+  const int32_t* trowptr;
+  const uint16_t* tcols;
+  const float* tvals;
+  int n1, n2, L1, L2;        // profile sizes (sequences, columns)
+  const int64_t* rpb;        // n1 x n2: row_ptr base of block (i, j); ~base: transposed block
+  const int64_t* eb;         // n1 x n2: entry base of block (i, j)
+  const int32_t* inv1;       // n1 x (L1 + 1): residue of sequence i in column r, 0 = gap
+  const int32_t* map2;       // per sequence j of B: column of its residue k (k = 1..len)
+  const int64_t* map2_off;   // per j: offset of its map (k = 0 at map2_off[j])
+  const float* w;            // n1 x n2: (float)(w_i w_j / sum)
+  float* out;                // (L1 + 1) x (L2 + 1); rows 1..L1 written
+};
+size_t profile_lds(int L2);
+hipError_t launch_profile_posterior(const ProfileArgs& a, hipStream_t st);
 hipError_t launch_transpose(const TransposeArgs& a, hipStream_t st);
 hipError_t launch_relax_tasks(const RelaxArgs& a, hipStream_t st);
 hipError_t launch_filter(const FilterArgs& a, hipStream_t st);

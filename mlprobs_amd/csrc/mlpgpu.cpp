@@ -72,6 +72,7 @@ struct mlp_ctx {
   std::vector<int64_t> ent_off;       // host mirror (P + 1)
   int64_t store_p0 = 0, store_p1 = 0; // pairs currently held (contiguous)
   int64_t store_total = 0;
+  uint64_t store_ver = 0, tr_ver = ~0ull;  // store generation; generation of the transposes in r_t*
   std::vector<float> dist, mea;
   std::vector<int64_t> nnz;
   // Viterbi family test (per pair, pair order)
@@ -85,7 +86,7 @@ struct mlp_ctx {
   size_t scratch_budget = 0;
   // relaxation buffers
   DevBuf r_trowptr, r_tcols, r_tvals, r_raw, r_newrp, r_newcols, r_newvals, r_tasks_p, r_tasks_r,
-      r_pairs, r_nnz, r_newoff, r_img, r_imgoff, r_tiles, r_nwords, r_weights, r_seldist;
+      r_pairs, r_nnz, r_newoff, r_img, r_imgoff, r_tiles, r_nwords, r_weights, r_seldist, r_profile;
   // comm
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
@@ -341,7 +342,7 @@ void mlp_ctx_destroy(mlp_ctx* c) {
   DevBuf* bufs[] = {&c->scratch, &c->scratch2, &c->r_trowptr, &c->r_tcols, &c->r_tvals, &c->r_raw, &c->r_newrp,
                     &c->r_newcols, &c->r_newvals, &c->r_tasks_p, &c->r_tasks_r, &c->r_pairs,
                     &c->r_nnz, &c->r_newoff, &c->r_img, &c->r_imgoff, &c->r_tiles, &c->r_nwords, &c->r_weights,
-                    &c->r_seldist};
+                    &c->r_seldist, &c->r_profile};
   for (DevBuf* b : bufs)
     if (b->p) hipFree(b->p);
   if (c->comm) ncclCommDestroy(c->comm);
@@ -417,7 +418,7 @@ int mlp_family_load(mlp_ctx* c, int n, const char* residues, const int64_t* offs
   c->mea.assign(c->P, 0.f);
   c->nnz.assign(c->P, 0);
   c->store_p0 = c->store_p1 = 0;
-  c->store_total = 0;
+  c->store_total = 0; ++c->store_ver;
   c->vit_len.assign(c->P, 0);
   c->vit_match.assign(c->P, 0.f);
   c->vit_off.assign(c->P + 1, 0);
@@ -655,7 +656,7 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
   // a range that continues the held one is appended; anything else restarts
   if (c->store_p0 == c->store_p1 || p0 != c->store_p1) {
     c->store_p0 = c->store_p1 = p0;
-    c->store_total = 0;
+    c->store_total = 0; ++c->store_ver;
   }
   ModelScalars ms;
   build_tables(c->h_tables, ms, delta, pid == kPidQP);
@@ -741,7 +742,7 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
       HIPCHK(c, launch_compact(seqs, B.pm, B.d_rec, B.sc, (const int64_t*)(B.base + B.o_entb), c->d_rowptr,
                                (const int64_t*)(B.base + B.o_rpb), c->d_cols, c->d_vals, np, st));
     }
-    c->store_total = run;
+    c->store_total = run; ++c->store_ver;
     c->store_p1 = B.q;
     return MLP_OK;
   };
@@ -839,6 +840,147 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
   HIPCHK(c, hipStreamSynchronize(c->stream2));
   HIPCHK(c, hipMemcpyAsync(c->d_ent_off, c->ent_off.data(), sizeof(int64_t) * (c->P + 1),
                            hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return MLP_OK;
+}
+
+// ------------------------------------------------------------ profile posterior
+// Transposed blocks of the current store (r_trowptr / r_tcols / r_tvals).
+static int ensure_transposes(mlp_ctx* c) {
+  if (c->tr_ver == c->store_ver) return MLP_OK;
+  const int64_t total = c->store_total;
+  int rc;
+  if ((rc = ensure(c, c->r_trowptr, sizeof(int32_t) * c->trp_off[c->P]))) return rc;
+  if ((rc = ensure(c, c->r_tcols, sizeof(uint16_t) * std::max<int64_t>(total, 1)))) return rc;
+  if ((rc = ensure(c, c->r_tvals, sizeof(float) * std::max<int64_t>(total, 1)))) return rc;
+  if ((rc = ensure(c, c->r_pairs, sizeof(int64_t) * std::max<int64_t>(c->P, 1)))) return rc;
+  std::vector<int64_t> allp(c->P);
+  std::iota(allp.begin(), allp.end(), 0);
+  HIPCHK(c, hipMemcpyAsync(c->r_pairs.p, allp.data(), sizeof(int64_t) * c->P, hipMemcpyHostToDevice, c->stream));
+  TransposeArgs ta;
+  ta.n = c->n;
+  ta.lens = c->d_len;
+  ta.rp_off = c->d_rp_off;
+  ta.rowptr = c->d_rowptr;
+  ta.ent_off = c->d_ent_off;
+  ta.cols = c->d_cols;
+  ta.vals = c->d_vals;
+  ta.trp_off = c->d_trp_off;
+  ta.trowptr = (int32_t*)c->r_trowptr.p;
+  ta.tcols = (uint16_t*)c->r_tcols.p;
+  ta.tvals = (float*)c->r_tvals.p;
+  ta.pairs = (const int64_t*)c->r_pairs.p;
+  ta.npairs = c->P;
+  ta.max_len = c->max_len;
+  HIPCHK(c, launch_transpose(ta, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->tr_ver = c->store_ver;
+  return MLP_OK;
+}
+
+int mlp_profile_posterior(mlp_ctx* c, const float* seq_weights, int n1, const int32_t* labels1, int L1,
+                          const int32_t* map1, int n2, const int32_t* labels2, int L2, const int32_t* map2,
+                          float* out) {
+  if (!c || !seq_weights || !labels1 || !labels2 || !map1 || !map2 || !out || n1 < 1 || n2 < 1 || L1 < 1 ||
+      L2 < 1)
+    return MLP_ERR_ARG;
+  if (c->store_p0 != 0 || c->store_p1 != c->P) {
+    c->err = "the profile posterior needs every pair";
+    return MLP_ERR_STATE;
+  }
+  if (profile_lds(L2) > 160 * 1024) {
+    c->err = "profile too wide for one LDS row";
+    return MLP_ERR_STATE;
+  }
+  hipSetDevice(c->device);
+  int rc;
+  if ((rc = ensure_transposes(c))) return rc;
+  const int64_t np = (int64_t)n1 * n2;
+  // host side of buildPosterior: weights w1 w2 / sum in double
+  // (ParallelProbabilisticModel.cpp:317-330, 350-352), block bases, the
+  // column -> residue map of A and the residue -> column maps of B
+  std::vector<int64_t> rpb(np), eb(np), moff(n2);
+  std::vector<float> w(np);
+  double total = 0;
+  for (int i = 0; i < n1; i++) {
+    const double w1 = seq_weights[labels1[i]];
+    for (int j = 0; j < n2; j++) total += w1 * (double)seq_weights[labels2[j]];
+  }
+  for (int i = 0; i < n1; i++) {
+    const int a = labels1[i];
+    const double w1 = seq_weights[a];
+    for (int j = 0; j < n2; j++) {
+      const int b = labels2[j];
+      if (a < 0 || b < 0 || a >= c->n || b >= c->n || a == b) return MLP_ERR_ARG;
+      const int64_t q = (int64_t)i * n2 + j;
+      const double w2 = seq_weights[b];
+      w[q] = (float)((w1 * w2) / total);
+      const int64_t p = a < b ? pair_index_host(c->n, a, b) : pair_index_host(c->n, b, a);
+      rpb[q] = a < b ? c->rp_off[p] : ~c->trp_off[p];
+      eb[q] = c->ent_off[p];
+    }
+  }
+  std::vector<int32_t> inv1((size_t)n1 * (L1 + 1), 0);
+  for (int i = 0, o = 0; i < n1; i++) {
+    const int len = c->lens[labels1[i]];
+    for (int k = 1; k <= len; k++) {
+      const int col = map1[o + k];
+      if (col < 1 || col > L1) return MLP_ERR_ARG;
+      inv1[(size_t)i * (L1 + 1) + col] = k;
+    }
+    o += len + 1;
+  }
+  int64_t m2len = 0;
+  for (int j = 0; j < n2; j++) {
+    moff[j] = m2len;
+    m2len += c->lens[labels2[j]] + 1;
+  }
+  for (int64_t k = 0; k < m2len; k++)
+    if (map2[k] < 0 || map2[k] > L2) return MLP_ERR_ARG;
+  // device buffers: one carve of the profile scratch
+  const size_t b_rpb = np * 8, b_eb = np * 8, b_w = np * 4, b_inv = inv1.size() * 4, b_m2 = m2len * 4,
+               b_mo = n2 * 8, b_out = (size_t)(L1 + 1) * (L2 + 1) * 4;
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  const size_t need = al(b_rpb) + al(b_eb) + al(b_w) + al(b_inv) + al(b_m2) + al(b_mo) + al(b_out);
+  if ((rc = ensure(c, c->r_profile, need))) return rc;
+  char* base = (char*)c->r_profile.p;
+  size_t off = 0;
+  auto take = [&](size_t bytes) { char* p = base + off; off += al(bytes); return p; };
+  int64_t* d_rpb = (int64_t*)take(b_rpb);
+  int64_t* d_eb = (int64_t*)take(b_eb);
+  float* d_w = (float*)take(b_w);
+  int32_t* d_inv = (int32_t*)take(b_inv);
+  int32_t* d_m2 = (int32_t*)take(b_m2);
+  int64_t* d_mo = (int64_t*)take(b_mo);
+  float* d_out = (float*)take(b_out);
+  HIPCHK(c, hipMemcpyAsync(d_rpb, rpb.data(), b_rpb, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(d_eb, eb.data(), b_eb, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(d_w, w.data(), b_w, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(d_inv, inv1.data(), b_inv, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(d_m2, map2, b_m2, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(d_mo, moff.data(), b_mo, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemsetAsync(d_out, 0, (size_t)(L2 + 1) * 4, c->stream));  // row 0
+  ProfileArgs pa;
+  pa.n = c->n;
+  pa.rowptr = c->d_rowptr;
+  pa.cols = c->d_cols;
+  pa.vals = c->d_vals;
+  pa.trowptr = (const int32_t*)c->r_trowptr.p;
+  pa.tcols = (const uint16_t*)c->r_tcols.p;
+  pa.tvals = (const float*)c->r_tvals.p;
+  pa.n1 = n1;
+  pa.n2 = n2;
+  pa.L1 = L1;
+  pa.L2 = L2;
+  pa.rpb = d_rpb;
+  pa.eb = d_eb;
+  pa.inv1 = d_inv;
+  pa.map2 = d_m2;
+  pa.map2_off = d_mo;
+  pa.w = d_w;
+  pa.out = d_out;
+  HIPCHK(c, launch_profile_posterior(pa, c->stream));
+  HIPCHK(c, hipMemcpyAsync(out, d_out, b_out, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return MLP_OK;
 }
@@ -1120,7 +1262,7 @@ int mlp_csr_import(mlp_ctx* c, const int32_t* row_ptr, const int64_t* ent_off, c
   for (int64_t p = 0; p < c->P; p++) c->nnz[p] = ent_off[p + 1] - ent_off[p];
   c->store_p0 = 0;
   c->store_p1 = c->P;
-  c->store_total = total;
+  c->store_total = total; ++c->store_ver;
   return MLP_OK;
 }
 
@@ -1266,7 +1408,7 @@ int mlp_allgather(mlp_ctx* c) {
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->store_p0 = 0;
   c->store_p1 = c->P;
-  c->store_total = total;
+  c->store_total = total; ++c->store_ver;
   return MLP_OK;
 }
 
@@ -1583,7 +1725,7 @@ static int relax_rounds(mlp_ctx* c, int iters, const QpRelax& qp) {
     c->ent_off[r1] = run;
     c->store_p0 = r0;
     c->store_p1 = r1;
-    c->store_total = run;
+    c->store_total = run; ++c->store_ver;
     HIPCHK(c, hipMemcpyAsync(c->d_ent_off, c->ent_off.data(), sizeof(int64_t) * (c->P + 1), hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (c->comm && c->nranks > 1) {

@@ -70,6 +70,8 @@ def lib():
         L.mlp_relax.argtypes = [P, C.c_int]
         L.mlp_relax_qp.argtypes = [P, C.c_int, F32P]
         L.mlp_relax_qp_selective.argtypes = [P, C.c_int, F32P, C.c_void_p, C.c_float]
+        L.mlp_profile_posterior.argtypes = [P, F32P, C.c_int, I32P, C.c_int, I32P, C.c_int, I32P, C.c_int, I32P,
+                                            F32P]
         L.mlp_viterbi.argtypes = [P, I64, I64, C.c_int]
         L.mlp_viterbi_results.argtypes = [P, I64, I64, C.c_void_p, C.c_void_p]
         L.mlp_viterbi_path.argtypes = [P, I64, C.c_void_p, C.c_void_p]
@@ -92,7 +94,7 @@ def lib():
 EXPORTED = ['mlp_ctx_create', 'mlp_ctx_destroy', 'mlp_last_error', 'mlp_set_scratch', 'mlp_family_load',
             'mlp_family_npairs', 'mlp_posteriors', 'mlp_pair_results', 'mlp_csr_total',
             'mlp_csr_export', 'mlp_csr_import', 'mlp_relax', 'mlp_relax_qp',
-            'mlp_relax_qp_selective', 'mlp_viterbi', 'mlp_viterbi_results',
+            'mlp_relax_qp_selective', 'mlp_profile_posterior', 'mlp_viterbi', 'mlp_viterbi_results',
             'mlp_viterbi_path', 'mlp_model_adjustment', 'mlp_family_features', 'mlp_comm_unique_id', 'mlp_comm_init',
             'mlp_shard_range', 'mlp_shard_plan', 'mlp_gather_layout', 'mlp_allgather', 'mlp_synchronize', 'mlp_profile',
             'mlp_kernel_times', 'mlp_profile_reset']
@@ -234,6 +236,19 @@ class Family:
         d = np.ascontiguousarray(sel_dist, np.float32)
         assert d.shape == (self.n, self.n)
         self._chk(self._L.mlp_relax_qp_selective(self._ctx, int(iters), w, d.ctypes.data, float(selectivity)))
+
+    def profile_posterior(self, weights, labels1, maps1, L1, labels2, maps2, L2):
+        """Weighted profile-profile posterior (include/mlpgpu.h
+        mlp_profile_posterior); maps: per sequence its getMapping array."""
+        w = np.ascontiguousarray(weights, np.float32)
+        l1 = np.ascontiguousarray(labels1, np.int32)
+        l2 = np.ascontiguousarray(labels2, np.int32)
+        m1 = np.ascontiguousarray(np.concatenate(maps1), np.int32)
+        m2 = np.ascontiguousarray(np.concatenate(maps2), np.int32)
+        out = np.empty((L1 + 1) * (L2 + 1), np.float32)
+        self._chk(self._L.mlp_profile_posterior(self._ctx, w, len(l1), l1, int(L1), m1, len(l2), l2, int(L2), m2,
+                                                out))
+        return out.reshape(L1 + 1, L2 + 1)
 
     def relax(self, iters):
         self._csr = None

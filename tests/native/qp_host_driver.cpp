@@ -77,7 +77,9 @@ int main(int argc, char** argv) {
   fclose(f);
   sp.build_views();
   const qph::Tree tree = qph::build_tree(D, n);
-  const qph::Profile aln = qph::construct_and_refine(seqs, sp, tree, opt, 4);
+  qph::PosteriorBackend be;
+  be.host_sparse = [&]() -> const qph::Sparse& { return sp; };
+  const qph::Profile aln = qph::construct_and_refine(seqs, be, tree, opt, 4);
   std::string out;
   qph::write_fasta(out, aln);
   fwrite(out.data(), 1, out.size(), stdout);

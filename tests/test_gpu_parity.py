@@ -395,3 +395,66 @@ def test_qp_stage_vs_oracle(n, L, s, iters, seed, sel):
     for k in range(len(cur)):
         csr_equal(cur[k], fam.sparse(k), f'qp stage p{k}')
     fam.close()
+
+
+def _gapped(rng, s, L):
+    """s with gaps inserted at random to length L, and its getMapping array."""
+    pos = np.sort(rng.choice(np.arange(1, L + 1), size=len(s), replace=False))
+    row = ['-'] * (L + 1)
+    for k, c in zip(pos, s):
+        row[k] = c
+    return ''.join(row[1:]), np.concatenate([[0], pos]).astype(np.int32)
+
+
+def _pair(n, a, b):
+    return a * n - a * (a + 1) // 2 + (b - a - 1)
+
+
+@pytest.mark.parametrize('seed', [81, 82])
+def test_profile_posterior_vs_restatement(seed):
+    """mlp_profile_posterior (QuickProbs' buildPosterior on the GPU) against a
+    plain restatement of ParallelProbabilisticModel.cpp:301-430 over the same
+    relaxed sparse set: weights in double cast to float, terms in (i, j, row,
+    entry) order, w * v then +=; bit-exact."""
+    rng = np.random.default_rng(seed)
+    n = 9
+    seqs = [x for _, x in synth.family(n, 70, 0.5, seed=seed)]
+    fam = Family(seqs)
+    fam.posteriors(PID_QP, 0.0)
+    w = rng.uniform(0.01, 0.3, n).astype(np.float32)
+    fam.relax_qp(2, w)
+    # dense views of every ordered block
+    dense = {}
+    for a in range(n):
+        for b in range(a + 1, n):
+            rp, c, v = fam.sparse(_pair(n, a, b))
+            rows = [[] for _ in range(len(seqs[a]) + 1)]
+            trows = [[] for _ in range(len(seqs[b]) + 1)]
+            for i in range(1, len(seqs[a]) + 1):
+                for e in range(rp[i], rp[i + 1]):
+                    rows[i].append((int(c[e]), float(v[e])))
+                    trows[int(c[e])].append((i, float(v[e])))
+            dense[(a, b)] = rows
+            dense[(b, a)] = trows
+    A, B = [0, 3, 5, 8], [1, 2, 6]
+    L1 = max(len(seqs[k]) for k in A) + 9
+    L2 = max(len(seqs[k]) for k in B) + 5
+    mA = [_gapped(rng, seqs[k], L1)[1] for k in A]
+    mB = [_gapped(rng, seqs[k], L2)[1] for k in B]
+    got = fam.profile_posterior(w, A, mA, L1, B, mB, L2)
+    ref = np.zeros((L1 + 1, L2 + 1), np.float32)
+    total = 0.0
+    for a in A:
+        for b in B:
+            total += float(w[a]) * float(w[b])
+    for ia, a in enumerate(A):
+        for jb, b in enumerate(B):
+            wf = np.float32((float(w[a]) * float(w[b])) / total)
+            rows = dense[(a, b)]
+            for ii in range(1, len(seqs[a]) + 1):
+                r = mA[ia][ii]
+                for col, v in rows[ii]:
+                    c = mB[jb][col]
+                    ref[r, c] = np.float32(ref[r, c] + np.float32(wf * np.float32(v)))
+    np.testing.assert_array_equal(got, ref)
+    fam.close()
