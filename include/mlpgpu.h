@@ -146,6 +146,9 @@ int mlp_relax_qp_selective(mlp_ctx *ctx, int iters, const float *seq_weights, co
 int mlp_profile_posterior(mlp_ctx *ctx, const float *seq_weights, int n1, const int32_t *labels1, int L1,
                           const int32_t *map1, int n2, const int32_t *labels2, int L2, const int32_t *map2,
                           float *out);
+/* out = NULL: the matrix stays in a pinned host buffer of the context,
+ * returned here and valid until the next mlp_profile_posterior call. */
+const float *mlp_profile_result(const mlp_ctx *ctx);
 
 /* Multi-GPU (one process per GPU): RCCL over xGMI. */
 int mlp_comm_unique_id(unsigned char id[128]);

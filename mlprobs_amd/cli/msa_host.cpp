@@ -252,6 +252,10 @@ std::vector<float> build_posterior(const Profile& A, const Profile& B, const Spa
 }
 
 std::string mea_path(int len1, int len2, const std::vector<float>& post, float* score) {
+  return mea_path(len1, len2, post.data(), score);
+}
+
+std::string mea_path(int len1, int len2, const float* post, float* score) {
   const int W2 = len2 + 1;
   std::vector<float> rows(2 * (size_t)W2);
   float* oldr = rows.data();
@@ -264,7 +268,7 @@ std::string mea_path(int len1, int len2, const std::vector<float>& post, float* 
   for (int i = 1; i <= len1; i++) {
     newr[0] = 0;
     tb[(size_t)i * W2] = 'U';
-    const float* pr = post.data() + (size_t)i * W2;
+    const float* pr = post + (size_t)i * W2;
     for (int j = 1; j <= len2; j++) {
       // ChooseBestOfThree (ScoreType.h:347-366): D, L, U
       const float x1 = pr[j] + oldr[j - 1], x2 = newr[j - 1], x3 = oldr[j];

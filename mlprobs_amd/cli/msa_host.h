@@ -70,6 +70,7 @@ std::vector<float> build_posterior(const Profile& a, const Profile& b, const Spa
 // MEA alignment of two profiles (ProbabilisticModel.h:804-864): the path
 // ('B', 'X', 'Y') and its score.
 std::string mea_path(int len1, int len2, const std::vector<float>& post, float* score);
+std::string mea_path(int len1, int len2, const float* post, float* score);  // (len1 + 1) x (len2 + 1) row-major
 
 // Profile merge along a path (Sequence.h AddGaps) and helpers.
 Profile merge(const Profile& a, const Profile& b, const std::string& path, bool sort_by_label);

@@ -84,8 +84,9 @@ struct Options {
 // succeeds, else the host restatement over `host_sparse()` (built on first
 // use).
 struct PosteriorBackend {
-  std::function<bool(const std::vector<float>& w, const Profile& A, const Profile& B, std::vector<float>& post)>
-      device;
+  // returns the dense (L1 + 1) x (L2 + 1) matrix (valid until the next call)
+  // or nullptr to use the host path
+  std::function<const float*(const std::vector<float>& w, const Profile& A, const Profile& B)> device;
   std::function<const Sparse&()> host_sparse;
 };
 

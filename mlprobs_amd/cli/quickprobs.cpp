@@ -168,19 +168,18 @@ int main(int argc, char** argv) {
       // if a profile is too wide for the kernel's LDS row
       std::unique_ptr<qph::Sparse> host_sp;
       qph::PosteriorBackend be;
-      be.device = [&](const std::vector<float>& w, const qph::Profile& A, const qph::Profile& B,
-                      std::vector<float>& post) {
+      be.device = [&](const std::vector<float>& w, const qph::Profile& A, const qph::Profile& B) -> const float* {
         const int L1 = A[0].length(), L2 = B[0].length();
         std::vector<int32_t> l1, l2;
         for (const qph::Seq& q : A) l1.push_back(q.label);
         for (const qph::Seq& q : B) l2.push_back(q.label);
         const std::vector<int32_t> m1 = qph::profile_maps(A), m2 = qph::profile_maps(B);
-        if (post.size() < (size_t)(L1 + 1) * (L2 + 1)) post.resize((size_t)(L1 + 1) * (L2 + 1));
+        // out = NULL: the matrix stays in the library's pinned buffer
         const int rc = mlp_profile_posterior(ctx, w.data(), (int)A.size(), l1.data(), L1, m1.data(), (int)B.size(),
-                                             l2.data(), L2, m2.data(), post.data());
-        if (rc == MLP_ERR_STATE) return false;  // too wide: the host restatement
+                                             l2.data(), L2, m2.data(), nullptr);
+        if (rc == MLP_ERR_STATE) return nullptr;  // too wide: the host restatement
         check(ctx, rc, "profile posterior");
-        return true;
+        return mlp_profile_result(ctx);
       };
       be.host_sparse = [&]() -> const qph::Sparse& {
         if (!host_sp) {

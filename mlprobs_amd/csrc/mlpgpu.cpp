@@ -72,7 +72,12 @@ struct mlp_ctx {
   std::vector<int64_t> ent_off;       // host mirror (P + 1)
   int64_t store_p0 = 0, store_p1 = 0; // pairs currently held (contiguous)
   int64_t store_total = 0;
-  uint64_t store_ver = 0, tr_ver = ~0ull;  // store generation; generation of the transposes in r_t*
+  uint64_t store_ver = 0, tr_ver = ~0ull;
+  // pinned host staging of the profile posterior (uploads; result)
+  void* h_prof_in = nullptr;
+  size_t h_prof_in_bytes = 0;
+  float* h_prof_out = nullptr;
+  size_t h_prof_out_bytes = 0;  // store generation; generation of the transposes in r_t*
   std::vector<float> dist, mea;
   std::vector<int64_t> nnz;
   // Viterbi family test (per pair, pair order)
@@ -347,6 +352,8 @@ void mlp_ctx_destroy(mlp_ctx* c) {
     if (b->p) hipFree(b->p);
   if (c->comm) ncclCommDestroy(c->comm);
   for (hipEvent_t e : c->evpool) hipEventDestroy(e);
+  if (c->h_prof_in) hipHostFree(c->h_prof_in);
+  if (c->h_prof_out) hipHostFree(c->h_prof_out);
   hipStreamDestroy(c->stream);
   hipStreamDestroy(c->stream2);
   delete c;
@@ -881,7 +888,7 @@ static int ensure_transposes(mlp_ctx* c) {
 int mlp_profile_posterior(mlp_ctx* c, const float* seq_weights, int n1, const int32_t* labels1, int L1,
                           const int32_t* map1, int n2, const int32_t* labels2, int L2, const int32_t* map2,
                           float* out) {
-  if (!c || !seq_weights || !labels1 || !labels2 || !map1 || !map2 || !out || n1 < 1 || n2 < 1 || L1 < 1 ||
+  if (!c || !seq_weights || !labels1 || !labels2 || !map1 || !map2 || n1 < 1 || n2 < 1 || L1 < 1 ||
       L2 < 1)
     return MLP_ERR_ARG;
   if (c->store_p0 != 0 || c->store_p1 != c->P) {
@@ -937,28 +944,44 @@ int mlp_profile_posterior(mlp_ctx* c, const float* seq_weights, int n1, const in
   }
   for (int64_t k = 0; k < m2len; k++)
     if (map2[k] < 0 || map2[k] > L2) return MLP_ERR_ARG;
-  // device buffers: one carve of the profile scratch
+  // one pinned staging buffer for every upload (a single copy) and a pinned
+  // result buffer: pageable copies cost more than the kernel here
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
   const size_t b_rpb = np * 8, b_eb = np * 8, b_w = np * 4, b_inv = inv1.size() * 4, b_m2 = m2len * 4,
                b_mo = n2 * 8, b_out = (size_t)(L1 + 1) * (L2 + 1) * 4;
-  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-  const size_t need = al(b_rpb) + al(b_eb) + al(b_w) + al(b_inv) + al(b_m2) + al(b_mo) + al(b_out);
-  if ((rc = ensure(c, c->r_profile, need))) return rc;
+  const size_t o_rpb = 0, o_eb = o_rpb + al(b_rpb), o_w = o_eb + al(b_eb), o_inv = o_w + al(b_w),
+               o_m2 = o_inv + al(b_inv), o_mo = o_m2 + al(b_m2), in_bytes = o_mo + al(b_mo);
+  if (c->h_prof_in_bytes < in_bytes) {
+    if (c->h_prof_in) hipHostFree(c->h_prof_in);
+    c->h_prof_in = nullptr;
+    c->h_prof_in_bytes = 0;
+    if (hipHostMalloc(&c->h_prof_in, in_bytes * 2, hipHostMallocDefault) != hipSuccess) return MLP_ERR_MEMORY;
+    c->h_prof_in_bytes = in_bytes * 2;
+  }
+  if (c->h_prof_out_bytes < b_out) {
+    if (c->h_prof_out) hipHostFree(c->h_prof_out);
+    c->h_prof_out = nullptr;
+    c->h_prof_out_bytes = 0;
+    if (hipHostMalloc((void**)&c->h_prof_out, b_out * 2, hipHostMallocDefault) != hipSuccess) return MLP_ERR_MEMORY;
+    c->h_prof_out_bytes = b_out * 2;
+  }
+  char* hin = (char*)c->h_prof_in;
+  memcpy(hin + o_rpb, rpb.data(), b_rpb);
+  memcpy(hin + o_eb, eb.data(), b_eb);
+  memcpy(hin + o_w, w.data(), b_w);
+  memcpy(hin + o_inv, inv1.data(), b_inv);
+  memcpy(hin + o_m2, map2, b_m2);
+  memcpy(hin + o_mo, moff.data(), b_mo);
+  if ((rc = ensure(c, c->r_profile, in_bytes + al(b_out)))) return rc;
   char* base = (char*)c->r_profile.p;
-  size_t off = 0;
-  auto take = [&](size_t bytes) { char* p = base + off; off += al(bytes); return p; };
-  int64_t* d_rpb = (int64_t*)take(b_rpb);
-  int64_t* d_eb = (int64_t*)take(b_eb);
-  float* d_w = (float*)take(b_w);
-  int32_t* d_inv = (int32_t*)take(b_inv);
-  int32_t* d_m2 = (int32_t*)take(b_m2);
-  int64_t* d_mo = (int64_t*)take(b_mo);
-  float* d_out = (float*)take(b_out);
-  HIPCHK(c, hipMemcpyAsync(d_rpb, rpb.data(), b_rpb, hipMemcpyHostToDevice, c->stream));
-  HIPCHK(c, hipMemcpyAsync(d_eb, eb.data(), b_eb, hipMemcpyHostToDevice, c->stream));
-  HIPCHK(c, hipMemcpyAsync(d_w, w.data(), b_w, hipMemcpyHostToDevice, c->stream));
-  HIPCHK(c, hipMemcpyAsync(d_inv, inv1.data(), b_inv, hipMemcpyHostToDevice, c->stream));
-  HIPCHK(c, hipMemcpyAsync(d_m2, map2, b_m2, hipMemcpyHostToDevice, c->stream));
-  HIPCHK(c, hipMemcpyAsync(d_mo, moff.data(), b_mo, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(base, hin, in_bytes, hipMemcpyHostToDevice, c->stream));
+  int64_t* d_rpb = (int64_t*)(base + o_rpb);
+  int64_t* d_eb = (int64_t*)(base + o_eb);
+  float* d_w = (float*)(base + o_w);
+  int32_t* d_inv = (int32_t*)(base + o_inv);
+  int32_t* d_m2 = (int32_t*)(base + o_m2);
+  int64_t* d_mo = (int64_t*)(base + o_mo);
+  float* d_out = (float*)(base + in_bytes);
   HIPCHK(c, hipMemsetAsync(d_out, 0, (size_t)(L2 + 1) * 4, c->stream));  // row 0
   ProfileArgs pa;
   pa.n = c->n;
@@ -980,10 +1003,13 @@ int mlp_profile_posterior(mlp_ctx* c, const float* seq_weights, int n1, const in
   pa.w = d_w;
   pa.out = d_out;
   HIPCHK(c, launch_profile_posterior(pa, c->stream));
-  HIPCHK(c, hipMemcpyAsync(out, d_out, b_out, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->h_prof_out, d_out, b_out, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (out) memcpy(out, c->h_prof_out, b_out);
   return MLP_OK;
 }
+
+const float* mlp_profile_result(const mlp_ctx* c) { return c ? c->h_prof_out : nullptr; }
 
 int mlp_pair_results(mlp_ctx* c, int64_t p0, int64_t p1, float* dist, float* mea, int64_t* nnz) {
   if (!c || p0 < 0 || p1 > c->P || p0 > p1) return MLP_ERR_ARG;

@@ -94,7 +94,7 @@ def lib():
 EXPORTED = ['mlp_ctx_create', 'mlp_ctx_destroy', 'mlp_last_error', 'mlp_set_scratch', 'mlp_family_load',
             'mlp_family_npairs', 'mlp_posteriors', 'mlp_pair_results', 'mlp_csr_total',
             'mlp_csr_export', 'mlp_csr_import', 'mlp_relax', 'mlp_relax_qp',
-            'mlp_relax_qp_selective', 'mlp_profile_posterior', 'mlp_viterbi', 'mlp_viterbi_results',
+            'mlp_relax_qp_selective', 'mlp_profile_posterior', 'mlp_profile_result', 'mlp_viterbi', 'mlp_viterbi_results',
             'mlp_viterbi_path', 'mlp_model_adjustment', 'mlp_family_features', 'mlp_comm_unique_id', 'mlp_comm_init',
             'mlp_shard_range', 'mlp_shard_plan', 'mlp_gather_layout', 'mlp_allgather', 'mlp_synchronize', 'mlp_profile',
             'mlp_kernel_times', 'mlp_profile_reset']
