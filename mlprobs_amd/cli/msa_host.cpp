@@ -255,7 +255,72 @@ std::string mea_path(int len1, int len2, const std::vector<float>& post, float* 
   return mea_path(len1, len2, post.data(), score);
 }
 
+// The same recurrence over 128 x 128 tiles, one anti-diagonal of tiles at a
+// time in parallel (every cell still sees exactly its three neighbours'
+// final values, so the result is the serial one bit for bit).
+std::string mea_path_tiled(int len1, int len2, const float* post, float* score) {
+  const int W2 = len2 + 1;
+  constexpr int T = 128;
+  std::vector<float> V((size_t)(len1 + 1) * W2);
+  std::vector<char> tb((size_t)(len1 + 1) * W2);
+  for (int j = 0; j <= len2; j++) {
+    V[j] = 0;
+    tb[j] = 'L';
+  }
+  for (int i = 1; i <= len1; i++) {
+    V[(size_t)i * W2] = 0;
+    tb[(size_t)i * W2] = 'U';
+  }
+  const int ti_n = (len1 + T - 1) / T, tj_n = (len2 + T - 1) / T;
+  for (int d = 0; d < ti_n + tj_n - 1; d++) {
+    const int lo = std::max(0, d - (tj_n - 1)), hi = std::min(d, ti_n - 1);
+#pragma omp parallel for schedule(static) if (hi - lo >= 2)
+    for (int ti = lo; ti <= hi; ti++) {
+      const int tj = d - ti;
+      const int i0 = 1 + ti * T, i1 = std::min(len1, i0 + T - 1);
+      const int j0 = 1 + tj * T, j1 = std::min(len2, j0 + T - 1);
+      for (int i = i0; i <= i1; i++) {
+        const float* pr = post + (size_t)i * W2;
+        float* cur = V.data() + (size_t)i * W2;
+        const float* up = cur - W2;
+        char* t = tb.data() + (size_t)i * W2;
+        for (int j = j0; j <= j1; j++) {
+          const float x1 = pr[j] + up[j - 1], x2 = cur[j - 1], x3 = up[j];
+          float v;
+          char b;
+          if (x1 >= x2) {
+            if (x1 >= x3) { v = x1; b = 'D'; } else { v = x3; b = 'U'; }
+          } else if (x2 >= x3) {
+            v = x2; b = 'L';
+          } else {
+            v = x3; b = 'U';
+          }
+          cur[j] = v;
+          t[j] = b;
+        }
+      }
+    }
+  }
+  if (score) *score = V[(size_t)len1 * W2 + len2];
+  std::string path;
+  int r = len1, c = len2;
+  while (r != 0 || c != 0) {
+    switch (tb[(size_t)r * W2 + c]) {
+      case 'L': c--; path += 'Y'; break;
+      case 'U': r--; path += 'X'; break;
+      default: c--; r--; path += 'B'; break;
+    }
+  }
+  std::reverse(path.begin(), path.end());
+  return path;
+}
+
 std::string mea_path(int len1, int len2, const float* post, float* score) {
+  if ((int64_t)len1 * len2 >= (int64_t)512 * 512) return mea_path_tiled(len1, len2, post, score);
+  return mea_path_serial(len1, len2, post, score);
+}
+
+std::string mea_path_serial(int len1, int len2, const float* post, float* score) {
   const int W2 = len2 + 1;
   std::vector<float> rows(2 * (size_t)W2);
   float* oldr = rows.data();

@@ -71,6 +71,10 @@ std::vector<float> build_posterior(const Profile& a, const Profile& b, const Spa
 // ('B', 'X', 'Y') and its score.
 std::string mea_path(int len1, int len2, const std::vector<float>& post, float* score);
 std::string mea_path(int len1, int len2, const float* post, float* score);  // (len1 + 1) x (len2 + 1) row-major
+// the two evaluations mea_path chooses between (tiled: anti-diagonals of
+// 128 x 128 tiles in parallel, for large matrices); identical results
+std::string mea_path_serial(int len1, int len2, const float* post, float* score);
+std::string mea_path_tiled(int len1, int len2, const float* post, float* score);
 
 // Profile merge along a path (Sequence.h AddGaps) and helpers.
 Profile merge(const Profile& a, const Profile& b, const std::string& path, bool sort_by_label);

@@ -438,10 +438,12 @@ int mlp_family_load(mlp_ctx* c, int n, const char* residues, const int64_t* offs
 int64_t mlp_family_npairs(const mlp_ctx* c) { return c ? c->P : 0; }
 
 // grow the entry store to hold `need` entries, keeping `keep` existing ones
-static int grow_store(mlp_ctx* c, int64_t need, int64_t keep) {
+static int grow_store(mlp_ctx* c, int64_t need, int64_t keep, int64_t want = 0) {
   if (need <= c->ent_cap) return MLP_OK;
   HIPCHK(c, hipStreamSynchronize(c->stream2));  // a compaction may still be writing the old store
-  int64_t cap = std::max<int64_t>(need, c->ent_cap + c->ent_cap / 2);
+  // `want`: the caller's estimate of the final size, so a growing store is
+  // reallocated (and copied) once rather than every 1.5x
+  int64_t cap = std::max<int64_t>(std::max<int64_t>(need, want), c->ent_cap + c->ent_cap / 2);
   uint16_t* nc = nullptr;
   float* nv = nullptr;
   if (hipMalloc((void**)&nc, sizeof(uint16_t) * cap) != hipSuccess ||
@@ -686,6 +688,9 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
   // compaction into the store) before batch b + 1 reuses the scratch.
   const bool two = false;
   size_t batch_target = batch_target_for(c, p0, p1, pair_bytes);
+  int64_t all_cells = 0, done_cells = 0;
+  for (int64_t k = p0; k < p1; k++) all_cells += pair_cost_cells(c, k);
+  const int64_t base_total = c->store_total;
   hipStream_t streams[2] = {c->stream, c->stream2};
   DevBuf* scr[2] = {&c->scratch, &c->scratch2};
   if (two) {  // stream2 must not run ahead of the tables upload on stream
@@ -741,7 +746,11 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
     }
     c->ent_off[B.q] = run;
     int rc;
-    if ((rc = grow_store(c, run, c->store_total))) return rc;
+    done_cells += B.bcells;
+    // the set's final size, extrapolated from the pairs done so far (+10%)
+    const int64_t want = run + (int64_t)((double)(run - base_total) / (double)done_cells *
+                                         (double)(all_cells - done_cells) * 1.1);
+    if ((rc = grow_store(c, run, c->store_total, want))) return rc;
     HIPCHK(c, hipMemcpyAsync(B.base + B.o_entb, h_entb.data(), np * 8, hipMemcpyHostToDevice, st));
     HIPCHK(c, hipMemcpyAsync(B.base + B.o_rpb, h_rpb.data(), np * 8, hipMemcpyHostToDevice, st));
     {

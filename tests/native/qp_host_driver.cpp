@@ -15,6 +15,9 @@
 #include <string>
 #include <vector>
 
+#include <random>
+
+#include "msa_host.h"
 #include "qp_host.h"
 
 template <class T>
@@ -24,6 +27,18 @@ static void rd(FILE* f, T* p, size_t n) {
 
 int main(int argc, char** argv) {
   if (argc < 3) return 2;
+  if (!strcmp(argv[1], "mea") && argc == 5) {  // tiled vs serial MEA on a random matrix
+    const int L1 = atoi(argv[3]), L2 = atoi(argv[4]);
+    std::mt19937 g((unsigned)atoi(argv[2]));
+    std::uniform_real_distribution<float> u(0.f, 1.f);
+    std::vector<float> post((size_t)(L1 + 1) * (L2 + 1));
+    for (float& x : post) x = u(g) < 0.9f ? 0.f : u(g);  // sparse-ish, with ties
+    float s1 = 0, s2 = 0;
+    const std::string a = cpnp::mea_path_serial(L1, L2, post.data(), &s1);
+    const std::string b = cpnp::mea_path_tiled(L1, L2, post.data(), &s2);
+    printf("%s\n", (a == b && s1 == s2) ? "same" : "DIFF");
+    return 0;
+  }
   FILE* f = fopen(argv[2], "rb");
   if (!f) return 2;
   if (!strcmp(argv[1], "tree")) {

@@ -24,7 +24,7 @@ CLI = os.path.join(ROOT, 'mlprobs_amd', 'cli')
 @pytest.fixture(scope='module')
 def driver(tmp_path_factory):
     out = str(tmp_path_factory.mktemp('drv') / 'host_driver')
-    subprocess.check_call(['g++', '-O2', '-std=c++17', '-I', CLI,
+    subprocess.check_call(['g++', '-O2', '-std=c++17', '-fopenmp', '-I', CLI,
                            os.path.join(ROOT, 'tests', 'native', 'host_driver.cpp'),
                            os.path.join(CLI, 'msa_host.cpp'), '-o', out])
     return out
