@@ -261,15 +261,21 @@ std::string mea_path(int len1, int len2, const std::vector<float>& post, float* 
 std::string mea_path_tiled(int len1, int len2, const float* post, float* score) {
   const int W2 = len2 + 1;
   constexpr int T = 128;
-  std::vector<float> V((size_t)(len1 + 1) * W2);
-  std::vector<char> tb((size_t)(len1 + 1) * W2);
+  static thread_local std::vector<float> V;  // reused: first touches cost more than the DP
+  static thread_local std::vector<char> tb;
+  if (V.size() < (size_t)(len1 + 1) * W2) {
+    V.resize((size_t)(len1 + 1) * W2);
+    tb.resize((size_t)(len1 + 1) * W2);
+  }
+  float* Vp = V.data();  // (the parallel region's threads have their own thread_locals)
+  char* tbp = tb.data();
   for (int j = 0; j <= len2; j++) {
-    V[j] = 0;
-    tb[j] = 'L';
+    Vp[j] = 0;
+    tbp[j] = 'L';
   }
   for (int i = 1; i <= len1; i++) {
-    V[(size_t)i * W2] = 0;
-    tb[(size_t)i * W2] = 'U';
+    Vp[(size_t)i * W2] = 0;
+    tbp[(size_t)i * W2] = 'U';
   }
   const int ti_n = (len1 + T - 1) / T, tj_n = (len2 + T - 1) / T;
   for (int d = 0; d < ti_n + tj_n - 1; d++) {
@@ -281,9 +287,9 @@ std::string mea_path_tiled(int len1, int len2, const float* post, float* score) 
       const int j0 = 1 + tj * T, j1 = std::min(len2, j0 + T - 1);
       for (int i = i0; i <= i1; i++) {
         const float* pr = post + (size_t)i * W2;
-        float* cur = V.data() + (size_t)i * W2;
+        float* cur = Vp + (size_t)i * W2;
         const float* up = cur - W2;
-        char* t = tb.data() + (size_t)i * W2;
+        char* t = tbp + (size_t)i * W2;
         for (int j = j0; j <= j1; j++) {
           const float x1 = pr[j] + up[j - 1], x2 = cur[j - 1], x3 = up[j];
           float v;
@@ -301,11 +307,11 @@ std::string mea_path_tiled(int len1, int len2, const float* post, float* score) 
       }
     }
   }
-  if (score) *score = V[(size_t)len1 * W2 + len2];
+  if (score) *score = Vp[(size_t)len1 * W2 + len2];
   std::string path;
   int r = len1, c = len2;
   while (r != 0 || c != 0) {
-    switch (tb[(size_t)r * W2 + c]) {
+    switch (tbp[(size_t)r * W2 + c]) {
       case 'L': c--; path += 'Y'; break;
       case 'U': r--; path += 'X'; break;
       default: c--; r--; path += 'B'; break;
@@ -316,7 +322,10 @@ std::string mea_path_tiled(int len1, int len2, const float* post, float* score) 
 }
 
 std::string mea_path(int len1, int len2, const float* post, float* score) {
-  if ((int64_t)len1 * len2 >= (int64_t)512 * 512) return mea_path_tiled(len1, len2, post, score);
+  // the tiled form pays ~20 parallel regions per call: only for very large
+  // matrices (measured: 1100 x 1100 on 16 threads of the GPU box is slower
+  // tiled once the thread wake-ups are counted)
+  if ((int64_t)len1 * len2 >= (int64_t)2048 * 2048) return mea_path_tiled(len1, len2, post, score);
   return mea_path_serial(len1, len2, post, score);
 }
 
