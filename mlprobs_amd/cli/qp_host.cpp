@@ -451,12 +451,12 @@ struct ColumnRefiner {
 
 std::vector<int32_t> profile_maps(const Profile& p) {
   std::vector<int32_t> out;
-  std::vector<int> m;
-  for (const Seq& s : p) {
-    mapping(s, m);
-    int n = 0;
-    for (int i = 1; i <= s.length(); i++) n += s.data[i] != '-';
-    out.insert(out.end(), m.begin(), m.begin() + n + 1);
+  out.reserve(p.size() * (size_t)(p.empty() ? 0 : p[0].length() + 1));
+  for (const Seq& s : p) {  // Sequence::getMapping, appended
+    out.push_back(0);
+    const char* d = s.data.data();
+    for (int i = 1, L = s.length(); i <= L; i++)
+      if (d[i] != '-') out.push_back(i);
   }
   return out;
 }

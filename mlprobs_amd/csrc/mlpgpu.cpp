@@ -18,6 +18,7 @@
 #include <cctype>
 #include <cmath>
 #include <cstdio>
+#include <chrono>
 #include <cstring>
 #include <numeric>
 #include <string>
@@ -77,7 +78,8 @@ struct mlp_ctx {
   void* h_prof_in = nullptr;
   size_t h_prof_in_bytes = 0;
   float* h_prof_out = nullptr;
-  size_t h_prof_out_bytes = 0;  // store generation; generation of the transposes in r_t*
+  size_t h_prof_out_bytes = 0;
+  double prof_t[2] = {0, 0};  // host preparation, device round trip (MLP_PROFILE_TIMES)
   std::vector<float> dist, mea;
   std::vector<int64_t> nnz;
   // Viterbi family test (per pair, pair order)
@@ -352,6 +354,9 @@ void mlp_ctx_destroy(mlp_ctx* c) {
     if (b->p) hipFree(b->p);
   if (c->comm) ncclCommDestroy(c->comm);
   for (hipEvent_t e : c->evpool) hipEventDestroy(e);
+  if (getenv("MLP_PROFILE_TIMES") && (c->prof_t[0] > 0 || c->prof_t[1] > 0))
+    fprintf(stderr, "[profile posterior] host preparation %.3f s, device round trips %.3f s\n", c->prof_t[0],
+            c->prof_t[1]);
   if (c->h_prof_in) hipHostFree(c->h_prof_in);
   if (c->h_prof_out) hipHostFree(c->h_prof_out);
   hipStreamDestroy(c->stream);
@@ -911,6 +916,7 @@ int mlp_profile_posterior(mlp_ctx* c, const float* seq_weights, int n1, const in
   hipSetDevice(c->device);
   int rc;
   if ((rc = ensure_transposes(c))) return rc;
+  const auto tp0 = std::chrono::steady_clock::now();
   const int64_t np = (int64_t)n1 * n2;
   // host side of buildPosterior: weights w1 w2 / sum in double
   // (ParallelProbabilisticModel.cpp:317-330, 350-352), block bases, the
@@ -981,6 +987,8 @@ int mlp_profile_posterior(mlp_ctx* c, const float* seq_weights, int n1, const in
   memcpy(hin + o_inv, inv1.data(), b_inv);
   memcpy(hin + o_m2, map2, b_m2);
   memcpy(hin + o_mo, moff.data(), b_mo);
+  const auto tp1 = std::chrono::steady_clock::now();
+  c->prof_t[0] += std::chrono::duration<double>(tp1 - tp0).count();
   if ((rc = ensure(c, c->r_profile, in_bytes + al(b_out)))) return rc;
   char* base = (char*)c->r_profile.p;
   HIPCHK(c, hipMemcpyAsync(base, hin, in_bytes, hipMemcpyHostToDevice, c->stream));
@@ -1014,6 +1022,7 @@ int mlp_profile_posterior(mlp_ctx* c, const float* seq_weights, int n1, const in
   HIPCHK(c, launch_profile_posterior(pa, c->stream));
   HIPCHK(c, hipMemcpyAsync(c->h_prof_out, d_out, b_out, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->prof_t[1] += std::chrono::duration<double>(std::chrono::steady_clock::now() - tp1).count();
   if (out) memcpy(out, c->h_prof_out, b_out);
   return MLP_OK;
 }
