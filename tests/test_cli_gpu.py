@@ -89,3 +89,19 @@ def test_real_families(name):
         assert r.returncode == 0 and r.stderr == '', (tag, r.stderr)
         with open(os.path.join(REAL, f'{name}.{tag}.out')) as fh:
             assert r.stdout == fh.read(), (name, tag)
+
+
+EDGE = os.path.join(GOLDEN, 'edge')
+_EDGE = sorted(f[:-3] for f in os.listdir(EDGE) if f.endswith('.fa')) if os.path.isdir(EDGE) else []
+
+
+@pytest.mark.parametrize('name', _EDGE)
+def test_edge_families(name):
+    """Two sequences, single residues, identical sequences, lower case and
+    X/B/Z, CRLF line ends (tests/golden/gen_edge.py)."""
+    fa = os.path.join(EDGE, f'{name}.fa')
+    for tag, cmd in (('G', [BIN, '-G', fa]), ('p_0', [BIN, '-p', '0', fa]), ('qp', [QP_BIN, fa])):
+        r = subprocess.run(cmd, capture_output=True, timeout=120)  # bytes: CR stays CR
+        assert r.returncode == 0 and r.stderr == b'', (tag, r.stderr)
+        with open(os.path.join(EDGE, f'{name}.{tag}.out'), 'rb') as fh:
+            assert r.stdout == fh.read(), (name, tag)

@@ -1,4 +1,4 @@
 set -e -o pipefail
-O=gpurun_out/r01fin; mkdir -p $O
-timeout -k 10 500 python -u bench.py > $O/bench_plain.log 2>&1
-bash tools/prof_bench.sh r01fin_prof
+O=gpurun_out/r01e; mkdir -p $O
+timeout -k 10 300 python -u -m pytest tests/test_cli_gpu.py -m gpu -v --timeout 120 --timeout-method thread -k edge > $O/pytest.log 2>&1 || true
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
