@@ -1,0 +1,68 @@
+"""Parity sweep on the GPU box: both drop-in CLIs over every family in
+tests/golden/sweep.json.xz (the reference's own benchmark families with the
+outputs of the reference CLIs built from source, tools/gen_sweep.py),
+compared byte for byte.  Runs `workers` CLI processes at a time (8 GB batch
+scratch each) and writes a summary and any mismatches to OUT.
+    python tools/parity_sweep.py OUT [workers]
+"""
+import json
+import lzma
+import os
+import subprocess
+import sys
+import tempfile
+import time
+from concurrent.futures import ThreadPoolExecutor
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CP = os.path.join(ROOT, 'mlprobs_amd', 'cli', 'c_p_np_aln')
+QP = os.path.join(ROOT, 'mlprobs_amd', 'cli', 'quickprobs')
+
+
+def main():
+    out = sys.argv[1]
+    workers = int(sys.argv[2]) if len(sys.argv) > 2 else 8
+    with lzma.open(os.path.join(ROOT, 'tests', 'golden', 'sweep.json.xz'), 'rt') as fh:
+        fams = json.load(fh)
+    env = dict(os.environ, MLP_SCRATCH_GB='8')
+    td = tempfile.mkdtemp()
+    jobs = []
+    for name, e in sorted(fams.items()):
+        fa = os.path.join(td, name.replace('/', '_') + '.fa')
+        with open(fa, 'wb') as fh:
+            fh.write(e['fa'].encode('latin-1'))
+        for tag, cmd in (('G', [CP, '-G', fa]), ('p_0', [CP, '-p', '0', fa]), ('qp', [QP, fa])):
+            if tag in e:
+                jobs.append((name, tag, cmd, e[tag]))
+
+    def run(job):
+        name, tag, cmd, (rc, ref) = job
+        r = subprocess.run(cmd, capture_output=True, timeout=600, env=env)
+        got = r.stdout.decode('latin-1')
+        ok = (r.returncode == 0) == (rc == 0) and (rc != 0 or got == ref)
+        return name, tag, ok, r.returncode, rc
+
+    t0 = time.time()
+    res = []
+    with ThreadPoolExecutor(workers) as ex:
+        for i, x in enumerate(ex.map(run, jobs)):
+            res.append(x)
+            if i % 200 == 0:
+                print(f'{i}/{len(jobs)} {time.time() - t0:.0f} s', flush=True)
+    bad = [x for x in res if not x[2]]
+    by = {}
+    for name, tag, ok, _, _ in res:
+        s = by.setdefault(tag, [0, 0])
+        s[0] += ok
+        s[1] += 1
+    with open(out, 'w') as fh:
+        fh.write(f'families {len(fams)}, runs {len(res)}, {time.time() - t0:.0f} s\n')
+        for tag, (ok, n) in sorted(by.items()):
+            fh.write(f'{tag}: {ok}/{n} byte-identical (or both failing)\n')
+        for name, tag, ok, rc, rrc in bad:
+            fh.write(f'MISMATCH {name} {tag} rc {rc} (reference {rrc})\n')
+    print(open(out).read())
+
+
+if __name__ == '__main__':
+    main()
