@@ -37,7 +37,13 @@ static inline dim3 wave_grid(int64_t n) {
 // wave in parallel.  The candidate list is a superset of the elements that
 // change acc: LOG_ADD(acc, x) for acc - x >= 7.5 returns acc exactly, so
 // folding every listed element reproduces the reference's serial chain.
-constexpr int kTotPairs = 8;   // pairs per wave
+#ifndef MLP_TOT_PAIRS
+#define MLP_TOT_PAIRS 8
+#endif
+constexpr int kTotPairs = MLP_TOT_PAIRS;   // pairs per wave
+constexpr int kTotLP = 64 / kTotPairs;      // lanes per pair
+constexpr int kTotEL = 64 / kTotLP;         // elements per lane per 64-element chunk (float4 pieces: >= 4)
+static_assert(kTotEL >= 4 && kTotEL % 4 == 0, "MLP_TOT_PAIRS must be 4, 8 or 16");
 __global__ __launch_bounds__(256) void k_local_totals_multi(SeqSet sq, PairMeta pm, PairRec* __restrict__ rec,
                                                             Scratch sc, int64_t npairs) {
   __shared__ float4 lk[kLookupRows];
@@ -46,7 +52,7 @@ __global__ __launch_bounds__(256) void k_local_totals_multi(SeqSet sq, PairMeta 
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
-  const int g = lane >> 3, sub = lane & 7;
+  const int g = lane / kTotLP, sub = lane % kTotLP;
   const int64_t p = ((int64_t)blockIdx.x * kWavesPerBlock + w) * kTotPairs + g;
   int64_t ne = 0, base = 0;
   if (p < npairs) {
@@ -55,16 +61,16 @@ __global__ __launch_bounds__(256) void k_local_totals_multi(SeqSet sq, PairMeta 
     base = pm.rm_off[p];
   }
   int64_t emax = ne;
-  for (int off = 32; off >= 8; off >>= 1) emax = max(emax, (int64_t)__shfl_xor(emax, off));
+  for (int off = 32; off >= kTotLP; off >>= 1) emax = max(emax, (int64_t)__shfl_xor(emax, off));
   const float* __restrict__ cf = sc.chf + base;
   const float* __restrict__ cb = sc.chb + base;
   // chain c = 2g (forward) / 2g+1 (backward) is folded on lane c
   float acc = LZ;
-  float nf[8], nb[8];
+  float nf[kTotEL], nb[kTotEL];
   auto load = [&](int64_t e0, float* f, float* b) {
-    const int64_t e = e0 + sub * 8;   // ne is a multiple of 4: float4 pieces are all-in or all-out
+    const int64_t e = e0 + sub * kTotEL;   // ne is a multiple of 4: float4 pieces are all-in or all-out
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < kTotEL / 4; ++h) {
       float4 vf = make_float4(LZ, LZ, LZ, LZ), vb = vf;
       if (e + 4 * h < ne) {
         vf = *reinterpret_cast<const float4*>(cf + e + 4 * h);
@@ -75,25 +81,25 @@ __global__ __launch_bounds__(256) void k_local_totals_multi(SeqSet sq, PairMeta 
     }
   };
   // two chunks in flight: HBM latency exceeds one chunk's fold
-  float nf2[8], nb2[8];
+  float nf2[kTotEL], nb2[kTotEL];
   load(0, nf, nb);
   load(64, nf2, nb2);
-  // exclusive prefix of a per-lane count over the 8 lanes of its group
+  // exclusive prefix of a per-lane count over the kTotLP lanes of its group
   auto group_scan = [&](int c) {
     int x = c;
 #pragma unroll
-    for (int d = 1; d < 8; d <<= 1) {
-      const int y = __shfl_up(x, d, 8);
+    for (int d = 1; d < kTotLP; d <<= 1) {
+      const int y = __shfl_up(x, d, kTotLP);
       x += (sub >= d) ? y : 0;
     }
     return x - c;
   };
   auto chunk = [&](int64_t e0, float* xf, float* xb) {
     const float af = __shfl(acc, 2 * g), ab = __shfl(acc, 2 * g + 1);
-    const int64_t e = e0 + sub * 8;
+    const int64_t e = e0 + sub * kTotEL;
     unsigned ff = 0, fb = 0;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
+    for (int k = 0; k < kTotEL; ++k) {
       const bool in = e + k < ne;
       ff |= (in && !(af - xf[k] >= 7.5f)) ? (1u << k) : 0u;
       fb |= (in && !(ab - xb[k] >= 7.5f)) ? (1u << k) : 0u;
@@ -103,17 +109,17 @@ __global__ __launch_bounds__(256) void k_local_totals_multi(SeqSet sq, PairMeta 
     float* lf = list[w][2 * g];
     float* lb = list[w][2 * g + 1];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
+    for (int k = 0; k < kTotEL; ++k) {
       if (ff & (1u << k)) lf[pf++] = xf[k];
       if (fb & (1u << k)) lb[pb++] = xb[k];
     }
     // totals per chain: last lane of the group holds the inclusive sums
-    const int tot_f = __shfl(pf, g * 8 + 7), tot_b = __shfl(pb, g * 8 + 7);
+    const int tot_f = __shfl(pf, g * kTotLP + kTotLP - 1), tot_b = __shfl(pb, g * kTotLP + kTotLP - 1);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     // chain `lane` (< 16) folds its list; count from its group's last lane
-    const int cnt_f = __shfl(tot_f, (lane >> 1) * 8), cnt_b = __shfl(tot_b, (lane >> 1) * 8);
+    const int cnt_f = __shfl(tot_f, (lane >> 1) * kTotLP), cnt_b = __shfl(tot_b, (lane >> 1) * kTotLP);
     const int cnt = lane < 2 * kTotPairs ? ((lane & 1) ? cnt_b : cnt_f) : 0;
     const float* my = list[w][lane & (2 * kTotPairs - 1)];
     for (int k = 0; __any(k < cnt); ++k) {
@@ -122,14 +128,14 @@ __global__ __launch_bounds__(256) void k_local_totals_multi(SeqSet sq, PairMeta 
     __builtin_amdgcn_wave_barrier();
   };
   for (int64_t e0 = 0; e0 < emax; e0 += 128) {
-    float xf[8], xb[8];
+    float xf[kTotEL], xb[kTotEL];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) { xf[k] = nf[k]; xb[k] = nb[k]; }
+    for (int k = 0; k < kTotEL; ++k) { xf[k] = nf[k]; xb[k] = nb[k]; }
     if (e0 + 128 < emax) load(e0 + 128, nf, nb);
     chunk(e0, xf, xb);
     if (e0 + 64 >= emax) break;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) { xf[k] = nf2[k]; xb[k] = nb2[k]; }
+    for (int k = 0; k < kTotEL; ++k) { xf[k] = nf2[k]; xb[k] = nb2[k]; }
     if (e0 + 192 < emax) load(e0 + 192, nf2, nb2);
     chunk(e0 + 64, xf, xb);
   }

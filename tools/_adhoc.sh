@@ -1,7 +1,10 @@
 set -e -o pipefail
-O=gpurun_out/r01cr3; mkdir -p $O
+O=gpurun_out/r01tp; mkdir -p $O
 for rep in 1 2; do
-  MLP_CHAIN_ROWS=1282 timeout -k 10 300 python -u bench.py --no-e2e --no-qp --relax 0 --no-cpu --steps 5 > $O/old$rep.log 2>&1
-  timeout -k 10 300 python -u bench.py --no-e2e --no-qp --relax 0 --no-cpu --steps 5 > $O/new$rep.log 2>&1
+for v in base tp4 tp16; do
+  if [ $v = base ]; then unset MLP_LIB_VARIANT; else export MLP_LIB_VARIANT=$v; fi
+  timeout -k 10 300 python -u bench.py --no-e2e --no-qp --relax 0 --no-cpu --steps 5 > $O/$v$rep.log 2>&1
 done
-timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1
+done
+MLP_LIB_VARIANT=tp4 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest4.log 2>&1
+MLP_LIB_VARIANT=tp16 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest16.log 2>&1
