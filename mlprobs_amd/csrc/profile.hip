@@ -7,18 +7,32 @@
 // (i in profile A, j in profile B) where sequence i has residue ii in column r
 // and j has jj in column c, in the reference's order: i, then j, then the row
 // ii of block (i, j), then its entries.  One wave owns one dense row r and
-// keeps it in LDS; for a run of up to 64 j's it loads the rows' extents (one
-// lane per j), computes the products of all their entries in parallel into an
-// LDS stage, and then adds the stage into the row one j after another.  The
-// entries of one row hit distinct columns, so each j's adds are one parallel
-// step, and a wave's LDS operations retire in order: every cell sees its
-// terms in the reference's sequence, with the reference's float operations
+// keeps it in LDS; for a run of up to 64 consecutive pairs (i, j) it loads
+// the rows' extents (one lane per pair, so a small profile B still fills the
+// wave), computes the products of all their entries in parallel into an LDS
+// stage, and then adds the stage into the row one pair after another.  The
+// entries of one row hit distinct columns, so each pair's adds are one
+// parallel step, and a wave's LDS operations retire in order: every cell
+// sees its terms in the reference's sequence, with the reference's float
+// operations
 // (w * v, then +=).
+//
+// Sequences i with a gap in column r contribute nothing; each wave compacts
+// them away 64 at a time before forming its runs (most of a long alignment's
+// cells are gaps).  A short profile A leaves most of the chip idle (a wave
+// per column), so gridDim.y waves can then share a row: wave k owns the
+// column range [c0, c1) of row r, walks the same entries and adds only the
+// ones landing in its range.  Each cell still has one owner and its terms in
+// the same order, so the split changes no bit of the result.
+#include <stdlib.h>
+
+#include <algorithm>
+
 #include "mlp_kernels.h"
 
 namespace mlp {
 
-constexpr int kProfStage = 2048;  // staged entries per run of j's
+constexpr int kProfStage = 1024;  // staged entries per run of pairs
 
 // LDS writes of some lanes made visible to the other lanes of the wave
 __device__ __forceinline__ void wave_sync() {
@@ -27,38 +41,70 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-static __host__ __device__ inline size_t prof_acc_bytes(int L2) { return ((size_t)(L2 + 1) * 4 + 15) & ~(size_t)15; }
-size_t profile_lds(int L2) { return prof_acc_bytes(L2) + (size_t)kProfStage * 8 + 3 * 65 * 8; }
+// acc += v as one ds_add_f32 (IEEE round-to-nearest add, like acc + v)
+__device__ __forceinline__ void lds_add(float* a, float v) {
+  __hip_atomic_fetch_add(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
+
+static __host__ __device__ inline size_t prof_acc_bytes(int cols) { return ((size_t)cols * 4 + 15) & ~(size_t)15; }
+static size_t profile_lds_cols(int cols) { return prof_acc_bytes(cols) + (size_t)kProfStage * 9 + 7 * 65 * 8; }
+size_t profile_lds(int L2) { return profile_lds_cols(L2 + 1); }
 
 __global__ __launch_bounds__(64) void k_profile_post(ProfileArgs A) {
+  const int lane = threadIdx.x;
+  const int r = blockIdx.x + 1;
+  const int W2 = A.L2 + 1;
+  const int cw = (W2 + gridDim.y - 1) / gridDim.y;
+  const int c0 = blockIdx.y * cw, c1 = min(W2, c0 + cw);
   extern __shared__ __align__(16) uint8_t lds[];
-  float* acc = (float*)lds;                                     // L2 + 1
-  int32_t* st_c = (int32_t*)(lds + prof_acc_bytes(A.L2));      // staged dense columns
+  float* acc = (float*)lds;                                     // columns c0 .. c1 - 1
+  int32_t* st_c = (int32_t*)(lds + prof_acc_bytes(cw));         // staged dense columns
   float* st_p = (float*)(st_c + kProfStage);                    // staged products
   int64_t* l_e = (int64_t*)(st_p + kProfStage);                 // per lane: first entry (absolute)
   int32_t* l_st = (int32_t*)(l_e + 65);                         // per lane: stage start (prefix), [64] = total
   int32_t* l_tr = l_st + 65;                                    // per lane: transposed block
-  const int lane = threadIdx.x;
-  const int r = blockIdx.x + 1;
-  const int W2 = A.L2 + 1;
-  for (int c = lane; c < W2; c += 64) acc[c] = 0.f;
-  for (int i = 0; i < A.n1; ++i) {
-    const int ii = __builtin_amdgcn_readfirstlane(A.inv1[(int64_t)i * (A.L1 + 1) + r]);
-    if (ii == 0) continue;  // sequence i has a gap in column r
-    for (int j0 = 0; j0 < A.n2;) {
-      // ---- extents of the rows ii of blocks (i, j0 + lane)
-      const int j = j0 + lane;
-      int cnt = 0;
+  int32_t* l_j = l_tr + 65;                                     // per lane: sequence j of profile B
+  float* l_w = (float*)(l_j + 65);                              // per lane: pair weight
+  int32_t* l_i = (int32_t*)(l_w + 65);                          // sequences i with a residue in column r
+  int32_t* l_ii = l_i + 65;                                     // ... and that residue
+  uint8_t* st_l = (uint8_t*)(l_ii + 65);                        // staged entry -> its lane
+  for (int c = c0 + lane; c < c1; c += 64) acc[c - c0] = 0.f;
+  for (int i0 = 0; i0 < A.n1; i0 += 64) {
+    // the next (up to) 64 sequences i, compacted to those with a residue in
+    // column r (the others contribute nothing)
+    {
+      const int i = i0 + lane;
+      const int ii = i < A.n1 ? A.inv1[(int64_t)i * (A.L1 + 1) + r] : 0;
+      const unsigned long long m = __ballot(ii != 0);
+      if (ii != 0) {
+        const int pos = __popcll(m & ((1ull << lane) - 1));
+        l_i[pos] = i;
+        l_ii[pos] = ii;
+      }
+      if (lane == 0) l_i[64] = __popcll(m);
+    }
+    wave_sync();
+    const int64_t Q = (int64_t)l_i[64] * A.n2;
+    // runs of 64 consecutive pairs (i, j) of the compacted list, i-major:
+    // the reference's order
+    for (int64_t q0 = 0; q0 < Q;) {
+      // ---- extents of the rows ii of blocks (i, j), one lane per pair
+      const int64_t q = q0 + lane;
+      int cnt = 0, jl = 0, tr = 0;
       int64_t e = 0;
-      int tr = 0;
-      if (j < A.n2) {
-        const int64_t q = (int64_t)i * A.n2 + j;
-        const int64_t rb = A.rpb[q];
+      float wv = 0.f;
+      if (q < Q) {
+        const int k = (int)(q / A.n2);
+        jl = (int)(q - (int64_t)k * A.n2);
+        const int ii = l_ii[k];
+        const int64_t pair = (int64_t)l_i[k] * A.n2 + jl;
+        const int64_t rb = A.rpb[pair];
         tr = rb < 0;
         const int32_t* rp = tr ? A.trowptr + (~rb) : A.rowptr + rb;
         const int b = rp[ii];
         cnt = rp[ii + 1] - b;
-        e = A.eb[q] + b;
+        e = A.eb[pair] + b;
+        wv = A.w[pair];
       }
       // inclusive prefix of cnt over the lanes
       int x = cnt;
@@ -70,66 +116,77 @@ __global__ __launch_bounds__(64) void k_profile_post(ProfileArgs A) {
       // lanes whose rows fit the stage (a prefix of the run; the first lane
       // always takes part, a longer row is added in pieces below)
       const bool fits = x <= kProfStage || lane == 0;
-      const unsigned long long fitm = __ballot(fits && j < A.n2);
+      const unsigned long long fitm = __ballot(fits && q < Q);
       const int nl = __popcll(~fitm) ? __builtin_ctzll(~fitm) : 64;
       l_e[lane] = e;
       l_st[lane] = start;
       l_tr[lane] = tr;
+      l_j[lane] = jl;
+      l_w[lane] = wv;
       if (lane == 63) l_st[64] = x;
       wave_sync();
       const int total_staged = l_st[nl];  // entries of lanes 0 .. nl-1
       const bool big = nl == 1 && total_staged > kProfStage;
       if (!big) {
+        // ---- which pair each staged entry belongs to (lane-serial fill)
+        if (lane < nl)
+          for (int k = 0; k < cnt; ++k) st_l[start + k] = (uint8_t)lane;
+        wave_sync();
         // ---- products of every staged entry, in parallel
         for (int t = lane; t < total_staged; t += 64) {
-          int lo = 0, hi = nl - 1;  // last lane l with l_st[l] <= t
-          while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (l_st[mid] <= t) lo = mid; else hi = mid - 1;
-          }
+          const int lo = st_l[t];
           const int64_t ent = l_e[lo] + (t - l_st[lo]);
           const int col = l_tr[lo] ? A.tcols[ent] : A.cols[ent];
           const float v = l_tr[lo] ? A.tvals[ent] : A.vals[ent];
-          const int jj = j0 + lo;
-          st_c[t] = A.map2[A.map2_off[jj] + col];
-          st_p[t] = A.w[(int64_t)i * A.n2 + jj] * v;  // posterior[id] += w * v
+          const int c = A.map2[A.map2_off[l_j[lo]] + col];
+          st_c[t] = c;
+          if (c >= c0 && c < c1) st_p[t] = l_w[lo] * v;  // posterior[id] += w * v
         }
         wave_sync();
-        // ---- add them j by j (a wave's LDS operations retire in order)
+        // ---- add them pair by pair: LDS float adds without return, which a
+        // wave's LDS pipe applies in issue order (one pair's entries hit
+        // distinct columns; a later pair's add to the same cell lands after)
         for (int l = 0; l < nl; ++l) {
           const int s0 = l_st[l], s1 = l_st[l + 1];
           for (int t = s0 + lane; t < s1; t += 64) {
             const int c = st_c[t];
-            acc[c] = acc[c] + st_p[t];
+            if (c >= c0 && c < c1) lds_add(&acc[c - c0], st_p[t]);
           }
         }
       } else {
         // ---- one row longer than the stage: add it piecewise, in order
         const int64_t e0 = l_e[0];
         const int n = total_staged, tr0 = l_tr[0];
-        const float w = A.w[(int64_t)i * A.n2 + j0];
-        const int32_t* m2 = A.map2 + A.map2_off[j0];
+        const float w = l_w[0];
+        const int32_t* m2 = A.map2 + A.map2_off[l_j[0]];
         for (int t = lane; t < n; t += 64) {
           const int col = tr0 ? A.tcols[e0 + t] : A.cols[e0 + t];
           const float v = tr0 ? A.tvals[e0 + t] : A.vals[e0 + t];
           const int c = m2[col];
-          acc[c] = acc[c] + w * v;
+          if (c >= c0 && c < c1) acc[c - c0] = acc[c - c0] + w * v;
         }
       }
       wave_sync();
-      j0 += nl;
+      q0 += nl;
     }
   }
   wave_sync();
   float* o = A.out + (int64_t)r * W2;
-  for (int c = lane; c < W2; c += 64) o[c] = acc[c];
+  for (int c = c0 + lane; c < c1; c += 64) o[c] = acc[c - c0];
 }
 
 hipError_t launch_profile_posterior(const ProfileArgs& a, hipStream_t st) {
   if (a.L1 <= 0) return hipSuccess;
-  const size_t lds = profile_lds(a.L2);
-  hipFuncSetAttribute((const void*)k_profile_post, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL(k_profile_post, dim3((unsigned)a.L1), dim3(64), lds, st, a);
+  // column ranges per row: only rows too few to give every CU a wave are
+  // split (at C3 refinement, one range per row measured fastest: 376 ms of
+  // profile kernels against 393 / 466 ms for 2 / 4 ranges); ranges of at
+  // least 64 columns (MLP_PROFILE_SPLIT overrides, for measurement)
+  int k = (256 + a.L1 - 1) / a.L1;
+  if (const char* e = getenv("MLP_PROFILE_SPLIT")) k = atoi(e);
+  k = std::max(1, std::min(k, std::min(16, (a.L2 + 1 + 63) / 64)));
+  const size_t lds = profile_lds_cols((a.L2 + 1 + k - 1) / k);
+  (void)hipFuncSetAttribute((const void*)k_profile_post, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(k_profile_post, dim3((unsigned)a.L1, (unsigned)k), dim3(64), lds, st, a);
   return hipGetLastError();
 }
 
