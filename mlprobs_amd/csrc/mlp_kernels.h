@@ -320,7 +320,11 @@ struct ProfileArgs {
   int n1, n2, L1, L2;        // profile sizes (sequences, columns)
   const int64_t* rpb;        // n1 x n2: row_ptr base of block (i, j); ~base: transposed block
   const int64_t* eb;         // n1 x n2: entry base of block (i, j)
-  const int32_t* inv1;       // n1 x (L1 + 1): residue of sequence i in column r, 0 = gap
+  int32_t* inv1;             // n1 x (L1 + 1): residue of sequence i in column r, 0 = gap
+                             // (zeroed by the caller, filled by launch_profile_posterior)
+  const int32_t* map1;       // per sequence i of A: column of its residue k (k = 1..len)
+  const int64_t* map1_off;   // per i: offset of its map (k = 0 at map1_off[i])
+  int64_t map1_len;          // entries of map1
   const int32_t* map2;       // per sequence j of B: column of its residue k (k = 1..len)
   const int64_t* map2_off;   // per j: offset of its map (k = 0 at map2_off[j])
   const float* w;            // n1 x n2: (float)(w_i w_j / sum)

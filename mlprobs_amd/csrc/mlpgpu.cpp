@@ -945,15 +945,17 @@ int mlp_profile_posterior(mlp_ctx* c, const float* seq_weights, int n1, const in
       eb[q] = c->ent_off[p];
     }
   }
-  std::vector<int32_t> inv1((size_t)n1 * (L1 + 1), 0);
-  for (int i = 0, o = 0; i < n1; i++) {
+  // the column -> residue map of A is built on the device from A's maps
+  std::vector<int64_t> moff1(n1);
+  int64_t m1len = 0;
+  for (int i = 0; i < n1; i++) {
     const int len = c->lens[labels1[i]];
+    moff1[i] = m1len;
     for (int k = 1; k <= len; k++) {
-      const int col = map1[o + k];
+      const int col = map1[m1len + k];
       if (col < 1 || col > L1) return MLP_ERR_ARG;
-      inv1[(size_t)i * (L1 + 1) + col] = k;
     }
-    o += len + 1;
+    m1len += len + 1;
   }
   int64_t m2len = 0;
   for (int j = 0; j < n2; j++) {
@@ -965,10 +967,11 @@ int mlp_profile_posterior(mlp_ctx* c, const float* seq_weights, int n1, const in
   // one pinned staging buffer for every upload (a single copy) and a pinned
   // result buffer: pageable copies cost more than the kernel here
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-  const size_t b_rpb = np * 8, b_eb = np * 8, b_w = np * 4, b_inv = inv1.size() * 4, b_m2 = m2len * 4,
-               b_mo = n2 * 8, b_out = (size_t)(L1 + 1) * (L2 + 1) * 4;
-  const size_t o_rpb = 0, o_eb = o_rpb + al(b_rpb), o_w = o_eb + al(b_eb), o_inv = o_w + al(b_w),
-               o_m2 = o_inv + al(b_inv), o_mo = o_m2 + al(b_m2), in_bytes = o_mo + al(b_mo);
+  const size_t b_rpb = np * 8, b_eb = np * 8, b_w = np * 4, b_m1 = m1len * 4, b_mo1 = n1 * 8, b_m2 = m2len * 4,
+               b_mo = n2 * 8, b_inv = (size_t)n1 * (L1 + 1) * 4, b_out = (size_t)(L1 + 1) * (L2 + 1) * 4;
+  const size_t o_rpb = 0, o_eb = o_rpb + al(b_rpb), o_w = o_eb + al(b_eb), o_m1 = o_w + al(b_w),
+               o_mo1 = o_m1 + al(b_m1), o_m2 = o_mo1 + al(b_mo1), o_mo = o_m2 + al(b_m2),
+               in_bytes = o_mo + al(b_mo);
   if (c->h_prof_in_bytes < in_bytes) {
     if (c->h_prof_in) hipHostFree(c->h_prof_in);
     c->h_prof_in = nullptr;
@@ -987,21 +990,25 @@ int mlp_profile_posterior(mlp_ctx* c, const float* seq_weights, int n1, const in
   memcpy(hin + o_rpb, rpb.data(), b_rpb);
   memcpy(hin + o_eb, eb.data(), b_eb);
   memcpy(hin + o_w, w.data(), b_w);
-  memcpy(hin + o_inv, inv1.data(), b_inv);
+  memcpy(hin + o_m1, map1, b_m1);
+  memcpy(hin + o_mo1, moff1.data(), b_mo1);
   memcpy(hin + o_m2, map2, b_m2);
   memcpy(hin + o_mo, moff.data(), b_mo);
   const auto tp1 = std::chrono::steady_clock::now();
   c->prof_t[0] += std::chrono::duration<double>(tp1 - tp0).count();
-  if ((rc = ensure(c, c->r_profile, in_bytes + al(b_out)))) return rc;
+  if ((rc = ensure(c, c->r_profile, in_bytes + al(b_inv) + al(b_out)))) return rc;
   char* base = (char*)c->r_profile.p;
   HIPCHK(c, hipMemcpyAsync(base, hin, in_bytes, hipMemcpyHostToDevice, c->stream));
   int64_t* d_rpb = (int64_t*)(base + o_rpb);
   int64_t* d_eb = (int64_t*)(base + o_eb);
   float* d_w = (float*)(base + o_w);
-  int32_t* d_inv = (int32_t*)(base + o_inv);
+  int32_t* d_m1 = (int32_t*)(base + o_m1);
+  int64_t* d_mo1 = (int64_t*)(base + o_mo1);
+  int32_t* d_inv = (int32_t*)(base + in_bytes);
   int32_t* d_m2 = (int32_t*)(base + o_m2);
   int64_t* d_mo = (int64_t*)(base + o_mo);
-  float* d_out = (float*)(base + in_bytes);
+  float* d_out = (float*)(base + in_bytes + al(b_inv));
+  HIPCHK(c, hipMemsetAsync(d_inv, 0, b_inv, c->stream));
   HIPCHK(c, hipMemsetAsync(d_out, 0, (size_t)(L2 + 1) * 4, c->stream));  // row 0
   ProfileArgs pa;
   pa.n = c->n;
@@ -1018,6 +1025,9 @@ int mlp_profile_posterior(mlp_ctx* c, const float* seq_weights, int n1, const in
   pa.rpb = d_rpb;
   pa.eb = d_eb;
   pa.inv1 = d_inv;
+  pa.map1 = d_m1;
+  pa.map1_off = d_mo1;
+  pa.map1_len = m1len;
   pa.map2 = d_m2;
   pa.map2_off = d_mo;
   pa.w = d_w;

@@ -175,8 +175,23 @@ __global__ __launch_bounds__(64) void k_profile_post(ProfileArgs A) {
   for (int c = c0 + lane; c < c1; c += 64) o[c] = acc[c - c0];
 }
 
+// inv1[i][map1_i[k]] = k: the column -> residue map of profile A, one
+// thread per map entry (k = 0 entries skipped)
+__global__ __launch_bounds__(256) void k_profile_inv(ProfileArgs A) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= A.map1_len) return;
+  int lo = 0, hi = A.n1 - 1;  // the sequence whose map holds entry t
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (A.map1_off[mid] <= t) lo = mid; else hi = mid - 1;
+  }
+  const int k = (int)(t - A.map1_off[lo]);
+  if (k > 0) A.inv1[(int64_t)lo * (A.L1 + 1) + A.map1[t]] = k;
+}
+
 hipError_t launch_profile_posterior(const ProfileArgs& a, hipStream_t st) {
   if (a.L1 <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_profile_inv, dim3((unsigned)((a.map1_len + 255) / 256)), dim3(256), 0, st, a);
   // column ranges per row: only rows too few to give every CU a wave are
   // split (at C3 refinement, one range per row measured fastest: 376 ms of
   // profile kernels against 393 / 466 ms for 2 / 4 ranges); ranges of at
