@@ -63,7 +63,7 @@ static bool get_float(const char* s, float* v) {   // MSA::GetFloat (CPNP/MSA.cp
 static void stage(const char* name) {
   static const bool on = getenv("MLP_CLI_TIMES") != nullptr;
   static auto t0 = std::chrono::steady_clock::now();
-  if (!on) return;
+  if (!on || !name) return;
   const auto t1 = std::chrono::steady_clock::now();
   std::cerr << "[stage] " << name << " " << std::chrono::duration<double>(t1 - t0).count() << " s" << std::endl;
   t0 = t1;
@@ -79,6 +79,7 @@ static void check(mlp_ctx* ctx, int rc, const char* what) {
 }
 
 int main(int argc, char** argv) {
+  stage(nullptr);  // start the stage clock
   if (argc < 2) {
     usage();
     return 1;
@@ -154,7 +155,9 @@ int main(int argc, char** argv) {
   const int n = (int)seqs.size();
 
   mlp_ctx* ctx = nullptr;
+  stage("parse");
   check(nullptr, mlp_ctx_create(0, &ctx), "device");
+  stage("device init");
   // one family per process: a moderate batch scratch.  A fresh process's
   // allocation waits for the driver to clear memory the previous process
   // released; back to back at C3 (512 x 400) the posterior stage took 1.09 s

@@ -34,7 +34,7 @@
 static void stage(const char* name) {  // MLP_CLI_TIMES=1: stage times on stderr
   static const bool on = getenv("MLP_CLI_TIMES") != nullptr;
   static auto t0 = std::chrono::steady_clock::now();
-  if (!on) return;
+  if (!on || !name) return;
   const auto t1 = std::chrono::steady_clock::now();
   std::cerr << "[stage] " << name << " " << std::chrono::duration<double>(t1 - t0).count() << " s" << std::endl;
   t0 = t1;
@@ -74,6 +74,7 @@ static bool parse_int(const std::string& s, long long* v) {
 }
 
 int main(int argc, char** argv) {
+  stage(nullptr);  // start the stage clock
   std::vector<std::string> args(argv + 1, argv + argc), rest;
   std::string outname;
   qph::Options opt;
@@ -130,7 +131,9 @@ int main(int argc, char** argv) {
       aln.push_back(seqs[0]);
     } else {
       mlp_ctx* ctx = nullptr;
+      stage("parse");
       check(nullptr, mlp_ctx_create(0, &ctx), "device");
+      stage("device init");
       // one family per process: a 16 GB batch scratch.  A fresh process's
       // allocation waits for the driver to clear memory the previous process
       // released: measured at C3 (512 x 400) 0.82 s posteriors at 16 GB vs

@@ -635,14 +635,22 @@ static int64_t relax_impl(int qp, const float *weights, float selfweight, float 
                           int N, const int32_t *lens, const int64_t *row_off, const int64_t *ent_off,
                           const int32_t *in_rp, const int32_t *in_cols, const float *in_vals,
                           int32_t *out_rp, int64_t *out_ent_off, int32_t *out_cols, float *out_vals,
-                          int64_t max_out);
+                          int64_t max_out, const uint8_t *select);
 
 int64_t orc_relax(int N, const int32_t *lens, const int64_t *row_off, const int64_t *ent_off,
                   const int32_t *in_rp, const int32_t *in_cols, const float *in_vals,
                   int32_t *out_rp, int64_t *out_ent_off, int32_t *out_cols, float *out_vals,
                   int64_t max_out) {
   return relax_impl(0, NULL, 0, 0, NULL, 200.0f, N, lens, row_off, ent_off, in_rp, in_cols, in_vals, out_rp, out_ent_off,
-                    out_cols, out_vals, max_out);
+                    out_cols, out_vals, max_out, NULL);
+}
+
+int64_t orc_relax_subset(int N, const int32_t *lens, const int64_t *row_off, const int64_t *ent_off,
+                         const int32_t *in_rp, const int32_t *in_cols, const float *in_vals,
+                         int32_t *out_rp, int64_t *out_ent_off, int32_t *out_cols, float *out_vals,
+                         int64_t max_out, const uint8_t *select) {
+  return relax_impl(0, NULL, 0, 0, NULL, 200.0f, N, lens, row_off, ent_off, in_rp, in_cols, in_vals, out_rp, out_ent_off,
+                    out_cols, out_vals, max_out, select);
 }
 
 int64_t orc_qp_relax(const float *weights, float selfweight, float cutoff,
@@ -651,7 +659,7 @@ int64_t orc_qp_relax(const float *weights, float selfweight, float cutoff,
                      int32_t *out_rp, int64_t *out_ent_off, int32_t *out_cols, float *out_vals,
                      int64_t max_out) {
   return relax_impl(1, weights, selfweight, cutoff, NULL, 200.0f, N, lens, row_off, ent_off, in_rp, in_cols, in_vals,
-                    out_rp, out_ent_off, out_cols, out_vals, max_out);
+                    out_rp, out_ent_off, out_cols, out_vals, max_out, NULL);
 }
 
 int64_t orc_qp_relax_sel(const float *weights, float selfweight, float cutoff, const float *seldist,
@@ -660,7 +668,7 @@ int64_t orc_qp_relax_sel(const float *weights, float selfweight, float cutoff, c
                          const float *in_vals, int32_t *out_rp, int64_t *out_ent_off, int32_t *out_cols,
                          float *out_vals, int64_t max_out) {
   return relax_impl(1, weights, selfweight, cutoff, seldist, selectivity, N, lens, row_off, ent_off, in_rp, in_cols,
-                    in_vals, out_rp, out_ent_off, out_cols, out_vals, max_out);
+                    in_vals, out_rp, out_ent_off, out_cols, out_vals, max_out, NULL);
 }
 
 /* The Deterministic selectivity filter (ConsistencyStage.cpp:35-47, 171-186):
@@ -697,7 +705,7 @@ static int64_t relax_impl(int qp, const float *weights, float selfweight, float 
                           int N, const int32_t *lens, const int64_t *row_off, const int64_t *ent_off,
                           const int32_t *in_rp, const int32_t *in_cols, const float *in_vals,
                           int32_t *out_rp, int64_t *out_ent_off, int32_t *out_cols, float *out_vals,
-                          int64_t max_out) {
+                          int64_t max_out, const uint8_t *select) {
   const int P = N * (N - 1) / 2;
   int64_t *cnt = calloc(P > 0 ? P : 1, sizeof(int64_t));
   float **dense = calloc(P > 0 ? P : 1, sizeof(float *));
@@ -710,6 +718,13 @@ static int64_t relax_impl(int qp, const float *weights, float selfweight, float 
     while (q >= N - 1 - i) { q -= N - 1 - i; i++; }
     int j = i + 1 + q;
     const int L1 = lens[i], L2 = lens[j], W = L2 + 1;
+    if (select && !select[p]) {  /* not requested: empty output rows */
+      int32_t *rp = out_rp + row_off[p];
+      for (int r = 0; r <= L1 + 1; r++) rp[r] = 0;
+      cnt[p] = 0;
+      dense[p] = NULL;
+      continue;
+    }
     float *post = calloc((size_t)(L1 + 1) * W, sizeof(float));
     csr_view xy = VIEW(i, j);
     for (int x = 1; x <= L1; x++)
@@ -786,6 +801,7 @@ static int64_t relax_impl(int qp, const float *weights, float selfweight, float 
     int i = 0, q = p;
     while (q >= N - 1 - i) { q -= N - 1 - i; i++; }
     int j = i + 1 + q;
+    if (!dense[p]) continue;
     if (qp)
       qp_sparsify_vals(lens[i], lens[j], dense[p], cutoff, out_rp + row_off[p], out_cols + out_ent_off[p],
                        out_vals + out_ent_off[p]);
@@ -1064,4 +1080,109 @@ int64_t orc_qp_sparsify(int L1, int L2, const float *post, int32_t *rowptr, int3
     rowptr[i + 1] = (int32_t)n;
   }
   return n;
+}
+
+/* ------------------------------------------------------------ bulk checkers
+ * The pdoAlign pair body (CPNP/MSA.cpp:939-1025: posterior by pid, MEA
+ * distance 1 - score/min(L), SparseMatrix at 0.01) for a list of pairs, with
+ * the sparse rows returned: rowptr (L_a + 2 per listed pair, pair-local
+ * values), ent_off[np + 1], cols/vals with room for max_out entries.
+ * Returns the total entries, or -1 when max_out is too small. */
+int64_t orc_pairs_csr(const orc_model *m, int N, const char *const *seqs, const int32_t *lens, int pid,
+                      const int64_t *pairs, int64_t np, int threads, float *dist_out, float *mea_out,
+                      int32_t *rowptr, int64_t *ent_off, int32_t *cols, float *vals, int64_t max_out) {
+  (void)N;
+  int32_t **pc = calloc(np > 0 ? np : 1, sizeof(int32_t *));
+  float **pv = calloc(np > 0 ? np : 1, sizeof(float *));
+  int64_t *cnt = calloc(np > 0 ? np : 1, sizeof(int64_t));
+  int64_t *roff = calloc(np + 1, sizeof(int64_t));
+  for (int64_t k = 0; k < np; k++) {
+    int a = 0;
+    int64_t q = pairs[k];
+    while (q >= N - 1 - a) { q -= N - 1 - a; a++; }
+    roff[k + 1] = roff[k] + lens[a] + 2;
+  }
+#ifdef _OPENMP
+  if (threads > 0) omp_set_num_threads(threads);
+#endif
+#pragma omp parallel for schedule(dynamic)
+  for (int64_t k = 0; k < np; k++) {
+    int a = 0;
+    int64_t q = pairs[k];
+    while (q >= N - 1 - a) { q -= N - 1 - a; a++; }
+    int b = a + 1 + (int)q;
+    int L1 = lens[a], L2 = lens[b];
+    float *post = malloc(sizeof(float) * (size_t)(L1 + 1) * (L2 + 1));
+    orc_pair_posterior(m, seqs[a], L1, seqs[b], L2, pid, post);
+    float score = orc_mea(L1, L2, post, NULL, NULL);
+    if (mea_out) mea_out[k] = score;
+    if (dist_out) dist_out[k] = 1.0f - score / (L1 < L2 ? L1 : L2);
+    int32_t *rp = rowptr + roff[k];
+    int64_t nnz = orc_sparsify(L1, L2, post, rp, NULL, NULL);
+    pc[k] = malloc(sizeof(int32_t) * (nnz ? nnz : 1));
+    pv[k] = malloc(sizeof(float) * (nnz ? nnz : 1));
+    orc_sparsify(L1, L2, post, rp, pc[k], pv[k]);
+    cnt[k] = nnz;
+    free(post);
+  }
+  int64_t total = 0;
+  for (int64_t k = 0; k < np; k++) { ent_off[k] = total; total += cnt[k]; }
+  ent_off[np] = total;
+  if (total <= max_out)
+    for (int64_t k = 0; k < np; k++) {
+      memcpy(cols + ent_off[k], pc[k], sizeof(int32_t) * cnt[k]);
+      memcpy(vals + ent_off[k], pv[k], sizeof(float) * cnt[k]);
+    }
+  for (int64_t k = 0; k < np; k++) { free(pc[k]); free(pv[k]); }
+  free(pc); free(pv); free(cnt); free(roff);
+  return total <= max_out ? total : -1;
+}
+
+/* Compare two sparse sets pair by pair under the parity rule of SURVEY.md
+ * section 8c: entries on both sides within rtol * max(|ref|, 1e-6); an entry
+ * on one side only is allowed iff its value lies within 10 * rtol of the
+ * cutoff; `exact` additionally counts every bit difference.  Pair k has L1[k]
+ * rows; its row pointers start at *_roff[k] and its entries at *_eoff[k].
+ * stats: {pairs, ref entries, our entries, common, max rel err, flips at the
+ * cutoff, violations, exact mismatches (value bits or presence)}. */
+void orc_csr_compare(int64_t np, const int32_t *L1, float rtol, float cutoff,
+                     const int64_t *r_roff, const int64_t *r_eoff, const int32_t *r_rp,
+                     const int32_t *r_cols, const float *r_vals,
+                     const int64_t *o_roff, const int64_t *o_eoff, const int32_t *o_rp,
+                     const uint16_t *o_cols, const float *o_vals, double *stats) {
+  double nref = 0, nours = 0, both = 0, worst = 0, flips = 0, bad = 0, inexact = 0;
+#pragma omp parallel for schedule(dynamic, 16) reduction(+ : nref, nours, both, flips, bad, inexact) reduction(max : worst)
+  for (int64_t k = 0; k < np; k++) {
+    const int32_t *rr = r_rp + r_roff[k], *orow = o_rp + o_roff[k];
+    const int32_t *rc = r_cols + r_eoff[k];
+    const float *rv = r_vals + r_eoff[k];
+    const uint16_t *oc = o_cols + o_eoff[k];
+    const float *ov = o_vals + o_eoff[k];
+    for (int i = 1; i <= L1[k]; i++) {
+      int a = rr[i], ae = rr[i + 1], b = orow[i], be = orow[i + 1];
+      nref += ae - a;
+      nours += be - b;
+      while (a < ae || b < be) {
+        const int ca = a < ae ? rc[a] : 1 << 30, cb = b < be ? (int)oc[b] : 1 << 30;
+        if (ca == cb) {
+          const double r = rv[a], o = ov[b];
+          const double den = fabs(r) > 1e-6 ? fabs(r) : 1e-6;
+          const double e = fabs(o - r) / den;
+          if (e > worst) worst = e;
+          if (e > rtol) bad += 1;
+          if (rv[a] != ov[b]) inexact += 1;
+          both += 1;
+          a++, b++;
+        } else {
+          const double v = ca < cb ? rv[a] : ov[b];
+          if (ca < cb) a++; else b++;
+          flips += 1;
+          inexact += 1;
+          if (fabs(v - cutoff) > 10.0 * rtol * cutoff) bad += 1;
+        }
+      }
+    }
+  }
+  stats[0] = (double)np; stats[1] = nref; stats[2] = nours; stats[3] = both;
+  stats[4] = worst; stats[5] = flips; stats[6] = bad; stats[7] = inexact;
 }

@@ -70,6 +70,16 @@ def lib():
         L.orc_qp_relax.restype = C.c_int64
         L.orc_qp_relax_sel.argtypes = [F32P, C.c_float, C.c_float, F32P, C.c_float] + L.orc_relax.argtypes
         L.orc_qp_relax_sel.restype = C.c_int64
+        U8P = np.ctypeslib.ndpointer(np.uint8, flags='C_CONTIGUOUS')
+        U16P = np.ctypeslib.ndpointer(np.uint16, flags='C_CONTIGUOUS')
+        F64P = np.ctypeslib.ndpointer(np.float64, flags='C_CONTIGUOUS')
+        L.orc_relax_subset.argtypes = L.orc_relax.argtypes + [U8P]
+        L.orc_relax_subset.restype = C.c_int64
+        L.orc_pairs_csr.argtypes = [C.POINTER(Model), C.c_int, C.POINTER(C.c_char_p), I32P, C.c_int, I64P, C.c_int64,
+                                    C.c_int, F32P, F32P, I32P, I64P, I32P, F32P, C.c_int64]
+        L.orc_pairs_csr.restype = C.c_int64
+        L.orc_csr_compare.argtypes = [C.c_int64, I32P, C.c_float, C.c_float, I64P, I64P, I32P, I32P, F32P,
+                                      I64P, I64P, I32P, U16P, F32P, F64P]
         _LIB = L
     return _LIB
 
@@ -236,3 +246,95 @@ def qp_sparsify(L1, L2, post):
     q = np.empty(max(n, 1), np.uint16)
     lib().orc_qp_sparsify(L1, L2, post, rp, cols.ctypes.data, q.ctypes.data)
     return rp, cols[:n], q[:n]
+
+
+# ---- bulk checkers (config-size parity tests and bench parity readouts)
+def pair_index(n, a, b):
+    return a * n - a * (a + 1) // 2 + (b - a - 1)
+
+
+def pair_of(n, p):
+    a = 0
+    while p >= n - 1 - a:
+        p -= n - 1 - a
+        a += 1
+    return a, a + 1 + p
+
+
+def pairs_csr(m, seqs, pid, pairs, threads=0):
+    """The pdoAlign pair body for a list of pairs (CPNP/MSA.cpp:939-1025):
+    (dist, mea, rowptr, ent_off, cols, vals); rowptr holds L_a + 2 entries
+    per listed pair (pair-local), ent_off len(pairs) + 1."""
+    pairs = np.ascontiguousarray(pairs, np.int64)
+    n = len(seqs)
+    arr = (C.c_char_p * n)(*[_s(s) for s in seqs])
+    lens = np.array([len(s) for s in seqs], np.int32)
+    la = np.array([lens[pair_of(n, int(p))[0]] for p in pairs], np.int64)
+    rp = np.zeros(max(int((la + 2).sum()), 1), np.int32)
+    eo = np.zeros(len(pairs) + 1, np.int64)
+    dist = np.zeros(max(len(pairs), 1), np.float32)
+    mea_ = np.zeros(max(len(pairs), 1), np.float32)
+    cap = int(sum(int(lens[pair_of(n, int(p))[0]]) * 64 for p in pairs)) + 1
+    while True:
+        cols = np.zeros(cap, np.int32)
+        vals = np.zeros(cap, np.float32)
+        tot = lib().orc_pairs_csr(C.byref(m), n, arr, lens, int(pid), pairs, len(pairs), int(threads), dist, mea_,
+                                  rp, eo, cols, vals, cap)
+        if tot >= 0:
+            return dist[:len(pairs)], mea_[:len(pairs)], rp, eo, cols[:tot], vals[:tot]
+        cap = int(eo[-1]) + 1
+
+
+def store_view(lens, pairs, rowptr, ent_off):
+    """Row/entry offsets of `pairs` inside a canonical store (include/mlpgpu.h
+    layout): (L_a, row offsets, entry offsets)."""
+    n = len(lens)
+    lens = np.asarray(lens, np.int64)
+    P = n * (n - 1) // 2
+    a_of = np.repeat(np.arange(n), np.arange(n - 1, -1, -1))[:P]
+    rp_off = np.zeros(P + 1, np.int64)
+    rp_off[1:] = np.cumsum(lens[a_of] + 2)
+    pairs = np.asarray(pairs, np.int64)
+    return lens[a_of[pairs]].astype(np.int32), rp_off[pairs], np.asarray(ent_off, np.int64)[pairs]
+
+
+def csr_compare(L1, ref, ours, rtol=1e-4, cutoff=0.01):
+    """ref = (row offsets, entry offsets, rowptr int32, cols int32, vals);
+    ours the same with uint16 cols.  Returns a dict of parity statistics
+    (SURVEY.md section 8c rule)."""
+    st = np.zeros(8, np.float64)
+    lib().orc_csr_compare(len(L1), np.ascontiguousarray(L1, np.int32), float(rtol), float(cutoff),
+                          *[np.ascontiguousarray(x) for x in ref], *[np.ascontiguousarray(x) for x in ours], st)
+    keys = ('pairs', 'ref_entries', 'our_entries', 'common', 'max_rel_err', 'cutoff_flips', 'violations',
+            'inexact')
+    return {k: (float(v) if k == 'max_rel_err' else int(v)) for k, v in zip(keys, st)}
+
+
+def relax_subset(lens, rowptr, ent_off, cols, vals, select):
+    """orc_relax of the pairs with select[p] on a whole canonical store
+    (flat arrays, include/mlpgpu.h layout).  Returns (rowptr, ent_off, cols,
+    vals) of the output in the same layout (unselected pairs empty)."""
+    n = len(lens)
+    lens = np.asarray(lens, np.int32)
+    P = n * (n - 1) // 2
+    a_of = np.repeat(np.arange(n), np.arange(n - 1, -1, -1))[:P]
+    row_off = np.zeros(P + 1, np.int64)
+    row_off[1:] = np.cumsum(lens[a_of].astype(np.int64) + 2)
+    eo = np.ascontiguousarray(ent_off, np.int64)
+    in_rp = np.ascontiguousarray(rowptr, np.int32)
+    in_c = np.ascontiguousarray(cols, np.int32) if len(cols) else np.zeros(1, np.int32)
+    in_v = np.ascontiguousarray(vals, np.float32) if len(vals) else np.zeros(1, np.float32)
+    sel = np.ascontiguousarray(select, np.uint8)
+    out_rp = np.zeros_like(in_rp)
+    out_off = np.zeros(max(P, 1), np.int64)
+    idx = np.nonzero(sel)[0]
+    cap = max(int((eo[idx + 1] - eo[idx]).sum()), 1)  # the output is masked to P_xy's entries
+    out_c = np.zeros(cap, np.int32)
+    out_v = np.zeros(cap, np.float32)
+    tot = lib().orc_relax_subset(n, lens, row_off[:P], eo[:P], in_rp, in_c, in_v, out_rp, out_off, out_c, out_v,
+                                 cap, sel)
+    assert tot >= 0
+    out_eo = np.zeros(P + 1, np.int64)
+    out_eo[:P] = out_off[:P]
+    out_eo[P] = tot
+    return out_rp, out_eo, out_c[:tot], out_v[:tot]

@@ -332,17 +332,60 @@ static int cmd_family(int argc, char **argv) {
   return 0;
 }
 
-// bench <fasta> <pid> <maxpairs> <threads>  -> JSON on stdout
+// Per-pair sparse dump (bench and relaxbench): int64 count, then per pair
+// int32 a, int32 b, int32 L1, float dist, float mea, int64 nnz,
+// int32 rowptr[L1 + 2] (pair-local), int32 cols[nnz], float vals[nnz].
+static void dump_pairs(const char *path, const std::vector<std::pair<int, int> > &pairs,
+                       const std::vector<SparseMatrix *> &sm, const std::vector<float> &dist,
+                       const std::vector<float> &mea) {
+  FILE *f = fopen(path, "wb");
+  if (!f) { fprintf(stderr, "cannot write %s\n", path); exit(3); }
+  int64_t np = pairs.size();
+  fwrite(&np, 8, 1, f);
+  std::vector<int32_t> rp, cols;
+  std::vector<float> vals;
+  for (int64_t p = 0; p < np; p++) {
+    SparseMatrix *m = sm[p];
+    int32_t hdr[3] = {pairs[p].first, pairs[p].second, m->GetSeq1Length()};
+    fwrite(hdr, 4, 3, f);
+    float dm[2] = {dist.empty() ? 0.f : dist[p], mea.empty() ? 0.f : mea[p]};
+    fwrite(dm, 4, 2, f);
+    const int L1 = m->GetSeq1Length();
+    rp.assign(L1 + 2, 0);
+    cols.clear();
+    vals.clear();
+    for (int i = 1; i <= L1; i++) {
+      auto r = m->GetRowPtr(i);
+      for (int k = 0; k < m->GetRowSize(i); k++) {
+        cols.push_back(r[k].first);
+        vals.push_back(r[k].second);
+      }
+      rp[i + 1] = (int32_t)cols.size();
+    }
+    int64_t nnz = cols.size();
+    fwrite(&nnz, 8, 1, f);
+    fwrite(rp.data(), 4, rp.size(), f);
+    fwrite(cols.data(), 4, cols.size(), f);
+    fwrite(vals.data(), 4, vals.size(), f);
+  }
+  fclose(f);
+}
+
+// bench <fasta> <pid> <maxpairs> <threads> [dump]  -> JSON on stdout
 // Times the reference's pdoAlign pair body (posterior + MEA + sparsify,
-// CPNP/MSA.cpp:939-1025) over the first `maxpairs` pairs in reference order.
+// CPNP/MSA.cpp:939-1025) over the first `maxpairs` pairs in reference order;
+// with `dump`, writes their sparse matrices, distances and MEA scores there
+// afterwards (same-run parity readouts in bench.py).
 static int cmd_bench(int argc, char **argv) {
   if (argc < 4) return 2;
   MultiSequence *seqs = load(argv[0]);
   int pid = atoi(argv[1]);
   long maxpairs = atol(argv[2]);
   int threads = atoi(argv[3]);
+  const char *dump = argc > 4 ? argv[4] : nullptr;
   MSA *m = fake_msa();
   setup_params(m);
+  if (getenv("REF_PROBE_DELTA")) initDistrib[2] = (float)atof(getenv("REF_PROBE_DELTA"));
   ProbabilisticModel model(initDistrib, gapOpen, gapExtend, emitPairs, emitSingle);
   const int n = seqs->GetNumSequences();
   std::vector<std::pair<int, int> > pairs;
@@ -354,7 +397,8 @@ static int cmd_bench(int argc, char **argv) {
     cells += (double)(seqs->GetSequence(pr.first)->GetLength() + 1) *
              (seqs->GetSequence(pr.second)->GetLength() + 1);
   omp_set_num_threads(threads);
-  std::vector<float> dist(np);
+  std::vector<float> dist(np), mea(np);
+  std::vector<SparseMatrix *> sm(np, nullptr);
   auto t0 = std::chrono::steady_clock::now();
 #pragma omp parallel for schedule(dynamic)
   for (long p = 0; p < np; p++) {
@@ -363,26 +407,111 @@ static int cmd_bench(int argc, char **argv) {
     VF *post = pair_posterior(model, s1, s2, a, b, pid);
     auto al = model.ComputeAlignment(s1->GetLength(), s2->GetLength(), *post);
     dist[p] = 1.0f - al.second / min(s1->GetLength(), s2->GetLength());
-    SparseMatrix *sm = new SparseMatrix(s1->GetLength(), s2->GetLength(), *post);
-    delete sm;
+    mea[p] = al.second;
+    sm[p] = new SparseMatrix(s1->GetLength(), s2->GetLength(), *post);
     delete al.first;
     delete post;
   }
   auto t1 = std::chrono::steady_clock::now();
   double sec = std::chrono::duration<double>(t1 - t0).count();
+  if (dump) dump_pairs(dump, pairs, sm, dist, mea);
+  for (auto *x : sm) delete x;
   printf("{\"pairs\": %ld, \"pair_cells\": %.0f, \"seconds\": %.6f, \"threads\": %d, "
          "\"pair_cells_per_s\": %.6e}\n",
          np, cells, sec, threads, cells / sec);
   return 0;
 }
 
+// relaxbench <fasta> <store> <sample> <threads> <dump>  -> JSON on stdout
+// Times the reference's MSA::DoRelaxation (CPNP/MSA.cpp:1172-1281, its own
+// pair loop over seqsPairs) on a strided sample of `sample` output pairs,
+// with every input block present.  The input is a sparse set in the
+// canonical layout of include/mlpgpu.h written by bench.py (int64 P, int64
+// total, int32 row_ptr, int64 ent_off[P + 1], uint16 cols, float vals),
+// loaded into the reference's own SparseMatrix objects.  The sample's output
+// matrices go to `dump` (dump_pairs format).
+static int cmd_relaxbench(int argc, char **argv) {
+  if (argc < 5) return 2;
+  MultiSequence *seqs = load(argv[0]);
+  const long sample = atol(argv[2]);
+  const int threads = atoi(argv[3]);
+  const int n = seqs->GetNumSequences();
+  FILE *f = fopen(argv[1], "rb");
+  if (!f) return 3;
+  int64_t P = 0, total = 0;
+  if (fread(&P, 8, 1, f) != 1 || fread(&total, 8, 1, f) != 1 || P != (int64_t)n * (n - 1) / 2) return 4;
+  std::vector<int> lens(n);
+  for (int i = 0; i < n; i++) lens[i] = seqs->GetSequence(i)->GetLength();
+  std::vector<std::pair<int, int> > pairs;
+  std::vector<int64_t> roff(P + 1, 0);
+  for (int a = 0; a < n; a++)
+    for (int b = a + 1; b < n; b++) {
+      roff[pairs.size() + 1] = roff[pairs.size()] + lens[a] + 2;
+      pairs.push_back({a, b});
+    }
+  std::vector<int32_t> rp(roff[P]);
+  std::vector<int64_t> eo(P + 1);
+  std::vector<uint16_t> cols(std::max<int64_t>(total, 1));
+  std::vector<float> vals(std::max<int64_t>(total, 1));
+  if (fread(rp.data(), 4, rp.size(), f) != rp.size() || fread(eo.data(), 8, P + 1, f) != (size_t)(P + 1) ||
+      fread(cols.data(), 2, total, f) != (size_t)total || fread(vals.data(), 4, total, f) != (size_t)total)
+    return 5;
+  fclose(f);
+  omp_set_num_threads(threads);
+  MSA *m = fake_msa();
+  SafeVector<SafeVector<SparseMatrix *> > sparse(n, SafeVector<SparseMatrix *>(n, NULL));
+#pragma omp parallel for schedule(dynamic, 64)
+  for (int64_t p = 0; p < P; p++) {
+    const int a = pairs[p].first, b = pairs[p].second, L1 = lens[a];
+    const int32_t *r = rp.data() + roff[p];
+    SparseMatrix *s = new SparseMatrix();  // the reference's own layout (SparseMatrix.h:28-33)
+    s->seq1Length = L1;
+    s->seq2Length = lens[b];
+    const int64_t nnz = r[L1 + 1];
+    s->data.resize(nnz);
+    for (int64_t k = 0; k < nnz; k++) {
+      s->data[k].first = cols[eo[p] + k];
+      s->data[k].second = vals[eo[p] + k];
+    }
+    s->rowSize.resize(L1 + 1);
+    s->rowSize[0] = -1;
+    s->rowPtrs.resize(L1 + 1);
+    s->rowPtrs[0] = s->data.end();
+    for (int i = 1; i <= L1; i++) {
+      s->rowPtrs[i] = s->data.begin() + r[i];
+      s->rowSize[i] = r[i + 1] - r[i];
+    }
+    sparse[a][b] = s;
+  }
+  std::vector<std::pair<int, int> > pick;
+  const int64_t stride = std::max<int64_t>(1, P / std::max<long>(sample, 1));
+  for (int64_t p = 0; p < P && (long)pick.size() < sample; p += stride) pick.push_back(pairs[p]);
+  m->numPairs = (int)pick.size();
+  m->seqsPairs = new MSA::SeqsPair[pick.size()];
+  for (size_t k = 0; k < pick.size(); k++) {
+    m->seqsPairs[k].seq1 = pick[k].first;
+    m->seqsPairs[k].seq2 = pick[k].second;
+  }
+  auto t0 = std::chrono::steady_clock::now();
+  SafeVector<SafeVector<SparseMatrix *> > ns = m->DoRelaxation(seqs, sparse);
+  auto t1 = std::chrono::steady_clock::now();
+  double sec = std::chrono::duration<double>(t1 - t0).count();
+  std::vector<SparseMatrix *> out;
+  for (auto &pr : pick) out.push_back(ns[pr.first][pr.second]);
+  dump_pairs(argv[4], pick, out, {}, {});
+  printf("{\"pairs\": %zu, \"stride\": %ld, \"seconds\": %.6f, \"threads\": %d}\n", pick.size(), (long)stride, sec,
+         threads);
+  return 0;
+}
+
 int main(int argc, char **argv) {
   if (argc < 2) {
-    fprintf(stderr, "usage: ref_probe params|pair|family|bench ...\n");
+    fprintf(stderr, "usage: ref_probe params|pair|family|bench|relaxbench ...\n");
     return 2;
   }
   std::string cmd = argv[1];
   if (cmd == "bench") return cmd_bench(argc - 2, argv + 2);
+  if (cmd == "relaxbench") return cmd_relaxbench(argc - 2, argv + 2);
   const char *outp = getenv("REF_PROBE_OUT");
   if (!outp) {
     fprintf(stderr, "set REF_PROBE_OUT\n");

@@ -105,3 +105,18 @@ def test_edge_families(name):
         assert r.returncode == 0 and r.stderr == b'', (tag, r.stderr)
         with open(os.path.join(EDGE, f'{name}.{tag}.out'), 'rb') as fh:
             assert r.stdout == fh.read(), (name, tag)
+
+
+# ---- BASELINE.json configurations end to end: the reference CLI's `-p 0`
+# output on the bench's own synthetic families (tests/golden/config,
+# tools/gen_config_goldens.sh: C2 single-threaded; C3 has more than 150
+# sequences, so refinement is off and the reference's threads cannot race)
+@pytest.mark.parametrize('name', ['c2_128x256_s11', 'c3_512x400_s11'])
+def test_cli_config_families(name):
+    out = os.path.join(GOLDEN, 'config', f'{name}.p_0.out')
+    if not os.path.exists(out):
+        pytest.skip('reference output not generated')
+    r = _run('-p', '0', os.path.join(GOLDEN, 'config', f'{name}.fa'))
+    assert r.returncode == 0 and r.stderr == '', r.stderr
+    with open(out) as fh:
+        assert r.stdout == fh.read()
