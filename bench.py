@@ -26,9 +26,9 @@ sys.path.insert(0, ROOT)
 
 METRIC = 'pair-HMM DP cell updates/s (all-pairs) + end-to-end MSA sec/family'
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
-# VALU issue peak: 256 CUs x 4 SIMDs x 2.4 GHz, one wave64 VALU instruction per
-# 4 cycles per SIMD (16 lanes wide) -- the bound the DP sweeps actually hit
-VALU_PEAK_WAVE_INSTS = 256 * 4 * 2.4e9 / 4
+# VALU issue peak: 256 CUs x 4 SIMD-32 x 2.4 GHz, one wave64 VALU instruction
+# per 2 cycles per SIMD (MI355X_MICROARCH.md, "Wave scheduling")
+VALU_PEAK_WAVE_INSTS = 256 * 4 * 2.4e9 / 2
 # Algorithmic HBM bytes per pair-cell for each kernel of the pid-0 pipeline
 # ("Kernels and their rooflines").
 ALGO_BYTES = {'forward': 20, 'backward': 32, 'local_totals': 8, 'merge_mea_sparsify': 12}
@@ -50,39 +50,222 @@ def parse():
     ap.add_argument('--cpu-threads', type=int, default=16)
     ap.add_argument('--no-cpu', action='store_true')
     ap.add_argument('--relax', type=int, default=-1,
-                    help='also time N relaxation rounds (reported separately; default 1 on one GPU, 0 on several)')
+                    help='also time N consistency rounds (C4; reported separately; default 4 on one GPU, 0 on several)')
+    ap.add_argument('--relax-cpu-pairs', type=int, default=768, help='reference DoRelaxation sample (output pairs)')
     ap.add_argument('--no-e2e', action='store_true',
                     help='skip the end-to-end c_p_np_aln / quickprobs family timings')
     ap.add_argument('--no-qp', action='store_true', help='skip the QuickProbs posterior/consistency timings')
     return ap.parse_args()
 
 
-def cpu_baseline(fasta, pid, pairs, threads, cells_per_pair):
-    """Time the reference's own pair loop (oracle/_ref/ref_probe, compiled from
-    /root/reference by `make -C oracle ref`) on a bounded sample of the same
-    family; fall back to the plain-C port if the reference build is absent."""
-    probe = os.path.join(ROOT, 'oracle', '_ref', 'ref_probe')
-    if os.path.exists(probe):
-        out = subprocess.run([probe, 'bench', fasta, str(pid), str(pairs), str(threads)],
-                             capture_output=True, text=True, timeout=600)
-        if out.returncode == 0:
-            r = json.loads(out.stdout.strip().splitlines()[-1])
-            return {'value': r['pair_cells_per_s'], 'unit': 'pair-cells/s', 'cores': threads,
-                    'kind': 'reference',
-                    'sample': f"first {r['pairs']} pairs of the same family, {r['seconds']:.1f} s, "
-                              f"reference C_P_NP_Aln pdoAlign pair body (posterior+MEA+sparsify)"}
+def _oracle():
     sys.path.insert(0, os.path.join(ROOT, 'oracle'))
     import orc
-    from mlprobs_amd import synth
-    seqs = [s for _, s in synth.read_fasta(fasta)]
-    m = orc.model(0.132548)
+    return orc
+
+
+def read_pair_dump(path):
+    """oracle/ref_probe's per-pair dump (dump_pairs): pair ids, L1, distances,
+    MEA scores and the sparse rows in the canonical layout."""
+    with open(path, 'rb') as fh:
+        buf = fh.read()
+    npairs = int(np.frombuffer(buf, np.int64, 1, 0)[0])
+    off = 8
+    ab, L1, dist, mea, rps, cols, vals, eo = [], [], [], [], [], [], [], [0]
+    for _ in range(npairs):
+        a, b, la = (int(x) for x in np.frombuffer(buf, np.int32, 3, off))
+        d, m = np.frombuffer(buf, np.float32, 2, off + 12)
+        nnz = int(np.frombuffer(buf, np.int64, 1, off + 20)[0])
+        off += 28
+        rps.append(np.frombuffer(buf, np.int32, la + 2, off))
+        off += 4 * (la + 2)
+        cols.append(np.frombuffer(buf, np.int32, nnz, off))
+        off += 4 * nnz
+        vals.append(np.frombuffer(buf, np.float32, nnz, off))
+        off += 4 * nnz
+        ab.append((a, b))
+        L1.append(la)
+        dist.append(d)
+        mea.append(m)
+        eo.append(eo[-1] + nnz)
+    L1 = np.array(L1, np.int32)
+    return {'ab': ab, 'L1': L1, 'dist': np.array(dist, np.float32), 'mea': np.array(mea, np.float32),
+            'roff': np.concatenate([[0], np.cumsum(L1.astype(np.int64) + 2)[:-1]]).astype(np.int64),
+            'eoff': np.array(eo[:-1], np.int64), 'rp': np.concatenate(rps).astype(np.int32),
+            'cols': np.concatenate(cols + [np.zeros(1, np.int32)]).astype(np.int32),
+            'vals': np.concatenate(vals + [np.zeros(1, np.float32)]).astype(np.float32)}
+
+
+def compare_with_dump(orc, dump, n, lens, store, exact):
+    """Parity readouts: the reference's sparse rows of
+    the dumped pairs against the GPU store (section 8c rule)."""
+    pairs = np.array([orc.pair_index(n, a, b) for a, b in dump['ab']], np.int64)
+    g_rp, g_eo, g_cols, g_vals = store
+    L1, ro, eo = orc.store_view(lens, pairs, g_rp, g_eo)
+    st = orc.csr_compare(dump['L1'], (dump['roff'], dump['eoff'], dump['rp'], dump['cols'], dump['vals']),
+                         (ro, eo, g_rp, g_cols, g_vals))
+    st['symmetric_difference'] = st.pop('cutoff_flips')
+    if exact:
+        st['bit_exact'] = st['inexact'] == 0
+    return pairs, st
+
+
+def cpu_baseline(fasta, args, n, lens, store, gpu_dist):
+    """The reference's own pair loop (oracle/_ref/ref_probe, compiled from
+    /root/reference by `make -C oracle ref`) timed on a bounded sample of the
+    same family, and its output for that sample compared with the GPU store
+    (same-run parity readouts); the plain-C port when the reference build is
+    absent (timing only)."""
+    probe = os.path.join(ROOT, 'oracle', '_ref', 'ref_probe')
+    orc = _oracle()
+    if os.path.exists(probe):
+        with tempfile.TemporaryDirectory() as td:
+            dump = os.path.join(td, 'ref.bin')
+            out = subprocess.run([probe, 'bench', fasta, str(args.pid), str(args.cpu_pairs), str(args.cpu_threads),
+                                  dump], capture_output=True, text=True, timeout=900,
+                                 env=dict(os.environ, REF_PROBE_DELTA=repr(args.delta)))
+            if out.returncode == 0:
+                r = json.loads(out.stdout.strip().splitlines()[-1])
+                res = {'value': r['pair_cells_per_s'], 'unit': 'pair-cells/s', 'cores': args.cpu_threads,
+                       'kind': 'reference',
+                       'sample': f"first {r['pairs']} pairs of the same family, {r['seconds']:.1f} s, "
+                                 f"reference C_P_NP_Aln pdoAlign pair body (posterior+MEA+sparsify)"}
+                parity = None
+                if store is not None:
+                    d = read_pair_dump(dump)
+                    pairs, parity = compare_with_dump(orc, d, n, lens, store, exact=args.pid == 2)
+                    rel = np.abs(gpu_dist[pairs] - d['dist']) / np.maximum(np.abs(d['dist']), 1e-6)
+                    parity['distance_max_rel_err'] = float(rel.max())
+                    parity['rule'] = ('|d| <= 1e-4 max(|ref|, 1e-6); one-sided entries within 1e-4 of the '
+                                      '0.01 cutoff (SURVEY.md 8c)')
+                    parity['sample'] = f'the {len(pairs)} pairs of the CPU baseline, reference output'
+                return res, parity
+    seqs = [s for _, s in __import__('mlprobs_amd.synth', fromlist=['x']).read_fasta(fasta)]
+    m = orc.model(args.delta)
     t0 = time.perf_counter()
-    d, nz, tot = orc.pair_loop(m, seqs, pid, max_pairs=pairs, threads=threads)
+    orc.pair_loop(m, seqs, args.pid, max_pairs=args.cpu_pairs, threads=args.cpu_threads)
     dt = time.perf_counter() - t0
     cells = sum((len(seqs[a]) + 1) * (len(seqs[b]) + 1) for a, b in
-                [(a, b) for a in range(len(seqs)) for b in range(a + 1, len(seqs))][:pairs])
-    return {'value': cells / dt, 'unit': 'pair-cells/s', 'cores': threads, 'kind': 'port',
-            'sample': f'first {pairs} pairs, {dt:.1f} s, oracle port'}
+                [(a, b) for a in range(len(seqs)) for b in range(a + 1, len(seqs))][:args.cpu_pairs])
+    return {'value': cells / dt, 'unit': 'pair-cells/s', 'cores': args.cpu_threads, 'kind': 'port',
+            'sample': f'first {args.cpu_pairs} pairs, {dt:.1f} s, oracle port'}, None
+
+
+def relax_work(n, lens, store):
+    """The reference's multiply-adds for one consistency round over this store
+    (for output (x, y) and each z, every entry of P_xz meets
+    the row of P_zy it selects), without enumerating them: with V_z[s][k] the
+    number of entries of block {s, z} at residue k of z, MACs(x, y) =
+    sum_z <V_z[x], V_z[y]>.  Returns (V, total MACs)."""
+    rp, eo, cols, _ = store
+    lens = np.asarray(lens, np.int64)
+    K = int(lens.max()) + 1
+    P = n * (n - 1) // 2
+    a_of = np.repeat(np.arange(n), np.arange(n - 1, -1, -1))[:P]
+    b_of = np.concatenate([np.arange(a + 1, n) for a in range(n)])
+    rp_off = np.zeros(P + 1, np.int64)
+    rp_off[1:] = np.cumsum(lens[a_of] + 2)
+    V = np.zeros((n, n, K), np.int32)
+    step = 4096
+    for p0 in range(0, P, step):
+        p1 = min(P, p0 + step)
+        for p in range(p0, p1):  # rows of a: row lengths
+            La = lens[a_of[p]]
+            r = rp[rp_off[p]: rp_off[p] + La + 2]
+            V[a_of[p], b_of[p], 1:La + 1] = np.diff(r[1:])
+        e0, e1 = int(eo[p0]), int(eo[p1])
+        pid_of = np.repeat(np.arange(p1 - p0), np.diff(eo[p0:p1 + 1]))
+        cnt = np.bincount(pid_of * K + cols[e0:e1].astype(np.int64), minlength=(p1 - p0) * K).reshape(p1 - p0, K)
+        V[b_of[p0:p1], a_of[p0:p1], :] = cnt  # columns of b: column counts
+    total = 0
+    for z in range(n):
+        v = V[z].astype(np.int64)
+        total += int(((v.sum(0) ** 2) - (v * v).sum(0)).sum()) // 2
+    return V, total
+
+
+def relax_leg(fam, args, n, lens, total_cells):
+    """C4 on one GPU: `args.relax` consistency rounds (CPNP/MSA.cpp:1172-1360)
+    over the posterior store, timed per round, with the section 8d accounting
+    of round 1 (reference multiply-adds, algorithmic bytes 16 (N - 1) nnz,
+    HBM roofline of k_relax_tile) and, on rank 0 with --cpu, the reference's
+    DoRelaxation timed on a strided sample of output pairs from the same input
+    and compared with the GPU's output for them."""
+    store0 = [a.copy() for a in fam.export()]
+    nnz0 = int(store0[1][-1])
+    V, macs = relax_work(n, lens, store0)
+    rounds = []
+    store1 = None
+    for it in range(args.relax):
+        fam.profile(True)
+        fam.synchronize()
+        t0 = time.perf_counter()
+        fam.relax(1)
+        fam.synchronize()
+        dt = time.perf_counter() - t0
+        kt = fam.kernel_times()
+        nnz = int(fam.results()[2].sum())
+        rounds.append({'seconds': dt, 'nnz_in': nnz0 if it == 0 else rounds[-1]['nnz_out'], 'nnz_out': nnz,
+                       'kernels_ms': {k: v['ms'] for k, v in kt.items() if v['launches']}})
+        if it == 0:
+            k_ms = kt['relax']['ms']
+            k_launch = max(kt['relax']['launches'], 1)
+            if not args.no_cpu:
+                store1 = [a.copy() for a in fam.export()]
+    algo = 16.0 * (n - 1) * nnz0
+    traffic = None
+    pmc = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
+    if os.path.exists(pmc):
+        with open(pmc) as fh:
+            g = json.load(fh).get('relax')
+        if g:
+            traffic = g['traffic_bytes_per_nnz_in'] * nnz0 / k_launch / 1e9
+    res = {'rounds': len(rounds), 'per_round': rounds, 'seconds': sum(r['seconds'] for r in rounds),
+           'nnz_per_round': [nnz0] + [r['nnz_out'] for r in rounds],
+           'round1': {'macs_reference': macs, 'mac_per_s': macs / (k_ms * 1e-3), 'flop_per_s': 2 * macs / (k_ms * 1e-3),
+                      'kernel_ms': k_ms},
+           'roofline': {'bound': 'hbm', 'kernel': 'k_relax_tile', 'achieved': algo / k_launch / (k_ms / k_launch * 1e-3) / 1e9,
+                        'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                        'frac': algo / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 'traffic': traffic,
+                        'algo_bytes': algo, 'algo_rule': '16 (N - 1) nnz_in (SURVEY.md 8d: every operand block '
+                                                         'read once per output pair, output read + written once)',
+                        'avg_launch_ms': k_ms / k_launch}}
+    probe = os.path.join(ROOT, 'oracle', '_ref', 'ref_probe')
+    if store1 is not None and os.path.exists(probe):
+        orc = _oracle()
+        from mlprobs_amd import synth
+        with tempfile.TemporaryDirectory() as td:
+            fa = os.path.join(td, 'fam.fa')
+            synth.write_fasta(fa, [('s%04d' % k, s) for k, s in enumerate(fam.seqs)])
+            path = os.path.join(td, 'store.bin')
+            rp, eo, cols, vals = store0
+            with open(path, 'wb') as fh:
+                fh.write(np.array([len(eo) - 1, int(eo[-1])], np.int64).tobytes())
+                fh.write(rp.tobytes())
+                fh.write(eo.tobytes())
+                fh.write(cols.tobytes())
+                fh.write(vals.tobytes())
+            dump = os.path.join(td, 'relax.bin')
+            out = subprocess.run([probe, 'relaxbench', fa, path, str(args.relax_cpu_pairs), str(args.cpu_threads),
+                                  dump], capture_output=True, text=True, timeout=900)
+            if out.returncode == 0:
+                r = json.loads(out.stdout.strip().splitlines()[-1])
+                d = read_pair_dump(dump)
+                pairs, st = compare_with_dump(orc, d, n, lens, store1, exact=True)
+                sample_macs = 0
+                for a, b in d['ab']:
+                    sample_macs += int(np.einsum('zk,zk->', V[:, a, :].astype(np.int64), V[:, b, :].astype(np.int64)))
+                res['cpu_baseline'] = {'value': sample_macs / r['seconds'], 'unit': 'MAC/s (reference multiply-adds)',
+                                       'cores': args.cpu_threads, 'kind': 'reference',
+                                       'sample': f"{r['pairs']} output pairs (every {r['stride']}th), "
+                                                 f"{r['seconds']:.1f} s, reference MSA::DoRelaxation on the "
+                                                 "GPU's posterior store"}
+                res['speedup_vs_cpu'] = res['round1']['mac_per_s'] / res['cpu_baseline']['value']
+                st['sample'] = 'the CPU baseline pairs: reference DoRelaxation output vs GPU round 1'
+                res['parity'] = st
+            else:
+                res['cpu_baseline_error'] = out.stderr[-400:]
+    return res
 
 
 def e2e_families(args):
@@ -194,7 +377,7 @@ def main():
     # follows a large release waits for the driver to clear that memory)
     e2e = e2e_families(args) if (not args.no_e2e and world == 1) else None
     if args.relax < 0:
-        args.relax = 1 if world == 1 else 0
+        args.relax = 4 if world == 1 else 0
     fam_in = synth.family(args.n, args.len, args.s, seed=args.seed)
     seqs = [s for _, s in fam_in]
     lens = np.array([len(s) for s in seqs], np.int64)
@@ -237,19 +420,11 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     kt = fam.kernel_times()
-    _, _, nnz = fam.results()  # posterior-stage sparse set (before any relaxation)
-    nnz = nnz.copy()
-    relax_info = None
-    if args.relax > 0:
-        fam.profile(True)
-        barrier()
-        tr = time.perf_counter()
-        fam.relax(args.relax)
-        barrier()
-        rk = fam.kernel_times()
-        relax_info = {'rounds': args.relax, 'seconds': time.perf_counter() - tr,
-                      'kernels_ms': {k: v['ms'] for k, v in rk.items() if v['launches']},
-                      'nnz_out': int(fam.results()[2].sum())}
+    gpu_dist, _, nnz = fam.results()  # posterior-stage sparse set (before any relaxation)
+    gpu_dist, nnz = gpu_dist.copy(), nnz.copy()
+    # the posterior store, kept for the same-run parity readouts (rank 0)
+    post_store = [a.copy() for a in fam.export()] if (rank == 0 and world == 1 and not args.no_cpu) else None
+    relax_info = relax_leg(fam, args, args.n, lens, total_cells) if (args.relax > 0 and world == 1) else None
     value = total_cells * args.steps / dt
     # roofline of the dominant kernel (largest accumulated device time)
     dom = max(ALGO_BYTES, key=lambda k: kt[k]['ms'])
@@ -275,12 +450,13 @@ def main():
     qp_info = quickprobs_stage(fam, fam_in, total_cells, args) if (world == 1 and not args.no_qp) else None
     out = None
     if rank == 0:
-        cpu = None
+        cpu, parity = None, None
         if not args.no_cpu and world == 1:
             with tempfile.TemporaryDirectory() as td:
                 fa = os.path.join(td, 'fam.fa')
                 synth.write_fasta(fa, fam_in)
-                cpu = cpu_baseline(fa, args.pid, args.cpu_pairs, args.cpu_threads, None)
+                cpu, parity = cpu_baseline(fa, args, args.n, lens, post_store, gpu_dist)
+            post_store = None
         out = {
             'metric': METRIC,
             'value': value,
@@ -310,6 +486,7 @@ def main():
                                'frac': value * STAGE_BYTES / 1e9 / HBM_PEAK_GBS},
             'kernels_ms_per_step': {k: v['ms'] / args.steps for k, v in kt.items() if v['launches']},
             'cpu_baseline': cpu,
+            'parity': parity,
         }
         if cpu:
             out['speedup_vs_cpu'] = value / cpu['value']
