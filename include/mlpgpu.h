@@ -45,6 +45,23 @@ typedef struct mlp_ctx mlp_ctx;
 
 /* Create a context bound to HIP device `device`. */
 int mlp_ctx_create(int device, mlp_ctx **out);
+/* A context that drives every GPU of `device_mask` (bit k = HIP device k;
+ * devices that do not exist are ignored) from this one host thread (SURVEY.md
+ * section 8b: "a ctx drives all GPUs in its mask").  For families of at least
+ * 1e9 pair-cells mlp_posteriors over all pairs and the relaxation rounds are
+ * split into contiguous pair ranges, one shard (child context) per device:
+ * posteriors balanced by DP cells (mlp_shard_plan), consistency rounds by
+ * estimated multiply-adds (mlp_relax_shard_plan); the shards' sparse sets are
+ * gathered over xGMI (peer copies) into this context's store, and the whole
+ * store goes back to every shard before each relaxation round.  Results are
+ * bit-identical to one device.  Everything else runs on the first device. */
+int mlp_ctx_create_mask(uint64_t device_mask, mlp_ctx **out);
+/* Number of shards (0: one per device of the mask when the family is large
+ * enough; k > 0: always k, spread round-robin over the mask's devices --
+ * several "virtual" shards may share a GPU). */
+int mlp_set_shards(mlp_ctx *ctx, int nshards);
+/* Shards the next whole-family call would use (1 = single device). */
+int mlp_shard_count(mlp_ctx *ctx);
 void mlp_ctx_destroy(mlp_ctx *ctx);
 const char *mlp_last_error(const mlp_ctx *ctx);
 /* Device bytes the posterior stage may hold as batch scratch (default: 45%
@@ -111,9 +128,10 @@ int mlp_csr_import(mlp_ctx *ctx, const int32_t *row_ptr, const int64_t *ent_off,
 
 /* `iters` rounds of the consistency transformation over the whole store.
  * Replaces MSA::DoRelaxation x numConsistencyReps (CPNP/MSA.cpp:1041-1051,
- * 1119-1129, 1172-1360).  With a communicator, each rank relaxes pairs
- * [p_begin, p_end) of its shard (mlp_shard_range) and the new store is
- * all-gathered after every round. */
+ * 1119-1129, 1172-1360).  With a communicator (or in-process shards), each
+ * rank relaxes the output pairs of its range from mlp_relax_shard_plan
+ * (balanced by estimated multiply-adds) and the new store is all-gathered
+ * after every round. */
 int mlp_relax(mlp_ctx *ctx, int iters);
 /* QuickProbs' consistency stage instead (ConsistencyStage::run / doRelaxation,
  * QP/Alignment/Multiple/ConsistencyStage.cpp:90-258), on a sparse set from
@@ -163,6 +181,11 @@ int mlp_shard_range(mlp_ctx *ctx, int nranks, int rank, int64_t *p_begin, int64_
  * first global entry of every rank's block to ebase[nranks + 1]. */
 int mlp_shard_plan(int n, const int32_t *lens, int nranks, int rank, int64_t *p_begin, int64_t *p_end);
 int mlp_gather_layout(int nranks, int64_t npairs, const int64_t *info, int64_t *ebase);
+/* Consistency-round sharding (host only): contiguous output-pair ranges
+ * bounds[r] .. bounds[r + 1] of equal estimated work, sum_z nnz(x, z)
+ * nnz(z, y) / L_z + (n - 2) nnz(x, y) per output pair (x, y), from the
+ * current per-pair entry counts.  bounds: nranks + 1. */
+int mlp_relax_shard_plan(int n, const int32_t *lens, const int64_t *pair_nnz, int nranks, int64_t *bounds);
 /* After every rank ran mlp_posteriors on its shard: all-gather the CSR
  * store and the per-pair scalars so every rank holds the whole family. */
 int mlp_allgather(mlp_ctx *ctx);

@@ -132,7 +132,8 @@ int main(int argc, char** argv) {
     } else {
       mlp_ctx* ctx = nullptr;
       stage("parse");
-      check(nullptr, mlp_ctx_create(0, &ctx), "device");
+      // every visible GPU: families of >= 1e9 pair-cells are sharded over them
+      check(nullptr, mlp_ctx_create_mask(~0ull, &ctx), "device");
       stage("device init");
       // one family per process: a 16 GB batch scratch.  A fresh process's
       // allocation waits for the driver to clear memory the previous process

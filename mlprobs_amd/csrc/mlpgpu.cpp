@@ -21,6 +21,7 @@
 #include <chrono>
 #include <cstring>
 #include <numeric>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -97,6 +98,12 @@ struct mlp_ctx {
   // comm
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
+  // in-process shards: child contexts, one per device of the mask (or
+  // virtual shards sharing devices); empty = the single-device path
+  uint64_t dev_mask = 0;
+  int shards_req = 0;                // 0: one per device when the family is large enough
+  std::vector<mlp_ctx*> shards;
+  int64_t rel_r0 = -1, rel_r1 = -1;  // a shard's output-pair range for one relaxation round
   // profiling
   bool profile = false;
   double kms[MLP_NKERNELS] = {0};
@@ -200,8 +207,8 @@ static void flush_timers(mlp_ctx* c) {
 
 // Parameter tables exactly as the reference builds them.
 static void build_tables(Tables& T, ModelScalars& ms, float delta, bool qp = false) {
-  static float emitPairs[256][256];
-  static float emitSingle[256];
+  static thread_local float emitPairs[256][256];  // shards build their tables concurrently
+  static thread_local float emitSingle[256];
   for (int i = 0; i < 256; i++) {
     emitSingle[i] = (float)1e-5;
     for (int j = 0; j < 256; j++) emitPairs[i][j] = (float)1e-10;
@@ -257,7 +264,7 @@ static void build_tables(Tables& T, ModelScalars& ms, float delta, bool qp = fal
   // Partition function (CPNP/MSAReadMatrix.cpp:85-116, MSAPartProbs.cpp:698-709)
   const char* bases = MLP_GONNET_MONOMERS;
   const int nb = (int)strlen(bases);
-  static double sm[26][26];
+  static thread_local double sm[26][26];
   int si[26];
   for (int i = 0; i < 26; i++) si[i] = -1;
   for (int i = 0; i < nb; i++) si[bases[i] - 'A'] = i;
@@ -299,6 +306,9 @@ static int pair_cost_cells(const mlp_ctx* c, int64_t p) {
   return (c->lens[c->pa[p]] + 1) * (c->lens[c->pb[p]] + 1);
 }
 
+static std::vector<int> mask_devices(uint64_t mask);
+static int shard_count(mlp_ctx* c);
+
 // ------------------------------------------------------------------ C ABI
 extern "C" {
 
@@ -337,8 +347,31 @@ int mlp_ctx_create(int device, mlp_ctx** out) {
   return MLP_OK;
 }
 
+int mlp_ctx_create_mask(uint64_t device_mask, mlp_ctx** out) {
+  if (!out) return MLP_ERR_ARG;
+  *out = nullptr;
+  const std::vector<int> devs = mask_devices(device_mask);
+  if (devs.empty()) return MLP_ERR_ARG;
+  int rc = mlp_ctx_create(devs[0], out);
+  if (rc) return rc;
+  uint64_t m = 0;
+  for (int d : devs) m |= 1ull << d;
+  (*out)->dev_mask = m;
+  return MLP_OK;
+}
+
+int mlp_set_shards(mlp_ctx* c, int nshards) {
+  if (!c || nshards < 0) return MLP_ERR_ARG;
+  c->shards_req = nshards;
+  return MLP_OK;
+}
+
+int mlp_shard_count(mlp_ctx* c) { return c ? shard_count(c) : 0; }
+
 void mlp_ctx_destroy(mlp_ctx* c) {
   if (!c) return;
+  for (mlp_ctx* ch : c->shards) mlp_ctx_destroy(ch);
+  c->shards.clear();
   hipSetDevice(c->device);
   hipStreamSynchronize(c->stream);
   hipStreamSynchronize(c->stream2);
@@ -374,6 +407,8 @@ int mlp_set_scratch(mlp_ctx* c, uint64_t bytes) {
 
 int mlp_family_load(mlp_ctx* c, int n, const char* residues, const int64_t* offsets) {
   if (!c || n < 1 || !residues || !offsets) return MLP_ERR_ARG;
+  for (mlp_ctx* ch : c->shards) mlp_ctx_destroy(ch);  // re-created for the new family when needed
+  c->shards.clear();
   hipSetDevice(c->device);
   c->n = n;
   c->lens.assign(n, 0);
@@ -663,12 +698,189 @@ static int64_t pair_width_bound(const mlp_ctx* c, int64_t q) {
 }
 static const size_t kPerSlotMeta = 4 * sizeof(int64_t) + 4 * sizeof(int32_t) + sizeof(PairRec) + 7 * 8 + 16;
 
+
+// ------------------------------------------------------------ in-process shards
+// One context can spread the posterior stage and the consistency rounds over
+// several GPUs of one process ("a ctx drives all GPUs
+// in its mask"): child contexts, one per device, each compute a contiguous
+// pair range; the parent gathers their sparse sets over xGMI (peer copies)
+// into its canonical store and, before every relaxation round, copies the
+// whole store back to every child.  Virtual shards (more shards than
+// devices, mlp_set_shards) exercise the same path on one GPU.
+static const double kShardMinCells = 1e9;  // smaller families stay on one device
+
+static std::vector<int> mask_devices(uint64_t mask) {
+  int cnt = 0;
+  if (hipGetDeviceCount(&cnt) != hipSuccess) cnt = 0;
+  std::vector<int> d;
+  for (int k = 0; k < cnt && k < 64; k++)
+    if (mask >> k & 1) d.push_back(k);
+  return d;
+}
+
+static int shard_count(mlp_ctx* c) {
+  if (c->shards_req > 0) return c->shards_req;
+  if (c->n < 2) return 1;
+  const std::vector<int> devs = mask_devices(c->dev_mask);
+  if (devs.size() < 2) return 1;
+  double cells = 0;
+  for (int64_t p = 0; p < c->P; p++) cells += pair_cost_cells(c, p);
+  return cells >= kShardMinCells ? (int)devs.size() : 1;
+}
+
+static hipError_t copy_from(mlp_ctx* dst, void* d, const mlp_ctx* src, const void* s, size_t bytes) {
+  if (!bytes) return hipSuccess;
+  if (dst->device == src->device) return hipMemcpyAsync(d, s, bytes, hipMemcpyDeviceToDevice, dst->stream);
+  return hipMemcpyPeerAsync(d, dst->device, s, src->device, bytes, dst->stream);
+}
+
+static int ensure_shards(mlp_ctx* c, int S) {
+  if ((int)c->shards.size() == S) return MLP_OK;
+  for (mlp_ctx* ch : c->shards) mlp_ctx_destroy(ch);
+  c->shards.clear();
+  std::vector<int> devs = mask_devices(c->dev_mask);
+  if (devs.empty()) devs.push_back(c->device);
+  std::vector<int> per(devs.size(), 0);
+  for (int s = 0; s < S; s++) per[s % devs.size()]++;
+  for (int s = 0; s < S; s++) {
+    const size_t di = s % devs.size();
+    mlp_ctx* ch = nullptr;
+    int rc = mlp_ctx_create(devs[di], &ch);
+    if (rc) {
+      c->err = "shard context on device " + std::to_string(devs[di]) + " failed";
+      return rc;
+    }
+    // shards sharing a device share its scratch budget (and the parent's cap)
+    ch->scratch_budget = std::min(ch->scratch_budget, c->scratch_budget) / per[di];
+    ch->profile = c->profile;
+    c->shards.push_back(ch);
+    if ((rc = mlp_family_load(ch, c->n, (const char*)c->h_res.data(), c->offs.data()))) {
+      c->err = "shard family load: " + ch->err;
+      return rc;
+    }
+  }
+  for (int d : devs)
+    if (d != c->device) {  // xGMI peer access both ways (errors: already enabled / no peer path)
+      hipSetDevice(c->device);
+      hipDeviceEnablePeerAccess(d, 0);
+      hipSetDevice(d);
+      hipDeviceEnablePeerAccess(c->device, 0);
+    }
+  hipGetLastError();
+  hipSetDevice(c->device);
+  return MLP_OK;
+}
+
+// run fn(shard, index) on every shard, one host thread each
+template <class F>
+static int run_shards(mlp_ctx* c, F fn) {
+  const int S = (int)c->shards.size();
+  std::vector<int> rcs(S, MLP_OK);
+  std::vector<std::thread> th;
+  for (int s = 0; s < S; s++)
+    th.emplace_back([&, s]() {
+      hipSetDevice(c->shards[s]->device);
+      rcs[s] = fn(c->shards[s], s);
+    });
+  for (auto& t : th) t.join();
+  hipSetDevice(c->device);
+  for (int s = 0; s < S; s++)
+    if (rcs[s] != MLP_OK) {
+      c->err = "shard " + std::to_string(s) + ": " + c->shards[s]->err;
+      return rcs[s];
+    }
+  return MLP_OK;
+}
+
+// The shards hold consecutive pair ranges tiling [0, P), entries from 0:
+// concatenate them into the parent's canonical store.
+static int gather_shards(mlp_ctx* c) {
+  const int S = (int)c->shards.size();
+  std::vector<int64_t> ebase(S + 1, 0);
+  for (int s = 0; s < S; s++) {
+    const mlp_ctx* ch = c->shards[s];
+    if (ch->store_p0 != (s ? c->shards[s - 1]->store_p1 : 0)) {
+      c->err = "shard ranges do not tile the pair range";
+      return MLP_ERR_STATE;
+    }
+    ebase[s + 1] = ebase[s] + ch->store_total;
+  }
+  if (c->shards[S - 1]->store_p1 != c->P) {
+    c->err = "shard ranges do not tile the pair range";
+    return MLP_ERR_STATE;
+  }
+  hipSetDevice(c->device);
+  const int64_t total = ebase[S];
+  int rc;
+  if ((rc = grow_store(c, total, 0))) return rc;
+  {
+    Timer tm(c, KGATHER, 0);
+    for (int s = 0; s < S; s++) {
+      mlp_ctx* ch = c->shards[s];
+      const int64_t p0 = ch->store_p0, p1 = ch->store_p1;
+      HIPCHK(c, copy_from(c, c->d_cols + ebase[s], ch, ch->d_cols, sizeof(uint16_t) * ch->store_total));
+      HIPCHK(c, copy_from(c, c->d_vals + ebase[s], ch, ch->d_vals, sizeof(float) * ch->store_total));
+      HIPCHK(c, copy_from(c, c->d_rowptr + c->rp_off[p0], ch, ch->d_rowptr + c->rp_off[p0],
+                          sizeof(int32_t) * (c->rp_off[p1] - c->rp_off[p0])));
+      for (int64_t p = p0; p < p1; p++) {
+        c->dist[p] = ch->dist[p];
+        c->mea[p] = ch->mea[p];
+        c->nnz[p] = ch->nnz[p];
+        c->ent_off[p] = ebase[s] + ch->ent_off[p] - ch->ent_off[p0];
+      }
+    }
+  }
+  c->ent_off[c->P] = total;
+  HIPCHK(c, hipMemcpyAsync(c->d_ent_off, c->ent_off.data(), sizeof(int64_t) * (c->P + 1), hipMemcpyHostToDevice,
+                           c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->store_p0 = 0;
+  c->store_p1 = c->P;
+  c->store_total = total;
+  ++c->store_ver;
+  return MLP_OK;
+}
+
+// The parent's whole store onto one shard (before a relaxation round).
+static int broadcast_store(mlp_ctx* c, mlp_ctx* ch) {
+  int rc;
+  if ((rc = grow_store(ch, c->store_total, 0))) return rc;
+  HIPCHK(ch, copy_from(ch, ch->d_rowptr, c, c->d_rowptr, sizeof(int32_t) * c->rp_off[c->P]));
+  HIPCHK(ch, copy_from(ch, ch->d_cols, c, c->d_cols, sizeof(uint16_t) * c->store_total));
+  HIPCHK(ch, copy_from(ch, ch->d_vals, c, c->d_vals, sizeof(float) * c->store_total));
+  ch->ent_off = c->ent_off;
+  ch->nnz = c->nnz;
+  ch->dist = c->dist;
+  ch->mea = c->mea;
+  HIPCHK(ch, hipMemcpyAsync(ch->d_ent_off, ch->ent_off.data(), sizeof(int64_t) * (c->P + 1), hipMemcpyHostToDevice,
+                            ch->stream));
+  HIPCHK(ch, hipStreamSynchronize(ch->stream));
+  ch->store_p0 = 0;
+  ch->store_p1 = c->P;
+  ch->store_total = c->store_total;
+  ++ch->store_ver;
+  return MLP_OK;
+}
+
+static int sharded_posteriors(mlp_ctx* c, int pid, float delta, int S) {
+  int rc;
+  if ((rc = ensure_shards(c, S))) return rc;
+  std::vector<int64_t> b(S), e(S);
+  for (int s = 0; s < S; s++) mlp_shard_plan(c->n, c->lens.data(), S, s, &b[s], &e[s]);
+  if ((rc = run_shards(c, [&](mlp_ctx* ch, int s) { return mlp_posteriors(ch, pid, delta, b[s], e[s]); })))
+    return rc;
+  return gather_shards(c);
+}
 extern "C" {
 
 int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
   if (!c) return MLP_ERR_ARG;
   if (c->n < 2) { c->err = "family needs >= 2 sequences"; return MLP_ERR_STATE; }
   if (p0 < 0 || p1 > c->P || p0 > p1) { c->err = "bad pair range"; return MLP_ERR_ARG; }
+  if (p0 == 0 && p1 == c->P && !c->comm) {
+    const int S = shard_count(c);
+    if (S > 1) return sharded_posteriors(c, pid, delta, S);
+  }
   hipSetDevice(c->device);
   // a range that continues the held one is appended; anything else restarts
   if (c->store_p0 == c->store_p1 || p0 != c->store_p1) {
@@ -694,8 +906,8 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
   // than the overlap wins); the host plans batch b + 1 while batch b's
   // kernels run, and finishes batch b (entry offsets from its pair records,
   // compaction into the store) before batch b + 1 reuses the scratch.
-  const bool two = false;
-  size_t batch_target = batch_target_for(c, p0, p1, pair_bytes);
+  const bool two = getenv("MLP_TWO") && atoi(getenv("MLP_TWO")) > 0;  // experiment hook
+  size_t batch_target = batch_target_for(c, p0, p1, pair_bytes, two ? c->scratch_budget / 2 : 0);
   int64_t all_cells = 0, done_cells = 0;
   for (int64_t k = p0; k < p1; k++) all_cells += pair_cost_cells(c, k);
   const int64_t base_total = c->store_total;
@@ -794,7 +1006,7 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
     if ((rc = ensure(c, *scr[slot], cv.off))) {
       if (rc != MLP_ERR_MEMORY || c->scratch_budget < (64u << 20)) return rc;
       c->scratch_budget /= 2;  // the device is shared: plan smaller batches and retry
-      batch_target = batch_target_for(c, p, p1, pair_bytes);
+      batch_target = batch_target_for(c, p, p1, pair_bytes, two ? c->scratch_budget / 2 : 0);
       continue;
     }
     char* base = (char*)scr[slot]->p;
@@ -1355,6 +1567,55 @@ int mlp_shard_range(mlp_ctx* c, int nranks, int rank, int64_t* b, int64_t* e) {
   return mlp_shard_plan(c->n, c->lens.data(), nranks, rank, b, e);
 }
 
+// Estimated work of output pair (x, y) in one consistency round: the
+// reference's multiply-adds if every block's entries spread evenly over the
+// residues of z, sum_z nnz(x, z) nnz(z, y) / L_z, plus (n - 2) nnz(x, y) for
+// the per-z visit of every mask cell.  Contiguous ranges of equal estimated
+// work (shard output pairs by MACs).
+int mlp_relax_shard_plan(int n, const int32_t* lens, const int64_t* pair_nnz, int nranks, int64_t* bounds) {
+  if (n < 0 || nranks < 1 || !bounds || (n > 0 && (!lens || !pair_nnz))) return MLP_ERR_ARG;
+  const int64_t P = (int64_t)n * (n - 1) / 2;
+  std::vector<double> cost(std::max<int64_t>(P, 1), 0.0);
+  if (n <= 2048) {
+    std::vector<float> M((size_t)n * n, 0.f);
+    for (int a = 0, p = 0; a < n; a++)
+      for (int b = a + 1; b < n; b++, p++) M[(size_t)a * n + b] = M[(size_t)b * n + a] = (float)pair_nnz[p];
+    std::vector<double> acc(n);
+    for (int x = 0; x < n; x++) {
+      std::fill(acc.begin(), acc.end(), 0.0);
+      for (int z = 0; z < n; z++) {
+        const double w = M[(size_t)x * n + z] / std::max(1, lens[z]);
+        if (w == 0) continue;
+        const float* mz = &M[(size_t)z * n];
+        for (int y = x + 1; y < n; y++) acc[y] += w * mz[y];
+      }
+      const int64_t base = pair_index_host(n, x, x + 1);
+      for (int y = x + 1; y < n; y++) cost[base + (y - x - 1)] = acc[y];
+    }
+  } else {  // large families: per-sequence totals only
+    std::vector<double> T(n, 0.0);
+    for (int a = 0, p = 0; a < n; a++)
+      for (int b = a + 1; b < n; b++, p++) T[a] += pair_nnz[p], T[b] += pair_nnz[p];
+    double Lm = 0;
+    for (int k = 0; k < n; k++) Lm += lens[k];
+    Lm = std::max(1.0, Lm / n);
+    for (int a = 0, p = 0; a < n; a++)
+      for (int b = a + 1; b < n; b++, p++) cost[p] = (double)pair_nnz[p] * (T[a] + T[b]) / (2 * Lm);
+  }
+  double total = 0;
+  for (int64_t p = 0; p < P; p++) total += cost[p] += (double)(n - 2) * pair_nnz[p];
+  bounds[0] = 0;
+  int64_t p = 0;
+  double run = 0;
+  for (int r = 1; r < nranks; r++) {
+    const double target = total * r / nranks;
+    while (p < P && run < target) run += cost[p++];
+    bounds[r] = p;
+  }
+  bounds[nranks] = P;
+  return MLP_OK;
+}
+
 int mlp_gather_layout(int nranks, int64_t npairs, const int64_t* info, int64_t* ebase) {
   if (nranks < 1 || !info || !ebase) return MLP_ERR_ARG;
   ebase[0] = 0;
@@ -1470,11 +1731,11 @@ int mlp_allgather(mlp_ctx* c) {
 }
 
 // ------------------------------------------------------------------ relax
-static int relax_rounds(mlp_ctx* c, int iters, const QpRelax& qp);
+static int relax_rounds(mlp_ctx* c, int iters, const QpRelax& qp, const float* h_w, const float* h_sel);
 
 int mlp_relax(mlp_ctx* c, int iters) {
   if (!c || iters < 0) return MLP_ERR_ARG;
-  return relax_rounds(c, iters, QpRelax{0, nullptr, 0.f, nullptr, 200.f});
+  return relax_rounds(c, iters, QpRelax{0, nullptr, 0.f, nullptr, 200.f}, nullptr, nullptr);
 }
 
 // QuickProbs' consistency stage (ConsistencyStage::operator() / run,
@@ -1501,21 +1762,96 @@ int mlp_relax_qp_selective(mlp_ctx* c, int iters, const float* seq_weights, cons
     dsel = (const float*)c->r_seldist.p;
   }
   HIPCHK(c, hipStreamSynchronize(c->stream));  // the caller's buffers may go away
-  return relax_rounds(c, iters, QpRelax{1, (const float*)c->r_weights.p, 3.0f, dsel, selectivity});
+  return relax_rounds(c, iters, QpRelax{1, (const float*)c->r_weights.p, 3.0f, dsel, selectivity}, seq_weights,
+                      sel_dist);
 }
 
-static int relax_rounds(mlp_ctx* c, int iters, const QpRelax& qp) {
+// Output-pair ranges of one round for S shards / ranks, balanced by the
+// estimated work (mlp_relax_shard_plan).
+static void relax_bounds(const mlp_ctx* c, int S, std::vector<int64_t>& bounds) {
+  bounds.assign(S + 1, 0);
+  mlp_relax_shard_plan(c->n, c->lens.data(), c->nnz.data(), S, bounds.data());
+}
+
+static int relax_one(mlp_ctx* c, const QpRelax& qp, bool last);
+
+static int sharded_relax(mlp_ctx* c, int iters, const QpRelax& qp, const float* h_w, const float* h_sel, int S) {
+  int rc;
+  if ((rc = ensure_shards(c, S))) return rc;
+  std::vector<QpRelax> q(S, qp);
+  if (qp.on) {  // QuickProbs' weights and selectivity matrix on every shard
+    if ((rc = run_shards(c, [&](mlp_ctx* ch, int s) -> int {
+          int r;
+          if ((r = ensure(ch, ch->r_weights, sizeof(float) * c->n))) return r;
+          HIPCHK(ch, hipMemcpy(ch->r_weights.p, h_w, sizeof(float) * c->n, hipMemcpyHostToDevice));
+          q[s].weights = (const float*)ch->r_weights.p;
+          if (h_sel) {
+            const size_t bytes = sizeof(float) * (size_t)c->n * c->n;
+            if ((r = ensure(ch, ch->r_seldist, bytes))) return r;
+            HIPCHK(ch, hipMemcpy(ch->r_seldist.p, h_sel, bytes, hipMemcpyHostToDevice));
+            q[s].seldist = (const float*)ch->r_seldist.p;
+          }
+          return MLP_OK;
+        })))
+      return rc;
+  }
+  for (int it = 0; it < iters; it++) {
+    std::vector<int64_t> bounds;
+    relax_bounds(c, S, bounds);
+    if ((rc = run_shards(c, [&](mlp_ctx* ch, int s) -> int {
+          int r;
+          if ((r = broadcast_store(c, ch))) return r;
+          ch->rel_r0 = bounds[s];
+          ch->rel_r1 = bounds[s + 1];
+          r = relax_one(ch, q[s], it == iters - 1);
+          ch->rel_r0 = ch->rel_r1 = -1;
+          return r;
+        })))
+      return rc;
+    if ((rc = gather_shards(c))) return rc;
+  }
+  return MLP_OK;
+}
+
+static int relax_rounds(mlp_ctx* c, int iters, const QpRelax& qp, const float* h_w, const float* h_sel) {
   if (c->n < 2) return MLP_ERR_STATE;
+  if (c->store_p0 != 0 || c->store_p1 != c->P) {
+    c->err = "relaxation needs every pair (all-gather first)";
+    return MLP_ERR_STATE;
+  }
+  const int S = c->comm ? 1 : shard_count(c);
+  if (S > 1) return sharded_relax(c, iters, qp, h_w, h_sel, S);
+  int rc;
+  for (int it = 0; it < iters; it++) {
+    if ((rc = relax_one(c, qp, it == iters - 1))) return rc;
+    if (c->comm && c->nranks > 1) {
+      if ((rc = mlp_allgather(c))) return rc;
+    }
+  }
+  return MLP_OK;
+}
+
+// One consistency round over output pairs [r0, r1) (all pairs; a shard's
+// range; or this rank's MAC-balanced range with a communicator).
+static int relax_one(mlp_ctx* c, const QpRelax& qp, bool last) {
   if (c->store_p0 != 0 || c->store_p1 != c->P) {
     c->err = "relaxation needs every pair (all-gather first)";
     return MLP_ERR_STATE;
   }
   hipSetDevice(c->device);
   int64_t r0 = 0, r1 = c->P;
-  if (c->comm && c->nranks > 1) mlp_shard_range(c, c->nranks, c->rank, &r0, &r1);
+  if (c->rel_r0 >= 0) {
+    r0 = c->rel_r0;
+    r1 = c->rel_r1;
+  } else if (c->comm && c->nranks > 1) {
+    std::vector<int64_t> bounds;
+    relax_bounds(c, c->nranks, bounds);
+    r0 = bounds[c->rank];
+    r1 = bounds[c->rank + 1];
+  }
   const int64_t nout = r1 - r0;
   int rc;
-  for (int it = 0; it < iters; it++) {
+  {
     const int64_t total = c->store_total;
     if ((rc = ensure(c, c->r_trowptr, sizeof(int32_t) * c->trp_off[c->P]))) return rc;
     if ((rc = ensure(c, c->r_tcols, sizeof(uint16_t) * std::max<int64_t>(total, 1)))) return rc;
@@ -1740,14 +2076,16 @@ static int relax_rounds(mlp_ctx* c, int iters, const QpRelax& qp) {
     fa.pairs = (const int64_t*)c->r_pairs.p;
     fa.npairs = nout;
     fa.write = 0;
-    fa.cutoff = qp.on && it == iters - 1 ? 1e-5f : 0.01f;
+    fa.cutoff = qp.on && last ? 1e-5f : 0.01f;
     fa.fixed16 = qp.on;
     {
       Timer t(c, KFILTER, 0);
       HIPCHK(c, launch_filter(fa, c->stream));
     }
     std::vector<int64_t> pn(nout);
-    HIPCHK(c, hipMemcpyAsync(pn.data(), c->r_nnz.p, sizeof(int64_t) * nout, hipMemcpyDeviceToHost, c->stream));
+    // k_filter writes pair_nnz at the global pair index
+    HIPCHK(c, hipMemcpyAsync(pn.data(), (const int64_t*)c->r_nnz.p + r0, sizeof(int64_t) * nout, hipMemcpyDeviceToHost,
+                             c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     // new canonical offsets of my pairs, starting at 0 (gathered below)
     std::vector<int64_t> noff(c->P + 1, 0);
@@ -1785,15 +2123,16 @@ static int relax_rounds(mlp_ctx* c, int iters, const QpRelax& qp) {
     c->store_total = run; ++c->store_ver;
     HIPCHK(c, hipMemcpyAsync(c->d_ent_off, c->ent_off.data(), sizeof(int64_t) * (c->P + 1), hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    if (c->comm && c->nranks > 1) {
-      if ((rc = mlp_allgather(c))) return rc;
-    }
   }
   return MLP_OK;
 }
 
 int mlp_synchronize(mlp_ctx* c) {
   if (!c) return MLP_ERR_ARG;
+  for (mlp_ctx* ch : c->shards) {
+    hipSetDevice(ch->device);
+    HIPCHK(c, hipStreamSynchronize(ch->stream));
+  }
   hipSetDevice(c->device);
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return MLP_OK;
@@ -1802,11 +2141,13 @@ int mlp_synchronize(mlp_ctx* c) {
 int mlp_profile(mlp_ctx* c, int enable) {
   if (!c) return MLP_ERR_ARG;
   c->profile = enable != 0;
+  for (mlp_ctx* ch : c->shards) ch->profile = c->profile;
   return MLP_OK;
 }
 
 int mlp_profile_reset(mlp_ctx* c) {
   if (!c) return MLP_ERR_ARG;
+  for (mlp_ctx* ch : c->shards) mlp_profile_reset(ch);
   flush_timers(c);
   for (int k = 0; k < MLP_NKERNELS; k++) {
     c->kms[k] = 0;
@@ -1819,10 +2160,22 @@ int mlp_profile_reset(mlp_ctx* c) {
 int mlp_kernel_times(mlp_ctx* c, double* ms, int64_t* launches, int64_t* cells) {
   if (!c) return MLP_ERR_ARG;
   flush_timers(c);
-  for (int k = 0; k < MLP_NKERNELS; k++) {
-    if (ms) ms[k] = c->kms[k];
-    if (launches) launches[k] = c->klaunch[k];
-    if (cells) cells[k] = c->kcells[k];
+  for (mlp_ctx* ch : c->shards) {
+    hipSetDevice(ch->device);
+    flush_timers(ch);
+  }
+  hipSetDevice(c->device);
+  for (int k = 0; k < MLP_NKERNELS; k++) {  // shards: device time summed over the shards
+    double m = c->kms[k];
+    int64_t l = c->klaunch[k], e = c->kcells[k];
+    for (const mlp_ctx* ch : c->shards) {
+      m += ch->kms[k];
+      l += ch->klaunch[k];
+      e += ch->kcells[k];
+    }
+    if (ms) ms[k] = m;
+    if (launches) launches[k] = l;
+    if (cells) cells[k] = e;
   }
   return MLP_OK;
 }

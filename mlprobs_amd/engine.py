@@ -87,6 +87,10 @@ def lib():
         L.mlp_profile.argtypes = [P, C.c_int]
         L.mlp_profile_reset.argtypes = [P]
         L.mlp_kernel_times.argtypes = [P, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.mlp_ctx_create_mask.argtypes = [C.c_uint64, C.POINTER(P)]
+        L.mlp_set_shards.argtypes = [P, C.c_int]
+        L.mlp_shard_count.argtypes = [P]
+        L.mlp_relax_shard_plan.argtypes = [C.c_int, I32P, I64P, C.c_int, I64P]
         _LIB = L
     return _LIB
 
@@ -97,7 +101,8 @@ EXPORTED = ['mlp_ctx_create', 'mlp_ctx_destroy', 'mlp_last_error', 'mlp_set_scra
             'mlp_relax_qp_selective', 'mlp_profile_posterior', 'mlp_profile_result', 'mlp_viterbi', 'mlp_viterbi_results',
             'mlp_viterbi_path', 'mlp_model_adjustment', 'mlp_family_features', 'mlp_comm_unique_id', 'mlp_comm_init',
             'mlp_shard_range', 'mlp_shard_plan', 'mlp_gather_layout', 'mlp_allgather', 'mlp_synchronize', 'mlp_profile',
-            'mlp_kernel_times', 'mlp_profile_reset']
+            'mlp_kernel_times', 'mlp_profile_reset', 'mlp_ctx_create_mask', 'mlp_set_shards', 'mlp_shard_count',
+            'mlp_relax_shard_plan']
 
 
 def shard_plan(lens, nranks, rank):
@@ -109,6 +114,19 @@ def shard_plan(lens, nranks, rank):
     if rc != 0:
         raise MlpError(rc, 'mlp_shard_plan')
     return b.value, e.value
+
+
+def relax_shard_plan(lens, pair_nnz, nranks):
+    """bounds[nranks + 1] of the consistency-round output-pair ranges,
+    balanced by estimated multiply-adds (host only: the split every rank and
+    every in-process shard applies)."""
+    lens = np.ascontiguousarray(lens, np.int32)
+    nnz = np.ascontiguousarray(pair_nnz, np.int64)
+    b = np.zeros(int(nranks) + 1, np.int64)
+    rc = lib().mlp_relax_shard_plan(len(lens), lens, nnz, int(nranks), b)
+    if rc != 0:
+        raise MlpError(rc, 'mlp_relax_shard_plan')
+    return b
 
 
 def gather_layout(npairs, shards):
@@ -135,10 +153,19 @@ def pairs_of(n):
 class Family:
     """One MLProbs family resident on one GPU."""
 
-    def __init__(self, seqs, device=0):
+    def __init__(self, seqs, device=0, device_mask=None, shards=None):
+        """device: one GPU; device_mask: every GPU of the mask from this one
+        context (mlp_ctx_create_mask); shards: force that many shards (virtual
+        shards may share a GPU)."""
         self._L = lib()
         self._ctx = C.c_void_p()
-        self._chk(self._L.mlp_ctx_create(int(device), C.byref(self._ctx)), ctx=False)
+        if device_mask is not None or shards:
+            mask = device_mask if device_mask is not None else (1 << int(device))
+            self._chk(self._L.mlp_ctx_create_mask(int(mask), C.byref(self._ctx)), ctx=False)
+        else:
+            self._chk(self._L.mlp_ctx_create(int(device), C.byref(self._ctx)), ctx=False)
+        if shards:
+            self._chk(self._L.mlp_set_shards(self._ctx, int(shards)), ctx=False)
         self.seqs = [s.upper() for s in seqs]
         self.n = len(self.seqs)
         self.lens = np.array([len(s) for s in self.seqs], np.int64)

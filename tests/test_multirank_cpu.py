@@ -140,3 +140,91 @@ def test_gather_layout_rejects_gaps():
         engine.gather_layout(10, [(0, 3, 5), (4, 10, 2)])
     with pytest.raises(engine.MlpError):
         engine.gather_layout(10, [(0, 3, 5), (3, 9, 2)])
+
+
+# ---- consistency rounds: output pairs split by estimated multiply-adds
+def _relax_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        import orc
+        from mlprobs_amd import engine
+        fam = _family()
+        lens = np.array([len(s) for s in fam], np.int32)
+        P = len(fam) * (len(fam) - 1) // 2
+        rp, cols, vals, _ = _store(fam, 0, 0, P)  # every rank holds the whole set (after the gather)
+        eo = np.zeros(P + 1, np.int64)
+        L1, ro, _ = orc.store_view(lens, np.arange(P), rp, np.zeros(P + 1, np.int64))
+        for p in range(P):
+            eo[p + 1] = eo[p] + rp[ro[p] + L1[p] + 1]
+        bounds = engine.relax_shard_plan(lens, np.diff(eo), world)
+        sel = np.zeros(P, np.uint8)
+        sel[bounds[rank]:bounds[rank + 1]] = 1
+        o_rp, o_eo, o_c, o_v = orc.relax_subset(lens, rp, eo, cols, vals, sel)
+        mine = [(p, o_rp[ro[p]:ro[p] + L1[p] + 2].copy(), o_c[o_eo[p]:o_eo[p + 1]].copy(),
+                 o_v[o_eo[p]:o_eo[p + 1]].copy()) for p in range(bounds[rank], bounds[rank + 1])]
+        allb = [None] * world
+        dist.all_gather_object(allb, (list(bounds), mine))
+        q.put((rank, allb))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_relaxation_matches_single_process():
+    import orc
+    world = 3
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_relax_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    fam = _family()
+    lens = [len(s) for s in fam]
+    P = len(fam) * (len(fam) - 1) // 2
+    rp, cols, vals, _ = _store(fam, 0, 0, P)
+    L1, ro, _ = orc.store_view(lens, np.arange(P), rp, np.zeros(P + 1, np.int64))
+    blocks, e = [], 0
+    for p in range(P):
+        r = rp[ro[p]:ro[p] + L1[p] + 2]
+        blocks.append((r.astype(np.int32), cols[e:e + r[-1]].astype(np.int32), vals[e:e + r[-1]]))
+        e += r[-1]
+    ref = orc.relax(lens, blocks)
+    for rank, allb in got:
+        bounds = allb[0][0]
+        assert all(b[0] == bounds for b in allb) and bounds[0] == 0 and bounds[-1] == P
+        seen = set()
+        for _, mine in allb:
+            for p, r, c, v in mine:
+                assert np.array_equal(r, ref[p][0]) and np.array_equal(c, ref[p][1]) and np.array_equal(v, ref[p][2])
+                seen.add(p)
+        assert seen == set(range(P))
+
+
+def test_relax_shard_plan_balance():
+    """Ranges tile the pairs in order; each range's estimated work is within
+    one pair of the mean (the estimate is recomputed here in numpy)."""
+    from mlprobs_amd import engine
+    rng = np.random.default_rng(9)
+    n = 40
+    lens = rng.integers(30, 300, size=n).astype(np.int32)
+    P = n * (n - 1) // 2
+    nnz = rng.integers(0, 4000, size=P).astype(np.int64)
+    nnz[rng.random(P) < 0.2] = 0
+    M = np.zeros((n, n))
+    k = 0
+    for a in range(n):
+        for b in range(a + 1, n):
+            M[a, b] = M[b, a] = nnz[k]
+            k += 1
+    est = (M / lens[None, :]) @ M
+    cost = np.array([est[a, b] for a in range(n) for b in range(a + 1, n)]) + (n - 2) * nnz
+    for R in (1, 2, 5, 8):
+        b = engine.relax_shard_plan(lens, nnz, R)
+        assert b[0] == 0 and b[-1] == P and all(b[r] <= b[r + 1] for r in range(R))
+        loads = [cost[b[r]:b[r + 1]].sum() for r in range(R)]
+        assert max(loads) <= cost.sum() / R + cost.max() * 1.0001
