@@ -479,6 +479,8 @@ int orc_pf_posterior(const char *s1, int L1, const char *s2, int L2, float *post
 
 int orc_pair_posterior(const orc_model *m, const char *s1, int L1, const char *s2, int L2,
                        int pid, float *post) {
+  const int npdo = pid & ORC_NPDO;  /* ArrangePosteriorProbs' merge order (CPNP/MSA.cpp:1699-1708) */
+  pid &= ~ORC_NPDO;
   size_t cells = (size_t)(L1 + 1) * (L2 + 1);
   if (pid >= 3) return orc_pf_posterior(s1, L1, s2, L2, post);
   float *F = malloc(sizeof(float) * 5 * cells), *B = malloc(sizeof(float) * 5 * cells);
@@ -497,10 +499,11 @@ int orc_pair_posterior(const orc_model *m, const char *s1, int L1, const char *s
   orc_forward(m, s1, L1, s2, L2, 0, F);
   orc_backward(m, s1, L1, s2, L2, 0, B);
   orc_posterior(m, s1, L1, s2, L2, F, B, 0, post);
-  /* CPNP/MSA.cpp:992-1007 */
+  /* CPNP/MSA.cpp:992-1007 (pdoAlign: double affine, global, local);
+   * CPNP/MSA.cpp:1699-1708 (ArrangePosteriorProbs: global, local, double affine) */
   for (size_t c = 0; c < cells; c++) {
     float v1 = p5[c], v2 = pg[c], v3 = post[c];
-    post[c] = sqrtf((v1 * v1 + v2 * v2 + v3 * v3) / 3);
+    post[c] = npdo ? sqrtf((v2 * v2 + v3 * v3 + v1 * v1) / 3) : sqrtf((v1 * v1 + v2 * v2 + v3 * v3) / 3);
   }
   free(F); free(B); free(p5); free(pg);
   return rc;
@@ -1114,9 +1117,19 @@ int64_t orc_pairs_csr(const orc_model *m, int N, const char *const *seqs, const 
     int L1 = lens[a], L2 = lens[b];
     float *post = malloc(sizeof(float) * (size_t)(L1 + 1) * (L2 + 1));
     orc_pair_posterior(m, seqs[a], L1, seqs[b], L2, pid, post);
-    float score = orc_mea(L1, L2, post, NULL, NULL);
+    float score;
+    if (pid & ORC_NPDO) {  /* distance = score / #B (CPNP/MSA.cpp:1744-1753) */
+      char *path = malloc((size_t)L1 + L2 + 1);
+      int plen = 0, nb = 0;
+      score = orc_mea(L1, L2, post, path, &plen);
+      for (int t = 0; t < plen; t++) nb += path[t] == 'B';
+      free(path);
+      if (dist_out) dist_out[k] = score / nb;
+    } else {
+      score = orc_mea(L1, L2, post, NULL, NULL);
+      if (dist_out) dist_out[k] = 1.0f - score / (L1 < L2 ? L1 : L2);
+    }
     if (mea_out) mea_out[k] = score;
-    if (dist_out) dist_out[k] = 1.0f - score / (L1 < L2 ? L1 : L2);
     int32_t *rp = rowptr + roff[k];
     int64_t nnz = orc_sparsify(L1, L2, post, rp, NULL, NULL);
     pc[k] = malloc(sizeof(int32_t) * (nnz ? nnz : 1));

@@ -422,6 +422,41 @@ static int cmd_bench(int argc, char **argv) {
   return 0;
 }
 
+// npdo <fasta> <pid> <delta> <dump>
+// The reference's own ArrangePosteriorProbs (CPNP/MSA.cpp:1636-1765, the
+// npdoAlign pair loop) over every pair: sparse matrices and the distances
+// score / #B, in the dump_pairs format (mea field unused).
+static int cmd_npdo(int argc, char **argv) {
+  if (argc < 4) return 2;
+  MultiSequence *seqs = load(argv[0]);
+  const int pid = atoi(argv[1]);
+  MSA *m = fake_msa();
+  setup_params(m);
+  initDistrib[2] = (float)atof(argv[2]);
+  ProbabilisticModel model(initDistrib, gapOpen, gapExtend, emitPairs, emitSingle);
+  const int n = seqs->GetNumSequences();
+  std::vector<std::pair<int, int> > pairs;
+  for (int a = 0; a < n; a++)
+    for (int b = a + 1; b < n; b++) pairs.push_back({a, b});
+  m->numPairs = (int)pairs.size();
+  m->seqsPairs = new MSA::SeqsPair[pairs.size()];
+  for (size_t k = 0; k < pairs.size(); k++) {
+    m->seqsPairs[k].seq1 = pairs[k].first;
+    m->seqsPairs[k].seq2 = pairs[k].second;
+  }
+  SafeVector<SafeVector<SparseMatrix *> > sparse(n, SafeVector<SparseMatrix *>(n, NULL));
+  VVF distances(n, VF(n, 0));
+  m->ArrangePosteriorProbs(seqs, model, sparse, distances, pid);
+  std::vector<SparseMatrix *> sm;
+  std::vector<float> dist;
+  for (auto &pr : pairs) {
+    sm.push_back(sparse[pr.first][pr.second]);
+    dist.push_back(distances[pr.first][pr.second]);
+  }
+  dump_pairs(argv[3], pairs, sm, dist, {});
+  return 0;
+}
+
 // relaxbench <fasta> <store> <sample> <threads> <dump>  -> JSON on stdout
 // Times the reference's MSA::DoRelaxation (CPNP/MSA.cpp:1172-1281, its own
 // pair loop over seqsPairs) on a strided sample of `sample` output pairs,
@@ -512,6 +547,7 @@ int main(int argc, char **argv) {
   std::string cmd = argv[1];
   if (cmd == "bench") return cmd_bench(argc - 2, argv + 2);
   if (cmd == "relaxbench") return cmd_relaxbench(argc - 2, argv + 2);
+  if (cmd == "npdo") return cmd_npdo(argc - 2, argv + 2);
   const char *outp = getenv("REF_PROBE_OUT");
   if (!outp) {
     fprintf(stderr, "set REF_PROBE_OUT\n");
