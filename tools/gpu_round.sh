@@ -1,0 +1,17 @@
+#!/bin/bash
+# One GPU-box call: the -m gpu suite, smoke(), then the bench line with its
+# rocprofv3 kernel statistics from the same command.
+#   tools/gpu_round.sh TAG [pytest args...] -> gpurun_out/TAG/{gputest.log,smoke.log,bench.json,stats/}
+set -o pipefail
+export TMPDIR=/tmp
+TAG=${1:-round}; shift
+O=gpurun_out/$TAG
+mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "$@" \
+    > $O/gputest.log 2>&1 || { tail -30 $O/gputest.log; exit 1; }
+tail -3 $O/gputest.log
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { cat $O/smoke.log; exit 1; }
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o stats -- python3 bench.py \
+    > $O/bench.log 2>&1 || { tail -30 $O/bench.log; exit 1; }
+grep '^{"metric"' $O/bench.log | tail -1 > $O/bench.json
+echo done
