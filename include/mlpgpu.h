@@ -77,11 +77,14 @@ int mlp_family_load(mlp_ctx *ctx, int n, const char *residues, const int64_t *of
 int64_t mlp_family_npairs(const mlp_ctx *ctx);
 
 /* Posterior stage for pairs [p_begin, p_end) in pair order.  Replaces the
- * body of the pdoAlign / ArrangePosteriorProbs pair loop
- * (CPNP/MSA.cpp:927-1032, 1652-1765): per pid, the 5-state + partition
- * function + local posteriors merged by RMS (pid 0/1), local only (pid 2) or
- * partition function only (pid >= 3); the MEA distance
+ * body of the pdoAlign pair loop (CPNP/MSA.cpp:927-1032): per pid, the
+ * 5-state + partition function + local posteriors merged by RMS (pid 0/1),
+ * local only (pid 2) or partition function only (pid >= 3); the MEA distance
  * 1 - score / min(L_a, L_b); and the sparse matrix (>= 0.01).
+ * pid | MLP_PID_NPDO replaces npdoAlign's ArrangePosteriorProbs loop
+ * (CPNP/MSA.cpp:1636-1765) instead: the same models, the RMS terms summed in
+ * its order (global, local, 5-state) and the distance score / #B, #B = the
+ * match columns of the MEA path (CPNP/MSA.cpp:1744-1753).
  * delta = initDistrib[2] after ModelAdjustmentTest (CPNP/MSA.cpp:861-870).
  * pid = MLP_PID_QP runs QuickProbs' posterior stage instead (the realigner
  * MLProbs calls, PosteriorStage::computePairwise + combineMatrices,
@@ -91,6 +94,7 @@ int64_t mlp_family_npairs(const mlp_ctx *ctx);
  * 16-bit fixed point q read back as q / 65535 (delta is ignored).
  * Results stay in device memory in the context's canonical CSR store. */
 #define MLP_PID_QP 16
+#define MLP_PID_NPDO 32
 int mlp_posteriors(mlp_ctx *ctx, int pid, float delta, int64_t p_begin, int64_t p_end);
 
 /* Per-pair scalars of pairs [p_begin, p_end) (host arrays, may be NULL):

@@ -6,8 +6,8 @@
 // print to stderr and exit(1); success is silent on stderr, exit 0.
 //   -G            the family-test feature line (Alter_ModelAdjustmentTest)
 //   -p 0          progressive alignment (pdoAlign, CPNP/MSA.cpp:895-1081)
-//   -p 1          non-progressive alignment (npdoAlign): not in this build,
-//                 exits 1 so MLProbs.py falls back to its realigner
+//   -p 1          non-progressive alignment (npdoAlign, CPNP/MSA.cpp:1084-1140):
+//                 alignment graph + similarity-set refinement (np_host.cpp)
 //   -c N, -ir N, -co F, -o FILE, -a, -v, -annot FILE, -clustalw, -timeon/-timeoff
 #include <stdio.h>
 #include <stdlib.h>
@@ -183,11 +183,6 @@ int main(int argc, char** argv) {
     mlp_ctx_destroy(ctx);
     return 0;
   }
-  if (!progressive) {
-    mlp_ctx_destroy(ctx);
-    fail("ERROR: the non-progressive strategy (-p 1) is not available in this build");
-  }
-
   cpnp::Profile aln;
   if (n == 1) {
     aln.push_back(seqs[0]);
@@ -198,17 +193,22 @@ int main(int argc, char** argv) {
     check(ctx, mlp_model_adjustment(ctx, &identity, &variance, &delta, &code), "family test");
     stage("family test (Viterbi)");
     const int pid = code % 10, vpid = code / 10;
-    // pdoAlign (CPNP/MSA.cpp:895-1081): posteriors, distances, tree, consistency
+    // pdoAlign (CPNP/MSA.cpp:895-1081): posteriors, distances, tree, consistency;
+    // npdoAlign (CPNP/MSA.cpp:1084-1140): ArrangePosteriorProbs' pair body,
+    // consistency, alignment graph, refinement
     const int64_t P = mlp_family_npairs(ctx);
-    check(ctx, mlp_posteriors(ctx, pid, delta, 0, P), "posteriors");
+    check(ctx, mlp_posteriors(ctx, progressive ? pid : pid | MLP_PID_NPDO, delta, 0, P), "posteriors");
     std::vector<float> dist(P);
     check(ctx, mlp_pair_results(ctx, 0, P, dist.data(), nullptr, nullptr), "results");
     std::vector<std::vector<float>> D(n, std::vector<float>(n, 0.f));
     for (int a = 0, p = 0; a < n; a++)
       for (int b = a + 1; b < n; b++, p++) D[a][b] = D[b][a] = dist[p];
     stage("posteriors");
-    const cpnp::GuideTree tree = cpnp::build_tree(D, vpid);
-    stage("guide tree");
+    cpnp::GuideTree tree;
+    if (progressive) {
+      tree = cpnp::build_tree(D, vpid);
+      stage("guide tree");
+    }
     if (opt.consistency > 0) check(ctx, mlp_relax(ctx, opt.consistency), "consistency");
     check(ctx, mlp_synchronize(ctx), "consistency");
     stage("consistency");
@@ -228,8 +228,15 @@ int main(int argc, char** argv) {
     check(ctx, mlp_csr_export(ctx, sp.row_ptr.data(), sp.ent_off.data(), sp.cols.data(), sp.vals.data()),
           "sparse set");
     stage("sparse set to host");
-    aln = cpnp::progressive_alignment(seqs, sp, tree, pid, opt);
-    stage("progressive + refinement");
+    if (progressive) {
+      aln = cpnp::progressive_alignment(seqs, sp, tree, pid, opt);
+      stage("progressive + refinement");
+    } else {
+      aln = cpnp::graph_alignment(seqs, sp);
+      stage("alignment graph");
+      aln = cpnp::np_refinement(std::move(aln), sp, D, opt);
+      stage("refinement");
+    }
   }
   mlp_ctx_destroy(ctx);
   std::string out;

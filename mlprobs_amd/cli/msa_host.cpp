@@ -403,7 +403,7 @@ Profile merge(const Profile& a, const Profile& b, const std::string& path, bool 
 }
 
 // MultiSequence::Project (MultiSequence.h:662-734)
-static Profile project(const Profile& p, const std::set<int>& idx) {
+Profile project(const Profile& p, const std::set<int>& idx) {
   const int L = p[*idx.begin()].length();
   std::vector<int> keep;
   for (int i = 1; i <= L; i++) {
@@ -438,22 +438,27 @@ static Profile process_tree(const GuideTree& t, int node, const std::vector<Row>
   return merge(left, right, path, !opt.align_order);
 }
 
-// The refinement splits come from the C library's rand() at its default seed
-// (the -p 0 path never seeds it, CPNP/MSA.cpp:1545).  The GPU runtime
+// The refinement splits come from the C library's rand(): at its default
+// seed in the -p 0 path (which never seeds it, CPNP/MSA.cpp:1545), seeded with
+// srand(time(0)) in the -p 1 refinement (CPNP/MSA.cpp:1896).  The GPU runtime
 // libraries of this build may draw from the shared libc generator during
-// initialisation, so the sequence is reproduced here instead: glibc's
-// TYPE_3 additive feedback generator (r[i] = r[i-3] + r[i-31], seeded by
-// the Park-Miller recurrence, first 310 outputs discarded), seed 1.
+// initialisation, so the generator is reproduced here instead: glibc's
+// TYPE_3 additive feedback generator (r[i] = r[i-3] + r[i-31]) seeded as
+// srandom_r does (Park-Miller by Schrage's method, first 310 outputs
+// discarded).
 namespace {
 struct LibcRand {
   uint32_t r[34];
   int k = 0;
-  LibcRand() {
+  explicit LibcRand(uint32_t seed = 1) {
     int32_t s[34];
-    s[0] = 1;
+    s[0] = (int32_t)(seed ? seed : 1);
+    int32_t word = s[0];
     for (int i = 1; i < 31; i++) {
-      const int64_t v = (16807LL * s[i - 1]) % 2147483647;
-      s[i] = (int32_t)(v < 0 ? v + 2147483647 : v);
+      const long hi = word / 127773, lo = word % 127773;
+      long w = 16807 * lo - 2836 * hi;
+      if (w < 0) w += 2147483647;
+      s[i] = word = (int32_t)w;
     }
     for (int i = 31; i < 34; i++) s[i] = s[i - 31];
     for (int i = 0; i < 34; i++) r[i] = (uint32_t)s[i];
@@ -474,6 +479,9 @@ LibcRand& libc_rand() {
   return g;
 }
 }  // namespace
+
+void libc_srand(uint32_t seed) { libc_rand() = LibcRand(seed); }
+int libc_rand_next() { return libc_rand().next(); }
 
 // DoIterativeRefinement (MSA.cpp:1537-1625): 2 = no split, 1 = unchanged score
 static int refine_once(Profile& aln, const SparseSet& sp, const Options& opt) {

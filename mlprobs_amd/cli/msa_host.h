@@ -7,6 +7,7 @@
 #pragma once
 #include <stdint.h>
 
+#include <set>
 #include <string>
 #include <vector>
 
@@ -79,6 +80,14 @@ std::string mea_path_tiled(int len1, int len2, const float* post, float* score);
 // Profile merge along a path (Sequence.h AddGaps) and helpers.
 Profile merge(const Profile& a, const Profile& b, const std::string& path, bool sort_by_label);
 
+// MultiSequence::Project (MultiSequence.h:662-734): the rows of `idx`, in
+// index order, without the columns that are gaps in all of them.
+Profile project(const Profile& p, const std::set<int>& idx);
+
+// The C library's rand() / srand() sequence (glibc TYPE_3), reproduced.
+void libc_srand(uint32_t seed);
+int libc_rand_next();
+
 struct Options {
   int consistency = 2;          // -c
   int refinement = 100;         // -ir
@@ -91,5 +100,16 @@ struct Options {
 // refinement (MSA.cpp:1369-1635, ComputeFinalAlignment).
 Profile progressive_alignment(const std::vector<Row>& seqs, const SparseSet& sp, const GuideTree& tree,
                               int pid, Options& opt);
+
+// Non-progressive strategy (c_p_np_aln -p 1, MSA::npdoAlign,
+// CPNP/MSA.cpp:1084-1140) after posteriors and consistency:
+// the alignment graph of every sparse entry (ComputeGraph + AlignGraph,
+// CPNP/MSA.cpp:1776-1844, AlignGraph.h:894-1160), rows in input order ...
+Profile graph_alignment(const std::vector<Row>& seqs, const SparseSet& sp);
+// ... and its refinement (DoRefinement + FindSimilar, CPNP/MSA.cpp:1852-2082)
+// over the npdoAlign distances (score / #B).  Seeds rand() from time(0) per
+// pass like the reference; MLP_SRAND_TIME fixes that clock (tests).
+Profile np_refinement(Profile aln, const SparseSet& sp, const std::vector<std::vector<float>>& dist,
+                      const Options& opt);
 
 }  // namespace cpnp

@@ -87,7 +87,7 @@ struct PairRec {           // per-pair scalars produced along the pipeline
   int32_t zexp;            // PF total Z frame
   int32_t flags;           // bit0: PF overflow, bit1: ELL overflow
   float mea;               // MEA score
-  float dist;              // 1 - mea / min(L1, L2)
+  float dist;              // 1 - mea / min(L1, L2); npdoAlign: mea / #B
   int64_t nnz;             // sparse entries of the pair
 };
 
@@ -109,6 +109,7 @@ struct Scratch {
   double* bndz;            // 3 doubles per column
   int32_t* bnde;           // 1 int per column
   float* bndm;             // MEA boundary: 1 float per column
+  int32_t* bndc;           // MEA boundary #B counts (npdoAlign distance): 1 int per column
   uint16_t* ell_col;       // [ell row][kEll]
   float* ell_val;
   int32_t* ell_cnt;        // [ell row]
@@ -130,8 +131,10 @@ struct VitOut {
 // posteriors in [0.001, 1]; the merge is the RMS of two models.
 enum ModelSet : int { kHmm5 = 1, kLocal = 2, kPF = 4, kQP = 8 };
 constexpr int kPidQP = 16;  // pid code of the QuickProbs posterior stage (include/mlpgpu.h MLP_PID_QP)
+constexpr int kPidNpdo = 32;  // flag: npdoAlign's pair body (include/mlpgpu.h MLP_PID_NPDO)
 
 inline int model_set_for_pid(int pid) {
+  pid &= ~kPidNpdo;
   if (pid == kPidQP) return kHmm5 | kPF | kQP;
   if (pid == 2) return kLocal;
   if (pid >= 3) return kPF;

@@ -897,7 +897,7 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
     const int L1 = c->lens[c->pa[q]], L2 = c->lens[c->pb[q]];
     const int64_t rmc = (int64_t)L1 * ((L2 + 3) & ~3);
     return (size_t)(pair_slots_bound(c, q) * 20 + rmc * 8) +
-           (size_t)pair_width_bound(c, q) * (5 * 4 + 3 * 4 + 3 * 8 + 4 + 4) +
+           (size_t)pair_width_bound(c, q) * (5 * 4 + 3 * 4 + 3 * 8 + 4 + 4 + 4) +
            (size_t)L1 * (kEll * 6 + 4) + kPerSlotMeta;
   };
   // Batches run one after another on the context stream (two batches
@@ -999,7 +999,7 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
     const size_t o_f5 = cv.take(P.cells * 4), o_fl = cv.take(P.cells * 4), o_pg = cv.take(P.cells * 4),
                  o_zm = cv.take(P.cells * 8), o_chf = cv.take(P.rm_total * 4), o_chb = cv.take(P.rm_total * 4),
                  o_b5 = cv.take(P.bnd * 20), o_bl = cv.take(P.bnd * 12), o_bz = cv.take(P.bnd * 24),
-                 o_be = cv.take(P.bnd * 4), o_bm = cv.take(P.bnd * 4), o_ec = cv.take(P.ell_rows * kEll * 2),
+                 o_be = cv.take(P.bnd * 4), o_bm = cv.take(P.bnd * 4), o_bc = cv.take(P.bnd * 4), o_ec = cv.take(P.ell_rows * kEll * 2),
                  o_ev = cv.take(P.ell_rows * kEll * 4), o_en = cv.take(P.ell_rows * 4),
                  o_entb = cv.take(np * 8), o_rpb = cv.take(np * 8), o_rec = cv.take(np * sizeof(PairRec));
     const PlanDev pd = carve_plan(cv, P);
@@ -1022,6 +1022,7 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
     sc.bndz = (double*)(base + o_bz);
     sc.bnde = (int32_t*)(base + o_be);
     sc.bndm = (float*)(base + o_bm);
+    sc.bndc = (int32_t*)(base + o_bc);
     sc.ell_col = (uint16_t*)(base + o_ec);
     sc.ell_val = (float*)(base + o_ev);
     sc.ell_cnt = (int32_t*)(base + o_en);

@@ -512,7 +512,13 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
 // =====================================================================
 // Merge + MEA + sparsify: forward-order sweep over the merged posterior.
 // =====================================================================
-template <int M, int PID>
+// NP: the ArrangePosteriorProbs pair body of npdoAlign (CPNP/MSA.cpp:1670-1753):
+// pid 0/1 merge the squares in its order (global, local, 5-state), and the
+// distance is score / #B of the MEA path.  #B rides along the value
+// recurrence: every cell carries the B count of the path its ChooseBestOfThree
+// choice extends (the traceback follows exactly those choices), so the last
+// cell holds the count of the traced path without a traceback matrix.
+template <int M, int PID, bool NP = false>
 #ifndef MLP_MERGE_WAVES
 #define MLP_MERGE_WAVES 6
 #endif
@@ -536,9 +542,11 @@ __global__ __launch_bounds__(256, MLP_MERGE_WAVES) void k_merge(ModelScalars ms,
   Cursor c;
   cursor_start_fwd(c, C, noins, lane);
   float Lv = 0.f, Uv = 0.f, Dv = 0.f;
+  int Lc = 0, Uc = 0, Dc = 0;   // NP: #B of the path into the left / up / diagonal cell
   int cnt = 0;
   // MEA boundary row (stacked row 64k - 1), double-buffered as in BoundaryChunks
   float bch = 0.f, bnx = 0.f;
+  int cch = 0, cnx = 0;
   constexpr int QD = 8;
   // fixed-register load queue: slot u serves steps t0 + u (segments hold
   // whole groups of QD steps); values of idle cells are never used
@@ -560,6 +568,10 @@ __global__ __launch_bounds__(256, MLP_MERGE_WAVES) void k_merge(ModelScalars ms,
         boundary_fence();
         bch = bnx;
         bnx = sc.bndm[bo + min((m + 1 < nseg ? 64 * (m + 1) : 0) + lane, W - 1)];
+        if constexpr (NP) {
+          cch = cnx;
+          cnx = sc.bndc[bo + min((m + 1 < nseg ? 64 * (m + 1) : 0) + lane, W - 1)];
+        }
       }
       const bool take_bnd = k >= 1 && k < S;
       for (int t0 = t_lo; t0 < t_hi; t0 += QD)
@@ -570,6 +582,10 @@ __global__ __launch_bounds__(256, MLP_MERGE_WAVES) void k_merge(ModelScalars ms,
         const float f5v = q5[u], flv = ql[u], pgv = qg[u];
         Dv = Uv;
         Uv = take_bnd ? mlp_shr1(Lv, readlane_f(bch, t - t_lo)) : mlp_shr1z(Lv);
+        if constexpr (NP) {
+          Dc = Uc;
+          Uc = take_bnd ? mlp_shr1i(Lc, __builtin_amdgcn_readlane(cch, t - t_lo)) : mlp_shr1zi(Lc);
+        }
         const bool act = c.q >= 0 && i >= 1 && j >= 1 && j <= L2;
         float P = 0.f;
         if (act) {
@@ -587,14 +603,20 @@ __global__ __launch_bounds__(256, MLP_MERGE_WAVES) void k_merge(ModelScalars ms,
             const float v1 = mlp_post_from_sum_t(f5v, c.T5, ex);
             const float v2 = pgv;
             const float v3 = mlp_post_from_sum_t(flv, c.TL, ex);
-            P = sqrtf((v1 * v1 + v2 * v2 + v3 * v3) / 3);
+            if constexpr (NP)
+              P = sqrtf((v2 * v2 + v3 * v3 + v1 * v1) / 3);  // CPNP/MSA.cpp:1699-1708
+            else
+              P = sqrtf((v1 * v1 + v2 * v2 + v3 * v3) / 3);  // CPNP/MSA.cpp:992-1001
           }
         }
         // MEA (CPNP/ProbabilisticModel.h:831-834): value of ChooseBestOfThree
         float Cv = 0.f;
+        int Cc = 0;
         if (act) {
           const float x1 = P + Dv, x2 = Lv, x3 = Uv;
           Cv = fmaxf(fmaxf(x1, x2), x3);
+          if constexpr (NP)  // ChooseBestOfThree's pick (ScoreType.h:347-366): D, else L, else U
+            Cc = (x1 >= x2 && x1 >= x3) ? Dc + 1 : (x1 < x2 && x2 >= x3) ? Lc : Uc;
           const int64_t erow = c.ell + (i - 1);
           if (P >= 0.01f) {  // POSTERIOR_CUTOFF (CPNP/SparseMatrix.h:14)
             if (cnt < kEll) {
@@ -614,12 +636,19 @@ __global__ __launch_bounds__(256, MLP_MERGE_WAVES) void k_merge(ModelScalars ms,
             cnt = 0;
             if (i == L1) {
               rec[c.slot].mea = Cv;
-              rec[c.slot].dist = 1.0f - Cv / (float)min(L1, L2);
+              if constexpr (NP)
+                rec[c.slot].dist = Cv / (float)Cc;  // CPNP/MSA.cpp:1744-1753
+              else
+                rec[c.slot].dist = 1.0f - Cv / (float)min(L1, L2);
             }
           }
         }
         if (lane == 63) sc.bndm[bo + j] = Cv;
         Lv = Cv;
+        if constexpr (NP) {
+          if (lane == 63) sc.bndc[bo + j] = Cc;
+          Lc = Cc;
+        }
         // refill slot u once its value is dead (see k_backward)
         const int64_t at = base + (int64_t)min(t + QD, last) * 64;
         if constexpr ((M & kHmm5) != 0) q5[u] = sc.f5[at];
@@ -699,7 +728,15 @@ hipError_t launch_merge(int models, int pid, const ModelScalars& ms, SeqSet seqs
                         hipStream_t st) {
   if (nchains <= 0) return hipSuccess;
   const ChainLaunch l = chain_launch(nchains, lds_seq);
-  if (pid == kPidQP)
+  if (pid & kPidNpdo) {
+    pid &= ~kPidNpdo;
+    if (pid == 2)
+      hipLaunchKernelGGL((k_merge<kLocal, 2, true>), l.grid, l.block, l.lds, st, ms, seqs, pm, cm, rec, sc, nchains, lds_seq);
+    else if (pid >= 3)
+      hipLaunchKernelGGL((k_merge<kPF, 3, true>), l.grid, l.block, l.lds, st, ms, seqs, pm, cm, rec, sc, nchains, lds_seq);
+    else
+      hipLaunchKernelGGL((k_merge<kHmm5 | kLocal | kPF, 0, true>), l.grid, l.block, l.lds, st, ms, seqs, pm, cm, rec, sc, nchains, lds_seq);
+  } else if (pid == kPidQP)
     hipLaunchKernelGGL((k_merge<kHmm5 | kPF | kQP, kPidQP>), l.grid, l.block, l.lds, st, ms, seqs, pm, cm, rec, sc, nchains, lds_seq);
   else if (pid == 2)
     hipLaunchKernelGGL((k_merge<kLocal, 2>), l.grid, l.block, l.lds, st, ms, seqs, pm, cm, rec, sc, nchains, lds_seq);

@@ -124,6 +124,9 @@ def pf_posterior(s1, s2):
     return out
 
 
+NPDO = 32  # pid flag: npdoAlign's ArrangePosteriorProbs pair body (oracle.h ORC_NPDO)
+
+
 def pair_posterior(m, s1, s2, pid):
     out = np.empty((len(s1) + 1) * (len(s2) + 1), np.float32)
     lib().orc_pair_posterior(C.byref(m), _s(s1), len(s1), _s(s2), len(s2), int(pid), out)

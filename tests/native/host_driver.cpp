@@ -2,7 +2,8 @@
 // (mlprobs_amd/cli/msa_host.cpp): reads the family, distances and the
 // consistency-transformed sparse set from a binary file (written by
 // tests/test_cli_host.py from the CPU oracle) and prints the MFA that
-// tree + progressive alignment + refinement produce.  CPU only.
+// tree + progressive alignment + refinement produce (header flag bit 1: the
+// -p 1 stages instead, alignment graph + refinement).  CPU only.
 #include <stdio.h>
 #include <stdlib.h>
 
@@ -25,7 +26,8 @@ int main(int argc, char** argv) {
   const int n = hdr[0], pid = hdr[1], vpid = hdr[2];
   cpnp::Options opt;
   opt.refinement = hdr[3];
-  opt.align_order = hdr[4] != 0;
+  opt.align_order = (hdr[4] & 1) != 0;
+  const bool np = (hdr[4] & 2) != 0;
   std::vector<cpnp::Row> seqs(n);
   for (int k = 0; k < n; k++) {
     int32_t len;
@@ -56,8 +58,13 @@ int main(int argc, char** argv) {
   rd(f, sp.cols.data(), sp.ent_off[P]);
   rd(f, sp.vals.data(), sp.ent_off[P]);
   fclose(f);
-  const cpnp::GuideTree tree = cpnp::build_tree(D, vpid);
-  const cpnp::Profile aln = cpnp::progressive_alignment(seqs, sp, tree, pid, opt);
+  cpnp::Profile aln;
+  if (np) {
+    aln = cpnp::np_refinement(cpnp::graph_alignment(seqs, sp), sp, D, opt);
+  } else {
+    const cpnp::GuideTree tree = cpnp::build_tree(D, vpid);
+    aln = cpnp::progressive_alignment(seqs, sp, tree, pid, opt);
+  }
   std::string out;
   cpnp::write_mfa(out, aln);
   fwrite(out.data(), 1, out.size(), stdout);

@@ -38,8 +38,33 @@ def test_cli_errors():
     assert _run('-version').returncode == 1
     assert _run('-zz').returncode == 1
     assert _run('-p', '2', 'x.fa').returncode == 1
-    r = _run('-p', '1', os.path.join(GOLDEN, 'cli', 'sim8.fa'))
-    assert r.returncode != 0
+
+
+# ---- the non-progressive strategy (-p 1, npdoAlign) against the reference
+# CLI (tests/golden/np, tests/golden/gen_np.py): -ir 0 (alignment graph) and
+# the default refinement under the golden run's fixed clock
+NP = os.path.join(GOLDEN, 'np')
+_NP = sorted(f[:-len('.p_1.out')] for f in os.listdir(NP) if f.endswith('.p_1.out')) if os.path.isdir(NP) else []
+NP_TIME = '1700000000'
+
+
+def _fasta_of(name):
+    for sub in ('cli', 'real', 'edge'):
+        fa = os.path.join(GOLDEN, sub, f'{name}.fa')
+        if os.path.exists(fa):
+            return fa
+    raise FileNotFoundError(name)
+
+
+@pytest.mark.parametrize('name', _NP)
+def test_cli_nonprogressive(name):
+    fa = _fasta_of(name)
+    for tag, args in (('p_1_ir_0', ['-p', '1', '-ir', '0']), ('p_1', ['-p', '1'])):
+        r = subprocess.run([BIN, *args, fa], capture_output=True, timeout=300,
+                           env=dict(os.environ, MLP_SRAND_TIME=NP_TIME))
+        assert r.returncode == 0 and r.stderr == b'', (tag, r.stderr)
+        with open(os.path.join(NP, f'{name}.{tag}.out'), 'rb') as fh:
+            assert r.stdout == fh.read(), (name, tag)
 
 
 # ---- the quickprobs drop-in (QuickProbs 2 realigner) against the reference

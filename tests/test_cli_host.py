@@ -24,14 +24,14 @@ CLI = os.path.join(ROOT, 'mlprobs_amd', 'cli')
 @pytest.fixture(scope='module')
 def driver(tmp_path_factory):
     out = str(tmp_path_factory.mktemp('drv') / 'host_driver')
-    subprocess.check_call(['g++', '-O2', '-std=c++17', '-fopenmp', '-I', CLI,
+    subprocess.check_call(['g++', '-O2', '-std=c++17', '-ffp-contract=off', '-fopenmp', '-I', CLI,
                            os.path.join(ROOT, 'tests', 'native', 'host_driver.cpp'),
-                           os.path.join(CLI, 'msa_host.cpp'), '-o', out])
+                           os.path.join(CLI, 'msa_host.cpp'), os.path.join(CLI, 'np_host.cpp'), '-o', out])
     return out
 
 
-def _family_inputs(seqs, consistency):
-    """What the GPU computes in c_p_np_aln -p 0, from the oracle."""
+def _family_inputs(seqs, consistency, np_mode=False):
+    """What the GPU computes in c_p_np_aln -p 0 (np_mode: -p 1), from the oracle."""
     m0 = orc.model(0.132548)
     vm, ident, delta = orc.model_adjustment(m0, seqs)
     pid, vpid = vm % 10, vm // 10
@@ -41,10 +41,14 @@ def _family_inputs(seqs, consistency):
     csrs = []
     for a in range(n):
         for b in range(a + 1, n):
-            post = orc.pair_posterior(m, seqs[a], seqs[b], pid)
+            post = orc.pair_posterior(m, seqs[a], seqs[b], pid | (orc.NPDO if np_mode else 0))
             rp, cols, vals = orc.sparsify(len(seqs[a]), len(seqs[b]), post)
-            sc = orc.mea(len(seqs[a]), len(seqs[b]), post)
-            D[a, b] = D[b, a] = np.float32(1) - np.float32(sc) / np.float32(min(len(seqs[a]), len(seqs[b])))
+            if np_mode:  # ArrangePosteriorProbs: score / #B (CPNP/MSA.cpp:1744-1753)
+                sc, path = orc.mea(len(seqs[a]), len(seqs[b]), post, with_path=True)
+                D[a, b] = D[b, a] = np.float32(sc) / np.float32(path.count('B'))
+            else:
+                sc = orc.mea(len(seqs[a]), len(seqs[b]), post)
+                D[a, b] = D[b, a] = np.float32(1) - np.float32(sc) / np.float32(min(len(seqs[a]), len(seqs[b])))
             csrs.append((rp.astype(np.int32), cols.astype(np.int32), vals.astype(np.float32)))
     lens = [len(s) for s in seqs]
     for _ in range(consistency):
@@ -52,9 +56,9 @@ def _family_inputs(seqs, consistency):
     return pid, vpid, D, csrs
 
 
-def _write(path, headers, seqs, pid, vpid, refinement, D, csrs):
+def _write(path, headers, seqs, pid, vpid, refinement, D, csrs, flags=0):
     with open(path, 'wb') as fh:
-        fh.write(struct.pack('<5i', len(seqs), pid, vpid, refinement, 0))
+        fh.write(struct.pack('<5i', len(seqs), pid, vpid, refinement, flags))
         for h, s in zip(headers, seqs):
             hb = h.encode()
             fh.write(struct.pack('<i', len(hb)) + hb + struct.pack('<i', len(s)) + s.encode())
@@ -79,5 +83,36 @@ def test_progressive_vs_reference_cli(driver, tmp_path, name, variant):
     _write(inp, headers, seqs, pid, vpid, refinement, D, csrs)
     got = subprocess.run([driver, inp], capture_output=True, check=True).stdout.decode()
     with open(os.path.join(GOLDEN, 'cli', f'{name}_{variant}.out')) as fh:
+        ref = fh.read()
+    assert got == ref
+
+
+NP_TIME = '1700000000'  # the clock of tests/golden/np/*.p_1.out (tests/golden/gen_np.py)
+# the CPU suite takes the CLI goldens and a few real families; the drop-in
+# binary runs every family of tests/golden/np on the GPU (test_cli_gpu.py)
+NP_FAMILIES = ['div12', 'sim8', 'bb11028', 'bali3_BB11001', 'ox_104s10', 'oxx____8t2', 'sabre_sup_017']
+
+
+def _np_family(name):
+    sub = 'cli' if name in ('div12', 'sim8', 'bb11028') else 'real'
+    return synth.read_fasta(os.path.join(GOLDEN, sub, f'{name}.fa'))
+
+
+@pytest.mark.parametrize('name', NP_FAMILIES)
+@pytest.mark.parametrize('variant', ['p_1_ir_0', 'p_1'])
+def test_nonprogressive_vs_reference_cli(driver, tmp_path, name, variant):
+    """-p 1 host stages (np_host.cpp: alignment graph, FindSimilar +
+    DoRefinement) from the oracle's npdoAlign posteriors, distances and two
+    consistency rounds, against the reference CLI byte for byte (-p 1 with
+    the fixed clock of the golden run)."""
+    fam = _np_family(name)
+    headers = [h for h, _ in fam]
+    seqs = [s for _, s in fam]
+    pid, vpid, D, csrs = _family_inputs(seqs, 2, np_mode=True)
+    inp = str(tmp_path / 'in.bin')
+    _write(inp, headers, seqs, pid, vpid, 0 if variant.endswith('ir_0') else 100, D, csrs, flags=2)
+    got = subprocess.run([driver, inp], capture_output=True, check=True,
+                         env=dict(os.environ, MLP_SRAND_TIME=NP_TIME)).stdout.decode()
+    with open(os.path.join(GOLDEN, 'np', f'{name}.{variant}.out')) as fh:
         ref = fh.read()
     assert got == ref

@@ -458,3 +458,59 @@ def test_profile_posterior_vs_restatement(seed):
                     ref[r, c] = np.float32(ref[r, c] + np.float32(wf * np.float32(v)))
     np.testing.assert_array_equal(got, ref)
     fam.close()
+
+
+# ---- npdoAlign's pair body (MLP_PID_NPDO: ArrangePosteriorProbs,
+# CPNP/MSA.cpp:1636-1765): the RMS terms in its order and the distance
+# score / #B, #B carried along the MEA recurrence on the GPU
+@pytest.mark.parametrize('name', ['div12', 'sim8', 'bb11028'])
+def test_npdo_golden(name):
+    """Against the reference's own ArrangePosteriorProbs (ref_probe npdo,
+    tests/golden/gen_np.py) at the family's pid / delta."""
+    g = np.load(os.path.join(GOLDEN, f'np_pairs_{name}.npz'))
+    seqs = [s for _, s in synth.read_fasta(os.path.join(GOLDEN, 'cli', f'{name}.fa'))]
+    pid = int(g['pid'])
+    fam = Family(seqs)
+    fam.posteriors(pid | NPDO, float(g['delta']))
+    dist = fam.results()[0]
+    for k in range(len(g['ab'])):
+        la = int(g['L1'][k])
+        r0 = int(g['eoff'][k])
+        rp = g['rp'][sum(int(x) + 2 for x in g['L1'][:k]):][:la + 2]
+        ref = (rp, g['cols'][r0:r0 + rp[-1]], g['vals'][r0:r0 + rp[-1]])
+        _check_pair_csr(ref, fam.sparse(k), pid, f'{name} p{k}')
+        if pid in EXACT_PIDS:
+            assert dist[k] == g['dist'][k]
+        else:
+            assert close_scalar(g['dist'][k], dist[k]), (name, k)
+    fam.close()
+
+
+NPDO = 32
+
+
+@pytest.mark.parametrize('s,L,n,pid,seed', [(0.7, 150, 5, 2, 91), (0.6, 260, 4, 2, 92), (0.5, 200, 5, 0, 93),
+                                             (0.2, 130, 4, 3, 94)])
+def test_npdo_vs_oracle(s, L, n, pid, seed):
+    """Rows cross 64-row strips (the #B count rides the strip boundary row);
+    pid 2 bit-exact (no partition function), else the section 8c rule."""
+    seqs = _ragged_family(n, L // 2, L, seed)
+    delta = 0.132548
+    fam = Family(seqs)
+    fam.posteriors(pid | NPDO, delta)
+    m = orc.model(delta)
+    pairs = np.arange(fam.npairs)
+    dist, _, rp, eo, cols, vals = orc.pairs_csr(m, seqs, pid | orc.NPDO, pairs)
+    g = fam.results()[0]
+    roff = 0
+    for k in pairs:
+        a, b = orc.pair_of(n, int(k))
+        la = len(seqs[a])
+        ref = (rp[roff:roff + la + 2], cols[eo[k]:eo[k + 1]], vals[eo[k]:eo[k + 1]])
+        roff += la + 2
+        _check_pair_csr(ref, fam.sparse(int(k)), pid, f'p{k}')
+        if pid in EXACT_PIDS:
+            assert g[k] == dist[k], (k, g[k], dist[k])
+        else:
+            assert close_scalar(dist[k], g[k]), k
+    fam.close()
