@@ -168,8 +168,17 @@ int mlp_relax_qp_selective(mlp_ctx *ctx, int iters, const float *seq_weights, co
 int mlp_profile_posterior(mlp_ctx *ctx, const float *seq_weights, int n1, const int32_t *labels1, int L1,
                           const int32_t *map1, int n2, const int32_t *labels2, int L2, const int32_t *map2,
                           float *out);
+/* C_P_NP_Aln's profile-profile posterior instead (ProbabilisticModel::
+ * BuildPosterior, CPNP/ProbabilisticModel.h:1197-1379), cutoff 0: with
+ * seq_weights (int, the guide tree's getSeqsWeights) the weighted form of
+ * the progressive merges, w = (float)(w1 w2) / (float sum of w1 w2); NULL:
+ * the unweighted form of refinement (terms += v).  Same layout, same
+ * bit-identical term order. */
+int mlp_profile_posterior_cpnp(mlp_ctx *ctx, const int32_t *seq_weights, int n1, const int32_t *labels1, int L1,
+                               const int32_t *map1, int n2, const int32_t *labels2, int L2, const int32_t *map2,
+                               float *out);
 /* out = NULL: the matrix stays in a pinned host buffer of the context,
- * returned here and valid until the next mlp_profile_posterior call. */
+ * returned here and valid until the next mlp_profile_posterior* call. */
 const float *mlp_profile_result(const mlp_ctx *ctx);
 
 /* Multi-GPU (one process per GPU): RCCL over xGMI. */

@@ -12,6 +12,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 
 #include <chrono>
 #include <iostream>
@@ -63,7 +64,22 @@ static bool get_float(const char* s, float* v) {   // MSA::GetFloat (CPNP/MSA.cp
 static void stage(const char* name) {
   static const bool on = getenv("MLP_CLI_TIMES") != nullptr;
   static auto t0 = std::chrono::steady_clock::now();
-  if (!on || !name) return;
+  if (!on) return;
+  if (!name) {  // first call, from main: time since the process started (loader, static init)
+    double up = 0, start = 0;
+    if (FILE* f = fopen("/proc/uptime", "r")) { if (fscanf(f, "%lf", &up) != 1) up = 0; fclose(f); }
+    if (FILE* f = fopen("/proc/self/stat", "r")) {
+      char buf[1024];
+      const size_t n = fread(buf, 1, sizeof buf - 1, f);
+      fclose(f);
+      buf[n] = 0;
+      const char* q = strrchr(buf, ')');  // fields after the command name; starttime is field 22
+      for (int k = 2; q && k < 22; k++) q = strchr(q + 1, ' ');
+      if (q) start = strtod(q + 1, nullptr) / (double)sysconf(_SC_CLK_TCK);
+    }
+    std::cerr << "[stage] process start to main " << (up - start) << " s" << std::endl;
+    return;
+  }
   const auto t1 = std::chrono::steady_clock::now();
   std::cerr << "[stage] " << name << " " << std::chrono::duration<double>(t1 - t0).count() << " s" << std::endl;
   t0 = t1;
@@ -228,6 +244,40 @@ int main(int argc, char** argv) {
     check(ctx, mlp_csr_export(ctx, sp.row_ptr.data(), sp.ent_off.data(), sp.cols.data(), sp.vals.data()),
           "sparse set");
     stage("sparse set to host");
+    // BuildPosterior of the merges and refinement passes on the GPU
+    // (mlp_profile_posterior_cpnp) once the profile pair holds enough sparse
+    // entries to pay for a device round trip (~0.1-0.2 ms; the host adds
+    // ~5e4 entries in that time); the sparse set stays resident.  After
+    // consistency a divergent family's set is nearly empty (C2: 5e4 entries
+    // over 8128 pairs), a similar family's is not.
+    static const int64_t gpu_min = getenv("MLP_PROFILE_GPU_MIN") ? atoll(getenv("MLP_PROFILE_GPU_MIN")) : 100000;
+    std::vector<int32_t> lab1, lab2, map1, map2;
+    cpnp::set_profile_backend([&](const cpnp::Profile& a, const cpnp::Profile& b, const int* w) -> const float* {
+      int64_t entries = 0;
+      for (const Row& x : a)
+        for (const Row& y : b) {
+          const int64_t p = sp.pair(std::min(x.label, y.label), std::max(x.label, y.label));
+          entries += sp.ent_off[p + 1] - sp.ent_off[p];
+        }
+      if (entries < gpu_min) return nullptr;
+      auto fill = [](const cpnp::Profile& p, std::vector<int32_t>& lab, std::vector<int32_t>& map) {
+        lab.clear();
+        map.clear();
+        for (const Row& r : p) {   // Sequence::GetMapping: 0, then the column of each residue
+          lab.push_back(r.label);
+          map.push_back(0);
+          for (int c = 1; c <= r.length(); c++)
+            if (r.data[c] != '-') map.push_back(c);
+        }
+      };
+      fill(a, lab1, map1);
+      fill(b, lab2, map2);
+      const int rc = mlp_profile_posterior_cpnp(ctx, w, (int)a.size(), lab1.data(), a[0].length(), map1.data(),
+                                                (int)b.size(), lab2.data(), b[0].length(), map2.data(), nullptr);
+      if (rc == MLP_ERR_STATE) return nullptr;   // a profile wider than an LDS row: the host computes it
+      check(ctx, rc, "profile posterior");
+      return mlp_profile_result(ctx);
+    });
     if (progressive) {
       aln = cpnp::progressive_alignment(seqs, sp, tree, pid, opt);
       stage("progressive + refinement");
@@ -239,6 +289,7 @@ int main(int argc, char** argv) {
     }
   }
   mlp_ctx_destroy(ctx);
+  stage("context teardown");
   std::string out;
   cpnp::write_mfa(out, aln);
   if (outname.empty()) {
@@ -249,5 +300,6 @@ int main(int argc, char** argv) {
     fwrite(out.data(), 1, out.size(), f);
     fclose(f);
   }
+  stage("output");
   return 0;
 }

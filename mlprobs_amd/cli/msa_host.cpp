@@ -191,27 +191,36 @@ GuideTree build_tree(std::vector<std::vector<float>> dist, int varianceid) {
 }
 
 // ------------------------------------------------------------------ profiles
-static std::vector<int> mapping(const Row& r) {   // Sequence::GetMapping
-  std::vector<int> m(1, 0);
+static void mapping(const Row& r, std::vector<int>& m) {   // Sequence::GetMapping
+  m.clear();
+  m.reserve(r.length() + 1);
+  m.push_back(0);
   for (int i = 1; i <= r.length(); i++)
     if (r.data[i] != '-') m.push_back(i);
-  return m;
 }
 
 std::vector<float> build_posterior(const Profile& A, const Profile& B, const SparseSet& sp,
                                    const int* weights, float cutoff) {
+  std::vector<float> post;
+  build_posterior_into(A, B, sp, weights, cutoff, post);
+  return post;
+}
+
+void build_posterior_into(const Profile& A, const Profile& B, const SparseSet& sp, const int* weights,
+                          float cutoff, std::vector<float>& post) {
   const int len1 = A[0].length(), len2 = B[0].length();
   const int64_t W2 = len2 + 1;
-  std::vector<float> post((size_t)(len1 + 1) * W2, 0.f);
+  post.assign((size_t)(len1 + 1) * W2, 0.f);
   float total = 0;
   if (weights)
     for (const Row& x : A)
       for (const Row& y : B) total += weights[x.label] * weights[y.label];
-  std::vector<std::vector<int>> m2s;
-  m2s.reserve(B.size());
-  for (const Row& y : B) m2s.push_back(mapping(y));
+  static thread_local std::vector<std::vector<int>> m2s;
+  static thread_local std::vector<int> m1;
+  if (m2s.size() < B.size()) m2s.resize(B.size());
+  for (size_t yb = 0; yb < B.size(); yb++) mapping(B[yb], m2s[yb]);
   for (const Row& x : A) {
-    const std::vector<int> m1 = mapping(x);
+    mapping(x, m1);
     for (size_t yb = 0; yb < B.size(); yb++) {
       const Row& y = B[yb];
       const std::vector<int>& m2 = m2s[yb];
@@ -226,11 +235,26 @@ std::vector<float> build_posterior(const Profile& A, const Profile& B, const Spa
       // the reference subtracts the cutoff from every cell of the pair
       // (ProbabilisticModel.h:1229-1283); x - 0.0f == x for every value the
       // sums take (no -0.0: they start at +0 and add non-negative terms), so
-      // with the default cutoff 0 that O(L1 L2) sweep is skipped exactly
+      // with the default cutoff 0 that O(L1 L2) sweep is skipped exactly,
+      // and so is a pair without entries (consistency empties most of a
+      // divergent family's pairs)
       const float sub = weights ? w * cutoff : cutoff;
       const bool do_sub = sub != 0.f;
+      const int32_t nnz = (int32_t)(sp.ent_off[p + 1] - sp.ent_off[p]);
+      if (!do_sub && nnz == 0) continue;
+      // without the cutoff sweep only rows first .. last with entries matter
+      int r0 = 1, r1 = rows;
+      if (!do_sub) {
+        r0 = (int)(std::upper_bound(rp + 1, rp + rows + 2, 0) - rp) - 1;   // first row with rp[r + 1] > 0
+        r1 = (int)(std::lower_bound(rp + 1, rp + rows + 2, nnz) - rp) - 1;  // last row with rp[r] < nnz
+      }
+      // next row to visit: every row with the cutoff sweep, else the next
+      // one holding entries (consistency leaves few, scattered rows)
+      auto next_row = [&](int r) {
+        return do_sub ? r + 1 : (int)(std::upper_bound(rp + r + 2, rp + rows + 2, rp[r + 1]) - rp) - 1;
+      };
       if (first < second) {
-        for (int ii = 1; ii <= rows; ii++) {
+        for (int ii = r0; ii <= r1; ii = next_row(ii)) {
           const int64_t base = (int64_t)m1[ii] * W2;
           for (int32_t e = rp[ii]; e < rp[ii + 1]; e++)
             post[base + m2[cols[e]]] += weights ? w * vals[e] : vals[e];
@@ -238,7 +262,7 @@ std::vector<float> build_posterior(const Profile& A, const Profile& B, const Spa
             for (int jj = 0; jj < ncols; jj++) post[base + m2[jj]] -= sub;
         }
       } else {
-        for (int jj = 1; jj <= rows; jj++) {
+        for (int jj = r0; jj <= r1; jj = next_row(jj)) {
           const int64_t base = m2[jj];
           for (int32_t e = rp[jj]; e < rp[jj + 1]; e++)
             post[base + (int64_t)m1[cols[e]] * W2] += weights ? w * vals[e] : vals[e];
@@ -248,7 +272,21 @@ std::vector<float> build_posterior(const Profile& A, const Profile& B, const Spa
       }
     }
   }
-  return post;
+}
+
+static ProfileBackend& profile_backend() {
+  static ProfileBackend fn;
+  return fn;
+}
+void set_profile_backend(ProfileBackend fn) { profile_backend() = std::move(fn); }
+
+const float* profile_posterior(const Profile& a, const Profile& b, const SparseSet& sp, const int* weights,
+                               float cutoff) {
+  if (profile_backend() && cutoff == 0.f)
+    if (const float* p = profile_backend()(a, b, weights)) return p;
+  static thread_local std::vector<float> buf;   // reused: fresh pages cost more than the adds
+  build_posterior_into(a, b, sp, weights, cutoff, buf);
+  return buf.data();
 }
 
 std::string mea_path(int len1, int len2, const std::vector<float>& post, float* score) {
@@ -432,7 +470,7 @@ static Profile process_tree(const GuideTree& t, int node, const std::vector<Row>
   Profile left = process_tree(t, nd.left, seqs, sp, opt);
   Profile right = process_tree(t, nd.right, seqs, sp, opt);
   // AlignAlignments (MSA.cpp:1410-1474) with the tree weights
-  const std::vector<float> post = build_posterior(left, right, sp, t.weights.data(), opt.cutoff);
+  const float* post = profile_posterior(left, right, sp, t.weights.data(), opt.cutoff);
   float sc;
   const std::string path = mea_path(left[0].length(), right[0].length(), post, &sc);
   return merge(left, right, path, !opt.align_order);
@@ -493,7 +531,7 @@ static int refine_once(Profile& aln, const SparseSet& sp, const Options& opt) {
   }
   if (one.empty() || two.empty()) return 2;
   const Profile g1 = project(aln, one), g2 = project(aln, two);
-  const std::vector<float> post = build_posterior(g1, g2, sp, nullptr, opt.cutoff);
+  const float* post = profile_posterior(g1, g2, sp, nullptr, opt.cutoff);
   // accuracy of the current alignment
   const int L = aln[0].length();
   const int W2 = g2[0].length() + 1;

@@ -7,6 +7,7 @@
 #pragma once
 #include <stdint.h>
 
+#include <functional>
 #include <set>
 #include <string>
 #include <vector>
@@ -67,6 +68,19 @@ GuideTree build_tree(std::vector<std::vector<float>> dist, int varianceid);
 // `weights` is non-null.  Returns the dense (len1 + 1) x (len2 + 1) matrix.
 std::vector<float> build_posterior(const Profile& a, const Profile& b, const SparseSet& sp,
                                    const int* weights, float cutoff);
+void build_posterior_into(const Profile& a, const Profile& b, const SparseSet& sp, const int* weights,
+                          float cutoff, std::vector<float>& post);
+
+// A device implementation of build_posterior (the GPU's BuildPosterior):
+// returns the dense matrix, valid until its next call, or nullptr to fall
+// back to the host.  Used by the progressive merges and both refinements
+// when set and the cutoff is 0.
+using ProfileBackend = std::function<const float*(const Profile& a, const Profile& b, const int* weights)>;
+void set_profile_backend(ProfileBackend fn);
+// build_posterior through the backend when possible, else into a reused
+// host buffer; the result is valid until the next call
+const float* profile_posterior(const Profile& a, const Profile& b, const SparseSet& sp, const int* weights,
+                               float cutoff);
 
 // MEA alignment of two profiles (ProbabilisticModel.h:804-864): the path
 // ('B', 'X', 'Y') and its score.

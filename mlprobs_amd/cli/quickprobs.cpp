@@ -19,6 +19,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <chrono>
@@ -34,7 +35,22 @@
 static void stage(const char* name) {  // MLP_CLI_TIMES=1: stage times on stderr
   static const bool on = getenv("MLP_CLI_TIMES") != nullptr;
   static auto t0 = std::chrono::steady_clock::now();
-  if (!on || !name) return;
+  if (!on) return;
+  if (!name) {  // first call, from main: time since the process started (loader, static init)
+    double up = 0, start = 0;
+    if (FILE* f = fopen("/proc/uptime", "r")) { if (fscanf(f, "%lf", &up) != 1) up = 0; fclose(f); }
+    if (FILE* f = fopen("/proc/self/stat", "r")) {
+      char buf[1024];
+      const size_t n = fread(buf, 1, sizeof buf - 1, f);
+      fclose(f);
+      buf[n] = 0;
+      const char* q = strrchr(buf, ')');  // fields after the command name; starttime is field 22
+      for (int k = 2; q && k < 22; k++) q = strchr(q + 1, ' ');
+      if (q) start = strtod(q + 1, nullptr) / (double)sysconf(_SC_CLK_TCK);
+    }
+    std::cerr << "[stage] process start to main " << (up - start) << " s" << std::endl;
+    return;
+  }
   const auto t1 = std::chrono::steady_clock::now();
   std::cerr << "[stage] " << name << " " << std::chrono::duration<double>(t1 - t0).count() << " s" << std::endl;
   t0 = t1;

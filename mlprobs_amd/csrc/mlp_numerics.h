@@ -60,8 +60,13 @@ constexpr int kLookupRows = 16;
 __device__ __forceinline__ float mlp_log_add_t(float x, float y, const float4* __restrict__ lk) {
   const float hi = fmaxf(x, y), lo = fminf(x, y);
   const float d = hi - lo;
+#ifdef MLP_EXP_CONSTLK  // timing experiment only (wrong results): no table read
+  const float4 c = make_float4(-0.009350833524763f, 0.130659527668286f, 0.498799810682272f, 0.693203116424741f);
+  (void)lk;
+#else
   const int q = (int)fminf(d * 0x1.fffffep0f, 15.0f);
   const float4 c = lk[q];
+#endif
   const float r = (((c.x * d + c.y) * d + c.z) * d + c.w) + lo;
   return (d >= 7.5f) ? hi : r;
 }
@@ -204,6 +209,12 @@ __device__ __forceinline__ double mlp_shl1d(double v, double old) {
 // rescaling is exact, so every product/sum rounds like unscaled fp64.
 #define MLP_PF_STEP 200
 #define MLP_PF_HUGE 0x1p200
+// The reference stops with "ERROR: huge val error" once a forward value
+// reaches long double infinity, 2^16384 (CPNP/MSAPartProbs.cpp:547-589,
+// OS_HUGE_VALL = HUGE_VALL): the cell's largest value x 2^(200 e) >= 2^16384.
+__device__ __forceinline__ bool mlp_pf_ldbl_overflow(double m, double e, double f, int E) {
+  return E > 81 || (E == 81 && fmax(fmax(m, e), f) >= 0x1p184);
+}
 // Packed storage of (value, e): e in the 8 low mantissa bits (2^-44 rel.).
 __device__ __forceinline__ double mlp_pf_pack(double v, int e) {
   unsigned long long b = (unsigned long long)__double_as_longlong(v);

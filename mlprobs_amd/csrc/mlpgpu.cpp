@@ -938,6 +938,9 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
     hipStream_t st = streams[B.slot];
     HIPCHK(c, hipStreamSynchronize(st));
     const int64_t np = B.np;
+#if defined(MLP_EXP_NOCHAIN) || defined(MLP_EXP_CONSTLK)
+    for (int64_t s = 0; s < np; s++) B.rec[s].flags = 0;  // timing experiments: results are not meaningful
+#endif
     for (int64_t s = 0; s < np; s++) {
       if (B.rec[s].flags & 1) {
         c->err = "partition function overflow (pair " + std::to_string(B.order[s]) + ")";
@@ -1115,12 +1118,59 @@ static int ensure_transposes(mlp_ctx* c) {
   return MLP_OK;
 }
 
+// pair weights: QuickProbs' w1 w2 / sum in double (ParallelProbabilisticModel.cpp:
+// 317-330, 350-352) or C_P_NP_Aln's int weights, float sum, (float)(w1 w2) / sum
+// (CPNP/ProbabilisticModel.h:1303-1326); unweighted: 1 (1 * v == v)
+static int profile_posterior(mlp_ctx* c, const std::vector<float>& w, int n1, const int32_t* labels1, int L1,
+                             const int32_t* map1, int n2, const int32_t* labels2, int L2, const int32_t* map2,
+                             float* out);
+
 int mlp_profile_posterior(mlp_ctx* c, const float* seq_weights, int n1, const int32_t* labels1, int L1,
                           const int32_t* map1, int n2, const int32_t* labels2, int L2, const int32_t* map2,
                           float* out) {
-  if (!c || !seq_weights || !labels1 || !labels2 || !map1 || !map2 || n1 < 1 || n2 < 1 || L1 < 1 ||
-      L2 < 1)
-    return MLP_ERR_ARG;
+  if (!c || !seq_weights || !labels1 || !labels2 || n1 < 1 || n2 < 1) return MLP_ERR_ARG;
+  for (int i = 0; i < n1; i++)
+    if (labels1[i] < 0 || labels1[i] >= c->n) return MLP_ERR_ARG;
+  for (int j = 0; j < n2; j++)
+    if (labels2[j] < 0 || labels2[j] >= c->n) return MLP_ERR_ARG;
+  std::vector<float> w((int64_t)n1 * n2);
+  double total = 0;
+  for (int i = 0; i < n1; i++) {
+    const double w1 = seq_weights[labels1[i]];
+    for (int j = 0; j < n2; j++) total += w1 * (double)seq_weights[labels2[j]];
+  }
+  for (int i = 0; i < n1; i++)
+    for (int j = 0; j < n2; j++)
+      w[(int64_t)i * n2 + j] = (float)(((double)seq_weights[labels1[i]] * seq_weights[labels2[j]]) / total);
+  return profile_posterior(c, w, n1, labels1, L1, map1, n2, labels2, L2, map2, out);
+}
+
+int mlp_profile_posterior_cpnp(mlp_ctx* c, const int32_t* seq_weights, int n1, const int32_t* labels1, int L1,
+                               const int32_t* map1, int n2, const int32_t* labels2, int L2, const int32_t* map2,
+                               float* out) {
+  if (!c || !labels1 || !labels2 || n1 < 1 || n2 < 1) return MLP_ERR_ARG;
+  for (int i = 0; i < n1; i++)
+    if (labels1[i] < 0 || labels1[i] >= c->n) return MLP_ERR_ARG;
+  for (int j = 0; j < n2; j++)
+    if (labels2[j] < 0 || labels2[j] >= c->n) return MLP_ERR_ARG;
+  std::vector<float> w((int64_t)n1 * n2, 1.0f);
+  if (seq_weights) {
+    float total = 0;
+    for (int i = 0; i < n1; i++)
+      for (int j = 0; j < n2; j++) total += seq_weights[labels1[i]] * seq_weights[labels2[j]];
+    for (int i = 0; i < n1; i++)
+      for (int j = 0; j < n2; j++)
+        w[(int64_t)i * n2 + j] = (float)(seq_weights[labels1[i]] * seq_weights[labels2[j]]) / total;
+  }
+  return profile_posterior(c, w, n1, labels1, L1, map1, n2, labels2, L2, map2, out);
+}
+
+}  // extern "C"
+
+static int profile_posterior(mlp_ctx* c, const std::vector<float>& w, int n1, const int32_t* labels1, int L1,
+                             const int32_t* map1, int n2, const int32_t* labels2, int L2, const int32_t* map2,
+                             float* out) {
+  if (!map1 || !map2 || L1 < 1 || L2 < 1) return MLP_ERR_ARG;
   if (c->store_p0 != 0 || c->store_p1 != c->P) {
     c->err = "the profile posterior needs every pair";
     return MLP_ERR_STATE;
@@ -1134,25 +1184,15 @@ int mlp_profile_posterior(mlp_ctx* c, const float* seq_weights, int n1, const in
   if ((rc = ensure_transposes(c))) return rc;
   const auto tp0 = std::chrono::steady_clock::now();
   const int64_t np = (int64_t)n1 * n2;
-  // host side of buildPosterior: weights w1 w2 / sum in double
-  // (ParallelProbabilisticModel.cpp:317-330, 350-352), block bases, the
-  // column -> residue map of A and the residue -> column maps of B
+  // host side of buildPosterior: block bases, the column -> residue map of A
+  // and the residue -> column maps of B
   std::vector<int64_t> rpb(np), eb(np), moff(n2);
-  std::vector<float> w(np);
-  double total = 0;
-  for (int i = 0; i < n1; i++) {
-    const double w1 = seq_weights[labels1[i]];
-    for (int j = 0; j < n2; j++) total += w1 * (double)seq_weights[labels2[j]];
-  }
   for (int i = 0; i < n1; i++) {
     const int a = labels1[i];
-    const double w1 = seq_weights[a];
     for (int j = 0; j < n2; j++) {
       const int b = labels2[j];
       if (a < 0 || b < 0 || a >= c->n || b >= c->n || a == b) return MLP_ERR_ARG;
       const int64_t q = (int64_t)i * n2 + j;
-      const double w2 = seq_weights[b];
-      w[q] = (float)((w1 * w2) / total);
       const int64_t p = a < b ? pair_index_host(c->n, a, b) : pair_index_host(c->n, b, a);
       rpb[q] = a < b ? c->rp_off[p] : ~c->trp_off[p];
       eb[q] = c->ent_off[p];
@@ -1252,6 +1292,8 @@ int mlp_profile_posterior(mlp_ctx* c, const float* seq_weights, int n1, const in
   if (out) memcpy(out, c->h_prof_out, b_out);
   return MLP_OK;
 }
+
+extern "C" {
 
 const float* mlp_profile_result(const mlp_ctx* c) { return c ? c->h_prof_out : nullptr; }
 

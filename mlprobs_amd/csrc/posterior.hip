@@ -213,7 +213,11 @@ __global__ __launch_bounds__(256, SweepWaves<M>::fwd) void k_forward(ModelScalar
             sc.bndl[(bo + j) * 3 + 2] = Cy;
           }
           // row-major chain copy of interior M values (CPNP/ProbabilisticModel.h:438-447)
+#ifdef MLP_EXP_NOCHAIN  // timing experiment only (wrong totals): no row-major chain stores
+          if (false) {
+#else
           if (act && i >= 1 && j >= 1) {
+#endif
             const int qq = (j - 1) & 3;
             cb0 = qq == 0 ? Cm : cb0;
             cb1 = qq == 1 ? Cm : cb1;
@@ -253,7 +257,8 @@ __global__ __launch_bounds__(256, SweepWaves<M>::fwd) void k_forward(ModelScalar
           }
           sc.zm[idx] = mlp_pf_pack(Zm, E);
           if (act) {
-            if (E > 250) atomicOr(&rec[c.slot].flags, 1);
+            // QuickProbs' plain double has no such stop; frames past 2^50000 are ours
+            if ((M & kQP) != 0 ? E > 250 : mlp_pf_ldbl_overflow(Zm, Ze, Zf, E)) atomicOr(&rec[c.slot].flags, 1);
             if (i == L1 && j == L2) {  // CPNP/MSAPartProbs.cpp:591,612; QP/PartitionFunction.cpp:132,155
               rec[c.slot].zmant = (M & kQP) != 0 ? (Zm + Zf) + Ze : (Zm + Ze) + Zf;
               rec[c.slot].zexp = E;
@@ -435,7 +440,11 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
           }
           // chain element (CPNP/ProbabilisticModel.h:444-445); columns descend,
           // so a group of 4 is complete at its first column
+#ifdef MLP_EXP_NOCHAIN
+          if (false) {
+#else
           if (act && i >= 1 && j >= 1) {
+#endif
             const float e = Bm + T_.match[c1 * 26 + c2] - ins1 - T_.ins[c2] - two_rt1;
             const int qq = (j - 1) & 3;
             cb0 = qq == 0 ? e : cb0;

@@ -72,6 +72,8 @@ def lib():
         L.mlp_relax_qp_selective.argtypes = [P, C.c_int, F32P, C.c_void_p, C.c_float]
         L.mlp_profile_posterior.argtypes = [P, F32P, C.c_int, I32P, C.c_int, I32P, C.c_int, I32P, C.c_int, I32P,
                                             F32P]
+        L.mlp_profile_posterior_cpnp.argtypes = [P, C.c_void_p, C.c_int, I32P, C.c_int, I32P, C.c_int, I32P, C.c_int,
+                                                 I32P, F32P]
         L.mlp_viterbi.argtypes = [P, I64, I64, C.c_int]
         L.mlp_viterbi_results.argtypes = [P, I64, I64, C.c_void_p, C.c_void_p]
         L.mlp_viterbi_path.argtypes = [P, I64, C.c_void_p, C.c_void_p]
@@ -98,7 +100,7 @@ def lib():
 EXPORTED = ['mlp_ctx_create', 'mlp_ctx_destroy', 'mlp_last_error', 'mlp_set_scratch', 'mlp_family_load',
             'mlp_family_npairs', 'mlp_posteriors', 'mlp_pair_results', 'mlp_csr_total',
             'mlp_csr_export', 'mlp_csr_import', 'mlp_relax', 'mlp_relax_qp',
-            'mlp_relax_qp_selective', 'mlp_profile_posterior', 'mlp_profile_result', 'mlp_viterbi', 'mlp_viterbi_results',
+            'mlp_relax_qp_selective', 'mlp_profile_posterior', 'mlp_profile_posterior_cpnp', 'mlp_profile_result', 'mlp_viterbi', 'mlp_viterbi_results',
             'mlp_viterbi_path', 'mlp_model_adjustment', 'mlp_family_features', 'mlp_comm_unique_id', 'mlp_comm_init',
             'mlp_shard_range', 'mlp_shard_plan', 'mlp_gather_layout', 'mlp_allgather', 'mlp_synchronize', 'mlp_profile',
             'mlp_kernel_times', 'mlp_profile_reset', 'mlp_ctx_create_mask', 'mlp_set_shards', 'mlp_shard_count',

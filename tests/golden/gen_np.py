@@ -30,6 +30,7 @@ REFFT = os.path.join(ROOT, 'oracle', '_ref', 'c_p_np_aln_ft')
 PROBE = os.path.join(ROOT, 'oracle', '_ref', 'ref_probe')
 OUT = os.path.join(HERE, 'np')
 TIME = '1700000000'
+TIMEOUT = float(os.environ.get('NP_TIMEOUT', '60'))  # families whose reference run is slower are skipped
 
 
 def run(cmd, env=None, timeout=120):
@@ -53,8 +54,8 @@ def main():
     for name, fa in fams:
         ent = {'family': name}
         try:
-            r0 = run([REFCLI, '-p', '1', '-ir', '0', fa], timeout=60)
-            r1 = run([REFFT, '-p', '1', fa], env={'REF_FIXED_TIME': TIME}, timeout=60)
+            r0 = run([REFCLI, '-p', '1', '-ir', '0', fa], timeout=TIMEOUT)
+            r1 = run([REFFT, '-p', '1', fa], env={'REF_FIXED_TIME': TIME}, timeout=TIMEOUT)
         except subprocess.TimeoutExpired:
             print(name, 'skipped (slow)', flush=True)
             continue

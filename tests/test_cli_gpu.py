@@ -34,6 +34,22 @@ def test_cli_progressive(name, flags, suffix):
         assert r.stdout == fh.read()
 
 
+@pytest.mark.parametrize('name', ['bb11028', 'div12', 'sim8'])
+@pytest.mark.parametrize('flags,suffix', [((), 'p_0'), (('-p', '1'), 'p_1'), (('-p', '1', '-ir', '0'), 'p_1_ir_0')])
+def test_cli_profile_posterior_on_gpu(name, flags, suffix):
+    """Every progressive merge and refinement pass through the GPU's
+    BuildPosterior (MLP_PROFILE_GPU_MIN=1: no host fallback for small
+    profile pairs): still the reference's bytes."""
+    env = dict(os.environ, MLP_PROFILE_GPU_MIN='1', MLP_SRAND_TIME='1700000000')
+    r = subprocess.run([BIN, *(flags or ('-p', '0')), os.path.join(GOLDEN, 'cli', f'{name}.fa')], capture_output=True,
+                       text=True, timeout=300, env=env)
+    assert r.returncode == 0 and r.stderr == '', r.stderr
+    ref = os.path.join(GOLDEN, 'cli', f'{name}_{suffix}.out') if suffix == 'p_0' else \
+        os.path.join(GOLDEN, 'np', f'{name}.{suffix}.out')
+    with open(ref) as fh:
+        assert r.stdout == fh.read()
+
+
 def test_cli_errors():
     assert _run('-version').returncode == 1
     assert _run('-zz').returncode == 1

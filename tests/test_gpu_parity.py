@@ -514,3 +514,23 @@ def test_npdo_vs_oracle(s, L, n, pid, seed):
         else:
             assert close_scalar(dist[k], g[k]), k
     fam.close()
+
+
+def test_pf_long_double_overflow():
+    """The reference stops ("huge val error", exit 1) once a partition-function
+    value reaches long double infinity (CPNP/MSAPartProbs.cpp:547-589); the
+    oracle (x87 long double) overflows between 3400 and 3700 identical W
+    residues.  The GPU's fp64 frames reach much further, so it flags the same
+    bound: MLP_ERR_OVERFLOW at 3800, a normal result at 3300."""
+    from mlprobs_amd.engine import MlpError
+    ok = Family(['W' * 3300, 'W' * 3300])
+    ok.posteriors(3, 0.132548)
+    assert ok.results()[2][0] > 0
+    ok.close()
+    with pytest.raises(OverflowError):
+        orc.pf_posterior('W' * 3800, 'W' * 3800)
+    big = Family(['W' * 3800, 'W' * 3800])
+    with pytest.raises(MlpError) as e:
+        big.posteriors(3, 0.132548)
+    assert e.value.code == 3
+    big.close()
