@@ -45,6 +45,18 @@ typedef struct mlp_ctx mlp_ctx;
 
 /* Create a context bound to HIP device `device`. */
 int mlp_ctx_create(int device, mlp_ctx **out);
+/* A context that runs every stage below on the host CPU instead (host
+ * threads, MLP_HOST_THREADS, at most 16) and never initialises the HIP
+ * runtime: for families too small to pay for a device (runtime start-up and
+ * teardown alone cost 0.2-0.4 s per process).  Same results, bit for bit:
+ * the reference's own operation order, the partition function in x87 long
+ * double like the reference.  Covers the C_P_NP_Aln entry points
+ * (mlp_viterbi / mlp_model_adjustment / mlp_family_features, mlp_posteriors
+ * with pid 0-4 and MLP_PID_NPDO, mlp_relax, the CSR calls); the QuickProbs
+ * and profile-posterior calls return MLP_ERR_STATE. */
+int mlp_ctx_create_host(mlp_ctx **out);
+/* 1 for a host context. */
+int mlp_ctx_is_host(const mlp_ctx *ctx);
 /* A context that drives every GPU of `device_mask` (bit k = HIP device k;
  * devices that do not exist are ignored) from this one host thread (SURVEY.md
  * section 8b: "a ctx drives all GPUs in its mask").  For families of at least

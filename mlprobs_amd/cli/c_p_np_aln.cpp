@@ -172,14 +172,29 @@ int main(int argc, char** argv) {
 
   mlp_ctx* ctx = nullptr;
   stage("parse");
-  // every visible GPU: families of >= 1e9 pair-cells are sharded over them
-  check(nullptr, mlp_ctx_create_mask(~0ull, &ctx), "device");
-  stage("device init");
-  // one family per process: a moderate batch scratch.  A fresh process's
-  // allocation waits for the driver to clear memory the previous process
-  // released; back to back at C3 (512 x 400) the posterior stage took 1.09 s
-  // at 32 GB, 1.39 s at 16 GB, 7.4-10.5 s at 64 GB
-  if (!getenv("MLP_SCRATCH_GB")) check(ctx, mlp_set_scratch(ctx, 32ull << 30), "device");
+  // Small families run on the host (mlp_ctx_create_host: the same stages,
+  // bit for bit, without initialising the GPU runtime, whose start-up and
+  // teardown alone cost 0.2-0.4 s per process); at ~2e7 pair-cells/s on the
+  // host threads, families up to MLP_HOST_MAX_CELLS pair-cells (default 4e6,
+  // 0: always the GPU) finish there before a device would be ready.
+  double pair_cells = 0;
+  for (size_t a = 0; a < seqs.size(); a++)
+    for (size_t b = a + 1; b < seqs.size(); b++)
+      pair_cells += (double)(seqs[a].length() + 1) * (double)(seqs[b].length() + 1);
+  const double host_max = getenv("MLP_HOST_MAX_CELLS") ? atof(getenv("MLP_HOST_MAX_CELLS")) : 4e6;
+  if (pair_cells <= host_max) {
+    check(nullptr, mlp_ctx_create_host(&ctx), "host context");
+    stage("host context");
+  } else {
+    // every visible GPU: families of >= 1e9 pair-cells are sharded over them
+    check(nullptr, mlp_ctx_create_mask(~0ull, &ctx), "device");
+    stage("device init");
+    // one family per process: a moderate batch scratch.  A fresh process's
+    // allocation waits for the driver to clear memory the previous process
+    // released; back to back at C3 (512 x 400) the posterior stage took 1.09 s
+    // at 32 GB, 1.39 s at 16 GB, 7.4-10.5 s at 64 GB
+    if (!getenv("MLP_SCRATCH_GB")) check(ctx, mlp_set_scratch(ctx, 32ull << 30), "device");
+  }
   std::string res;
   std::vector<int64_t> off(1, 0);
   for (const Row& r : seqs) {

@@ -25,6 +25,7 @@
 #include <string>
 #include <vector>
 
+#include "host_backend.h"
 #include "mlp_kernels.h"
 #include "mlp_params_default.inc"
 #include "mlp_params_qp.inc"
@@ -44,6 +45,8 @@ enum KernelId { KFWD = 0, KBWD, KTOT, KMERGE, KCOMPACT, KRELAX, KTRANS, KFILTER,
 
 struct mlp_ctx {
   int device = 0;
+  bool host = false;                  // mlp_ctx_create_host: every stage on the CPU, no HIP call
+  mlph::Store hs;                     // the host context's canonical CSR store
   hipStream_t stream = nullptr;
   hipStream_t stream2 = nullptr;   // second posterior batch stream (pipelined batches)
   std::string err;
@@ -347,6 +350,15 @@ int mlp_ctx_create(int device, mlp_ctx** out) {
   return MLP_OK;
 }
 
+int mlp_ctx_create_host(mlp_ctx** out) {
+  if (!out) return MLP_ERR_ARG;
+  *out = new mlp_ctx();
+  (*out)->host = true;
+  return MLP_OK;
+}
+
+int mlp_ctx_is_host(const mlp_ctx* c) { return c && c->host ? 1 : 0; }
+
 int mlp_ctx_create_mask(uint64_t device_mask, mlp_ctx** out) {
   if (!out) return MLP_ERR_ARG;
   *out = nullptr;
@@ -366,10 +378,14 @@ int mlp_set_shards(mlp_ctx* c, int nshards) {
   return MLP_OK;
 }
 
-int mlp_shard_count(mlp_ctx* c) { return c ? shard_count(c) : 0; }
+int mlp_shard_count(mlp_ctx* c) { return c ? (c->host ? 1 : shard_count(c)) : 0; }
 
 void mlp_ctx_destroy(mlp_ctx* c) {
   if (!c) return;
+  if (c->host) {
+    delete c;
+    return;
+  }
   for (mlp_ctx* ch : c->shards) mlp_ctx_destroy(ch);
   c->shards.clear();
   hipSetDevice(c->device);
@@ -409,7 +425,7 @@ int mlp_family_load(mlp_ctx* c, int n, const char* residues, const int64_t* offs
   if (!c || n < 1 || !residues || !offsets) return MLP_ERR_ARG;
   for (mlp_ctx* ch : c->shards) mlp_ctx_destroy(ch);  // re-created for the new family when needed
   c->shards.clear();
-  hipSetDevice(c->device);
+  if (!c->host) hipSetDevice(c->device);
   c->n = n;
   c->lens.assign(n, 0);
   c->offs.assign(offsets, offsets + n + 1);
@@ -448,18 +464,6 @@ int mlp_family_load(mlp_ctx* c, int n, const char* residues, const int64_t* offs
       c->trp_off[p + 1] = c->trp_off[p] + c->lens[b] + 2;
     }
   int rc;
-  if ((rc = dalloc(c, &c->d_res, codes.size()))) return rc;
-  if ((rc = dalloc(c, &c->d_off, n + 1))) return rc;
-  if ((rc = dalloc(c, &c->d_len, n))) return rc;
-  if ((rc = dalloc(c, &c->d_rp_off, c->P + 1))) return rc;
-  if ((rc = dalloc(c, &c->d_trp_off, c->P + 1))) return rc;
-  if ((rc = dalloc(c, &c->d_rowptr, c->rp_off[c->P]))) return rc;
-  if ((rc = dalloc(c, &c->d_ent_off, c->P + 1))) return rc;
-  HIPCHK(c, hipMemcpy(c->d_res, codes.data(), codes.size(), hipMemcpyHostToDevice));
-  HIPCHK(c, hipMemcpy(c->d_off, offsets, sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice));
-  HIPCHK(c, hipMemcpy(c->d_len, c->lens.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice));
-  HIPCHK(c, hipMemcpy(c->d_rp_off, c->rp_off.data(), sizeof(int64_t) * (c->P + 1), hipMemcpyHostToDevice));
-  HIPCHK(c, hipMemcpy(c->d_trp_off, c->trp_off.data(), sizeof(int64_t) * (c->P + 1), hipMemcpyHostToDevice));
   c->ent_off.assign(c->P + 1, 0);
   c->dist.assign(c->P, 0.f);
   c->mea.assign(c->P, 0.f);
@@ -472,6 +476,25 @@ int mlp_family_load(mlp_ctx* c, int n, const char* residues, const int64_t* offs
   for (int64_t q = 0; q < c->P; q++) c->vit_off[q + 1] = c->vit_off[q] + c->lens[c->pa[q]] + c->lens[c->pb[q]];
   c->vit_path.clear();
   c->vit_done = c->vit_paths = false;
+  if (c->host) {
+    c->hs.rowptr.assign(c->rp_off[c->P], 0);
+    c->hs.ent_off.assign(c->P + 1, 0);
+    c->hs.cols.clear();
+    c->hs.vals.clear();
+    return MLP_OK;
+  }
+  if ((rc = dalloc(c, &c->d_res, codes.size()))) return rc;
+  if ((rc = dalloc(c, &c->d_off, n + 1))) return rc;
+  if ((rc = dalloc(c, &c->d_len, n))) return rc;
+  if ((rc = dalloc(c, &c->d_rp_off, c->P + 1))) return rc;
+  if ((rc = dalloc(c, &c->d_trp_off, c->P + 1))) return rc;
+  if ((rc = dalloc(c, &c->d_rowptr, c->rp_off[c->P]))) return rc;
+  if ((rc = dalloc(c, &c->d_ent_off, c->P + 1))) return rc;
+  HIPCHK(c, hipMemcpy(c->d_res, codes.data(), codes.size(), hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(c->d_off, offsets, sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(c->d_len, c->lens.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(c->d_rp_off, c->rp_off.data(), sizeof(int64_t) * (c->P + 1), hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(c->d_trp_off, c->trp_off.data(), sizeof(int64_t) * (c->P + 1), hipMemcpyHostToDevice));
   return MLP_OK;
 }
 
@@ -862,6 +885,38 @@ static int broadcast_store(mlp_ctx* c, mlp_ctx* ch) {
   return MLP_OK;
 }
 
+// ---- the host context (mlp_ctx_create_host): host_backend.cpp
+static mlph::FamilyView host_view(const mlp_ctx* c) {
+  return mlph::FamilyView{c->n, c->lens.data(), c->offs.data(), c->h_res.data(), c->pa.data(), c->pb.data()};
+}
+
+static int host_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
+  const bool npdo = (pid & kPidNpdo) != 0;
+  pid &= ~kPidNpdo;
+  if (pid == kPidQP) {
+    c->err = "the QuickProbs posterior stage runs on a device context";
+    return MLP_ERR_STATE;
+  }
+  if (c->store_p0 == c->store_p1 || p0 != c->store_p1) {  // as the device store: append or restart
+    c->store_p0 = c->store_p1 = p0;
+    c->store_total = 0; ++c->store_ver;
+    c->hs.ent_off[p0] = 0;
+    c->hs.cols.clear();
+    c->hs.vals.clear();
+  }
+  Tables T;
+  ModelScalars ms;
+  build_tables(T, ms, delta);
+  const int rc = mlph::posteriors(T, ms, host_view(c), pid, npdo, p0, p1, c->rp_off, c->hs, c->dist.data(),
+                                  c->mea.data(), c->nnz.data(), c->err);
+  if (rc) return rc == 3 ? MLP_ERR_OVERFLOW : MLP_ERR_STATE;
+  for (int64_t p = p0; p <= p1; p++) c->ent_off[p] = c->hs.ent_off[p];
+  c->store_p1 = p1;
+  c->store_total = c->hs.ent_off[p1];
+  ++c->store_ver;
+  return MLP_OK;
+}
+
 static int sharded_posteriors(mlp_ctx* c, int pid, float delta, int S) {
   int rc;
   if ((rc = ensure_shards(c, S))) return rc;
@@ -877,6 +932,7 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
   if (!c) return MLP_ERR_ARG;
   if (c->n < 2) { c->err = "family needs >= 2 sequences"; return MLP_ERR_STATE; }
   if (p0 < 0 || p1 > c->P || p0 > p1) { c->err = "bad pair range"; return MLP_ERR_ARG; }
+  if (c->host) return host_posteriors(c, pid, delta, p0, p1);
   if (p0 == 0 && p1 == c->P && !c->comm) {
     const int S = shard_count(c);
     if (S > 1) return sharded_posteriors(c, pid, delta, S);
@@ -1171,6 +1227,10 @@ static int profile_posterior(mlp_ctx* c, const std::vector<float>& w, int n1, co
                              const int32_t* map1, int n2, const int32_t* labels2, int L2, const int32_t* map2,
                              float* out) {
   if (!map1 || !map2 || L1 < 1 || L2 < 1) return MLP_ERR_ARG;
+  if (c->host) {
+    c->err = "the profile posterior runs on a device context";
+    return MLP_ERR_STATE;
+  }
   if (c->store_p0 != 0 || c->store_p1 != c->P) {
     c->err = "the profile posterior needs every pair";
     return MLP_ERR_STATE;
@@ -1312,6 +1372,19 @@ int mlp_viterbi(mlp_ctx* c, int64_t p0, int64_t p1, int keep_paths) {
   if (!c) return MLP_ERR_ARG;
   if (c->n < 2) { c->err = "family needs >= 2 sequences"; return MLP_ERR_STATE; }
   if (p0 < 0 || p1 > c->P || p0 > p1) { c->err = "bad pair range"; return MLP_ERR_ARG; }
+  if (c->host) {
+    Tables T;
+    ModelScalars ms;
+    build_tables(T, ms, -1.0f);
+    if (keep_paths && c->vit_path.size() != (size_t)c->vit_off[c->P]) c->vit_path.assign(c->vit_off[c->P], 0);
+    mlph::viterbi(T, ms, host_view(c), p0, p1, c->vit_len.data(), c->vit_match.data(), c->vit_off.data(),
+                  keep_paths ? c->vit_path.data() : nullptr);
+    if (p0 == 0 && p1 == c->P) {
+      c->vit_done = true;
+      c->vit_paths = keep_paths != 0;
+    }
+    return MLP_OK;
+  }
   hipSetDevice(c->device);
   ModelScalars ms;
   build_tables(c->h_tables, ms, -1.0f);
@@ -1547,6 +1620,13 @@ int mlp_csr_total(mlp_ctx* c, int64_t* total) {
 
 int mlp_csr_export(mlp_ctx* c, int32_t* row_ptr, int64_t* ent_off, uint16_t* cols, float* vals) {
   if (!c) return MLP_ERR_ARG;
+  if (c->host) {
+    if (row_ptr) memcpy(row_ptr, c->hs.rowptr.data(), sizeof(int32_t) * c->rp_off[c->P]);
+    if (ent_off) memcpy(ent_off, c->ent_off.data(), sizeof(int64_t) * (c->P + 1));
+    if (cols && c->store_total) memcpy(cols, c->hs.cols.data(), sizeof(uint16_t) * c->store_total);
+    if (vals && c->store_total) memcpy(vals, c->hs.vals.data(), sizeof(float) * c->store_total);
+    return MLP_OK;
+  }
   hipSetDevice(c->device);
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if (row_ptr) HIPCHK(c, hipMemcpy(row_ptr, c->d_rowptr, sizeof(int32_t) * c->rp_off[c->P], hipMemcpyDeviceToHost));
@@ -1560,8 +1640,20 @@ int mlp_csr_import(mlp_ctx* c, const int32_t* row_ptr, const int64_t* ent_off, c
                    const float* vals) {
   if (!c || !row_ptr || !ent_off) return MLP_ERR_ARG;
   if (c->n < 2) return MLP_ERR_STATE;
-  hipSetDevice(c->device);
   const int64_t total = ent_off[c->P];
+  if (c->host) {
+    c->hs.rowptr.assign(row_ptr, row_ptr + c->rp_off[c->P]);
+    c->hs.ent_off.assign(ent_off, ent_off + c->P + 1);
+    c->hs.cols.assign(cols, cols + total);
+    c->hs.vals.assign(vals, vals + total);
+    c->ent_off.assign(ent_off, ent_off + c->P + 1);
+    for (int64_t p = 0; p < c->P; p++) c->nnz[p] = ent_off[p + 1] - ent_off[p];
+    c->store_p0 = 0;
+    c->store_p1 = c->P;
+    c->store_total = total; ++c->store_ver;
+    return MLP_OK;
+  }
+  hipSetDevice(c->device);
   int rc;
   if ((rc = grow_store(c, total, 0))) return rc;
   HIPCHK(c, hipMemcpy(c->d_rowptr, row_ptr, sizeof(int32_t) * c->rp_off[c->P], hipMemcpyHostToDevice));
@@ -1682,6 +1774,7 @@ int mlp_comm_unique_id(unsigned char id[128]) {
 
 int mlp_comm_init(mlp_ctx* c, const unsigned char id[128], int nranks, int rank) {
   if (!c || !id || nranks < 1 || rank < 0 || rank >= nranks) return MLP_ERR_ARG;
+  if (c->host) return MLP_ERR_STATE;
   hipSetDevice(c->device);
   ncclUniqueId u;
   memcpy(&u, id, 128);
@@ -1778,6 +1871,18 @@ static int relax_rounds(mlp_ctx* c, int iters, const QpRelax& qp, const float* h
 
 int mlp_relax(mlp_ctx* c, int iters) {
   if (!c || iters < 0) return MLP_ERR_ARG;
+  if (c->host) {
+    if (c->n < 2) return MLP_ERR_STATE;
+    if (c->store_p0 != 0 || c->store_p1 != c->P) {
+      c->err = "relaxation needs every pair";
+      return MLP_ERR_STATE;
+    }
+    for (int it = 0; it < iters; it++) mlph::relax(host_view(c), c->rp_off, c->hs, c->nnz.data());
+    c->ent_off = c->hs.ent_off;
+    c->store_total = c->hs.ent_off[c->P];
+    ++c->store_ver;
+    return MLP_OK;
+  }
   return relax_rounds(c, iters, QpRelax{0, nullptr, 0.f, nullptr, 200.f}, nullptr, nullptr);
 }
 
@@ -1793,6 +1898,10 @@ int mlp_relax_qp_selective(mlp_ctx* c, int iters, const float* seq_weights, cons
                            float selectivity) {
   if (!c || !seq_weights || !(selectivity > 0)) return MLP_ERR_ARG;
   if (c->n < 2) return MLP_ERR_STATE;
+  if (c->host) {
+    c->err = "QuickProbs' consistency stage runs on a device context";
+    return MLP_ERR_STATE;
+  }
   if (iters < 0) iters = c->n > 50 ? 1 : 2;
   int rc;
   if ((rc = ensure(c, c->r_weights, sizeof(float) * c->n))) return rc;
@@ -2172,6 +2281,7 @@ static int relax_one(mlp_ctx* c, const QpRelax& qp, bool last) {
 
 int mlp_synchronize(mlp_ctx* c) {
   if (!c) return MLP_ERR_ARG;
+  if (c->host) return MLP_OK;
   for (mlp_ctx* ch : c->shards) {
     hipSetDevice(ch->device);
     HIPCHK(c, hipStreamSynchronize(ch->stream));
@@ -2190,6 +2300,7 @@ int mlp_profile(mlp_ctx* c, int enable) {
 
 int mlp_profile_reset(mlp_ctx* c) {
   if (!c) return MLP_ERR_ARG;
+  if (c->host) return MLP_OK;
   for (mlp_ctx* ch : c->shards) mlp_profile_reset(ch);
   flush_timers(c);
   for (int k = 0; k < MLP_NKERNELS; k++) {
@@ -2202,6 +2313,14 @@ int mlp_profile_reset(mlp_ctx* c) {
 
 int mlp_kernel_times(mlp_ctx* c, double* ms, int64_t* launches, int64_t* cells) {
   if (!c) return MLP_ERR_ARG;
+  if (c->host) {
+    for (int k = 0; k < MLP_NKERNELS; k++) {
+      if (ms) ms[k] = 0;
+      if (launches) launches[k] = 0;
+      if (cells) cells[k] = 0;
+    }
+    return MLP_OK;
+  }
   flush_timers(c);
   for (mlp_ctx* ch : c->shards) {
     hipSetDevice(ch->device);

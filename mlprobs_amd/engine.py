@@ -90,6 +90,8 @@ def lib():
         L.mlp_profile_reset.argtypes = [P]
         L.mlp_kernel_times.argtypes = [P, C.c_void_p, C.c_void_p, C.c_void_p]
         L.mlp_ctx_create_mask.argtypes = [C.c_uint64, C.POINTER(P)]
+        L.mlp_ctx_create_host.argtypes = [C.POINTER(P)]
+        L.mlp_ctx_is_host.argtypes = [P]
         L.mlp_set_shards.argtypes = [P, C.c_int]
         L.mlp_shard_count.argtypes = [P]
         L.mlp_relax_shard_plan.argtypes = [C.c_int, I32P, I64P, C.c_int, I64P]
@@ -104,7 +106,7 @@ EXPORTED = ['mlp_ctx_create', 'mlp_ctx_destroy', 'mlp_last_error', 'mlp_set_scra
             'mlp_viterbi_path', 'mlp_model_adjustment', 'mlp_family_features', 'mlp_comm_unique_id', 'mlp_comm_init',
             'mlp_shard_range', 'mlp_shard_plan', 'mlp_gather_layout', 'mlp_allgather', 'mlp_synchronize', 'mlp_profile',
             'mlp_kernel_times', 'mlp_profile_reset', 'mlp_ctx_create_mask', 'mlp_set_shards', 'mlp_shard_count',
-            'mlp_relax_shard_plan']
+            'mlp_relax_shard_plan', 'mlp_ctx_create_host', 'mlp_ctx_is_host']
 
 
 def shard_plan(lens, nranks, rank):
@@ -155,13 +157,16 @@ def pairs_of(n):
 class Family:
     """One MLProbs family resident on one GPU."""
 
-    def __init__(self, seqs, device=0, device_mask=None, shards=None):
+    def __init__(self, seqs, device=0, device_mask=None, shards=None, host=False):
         """device: one GPU; device_mask: every GPU of the mask from this one
         context (mlp_ctx_create_mask); shards: force that many shards (virtual
-        shards may share a GPU)."""
+        shards may share a GPU); host: the host-CPU context
+        (mlp_ctx_create_host), no GPU involved."""
         self._L = lib()
         self._ctx = C.c_void_p()
-        if device_mask is not None or shards:
+        if host:
+            self._chk(self._L.mlp_ctx_create_host(C.byref(self._ctx)), ctx=False)
+        elif device_mask is not None or shards:
             mask = device_mask if device_mask is not None else (1 << int(device))
             self._chk(self._L.mlp_ctx_create_mask(int(mask), C.byref(self._ctx)), ctx=False)
         else:

@@ -1,5 +1,7 @@
 """The c_p_np_aln drop-in binary (mlprobs_amd/cli) on the GPU against the
-reference CLI's single-thread outputs (tests/golden/cli)."""
+reference CLI's single-thread outputs (tests/golden/cli).  MLP_HOST_MAX_CELLS=0
+keeps every family on the GPU path (small families would otherwise take the
+host path, which tests/test_cli_hostpath.py covers in the CPU suite)."""
 import os
 import subprocess
 
@@ -11,10 +13,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BIN = os.path.join(ROOT, 'mlprobs_amd', 'cli', 'c_p_np_aln')
 
 pytestmark = pytest.mark.gpu
+ENV = dict(os.environ, MLP_HOST_MAX_CELLS='0')  # every CLI process of this module: the GPU path
 
 
 def _run(*args):
-    return subprocess.run([BIN, *args], capture_output=True, text=True, timeout=300)
+    return subprocess.run([BIN, *args], capture_output=True, text=True, timeout=300, env=ENV)
 
 
 @pytest.mark.parametrize('name', ['bb11028', 'div12', 'sim8'])
@@ -40,7 +43,7 @@ def test_cli_profile_posterior_on_gpu(name, flags, suffix):
     """Every progressive merge and refinement pass through the GPU's
     BuildPosterior (MLP_PROFILE_GPU_MIN=1: no host fallback for small
     profile pairs): still the reference's bytes."""
-    env = dict(os.environ, MLP_PROFILE_GPU_MIN='1', MLP_SRAND_TIME='1700000000')
+    env = dict(ENV, MLP_PROFILE_GPU_MIN='1', MLP_SRAND_TIME='1700000000')
     r = subprocess.run([BIN, *(flags or ('-p', '0')), os.path.join(GOLDEN, 'cli', f'{name}.fa')], capture_output=True,
                        text=True, timeout=300, env=env)
     assert r.returncode == 0 and r.stderr == '', r.stderr
@@ -77,7 +80,7 @@ def test_cli_nonprogressive(name):
     fa = _fasta_of(name)
     for tag, args in (('p_1_ir_0', ['-p', '1', '-ir', '0']), ('p_1', ['-p', '1'])):
         r = subprocess.run([BIN, *args, fa], capture_output=True, timeout=300,
-                           env=dict(os.environ, MLP_SRAND_TIME=NP_TIME))
+                           env=dict(ENV, MLP_SRAND_TIME=NP_TIME))
         assert r.returncode == 0 and r.stderr == b'', (tag, r.stderr)
         with open(os.path.join(NP, f'{name}.{tag}.out'), 'rb') as fh:
             assert r.stdout == fh.read(), (name, tag)
@@ -93,7 +96,7 @@ QP_BIN = os.path.join(ROOT, 'mlprobs_amd', 'cli', 'quickprobs')
                                        ('sim8', ['-c', '3', '-r', '50']), ('qp_div60', []), ('qp_big210', [])])
 def test_quickprobs_cli(name, args):
     r = subprocess.run([QP_BIN, *args, os.path.join(GOLDEN, 'cli', f'{name}.fa')], capture_output=True, text=True,
-                       timeout=300)
+                       timeout=300, env=ENV)
     assert r.returncode == 0 and r.stderr == '', r.stderr
     tag = 'qp_' + name.replace('qp_', '') + ''.join('_' + a.strip('-') for a in args)
     with open(os.path.join(GOLDEN, 'cli', f'{tag}.out')) as fh:
@@ -101,15 +104,15 @@ def test_quickprobs_cli(name, args):
 
 
 def test_quickprobs_cli_edges(tmp_path):
-    r = subprocess.run([QP_BIN], capture_output=True, text=True, timeout=60)
+    r = subprocess.run([QP_BIN], capture_output=True, text=True, timeout=60, env=ENV)
     assert r.returncode == 0 and r.stdout.startswith('Usage:')        # no input: usage (main.cpp:31-37)
     bad = tmp_path / 'bad.fa'
     bad.write_text('>a\nMK1V\n>b\nMKV\n')
-    r = subprocess.run([QP_BIN, str(bad)], capture_output=True, text=True, timeout=60)
+    r = subprocess.run([QP_BIN, str(bad)], capture_output=True, text=True, timeout=60, env=ENV)
     assert r.returncode == 255 and 'illegal sequence character:1' in r.stdout
     one = tmp_path / 'one.fa'
     one.write_text('>only one\nmkvlaa\nGG\n')
-    r = subprocess.run([QP_BIN, '-o', str(tmp_path / 'o.fa'), str(one)], capture_output=True, text=True, timeout=60)
+    r = subprocess.run([QP_BIN, '-o', str(tmp_path / 'o.fa'), str(one)], capture_output=True, text=True, timeout=60, env=ENV)
     assert r.returncode == 0 and (tmp_path / 'o.fa').read_text() == '>only one\nMKVLAAGG\n'
 
 
@@ -126,7 +129,7 @@ def test_real_families(name):
     for tag, cmd in (('G', [BIN, '-G', fa]), ('p_0', [BIN, '-p', '0', fa]), ('qp', [QP_BIN, fa])):
         if not os.path.exists(os.path.join(REAL, f'{name}.{tag}.out')):
             continue  # the larger oxxL_ families are quickprobs-only
-        r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=ENV)
         assert r.returncode == 0 and r.stderr == '', (tag, r.stderr)
         with open(os.path.join(REAL, f'{name}.{tag}.out')) as fh:
             assert r.stdout == fh.read(), (name, tag)
@@ -142,7 +145,7 @@ def test_edge_families(name):
     X/B/Z, CRLF line ends (tests/golden/gen_edge.py)."""
     fa = os.path.join(EDGE, f'{name}.fa')
     for tag, cmd in (('G', [BIN, '-G', fa]), ('p_0', [BIN, '-p', '0', fa]), ('qp', [QP_BIN, fa])):
-        r = subprocess.run(cmd, capture_output=True, timeout=120)  # bytes: CR stays CR
+        r = subprocess.run(cmd, capture_output=True, timeout=120, env=ENV)  # bytes: CR stays CR
         assert r.returncode == 0 and r.stderr == b'', (tag, r.stderr)
         with open(os.path.join(EDGE, f'{name}.{tag}.out'), 'rb') as fh:
             assert r.stdout == fh.read(), (name, tag)
