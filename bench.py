@@ -271,27 +271,35 @@ def relax_leg(fam, args, n, lens, total_cells):
 def e2e_families(args):
     """End-to-end seconds per family of the c_p_np_aln drop-in (-p 0: family
     test, posteriors, guide tree, 2 consistency rounds, progressive alignment,
-    refinement), one fresh process per family, wall clock around the process;
-    stage times from MLP_CLI_TIMES."""
+    refinement; -p 1: family test, posteriors, 2 consistency rounds, alignment
+    graph, refinement), one fresh process per run, wall clock around the
+    process; two runs each, the second reported (the first, which may wait
+    for memory an earlier process released, as first_run_seconds); stage
+    times from MLP_CLI_TIMES."""
     from mlprobs_amd import synth
     cli = os.path.join(ROOT, 'mlprobs_amd', 'cli', 'c_p_np_aln')
     if not os.path.exists(cli):
         return None
     res = {}
     for tag, n, L in (('C2 128x256', 128, 256), (f'C3 {args.n}x{args.len}', args.n, args.len)):
-        with tempfile.TemporaryDirectory() as td:
-            fa = os.path.join(td, 'fam.fa')
-            synth.write_fasta(fa, synth.family(n, L, args.s, seed=args.seed))
-            t0 = time.perf_counter()
-            r = subprocess.run([cli, '-p', '0', fa], capture_output=True, text=True, timeout=600,
-                               env=dict(os.environ, MLP_CLI_TIMES='1'))
-            dt = time.perf_counter() - t0
-        stages = {}
-        for line in r.stderr.splitlines():
-            if line.startswith('[stage] '):
-                name, sec = line[8:].rsplit(' ', 2)[0], line.rsplit(' ', 2)[1]
-                stages[name] = float(sec)
-        res[tag] = {'seconds': dt, 'exit': r.returncode, 'stages_s': stages}
+        for mode in ('0', '1'):
+            with tempfile.TemporaryDirectory() as td:
+                fa = os.path.join(td, 'fam.fa')
+                synth.write_fasta(fa, synth.family(n, L, args.s, seed=args.seed))
+                runs = []
+                for _ in range(2):  # the first process may wait for memory an earlier one released
+                    t0 = time.perf_counter()
+                    r = subprocess.run([cli, '-p', mode, fa], capture_output=True, text=True, timeout=600,
+                                       env=dict(os.environ, MLP_CLI_TIMES='1'))
+                    runs.append((time.perf_counter() - t0, r))
+            dt, r = runs[1]
+            stages = {}
+            for line in r.stderr.splitlines():
+                if line.startswith('[stage] '):
+                    name, sec = line[8:].rsplit(' ', 2)[0], line.rsplit(' ', 2)[1]
+                    stages[name] = float(sec)
+            res[tag if mode == '0' else f'{tag} -p 1'] = {'seconds': dt, 'first_run_seconds': runs[0][0],
+                                                          'exit': r.returncode, 'stages_s': stages}
     qp = os.path.join(ROOT, 'mlprobs_amd', 'cli', 'quickprobs')
     ref = os.path.join(ROOT, 'oracle', '_ref', 'quickprobs')
     if os.path.exists(qp):
@@ -319,6 +327,56 @@ def e2e_families(args):
                                         timeout=600)
                     res[tag]['reference_cpu'] = {'seconds': time.perf_counter() - t0, 'threads': args.cpu_threads,
                                                  'exit': rr.returncode, 'identical_output': rr.stdout == r.stdout}
+    return res
+
+
+def c5_families(args):
+    """C5-style end-to-end seconds per family (BASELINE.json configs[4]: the
+    reference's TEST/ox + TEST/sabre families) for the C_P_NP_Aln calls
+    MLProbs.py makes per family -- the `-G` feature line, then the MSA
+    (`-p 0`) -- one fresh process each, as MLProbs runs them: the drop-in
+    (small families take its host path, larger ones the GPU) against the
+    reference CLI built from source (oracle/_ref/c_p_np_aln, OpenMP with
+    --cpu-threads threads; its default of every host core oversubscribes the
+    box's CPU share), on every 15th family of tests/golden/sweep.json.xz,
+    with the outputs compared to the reference's stored ones.  The classifier
+    and the QuickProbs region realignment of MLProbs.py are not part of
+    this drop-in."""
+    import lzma
+    cli = os.path.join(ROOT, 'mlprobs_amd', 'cli', 'c_p_np_aln')
+    ref = os.path.join(ROOT, 'oracle', '_ref', 'c_p_np_aln')
+    if not os.path.exists(cli):
+        return None
+    with lzma.open(os.path.join(ROOT, 'tests', 'golden', 'sweep.json.xz'), 'rt') as fh:
+        fams = json.load(fh)
+    names = [k for k in sorted(fams) if k.split('/')[0] in ('ox', 'sabre') and 'p_0' in fams[k]][::15]
+    ours, theirs, same, host = [], [], 0, 0
+    env_ref = dict(os.environ, OMP_NUM_THREADS=str(args.cpu_threads))
+    with tempfile.TemporaryDirectory() as td:
+        for name in names:
+            e = fams[name]
+            fa = os.path.join(td, 'f.fa')
+            with open(fa, 'wb') as fh:
+                fh.write(e['fa'].encode('latin-1'))
+            t0 = time.perf_counter()
+            g = subprocess.run([cli, '-G', fa], capture_output=True, timeout=300)
+            m = subprocess.run([cli, '-p', '0', fa], capture_output=True, timeout=300)
+            ours.append(time.perf_counter() - t0)
+            same += (g.stdout.decode('latin-1') == e['G'][1]) and (m.stdout.decode('latin-1') == e['p_0'][1])
+            host += e['cells'] <= 4e6
+            if os.path.exists(ref) and not args.no_cpu:
+                t0 = time.perf_counter()
+                subprocess.run([ref, '-G', fa], capture_output=True, timeout=300, env=env_ref)
+                subprocess.run([ref, '-p', '0', fa], capture_output=True, timeout=300, env=env_ref)
+                theirs.append(time.perf_counter() - t0)
+    res = {'families': len(names), 'sample': 'every 15th TEST/ox + TEST/sabre family of tests/golden/sweep.json.xz',
+           'calls': '-G then -p 0, one process each', 'host_path_families': host,
+           'identical_outputs': same, 'drop_in_s_per_family': {'median': float(np.median(ours)),
+                                                                 'mean': float(np.mean(ours))}}
+    if theirs:
+        res['reference_s_per_family'] = {'median': float(np.median(theirs)), 'mean': float(np.mean(theirs)),
+                                         'threads': args.cpu_threads}
+        res['speedup_median'] = float(np.median(theirs)) / float(np.median(ours))
     return res
 
 
@@ -376,6 +434,7 @@ def main():
     # end-to-end family timings first, on an idle device (a process that
     # follows a large release waits for the driver to clear that memory)
     e2e = e2e_families(args) if (not args.no_e2e and world == 1) else None
+    c5 = c5_families(args) if (not args.no_e2e and world == 1 and rank == 0) else None
     if args.relax < 0:
         args.relax = 4 if world == 1 else 0
     fam_in = synth.family(args.n, args.len, args.s, seed=args.seed)
@@ -494,6 +553,8 @@ def main():
             out['relax'] = relax_info
         if e2e is not None:
             out['e2e'] = e2e
+        if c5 is not None:
+            out['c5_families'] = c5
         if qp_info is not None:
             out['quickprobs'] = qp_info
         print(json.dumps(out))

@@ -207,10 +207,19 @@ std::vector<float> build_posterior(const Profile& A, const Profile& B, const Spa
 }
 
 void build_posterior_into(const Profile& A, const Profile& B, const SparseSet& sp, const int* weights,
-                          float cutoff, std::vector<float>& post) {
+                          float cutoff, std::vector<float>& post, std::vector<size_t>* dirty) {
   const int len1 = A[0].length(), len2 = B[0].length();
   const int64_t W2 = len2 + 1;
-  post.assign((size_t)(len1 + 1) * W2, 0.f);
+  const size_t cells = (size_t)(len1 + 1) * W2;
+  // with `dirty` the buffer is all zero on entry (only the cells it lists were
+  // written since) and the written cells are listed: the long profiles of the
+  // -p 1 alignment graph make the dense fill cost more than the adds
+  if (dirty && cutoff == 0.f) {
+    if (post.size() < cells) post.resize(cells, 0.f);
+  } else {
+    dirty = nullptr;
+    post.assign(cells, 0.f);
+  }
   float total = 0;
   if (weights)
     for (const Row& x : A)
@@ -256,16 +265,20 @@ void build_posterior_into(const Profile& A, const Profile& B, const SparseSet& s
       if (first < second) {
         for (int ii = r0; ii <= r1; ii = next_row(ii)) {
           const int64_t base = (int64_t)m1[ii] * W2;
-          for (int32_t e = rp[ii]; e < rp[ii + 1]; e++)
+          for (int32_t e = rp[ii]; e < rp[ii + 1]; e++) {
             post[base + m2[cols[e]]] += weights ? w * vals[e] : vals[e];
+            if (dirty) dirty->push_back(base + m2[cols[e]]);
+          }
           if (do_sub)
             for (int jj = 0; jj < ncols; jj++) post[base + m2[jj]] -= sub;
         }
       } else {
         for (int jj = r0; jj <= r1; jj = next_row(jj)) {
           const int64_t base = m2[jj];
-          for (int32_t e = rp[jj]; e < rp[jj + 1]; e++)
+          for (int32_t e = rp[jj]; e < rp[jj + 1]; e++) {
             post[base + (int64_t)m1[cols[e]] * W2] += weights ? w * vals[e] : vals[e];
+            if (dirty) dirty->push_back(base + (int64_t)m1[cols[e]] * W2);
+          }
           if (do_sub)
             for (int ii = 0; ii < ncols; ii++) post[base + (int64_t)m1[ii] * W2] -= sub;
         }
@@ -284,8 +297,18 @@ const float* profile_posterior(const Profile& a, const Profile& b, const SparseS
                                float cutoff) {
   if (profile_backend() && cutoff == 0.f)
     if (const float* p = profile_backend()(a, b, weights)) return p;
-  static thread_local std::vector<float> buf;   // reused: fresh pages cost more than the adds
-  build_posterior_into(a, b, sp, weights, cutoff, buf);
+  // reused, kept all zero between calls: only the cells the previous call
+  // wrote are cleared (fresh pages, or a full fill, cost more than the adds)
+  static thread_local std::vector<float> buf;
+  static thread_local std::vector<size_t> dirty;
+  for (size_t k : dirty) buf[k] = 0.f;
+  dirty.clear();
+  build_posterior_into(a, b, sp, weights, cutoff, buf, &dirty);
+  if (cutoff != 0.f) {   // a full fill: the whole used range is dirty
+    const size_t cells = (size_t)(a[0].length() + 1) * (b[0].length() + 1);
+    dirty.resize(cells);
+    for (size_t k = 0; k < cells; k++) dirty[k] = k;
+  }
   return buf.data();
 }
 

@@ -69,7 +69,7 @@ GuideTree build_tree(std::vector<std::vector<float>> dist, int varianceid);
 std::vector<float> build_posterior(const Profile& a, const Profile& b, const SparseSet& sp,
                                    const int* weights, float cutoff);
 void build_posterior_into(const Profile& a, const Profile& b, const SparseSet& sp, const int* weights,
-                          float cutoff, std::vector<float>& post);
+                          float cutoff, std::vector<float>& post, std::vector<size_t>* dirty = nullptr);
 
 // A device implementation of build_posterior (the GPU's BuildPosterior):
 // returns the dense matrix, valid until its next call, or nullptr to fall

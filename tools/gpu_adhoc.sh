@@ -1,11 +1,15 @@
 #!/bin/bash
+# -p 1 at C2 / C3 (GPU posteriors + host alignment graph), stage times
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/np2
+O=gpurun_out/p1probe
 mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "profile_posterior_on_gpu or pf_long_double or cli_progressive or cli_config or npdo or test_real_families" > $O/gputest.log 2>&1 || { tail -30 $O/gputest.log; exit 1; }
-tail -2 $O/gputest.log
-timeout -k 10 300 python3 bench.py --no-cpu --no-qp --relax 0 --steps 1 --warmup 0 > $O/bench.json 2> $O/bench.err || { tail -5 $O/bench.err; exit 1; }
-python3 -c "
-import json; d=json.load(open('$O/bench.json'))
-for k,v in d['e2e'].items(): print(k, round(v['seconds'],3), {a: round(b,3) for a,b in v['stages_s'].items()})"
+for f in c2_128x256_s11 c3_512x400_s11; do
+  t0=$(date +%s.%N)
+  timeout -k 10 400 env MLP_CLI_TIMES=1 ./mlprobs_amd/cli/c_p_np_aln -p 1 tests/golden/config/$f.fa > $O/$f.p1.out 2> $O/$f.p1.err
+  rc=$?
+  t1=$(date +%s.%N)
+  echo "$f -p 1 rc=$rc wall $(awk "BEGIN{print $t1 - $t0}")" | tee -a $O/summary.txt
+  grep '^\[stage\]' $O/$f.p1.err | tee -a $O/summary.txt
+  [ $rc -eq 0 ] || exit 1
+done
