@@ -58,6 +58,11 @@ def parse():
     return ap.parse_args()
 
 
+def log(msg):
+    """Progress on stderr (a long silent run looks hung to the GPU box's watchdog)."""
+    print(f'[bench {time.strftime("%H:%M:%S")}] {msg}', file=sys.stderr, flush=True)
+
+
 def _oracle():
     sys.path.insert(0, os.path.join(ROOT, 'oracle'))
     import orc
@@ -293,6 +298,7 @@ def e2e_families(args):
                                        env=dict(os.environ, MLP_CLI_TIMES='1'))
                     runs.append((time.perf_counter() - t0, r))
             dt, r = runs[1]
+            log(f'e2e {tag} -p {mode}: {runs[0][0]:.2f} s, {dt:.2f} s (exit {r.returncode})')
             stages = {}
             for line in r.stderr.splitlines():
                 if line.startswith('[stage] '):
@@ -321,6 +327,7 @@ def e2e_families(args):
                         name, sec = line[8:].rsplit(' ', 2)[0], line.rsplit(' ', 2)[1]
                         stages[name] = float(sec)
                 res[tag] = {'seconds': dt, 'exit': r.returncode, 'stages_s': stages}
+                log(f'e2e {tag}: {dt:.2f} s (exit {r.returncode})')
                 if n <= 128 and os.path.exists(ref) and not args.no_cpu:
                     t0 = time.perf_counter()
                     rr = subprocess.run([ref, '-t', str(args.cpu_threads), fa], capture_output=True, text=True,
@@ -351,9 +358,15 @@ def c5_families(args):
         fams = json.load(fh)
     names = [k for k in sorted(fams) if k.split('/')[0] in ('ox', 'sabre') and 'p_0' in fams[k]][::15]
     ours, theirs, same, host = [], [], 0, 0
-    env_ref = dict(os.environ, OMP_NUM_THREADS=str(args.cpu_threads))
+    # the reference sets omp_set_num_threads(omp_get_num_procs()) itself
+    # (CPNP/MSA.cpp:146-151): on the GPU box that is every core of the node
+    # under a 16-core quota, and GOMP's spinning idle threads then stall a
+    # small family for ~23 s; passive waiting does not change its output
+    env_ref = dict(os.environ, OMP_NUM_THREADS=str(args.cpu_threads), OMP_WAIT_POLICY='passive')
     with tempfile.TemporaryDirectory() as td:
-        for name in names:
+        for k, name in enumerate(names):
+            if k % 10 == 0:
+                log(f'c5 family {k}/{len(names)}')
             e = fams[name]
             fa = os.path.join(td, 'f.fa')
             with open(fa, 'wb') as fh:
@@ -366,8 +379,8 @@ def c5_families(args):
             host += e['cells'] <= 4e6
             if os.path.exists(ref) and not args.no_cpu:
                 t0 = time.perf_counter()
-                subprocess.run([ref, '-G', fa], capture_output=True, timeout=300, env=env_ref)
-                subprocess.run([ref, '-p', '0', fa], capture_output=True, timeout=300, env=env_ref)
+                subprocess.run([ref, '-G', fa], capture_output=True, timeout=120, env=env_ref)
+                subprocess.run([ref, '-p', '0', fa], capture_output=True, timeout=120, env=env_ref)
                 theirs.append(time.perf_counter() - t0)
     res = {'families': len(names), 'sample': 'every 15th TEST/ox + TEST/sabre family of tests/golden/sweep.json.xz',
            'calls': '-G then -p 0, one process each', 'host_path_families': host,
@@ -375,7 +388,7 @@ def c5_families(args):
                                                                  'mean': float(np.mean(ours))}}
     if theirs:
         res['reference_s_per_family'] = {'median': float(np.median(theirs)), 'mean': float(np.mean(theirs)),
-                                         'threads': args.cpu_threads}
+                                         'threads': 'omp_get_num_procs() (its own setting), OMP_WAIT_POLICY=passive'}
         res['speedup_median'] = float(np.median(theirs)) / float(np.median(ours))
     return res
 
@@ -433,6 +446,7 @@ def main():
 
     # end-to-end family timings first, on an idle device (a process that
     # follows a large release waits for the driver to clear that memory)
+    log('start')
     e2e = e2e_families(args) if (not args.no_e2e and world == 1) else None
     c5 = c5_families(args) if (not args.no_e2e and world == 1 and rank == 0) else None
     if args.relax < 0:
@@ -463,6 +477,7 @@ def main():
             torch.cuda.synchronize()
             dist.barrier()
 
+    log('posterior stage')
     for _ in range(args.warmup):
         fam.profile(False)
         step()
@@ -483,6 +498,7 @@ def main():
     gpu_dist, nnz = gpu_dist.copy(), nnz.copy()
     # the posterior store, kept for the same-run parity readouts (rank 0)
     post_store = [a.copy() for a in fam.export()] if (rank == 0 and world == 1 and not args.no_cpu) else None
+    log('relaxation rounds')
     relax_info = relax_leg(fam, args, args.n, lens, total_cells) if (args.relax > 0 and world == 1) else None
     value = total_cells * args.steps / dt
     # roofline of the dominant kernel (largest accumulated device time)
@@ -506,6 +522,7 @@ def main():
             valu = {'achieved': issued, 'peak': VALU_PEAK_WAVE_INSTS, 'unit': 'wave-instr/s',
                     'frac': issued / VALU_PEAK_WAVE_INSTS,
                     'insts_per_cell': g['valu_insts_per_cell']}
+    log('quickprobs stage')
     qp_info = quickprobs_stage(fam, fam_in, total_cells, args) if (world == 1 and not args.no_qp) else None
     out = None
     if rank == 0:
@@ -514,6 +531,7 @@ def main():
             with tempfile.TemporaryDirectory() as td:
                 fa = os.path.join(td, 'fam.fa')
                 synth.write_fasta(fa, fam_in)
+                log('cpu baseline')
                 cpu, parity = cpu_baseline(fa, args, args.n, lens, post_store, gpu_dist)
             post_store = None
         out = {

@@ -11,7 +11,5 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout
     > $O/gputest.log 2>&1 || { tail -30 $O/gputest.log; exit 1; }
 tail -3 $O/gputest.log
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { cat $O/smoke.log; exit 1; }
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o stats -- python3 bench.py \
-    > $O/bench.log 2>&1 || { tail -30 $O/bench.log; exit 1; }
-grep '^{"metric"' $O/bench.log | tail -1 > $O/bench.json
+tools/gpu_bench.sh $TAG || exit 1
 echo done
