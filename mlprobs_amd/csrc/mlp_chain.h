@@ -12,22 +12,39 @@ namespace mlp {
 
 // LDS-resident tables of one workgroup: letter-indexed emissions, the PF
 // score factors and the LOOKUP coefficient rows (one ds_read_b128 per
-// LOG_ADD instead of compare/select chains).
-struct LdsTables {
+// LOG_ADD instead of compare/select chains).  Only the parts a kernel's
+// model set reads are staged: LDS bounds the sweeps' occupancy (the HMM
+// tables are 3 KB, the PF factors 5.4 KB).
+template <bool H> struct LdsHmmPart {
   float4 lk[kLookupRows];
   float match[26 * 26];
-  float ins[26];
-  double sub[26 * 26];
 };
+template <> struct LdsHmmPart<false> {};
+template <bool P> struct LdsPfPart { double sub[26 * 26]; };
+template <> struct LdsPfPart<false> {};
+template <bool H, bool P>
+struct LdsTablesT : LdsHmmPart<H>, LdsPfPart<P> {
+  float ins[26];   // row insert emissions (every cursor)
+};
+template <int M>
+using LdsTablesFor = LdsTablesT<(M & (kHmm5 | kLocal)) != 0, (M & kPF) != 0>;
 
-__device__ __forceinline__ void stage_tables(LdsTables& L, const Tables* __restrict__ tab) {
+template <bool H, bool P>
+__device__ __forceinline__ void stage_tables(LdsTablesT<H, P>& L, const Tables* __restrict__ tab) {
   for (int k = threadIdx.x; k < 26 * 26; k += blockDim.x) {
-    L.match[k] = tab->match[k];
-    L.sub[k] = tab->sub[k];
+    if constexpr (H) L.match[k] = tab->match[k];
+    if constexpr (P) L.sub[k] = tab->sub[k];
   }
   if (threadIdx.x < 26) L.ins[threadIdx.x] = tab->ins[threadIdx.x];
-  if (threadIdx.x == 0) mlp_lookup_table(L.lk);
+  if constexpr (H) {
+    if (threadIdx.x == 0) mlp_lookup_table(L.lk);
+  }
   __syncthreads();
+}
+template <bool H, bool P>
+__device__ __forceinline__ const float4* lookup_of(const LdsTablesT<H, P>& L) {
+  if constexpr (H) return L.lk;
+  else return nullptr;
 }
 
 __device__ __forceinline__ int64_t wave_index() {
@@ -61,9 +78,13 @@ struct ChainPair {
   double zmant;      // backward: PF total
   int zexp, pad;
 };
-constexpr int kChainLdsMeta = (int)sizeof(ChainPair) * (kChainMax + 1);
-__host__ __device__ constexpr int chain_lds_stride(int lds_seq) {
-  return kChainLdsMeta + ((lds_seq + 15) & ~15);
+// each wave's LDS region: the members' bookkeeping (count + 1 entries),
+// then the residues (chain_lds_pack)
+__host__ __device__ constexpr int chain_lds_meta(int lds) {
+  return (int)sizeof(ChainPair) * ((lds >> 24) + 1);
+}
+__host__ __device__ constexpr int chain_lds_stride(int lds) {
+  return chain_lds_meta(lds) + (((lds & 0xffffff) + 15) & ~15);
 }
 
 struct ChainView {
@@ -82,7 +103,7 @@ __device__ ChainView stage_chain(uint8_t* dyn, int lds_seq, int64_t ch, SeqSet s
   const int lane = threadIdx.x & 63;
   uint8_t* region = dyn + (threadIdx.x >> 6) * chain_lds_stride(lds_seq);
   ChainPair* P = reinterpret_cast<ChainPair*>(region);
-  uint8_t* seq = region + kChainLdsMeta;
+  uint8_t* seq = region + chain_lds_meta(lds_seq);
   const int K = cm.count[ch], first = cm.first[ch];
   int L1 = 0, L2 = 0, a = 0, b = 0;
   if (lane < K) {

@@ -18,7 +18,10 @@ constexpr int kEll = 64;         // sparse slots per posterior row before overfl
 // anti-diagonal wavefront that wraps from one 64-row strip into the next and
 // from one pair into the next without draining.
 constexpr int kChainMax = 32;    // pairs per chain
-constexpr int kChainSeqSoft = 8192;   // residue bytes per chain (LDS) when stacking pairs
+// residue bytes per chain (LDS) when stacking pairs: 4 regions + the PF
+// tables stay under 160 KB / 6 workgroups, so LDS never binds the sweeps'
+// occupancy before their VGPR budget does
+constexpr int kChainSeqSoft = 4800;
 constexpr int kChainSeqMax = 50000;   // residue bytes of a single-pair chain (one wave per block)
 constexpr int kMinWidth = 192;   // W floor: boundary chunks are loaded 64 columns ahead
 // W for a chain whose widest member has L2 columns (+1): multiple of 8 so the
@@ -31,6 +34,11 @@ __host__ __device__ constexpr int chain_width(int maxL2) {
 // (W + 1) sequences
 __host__ __device__ constexpr int chain_seq_bytes(int W, int sum_l1, int n) {
   return W + 2 + sum_l1 + n * (W + 3);
+}
+// A chain launch's LDS layout is one int: the largest member count (bits
+// 24+) and residue bytes (bits 0-23) over its chains.
+__host__ __device__ constexpr int chain_lds_pack(int seq_bytes, int max_members) {
+  return (max_members << 24) | seq_bytes;
 }
 // strips of a chain with `rows` stacked rows
 __host__ __device__ constexpr int chain_strips(int rows) { return (rows + 63) >> 6; }
@@ -141,13 +149,21 @@ inline int model_set_for_pid(int pid) {
   return kHmm5 | kLocal | kPF;
 }
 
-// launchers (posterior.hip).  lds_seq: max seq_bytes over the chains.
+// A second stream for the sweeps of one batch: when a model set runs as
+// two kernels (fp32 HMMs, fp64 partition function) they touch disjoint
+// scratch and run concurrently, so the one's tail of partly filled CUs
+// overlaps the other's body.  fork / join: events (timing disabled).
+struct SideStream {
+  hipStream_t st;
+  hipEvent_t fork, join;
+};
+// launchers (posterior.hip).  lds_seq: chain_lds_pack(max seq_bytes, max members).
 hipError_t launch_forward(int models, const ModelScalars& ms, const Tables* tab, SeqSet seqs,
                           PairMeta pm, ChainMeta cm, PairRec* rec, Scratch sc, int64_t nchains,
-                          int lds_seq, hipStream_t st);
+                          int lds_seq, hipStream_t st, const SideStream* side);
 hipError_t launch_backward(int models, const ModelScalars& ms, const Tables* tab, SeqSet seqs,
                            PairMeta pm, ChainMeta cm, PairRec* rec, Scratch sc, int64_t nchains,
-                           int lds_seq, int64_t npairs, hipStream_t st);
+                           int lds_seq, int64_t npairs, hipStream_t st, const SideStream* side);
 hipError_t launch_local_totals(SeqSet seqs, PairMeta pm, PairRec* rec, Scratch sc, int64_t npairs,
                                hipStream_t st);
 hipError_t launch_fold_totals(const ModelScalars& ms, const Tables* tab, SeqSet seqs, PairMeta pm,

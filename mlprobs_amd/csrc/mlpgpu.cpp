@@ -23,6 +23,7 @@
 #include <numeric>
 #include <thread>
 #include <string>
+#include <queue>
 #include <vector>
 
 #include "host_backend.h"
@@ -45,10 +46,12 @@ enum KernelId { KFWD = 0, KBWD, KTOT, KMERGE, KCOMPACT, KRELAX, KTRANS, KFILTER,
 
 struct mlp_ctx {
   int device = 0;
+  int cus = 256;                      // compute units (chain planning)
   bool host = false;                  // mlp_ctx_create_host: every stage on the CPU, no HIP call
   mlph::Store hs;                     // the host context's canonical CSR store
   hipStream_t stream = nullptr;
   hipStream_t stream2 = nullptr;   // second posterior batch stream (pipelined batches)
+  SideStream side{};                  // concurrent second sweep kernel of a batch (mlp_kernels.h)
   std::string err;
   // parameter tables
   Tables* d_tables = nullptr;
@@ -324,11 +327,18 @@ int mlp_ctx_create(int device, mlp_ctx** out) {
     delete c;
     return MLP_ERR_HIP;
   }
+  hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, device);
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return MLP_ERR_HIP;
   }
   if (hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return MLP_ERR_HIP;
+  }
+  if (hipStreamCreateWithFlags(&c->side.st, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->side.fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->side.join, hipEventDisableTiming) != hipSuccess) {
     delete c;
     return MLP_ERR_HIP;
   }
@@ -391,6 +401,7 @@ void mlp_ctx_destroy(mlp_ctx* c) {
   hipSetDevice(c->device);
   hipStreamSynchronize(c->stream);
   hipStreamSynchronize(c->stream2);
+  if (c->side.st) hipStreamSynchronize(c->side.st);
   void* ptrs[] = {c->d_tables, c->d_res, c->d_off, c->d_len, c->d_rp_off, c->d_trp_off,
                   c->d_rowptr, c->d_ent_off, c->d_cols, c->d_vals};
   for (void* p : ptrs)
@@ -410,6 +421,11 @@ void mlp_ctx_destroy(mlp_ctx* c) {
   if (c->h_prof_out) hipHostFree(c->h_prof_out);
   hipStreamDestroy(c->stream);
   hipStreamDestroy(c->stream2);
+  if (c->side.st) {
+    hipStreamDestroy(c->side.st);
+    hipEventDestroy(c->side.fork);
+    hipEventDestroy(c->side.join);
+  }
   delete c;
 }
 
@@ -570,7 +586,7 @@ struct ChainPlan {
   std::vector<int32_t> first, count, width, rows, seqb;  // per chain
   std::vector<int64_t> cell, bndo;                  // per chain
   int64_t cells = 0, rm_total = 0, bnd = 0, ell_rows = 0;
-  int lds_seq = 0;
+  int lds_seq = 0;   // chain_lds_pack(max residue bytes, max members)
 };
 
 static void plan_chains(const mlp_ctx* c, int64_t p, int64_t q, ChainPlan& P) {
@@ -582,13 +598,17 @@ static void plan_chains(const mlp_ctx* c, int64_t p, int64_t q, ChainPlan& P) {
     if (ax != ay) return ax > ay;
     return c->lens[c->pa[x]] > c->lens[c->pa[y]];
   });
+  // Chains are built greedily up to a row target.  The sweeps are
+  // throughput-bound at their occupancy (6 waves per SIMD): per-SIMD step
+  // rate measured at C3 (MI355X) 1.44 / 1.50 / 1.74 wave-steps per us at
+  // 4.3 / 5.1 / 6 resident waves, so what matters is keeping every slot
+  // busy -- at least ~2 waves per resident slot -- while the strip and
+  // skew waste stays small; with the two model kernels overlapped
+  // (SideStream) 640- to 4096-row chains run within 1 % of each other in
+  // the sweeps, and the merge (one kernel, its own tail) prefers ~1024.
   int64_t total_rows = 0;
   for (int64_t k = p; k < q; k++) total_rows += c->lens[c->pa[k]] + 1;
-  // enough chains to fill the device a few times over, long enough that the
-  // 63-step skew and the last partial strip stay small
-  // (~11k chains per large batch: about two waves per resident slot of the
-  // sweeps at 6 waves per SIMD; measured at C3 vs 8k chains: sweeps -5%)
-  int64_t target_rows = std::max<int64_t>(512, std::min<int64_t>(4096, total_rows / 11000));
+  int64_t target_rows = std::max<int64_t>(512, std::min<int64_t>(1024, total_rows / (2 * 6 * 4 * (int64_t)c->cus)));
   if (const char* e = getenv("MLP_CHAIN_ROWS")) target_rows = std::max(64, atoi(e));  // tuning hook
   struct ChainH { int64_t begin, end; int W, rows, seq; int64_t cost; };
   std::vector<ChainH> chains;
@@ -648,6 +668,9 @@ static void plan_chains(const mlp_ctx* c, int64_t p, int64_t q, ChainPlan& P) {
       P.ell_rows += L1;
     }
   }
+  int kmax = 0;
+  for (int64_t h = 0; h < P.nch; h++) kmax = std::max(kmax, P.count[h]);
+  P.lds_seq = chain_lds_pack(P.lds_seq, kmax);
 }
 
 // Scratch carving: 256-byte aligned sub-buffers of one device allocation.
@@ -963,6 +986,7 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
   // kernels run, and finishes batch b (entry offsets from its pair records,
   // compaction into the store) before batch b + 1 reuses the scratch.
   const bool two = getenv("MLP_TWO") && atoi(getenv("MLP_TWO")) > 0;  // experiment hook
+  const SideStream* side = (two || getenv("MLP_NO_SIDE")) ? nullptr : &c->side;  // MLP_NO_SIDE: experiment hook
   size_t batch_target = batch_target_for(c, p0, p1, pair_bytes, two ? c->scratch_budget / 2 : 0);
   int64_t all_cells = 0, done_cells = 0;
   for (int64_t k = p0; k < p1; k++) all_cells += pair_cost_cells(c, k);
@@ -1095,11 +1119,11 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
     for (int64_t k = p; k < q; k++) bcells += pair_cost_cells(c, k);
     {
       Timer t(c, KFWD, bcells, st);
-      HIPCHK(c, launch_forward(models, ms, c->d_tables, seqs, pm, cm, d_rec, sc, nch, lds_seq, st));
+      HIPCHK(c, launch_forward(models, ms, c->d_tables, seqs, pm, cm, d_rec, sc, nch, lds_seq, st, side));
     }
     {
       Timer t(c, KBWD, bcells, st);
-      HIPCHK(c, launch_backward(models, ms, c->d_tables, seqs, pm, cm, d_rec, sc, nch, lds_seq, np, st));
+      HIPCHK(c, launch_backward(models, ms, c->d_tables, seqs, pm, cm, d_rec, sc, nch, lds_seq, np, st, side));
     }
     if (models & kLocal) {
       Timer t(c, KTOT, bcells, st);

@@ -77,12 +77,12 @@ __global__ __launch_bounds__(256, SweepWaves<M>::fwd) void k_forward(ModelScalar
                                                  SeqSet sq, PairMeta pm, ChainMeta cm,
                                                  PairRec* __restrict__ rec, Scratch sc,
                                                  int64_t nchains, int lds_seq) {
-  __shared__ LdsTables T_;
+  __shared__ LdsTablesFor<M> T_;
   extern __shared__ __align__(16) uint8_t dyn[];
   stage_tables(T_, tab);
   const int64_t ch = wave_index();
   if (ch >= nchains) return;
-  const float4* __restrict__ lk = T_.lk;
+  const float4* __restrict__ lk = lookup_of(T_);
   const int lane = threadIdx.x & 63;
   const ChainView C = stage_chain<kStageFwd>(dyn, lds_seq, ch, sq, pm, cm, rec);
   const int W = C.W, S = C.S;
@@ -287,12 +287,12 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
                                                   SeqSet sq, PairMeta pm, ChainMeta cm,
                                                   PairRec* __restrict__ rec, Scratch sc,
                                                   int64_t nchains, int lds_seq) {
-  __shared__ LdsTables T_;
+  __shared__ LdsTablesFor<M> T_;
   extern __shared__ __align__(16) uint8_t dyn[];
   stage_tables(T_, tab);
   const int64_t ch = wave_index();
   if (ch >= nchains) return;
-  const float4* __restrict__ lk = T_.lk;
+  const float4* __restrict__ lk = lookup_of(T_);
   const int lane = threadIdx.x & 63;
   const ChainView C = stage_chain<kStageBwd>(dyn, lds_seq, ch, sq, pm, cm, rec);
   const int W = C.W, S = C.S;
@@ -683,28 +683,40 @@ static bool fuse_models() {
 template <template <int> class K>
 static hipError_t launch_sweep(int models, const ModelScalars& ms, const Tables* tab, SeqSet seqs,
                                PairMeta pm, ChainMeta cm, PairRec* rec, Scratch sc, int64_t nchains,
-                               int lds_seq, hipStream_t st) {
+                               int lds_seq, hipStream_t st, const SideStream* side) {
   const ChainLaunch l = chain_launch(nchains, lds_seq);
-  auto go = [&](auto m_tag) {
+  auto go = [&](auto m_tag, hipStream_t s) {
     constexpr int Mv = decltype(m_tag)::value;
-    hipLaunchKernelGGL((K<Mv>::fn), l.grid, l.block, l.lds, st, ms, tab, seqs, pm, cm, rec, sc, nchains, lds_seq);
+    hipLaunchKernelGGL((K<Mv>::fn), l.grid, l.block, l.lds, s, ms, tab, seqs, pm, cm, rec, sc, nchains, lds_seq);
+  };
+  // two kernels: the second on the side stream, joined back before returning
+  auto pair = [&](auto a_tag, auto b_tag) -> hipError_t {
+    if (!side) {
+      go(a_tag, st);
+      go(b_tag, st);
+      return hipSuccess;
+    }
+    hipError_t e;
+    if ((e = hipEventRecord(side->fork, st)) != hipSuccess) return e;
+    if ((e = hipStreamWaitEvent(side->st, side->fork, 0)) != hipSuccess) return e;
+    go(a_tag, st);
+    go(b_tag, side->st);
+    if ((e = hipEventRecord(side->join, side->st)) != hipSuccess) return e;
+    return hipStreamWaitEvent(st, side->join, 0);
   };
   switch (models) {
     case kHmm5 | kLocal | kPF:
       if (fuse_models()) {
-        go(std::integral_constant<int, kHmm5 | kLocal | kPF>{});
-      } else {  // fp32 HMMs and the fp64 partition function as two sweeps: fewer VGPRs each
-        go(std::integral_constant<int, kHmm5 | kLocal>{});
-        go(std::integral_constant<int, kPF>{});
+        go(std::integral_constant<int, kHmm5 | kLocal | kPF>{}, st);
+        return hipSuccess;
       }
-      break;
-    case kLocal: go(std::integral_constant<int, kLocal>{}); break;
-    case kPF: go(std::integral_constant<int, kPF>{}); break;
-    case kHmm5: go(std::integral_constant<int, kHmm5>{}); break;
+      // fp32 HMMs and the fp64 partition function as two sweeps: fewer VGPRs each
+      return pair(std::integral_constant<int, kHmm5 | kLocal>{}, std::integral_constant<int, kPF>{});
+    case kLocal: go(std::integral_constant<int, kLocal>{}, st); break;
+    case kPF: go(std::integral_constant<int, kPF>{}, st); break;
+    case kHmm5: go(std::integral_constant<int, kHmm5>{}, st); break;
     case kHmm5 | kPF | kQP:  // QuickProbs: the same fp32 pair-HMM sweep, its own partition function
-      go(std::integral_constant<int, kHmm5>{});
-      go(std::integral_constant<int, kPF | kQP>{});
-      break;
+      return pair(std::integral_constant<int, kHmm5>{}, std::integral_constant<int, kPF | kQP>{});
     default: return hipErrorInvalidValue;
   }
   return hipSuccess;
@@ -714,18 +726,18 @@ template <int M> struct BackwardK { static constexpr auto fn = k_backward<M>; };
 
 hipError_t launch_forward(int models, const ModelScalars& ms, const Tables* tab, SeqSet seqs,
                           PairMeta pm, ChainMeta cm, PairRec* rec, Scratch sc, int64_t nchains,
-                          int lds_seq, hipStream_t st) {
+                          int lds_seq, hipStream_t st, const SideStream* side) {
   if (nchains <= 0) return hipSuccess;
-  const hipError_t e = launch_sweep<ForwardK>(models, ms, tab, seqs, pm, cm, rec, sc, nchains, lds_seq, st);
+  const hipError_t e = launch_sweep<ForwardK>(models, ms, tab, seqs, pm, cm, rec, sc, nchains, lds_seq, st, side);
   if (e != hipSuccess) return e;
   return hipGetLastError();
 }
 
 hipError_t launch_backward(int models, const ModelScalars& ms, const Tables* tab, SeqSet seqs,
                            PairMeta pm, ChainMeta cm, PairRec* rec, Scratch sc, int64_t nchains,
-                           int lds_seq, int64_t npairs, hipStream_t st) {
+                           int lds_seq, int64_t npairs, hipStream_t st, const SideStream* side) {
   if (nchains <= 0) return hipSuccess;
-  const hipError_t e = launch_sweep<BackwardK>(models, ms, tab, seqs, pm, cm, rec, sc, nchains, lds_seq, st);
+  const hipError_t e = launch_sweep<BackwardK>(models, ms, tab, seqs, pm, cm, rec, sc, nchains, lds_seq, st, side);
   if (e != hipSuccess) return e;
   // fold the 5-state backward total (needs Tables for the initial cells)
   if (models & kHmm5) return launch_fold_totals(ms, tab, seqs, pm, rec, npairs, st);

@@ -16,7 +16,7 @@ namespace mlp {
 __global__ __launch_bounds__(256) void k_viterbi(ModelScalars ms, const Tables* __restrict__ tab,
                                                  SeqSet sq, PairMeta pm, ChainMeta cm, Scratch sc,
                                                  VitOut vo, int64_t nchains, int lds_seq) {
-  __shared__ LdsTables T_;
+  __shared__ LdsTablesT<true, false> T_;
   extern __shared__ __align__(16) uint8_t dyn[];
   stage_tables(T_, tab);
   const int64_t ch = wave_index();
