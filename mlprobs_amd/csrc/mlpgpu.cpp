@@ -15,6 +15,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cctype>
 #include <cmath>
 #include <cstdio>
@@ -2062,7 +2063,8 @@ static int relax_one(mlp_ctx* c, const QpRelax& qp, bool last) {
     }
     // Tiled path (k_relax_tile) for every output pair whose blocks fit the
     // LDS tile; the row-task kernel for the rest (MLP_RELAX=tasks: all).
-    const int64_t LDS_MAX = 160 * 1024 / kRelaxGroupsPerCU;
+    int64_t LDS_MAX = 160 * 1024 / kRelaxGroupsPerCU;
+    if (const char* e = getenv("MLP_RELAX_LDS_KB")) LDS_MAX = std::max(32, std::min(160, atoi(e))) * 1024;  // tuning hook
     const char* mode = getenv("MLP_RELAX");
     const char* tenv = getenv("MLP_RELAX_TILE");  // test hook: outputs per tile, 1..kTileMax
     const int tmax = tenv ? std::max(1, std::min(kTileMax, atoi(tenv))) : kTileMax;
@@ -2112,62 +2114,144 @@ static int relax_one(mlp_ctx* c, const QpRelax& qp, bool last) {
       }
     }
     if (img_off[2 * c->P] >= (1LL << 36)) tasks_only = true;  // z schedule holds offsets / 16 in 32 bits
-    const int64_t budget =
-        std::min<int64_t>(LDS_MAX - (int64_t)tile_relax_lds(0), tile_relax_max_cap()) & ~(int64_t)15;
-    // tiles: per y, consecutive x's (ascending) while the LDS bound and the
-    // cell slots allow; ordered by (first x, y) for the XCD-aware grid order
-    struct TileRec { int x0, y; int64_t first; };
-    std::vector<int32_t> tiles_raw;
-    std::vector<TileRec> order;
-    std::vector<int64_t> tp;
-    std::vector<int32_t> tr;
-    int64_t cap = 0, max_cells = 0;
-    auto row_tasks = [&](int64_t p) {
-      for (int g = 1; g <= c->lens[c->pa[p]]; g += 64) {
-        tp.push_back(p);
-        tr.push_back(g);
+    // Tiles: per y, consecutive x's (ascending) while the staged images fit
+    // and the cell slots allow.  A tile's LDS need is the largest, over z,
+    // of its images P(x_t, z) + P(y, z) (exact per z up to n = 2048; the
+    // per-sequence maxima beyond).  Two classes: tiles within half the LDS
+    // run two workgroups per CU (8 waves per SIMD, the kernel's latency
+    // hiding); the rest one.
+    const int64_t zs = (int64_t)tile_relax_lds(0);
+    const int64_t budget = std::min<int64_t>(LDS_MAX - zs, tile_relax_max_cap()) & ~(int64_t)15;
+    int64_t small_budget = std::min<int64_t>(budget, (80 * 1024 - zs) & ~(int64_t)15);
+    if (LDS_MAX < 160 * 1024 || getenv("MLP_RELAX_ONECLASS")) small_budget = 0;  // tuning hooks
+    const int n = c->n;
+    const bool exact = !tasks_only && n <= 2048;
+    const int64_t kSmallCells = 8 * (int64_t)kRelaxThreads;  // 8 slots: the 64-VGPR budget of 8 waves per SIMD
+    std::vector<int32_t> isz;  // image bytes of P(s, z), s's residues as rows: isz[s * n + z]
+    if (exact) {
+      isz.assign((size_t)n * n, 0);
+      for (int64_t p = 0; p < c->P; p++) {
+        const int a = c->pa[p], b = c->pb[p];
+        isz[(size_t)a * n + b] = (int32_t)(img_off[2 * p + 1] - img_off[2 * p]);
+        isz[(size_t)b * n + a] = (int32_t)(img_off[2 * p + 2] - img_off[2 * p + 1]);
       }
+    }
+    struct TileRec { int x0, y, cls; int64_t first, need, cells; };
+    struct YPlan {
+      std::vector<int32_t> ints;
+      std::vector<TileRec> recs;
+      std::vector<int64_t> tp;
+      std::vector<int32_t> tr;
     };
-    for (int yy = 1; yy < c->n; yy++) {
-      int32_t cur_p[kTileMax], cur_x[kTileMax];
-      int cnt = 0;
-      int64_t sumA = 0, ncell = 0;
-      auto flush = [&]() {
-        if (!cnt) return;
-        order.push_back({cur_x[0], yy, (int64_t)tiles_raw.size()});
-        for (int t = 0; t < kTileMax; t++) tiles_raw.push_back(t < cnt ? cur_p[t] : -1);
-        for (int t = 0; t < kTileMax; t++) tiles_raw.push_back(t < cnt ? cur_x[t] : 0);
-        tiles_raw.push_back(yy);
-        cap = std::max(cap, sumA + maxI[yy]);
-        max_cells = std::max(max_cells, ncell);
-        cnt = 0;
-        sumA = ncell = 0;
+    std::vector<YPlan> yplans(n);
+    auto plan_y = [&](int yy) {
+      YPlan& Y = yplans[yy];
+      struct Cur {
+        int cnt = 0;
+        int32_t p[kTileMax], x[kTileMax];
+        int64_t bound = 0, cells = 0, peak = 0;
+        std::vector<int64_t> sum;
+      } cur[2];
+      const int64_t lim[2] = {small_budget, budget};
+      const int32_t* iy = exact ? &isz[(size_t)yy * n] : nullptr;
+      auto flush = [&](int k) {
+        Cur& t = cur[k];
+        if (!t.cnt) return;
+        Y.recs.push_back({t.x[0], yy, k, (int64_t)Y.ints.size(), exact ? t.peak : t.bound + maxI[yy], t.cells});
+        for (int u = 0; u < kTileMax; u++) Y.ints.push_back(u < t.cnt ? t.p[u] : -1);
+        for (int u = 0; u < kTileMax; u++) Y.ints.push_back(u < t.cnt ? t.x[u] : 0);
+        Y.ints.push_back(yy);
+        t.cnt = 0;
+        t.bound = t.cells = t.peak = 0;
+      };
+      // LDS need of tile t with output x added
+      auto need_with = [&](const Cur& t, int x) -> int64_t {
+        if (!exact) return t.bound + maxI[x] + maxI[yy];
+        const int32_t* ix = &isz[(size_t)x * n];
+        int64_t m = 0;
+        if (t.cnt)
+          for (int z = 0; z < n; z++) m = std::max(m, t.sum[z] + ix[z]);
+        else
+          for (int z = 0; z < n; z++) m = std::max<int64_t>(m, (int64_t)iy[z] + ix[z]);
+        return m;
       };
       for (int x = 0; x < yy; x++) {
-        const int64_t p = pair_index_host(c->n, x, yy);
+        const int64_t p = pair_index_host(n, x, yy);
         if (p < r0 || p >= r1) continue;
         const int64_t nz = c->ent_off[p + 1] - c->ent_off[p];
         if (nz == 0) continue;  // empty mask: the filter writes an empty block
-        if (tasks_only || big[x] || big[yy] || maxI[x] + maxI[yy] > budget || !tile_relax_slots(nz)) {
-          row_tasks(p);
+        int k = -1;
+        int64_t alone = 0;
+        if (!tasks_only && !big[x] && !big[yy] && tile_relax_slots(nz)) {
+          const Cur empty{};
+          alone = need_with(empty, x);
+          k = alone <= small_budget && nz <= kSmallCells ? 0 : alone <= budget ? 1 : -1;
+        }
+        if (k < 0) {
+          for (int g = 1; g <= c->lens[x]; g += 64) {
+            Y.tp.push_back(p);
+            Y.tr.push_back(g);
+          }
           continue;
         }
-        if (cnt == tmax || sumA + maxI[x] + maxI[yy] > budget || !tile_relax_slots(ncell + nz)) flush();
-        cur_p[cnt] = (int32_t)p;
-        cur_x[cnt] = x;
-        cnt++;
-        sumA += maxI[x];
-        ncell += nz;
+        Cur& t = cur[k];
+        int64_t nd = t.cnt ? need_with(t, x) : alone;
+        if (t.cnt && (t.cnt == tmax || nd > lim[k] || !tile_relax_slots(t.cells + nz) ||
+                      (k == 0 && t.cells + nz > kSmallCells))) {
+          flush(k);
+          nd = alone;
+        }
+        if (exact) {
+          const int32_t* ix = &isz[(size_t)x * n];
+          if (!t.cnt) t.sum.assign(iy, iy + n);
+          for (int z = 0; z < n; z++) t.sum[z] += ix[z];
+        }
+        t.p[t.cnt] = (int32_t)p;
+        t.x[t.cnt] = x;
+        t.cnt++;
+        t.bound += maxI[x];
+        t.cells += nz;
+        t.peak = nd;
       }
-      flush();
+      flush(0);
+      flush(1);
+    };
+    {
+      const int nth = tasks_only ? 1 : mlph::threads_for((int64_t)n * n / 4096 + 1);
+      std::vector<std::thread> th;
+      std::atomic<int> next_y{1};
+      for (int w = 0; w < nth; w++)
+        th.emplace_back([&]() {
+          for (int yy; (yy = next_y.fetch_add(1)) < n;) plan_y(yy);
+        });
+      for (auto& t : th) t.join();
     }
-    std::stable_sort(order.begin(), order.end(),
-                     [](const TileRec& u, const TileRec& v) { return u.x0 != v.x0 ? u.x0 < v.x0 : u.y < v.y; });
+    // per class: tiles ordered by (first x, y) for the XCD-aware grid order
     std::vector<int32_t> tiles;
-    tiles.reserve(tiles_raw.size());
-    for (const TileRec& r : order)
-      tiles.insert(tiles.end(), tiles_raw.begin() + r.first, tiles_raw.begin() + r.first + kTileInts);
-    const int64_t ntiles = (int64_t)order.size();
+    std::vector<int64_t> tp;
+    std::vector<int32_t> tr;
+    int64_t cls_tiles[2] = {0, 0}, cls_cap[2] = {0, 0}, cls_cells[2] = {0, 0};
+    for (int k = 0; k < 2; k++) {
+      std::vector<std::pair<int, const TileRec*>> order;  // (y, record)
+      for (int yy = 1; yy < n; yy++)
+        for (const TileRec& r : yplans[yy].recs)
+          if (r.cls == k) order.push_back({yy, &r});
+      std::stable_sort(order.begin(), order.end(), [](const auto& u, const auto& v) {
+        return u.second->x0 != v.second->x0 ? u.second->x0 < v.second->x0 : u.first < v.first;
+      });
+      for (const auto& o : order) {
+        const std::vector<int32_t>& src = yplans[o.first].ints;
+        tiles.insert(tiles.end(), src.begin() + o.second->first, src.begin() + o.second->first + kTileInts);
+        cls_cap[k] = std::max(cls_cap[k], o.second->need);
+        cls_cells[k] = std::max(cls_cells[k], o.second->cells);
+      }
+      cls_tiles[k] = (int64_t)order.size();
+    }
+    for (int yy = 1; yy < n; yy++) {
+      tp.insert(tp.end(), yplans[yy].tp.begin(), yplans[yy].tp.end());
+      tr.insert(tr.end(), yplans[yy].tr.begin(), yplans[yy].tr.end());
+    }
+    const int64_t ntiles = cls_tiles[0] + cls_tiles[1];
     if (ntiles) {
       if ((rc = ensure(c, c->r_img, std::max<int64_t>(img_off[2 * c->P], 16)))) return rc;
       if ((rc = ensure(c, c->r_imgoff, sizeof(int64_t) * (2 * c->P + 1)))) return rc;
@@ -2183,6 +2267,16 @@ static int relax_one(mlp_ctx* c, const QpRelax& qp, bool last) {
       HIPCHK(c, launch_pack(pk, c->stream));
     }
     const int64_t nt = (int64_t)tp.size();
+    if (getenv("MLP_PLAN_LOG")) {
+      int64_t mx = 0;
+      for (int i = 0; i < c->n; i++) mx = std::max(mx, maxI[i]);
+      fprintf(stderr,
+              "relax plan: tiles %lld (cap %lld, cells %lld) + %lld (cap %lld, cells %lld) row tasks %lld budget %lld/%lld "
+              "max image %lld\n",
+              (long long)cls_tiles[0], (long long)cls_cap[0], (long long)cls_cells[0], (long long)cls_tiles[1],
+              (long long)cls_cap[1], (long long)cls_cells[1], (long long)nt, (long long)small_budget, (long long)budget,
+              (long long)mx);
+    }
     if (mode && !strcmp(mode, "pairs") && nt) {  // test hook: the pair-resident path must cover all
       c->err = "MLP_RELAX=pairs: " + std::to_string(nt) + " row tasks fell back";
       return MLP_ERR_STATE;
@@ -2222,15 +2316,30 @@ static int relax_one(mlp_ctx* c, const QpRelax& qp, bool last) {
     pr.nwords = (const int32_t*)c->r_nwords.p;
     pr.img = (const uint8_t*)c->r_img.p;
     pr.img_chunks = img_off[2 * c->P] / 16;
-    pr.tiles = (const int32_t*)c->r_tiles.p;
-    pr.ntiles = ntiles;
     pr.out = (float*)c->r_raw.p;
-    pr.cap = (int)mlp_align16(cap);
     pr.qp = qp;
+    TileRelaxArgs pc[2] = {pr, pr};
+    for (int k = 0; k < 2; k++) {
+      pc[k].tiles = (const int32_t*)c->r_tiles.p + (k ? cls_tiles[0] * kTileInts : 0);
+      pc[k].ntiles = cls_tiles[k];
+      pc[k].cap = (int)mlp_align16(cls_cap[k]);
+    }
     {
       Timer t(c, KRELAX, c->ent_off[r1] - c->ent_off[r0]);
-      HIPCHK(c, launch_relax_tiles(pr, tile_relax_slots(max_cells), c->stream));
+      // the one-workgroup-per-CU class on the side stream, concurrently
+      const bool fork = cls_tiles[0] && cls_tiles[1];
+      if (fork) {
+        HIPCHK(c, hipEventRecord(c->side.fork, c->stream));
+        HIPCHK(c, hipStreamWaitEvent(c->side.st, c->side.fork, 0));
+      }
+      if (cls_tiles[1])
+        HIPCHK(c, launch_relax_tiles(pc[1], tile_relax_slots(cls_cells[1]), fork ? c->side.st : c->stream));
+      if (cls_tiles[0]) HIPCHK(c, launch_relax_tiles(pc[0], tile_relax_slots(cls_cells[0]), c->stream));
       HIPCHK(c, launch_relax_tasks(ra, c->stream));
+      if (fork) {
+        HIPCHK(c, hipEventRecord(c->side.join, c->side.st));
+        HIPCHK(c, hipStreamWaitEvent(c->stream, c->side.join, 0));
+      }
     }
     // filter: count, host scan, write
     std::vector<int64_t> outp(nout);

@@ -670,6 +670,15 @@ __global__ __launch_bounds__(256, MLP_MERGE_WAVES) void k_merge(ModelScalars ms,
 }
 
 // ------------------------------------------------------------ launchers
+// MLP_SPLIT_HMM=1: the 5-state and local HMMs as separate sweeps (experiment)
+static bool split_hmm() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("MLP_SPLIT_HMM");
+    v = (e && e[0] == '1') ? 1 : 0;
+  }
+  return v == 1;
+}
 // MLP_FUSE=1 runs all three models in one sweep (default: two sweeps).
 static bool fuse_models() {
   static int v = -1;
@@ -690,17 +699,17 @@ static hipError_t launch_sweep(int models, const ModelScalars& ms, const Tables*
     hipLaunchKernelGGL((K<Mv>::fn), l.grid, l.block, l.lds, s, ms, tab, seqs, pm, cm, rec, sc, nchains, lds_seq);
   };
   // two kernels: the second on the side stream, joined back before returning
-  auto pair = [&](auto a_tag, auto b_tag) -> hipError_t {
+  auto pair = [&](auto a_tag, auto... b_tags) -> hipError_t {
     if (!side) {
       go(a_tag, st);
-      go(b_tag, st);
+      (go(b_tags, st), ...);
       return hipSuccess;
     }
     hipError_t e;
     if ((e = hipEventRecord(side->fork, st)) != hipSuccess) return e;
     if ((e = hipStreamWaitEvent(side->st, side->fork, 0)) != hipSuccess) return e;
     go(a_tag, st);
-    go(b_tag, side->st);
+    (go(b_tags, side->st), ...);
     if ((e = hipEventRecord(side->join, side->st)) != hipSuccess) return e;
     return hipStreamWaitEvent(st, side->join, 0);
   };
@@ -710,6 +719,9 @@ static hipError_t launch_sweep(int models, const ModelScalars& ms, const Tables*
         go(std::integral_constant<int, kHmm5 | kLocal | kPF>{}, st);
         return hipSuccess;
       }
+      if (split_hmm())
+        return pair(std::integral_constant<int, kHmm5>{}, std::integral_constant<int, kLocal>{},
+                    std::integral_constant<int, kPF>{});
       // fp32 HMMs and the fp64 partition function as two sweeps: fewer VGPRs each
       return pair(std::integral_constant<int, kHmm5 | kLocal>{}, std::integral_constant<int, kPF>{});
     case kLocal: go(std::integral_constant<int, kLocal>{}, st); break;

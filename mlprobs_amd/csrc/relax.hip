@@ -358,7 +358,9 @@ __device__ __forceinline__ uint4 rfl(uint4 v) {
 __device__ unsigned long long g_rtime[8];
 #endif
 template <int KP, int SL, bool QP>
-__global__ __launch_bounds__(kRelaxThreads, 4) void k_relax_tile(TileRelaxArgs A) {
+// KP = 5 (tiles within half the LDS): two workgroups per CU, so 8 waves per
+// SIMD and at most 64 VGPRs; KP = 9: one workgroup, 4 waves per SIMD
+__global__ __launch_bounds__(kRelaxThreads, KP == 5 && kRelaxThreads == 1024 ? 8 : 4) void k_relax_tile(TileRelaxArgs A) {
   extern __shared__ __align__(16) uint8_t lds[];
   constexpr int nt = kRelaxThreads;
   constexpr int TM = kTileMax;
@@ -581,9 +583,13 @@ __global__ __launch_bounds__(kRelaxThreads, 4) void k_relax_tile(TileRelaxArgs A
   unsigned long long t_max = 0, t_mean = 0, t_step = 0, t_steps = 0, t_seg[4] = {0, 0, 0, 0};
   uint64_t t_last = clock64();
 #endif
+  // KP = 9: the next z's tile is loaded into registers while this z computes;
+  // KP = 5 (two workgroups per CU): loaded at the stage, the other
+  // workgroup's compute covers the wait and the registers stay free
+  constexpr bool kRegPrefetch = KP == 9;
   fill();
   bool more = next();
-  if (more) MLP_ISSUE();
+  if (kRegPrefetch && more) MLP_ISSUE();
 #ifdef MLP_RELAX_NOSTAGE
   const uint4 fC = nC, fAo = nAo, fNa = nNa, fAc = nAc;
   const float4 fW = nW;
@@ -592,6 +598,7 @@ __global__ __launch_bounds__(kRelaxThreads, 4) void k_relax_tile(TileRelaxArgs A
 #ifdef MLP_RELAX_TIMING
     const uint64_t ts0 = clock64();
 #endif
+    if constexpr (!kRegPrefetch) MLP_ISSUE();
     // stage the prefetched tile; outputs' A bases (+ validity) into zb
     const int tot = sg[TM] + (int)nC.z;
 #pragma unroll
@@ -626,7 +633,7 @@ __global__ __launch_bounds__(kRelaxThreads, 4) void k_relax_tile(TileRelaxArgs A
 #ifdef MLP_RELAX_NOSTAGE  // timing experiment: every z computes on the first z's tile
     nC = fC; nAo = fAo; nNa = fNa; nAc = fAc; nW = fW;
 #else
-    if (more) MLP_ISSUE();
+    if (kRegPrefetch && more) MLP_ISSUE();
 #endif
 #ifdef MLP_RELAX_TIMING
     const uint64_t tc0 = clock64();
