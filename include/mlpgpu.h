@@ -193,6 +193,15 @@ int mlp_profile_posterior_cpnp(mlp_ctx *ctx, const int32_t *seq_weights, int n1,
  * returned here and valid until the next mlp_profile_posterior* call. */
 const float *mlp_profile_result(const mlp_ctx *ctx);
 
+/* Evaluation only (not a drop-in path): the consistency transform of the
+ * output pairs (x, y), x in xs, y in ys, x < y, as dense 16x16 block
+ * products on the fp32 matrix cores (v_mfma_f32_16x16x4_f32), from the
+ * current store.  Fused products: held to the 1e-4 relative rule, not to bit
+ * identity.  res[7] = {kernel seconds, dense MACs issued, outputs, max
+ * relative error vs a double-precision sum on sampled cells, cells checked,
+ * output tiles, operand blocks}. */
+int mlp_relax_blockmfma_eval(mlp_ctx *ctx, int nx, const int32_t *xs, int ny, const int32_t *ys, double *res);
+
 /* Multi-GPU (one process per GPU): RCCL over xGMI. */
 int mlp_comm_unique_id(unsigned char id[128]);
 int mlp_comm_init(mlp_ctx *ctx, const unsigned char id[128], int nranks, int rank);

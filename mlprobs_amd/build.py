@@ -15,7 +15,8 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, 'csrc')
 LIBDIR = os.path.join(HERE, 'lib')
 LIB = os.path.join(LIBDIR, 'libmlpgpu.so')
-SOURCES = ['posterior.hip', 'totals.hip', 'viterbi.hip', 'relax.hip', 'profile.hip', 'mlpgpu.cpp', 'host_backend.cpp']
+SOURCES = ['posterior.hip', 'totals.hip', 'viterbi.hip', 'relax.hip', 'relax_mfma.hip', 'profile.hip', 'mlpgpu.cpp',
+           'host_backend.cpp']
 HEADERS = ['mlp_kernels.h', 'mlp_numerics.h', 'mlp_chain.h', 'mlp_params_default.inc', 'mlp_params_qp.inc',
            'host_backend.h']
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <string>
+
 namespace mlp {
 
 constexpr int kWave = 64;        // CDNA wavefront
@@ -327,6 +329,11 @@ int tile_relax_slots(int64_t cells);           // cells per thread, 0 = too many
 int tile_relax_max_cap();                      // largest tile the prefetch registers hold
 hipError_t launch_pack(const PackArgs& a, hipStream_t st);
 hipError_t launch_relax_tiles(const TileRelaxArgs& a, int slots, hipStream_t st);
+// dense-block MFMA evaluation of the consistency transform (relax_mfma.hip):
+// res = {kernel s, dense MACs, outputs, max rel err, cells checked, tiles, blocks}
+int relax_blockmfma_eval(int n, const int32_t* lens, const int64_t* rp_off, const int32_t* rowptr,
+                         const int64_t* ent_off, const uint16_t* cols, const float* vals, int nx, const int32_t* xs,
+                         int ny, const int32_t* ys, double* res, std::string& err);
 // profile posterior (profile.hip)
 struct ProfileArgs {
   int n;                     // family size

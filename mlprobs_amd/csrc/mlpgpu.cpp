@@ -1661,6 +1661,27 @@ int mlp_csr_export(mlp_ctx* c, int32_t* row_ptr, int64_t* ent_off, uint16_t* col
   return MLP_OK;
 }
 
+int mlp_relax_blockmfma_eval(mlp_ctx* c, int nx, const int32_t* xs, int ny, const int32_t* ys, double* res) {
+  if (!c || !xs || !ys || !res || nx <= 0 || ny <= 0) return MLP_ERR_ARG;
+  if (c->host) return MLP_ERR_STATE;
+  if (c->store_p0 != 0 || c->store_p1 != c->P) {
+    c->err = "blockmfma eval needs every pair";
+    return MLP_ERR_STATE;
+  }
+  for (int k = 0; k < nx; k++)
+    if (xs[k] < 0 || xs[k] >= c->n) return MLP_ERR_ARG;
+  for (int k = 0; k < ny; k++)
+    if (ys[k] < 0 || ys[k] >= c->n) return MLP_ERR_ARG;
+  std::vector<int32_t> rp(c->rp_off[c->P]);
+  std::vector<uint16_t> cols(std::max<int64_t>(c->store_total, 1));
+  std::vector<float> vals(std::max<int64_t>(c->store_total, 1));
+  int rc;
+  if ((rc = mlp_csr_export(c, rp.data(), nullptr, cols.data(), vals.data()))) return rc;
+  hipSetDevice(c->device);
+  return mlp::relax_blockmfma_eval(c->n, c->lens.data(), c->rp_off.data(), rp.data(), c->ent_off.data(), cols.data(),
+                                   vals.data(), nx, xs, ny, ys, res, c->err);
+}
+
 int mlp_csr_import(mlp_ctx* c, const int32_t* row_ptr, const int64_t* ent_off, const uint16_t* cols,
                    const float* vals) {
   if (!c || !row_ptr || !ent_off) return MLP_ERR_ARG;

@@ -95,6 +95,7 @@ def lib():
         L.mlp_set_shards.argtypes = [P, C.c_int]
         L.mlp_shard_count.argtypes = [P]
         L.mlp_relax_shard_plan.argtypes = [C.c_int, I32P, I64P, C.c_int, I64P]
+        L.mlp_relax_blockmfma_eval.argtypes = [P, C.c_int, I32P, C.c_int, I32P, C.c_void_p]
         _LIB = L
     return _LIB
 
@@ -106,7 +107,7 @@ EXPORTED = ['mlp_ctx_create', 'mlp_ctx_destroy', 'mlp_last_error', 'mlp_set_scra
             'mlp_viterbi_path', 'mlp_model_adjustment', 'mlp_family_features', 'mlp_comm_unique_id', 'mlp_comm_init',
             'mlp_shard_range', 'mlp_shard_plan', 'mlp_gather_layout', 'mlp_allgather', 'mlp_synchronize', 'mlp_profile',
             'mlp_kernel_times', 'mlp_profile_reset', 'mlp_ctx_create_mask', 'mlp_set_shards', 'mlp_shard_count',
-            'mlp_relax_shard_plan', 'mlp_ctx_create_host', 'mlp_ctx_is_host']
+            'mlp_relax_shard_plan', 'mlp_ctx_create_host', 'mlp_ctx_is_host', 'mlp_relax_blockmfma_eval']
 
 
 def shard_plan(lens, nranks, rank):
@@ -283,6 +284,16 @@ class Family:
         self._chk(self._L.mlp_profile_posterior(self._ctx, w, len(l1), l1, int(L1), m1, len(l2), l2, int(L2), m2,
                                                 out))
         return out.reshape(L1 + 1, L2 + 1)
+
+    def relax_blockmfma_eval(self, xs, ys):
+        """Dense-block MFMA evaluation of one consistency round's transform
+        (include/mlpgpu.h mlp_relax_blockmfma_eval); returns a dict."""
+        x = np.ascontiguousarray(xs, np.int32)
+        y = np.ascontiguousarray(ys, np.int32)
+        res = np.zeros(7, np.float64)
+        self._chk(self._L.mlp_relax_blockmfma_eval(self._ctx, len(x), x, len(y), y, res.ctypes.data))
+        keys = ('seconds', 'dense_macs', 'outputs', 'max_rel_err', 'cells_checked', 'tiles', 'blocks')
+        return {k: float(v) for k, v in zip(keys, res)}
 
     def relax(self, iters):
         self._csr = None

@@ -288,6 +288,19 @@ def test_relax_pair_path_similar():
     _relax_both_paths(seqs, 3, 3, 'similar')
 
 
+def test_relax_blockmfma_eval():
+    """The dense-block MFMA evaluation variant (relax_mfma.hip): fused
+    products, so held to SURVEY 8c's 1e-4 relative rule against a
+    double-precision sum over the same blocks, not to bit identity."""
+    seqs = [x for _, x in synth.family(24, 150, 0.7, seed=44)]
+    fam = Family(seqs)
+    fam.posteriors(0, 0.0)
+    r = fam.relax_blockmfma_eval([0, 1, 2, 5], [7, 9, 20, 23])
+    fam.close()
+    assert r['outputs'] == 16 and r['cells_checked'] > 100 and r['dense_macs'] > 0
+    assert r['max_rel_err'] < 1e-4, r
+
+
 # ---- QuickProbs posterior stage (QP/Alignment/Multiple/PosteriorStage.cpp:123-196)
 def _qp_expected(seqs, a, b):
     """Oracle CSR (values as QuickProbs reads its 16-bit entries) and distance."""
