@@ -355,6 +355,7 @@ struct ProfileArgs {
   const int64_t* map2_off;   // per j: offset of its map (k = 0 at map2_off[j])
   const float* w;            // n1 x n2: (float)(w_i w_j / sum)
   float* out;                // (L1 + 1) x (L2 + 1); rows 1..L1 written
+  int stage;                 // staged entries per run (<= the LDS stage; set by launch_profile_posterior)
 };
 size_t profile_lds(int L2);
 hipError_t launch_profile_posterior(const ProfileArgs& a, hipStream_t st);

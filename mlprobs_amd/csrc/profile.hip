@@ -115,7 +115,7 @@ __global__ __launch_bounds__(64) void k_profile_post(ProfileArgs A) {
       const int start = x - cnt;
       // lanes whose rows fit the stage (a prefix of the run; the first lane
       // always takes part, a longer row is added in pieces below)
-      const bool fits = x <= kProfStage || lane == 0;
+      const bool fits = x <= A.stage || lane == 0;
       const unsigned long long fitm = __ballot(fits && q < Q);
       const int nl = __popcll(~fitm) ? __builtin_ctzll(~fitm) : 64;
       l_e[lane] = e;
@@ -126,7 +126,7 @@ __global__ __launch_bounds__(64) void k_profile_post(ProfileArgs A) {
       if (lane == 63) l_st[64] = x;
       wave_sync();
       const int total_staged = l_st[nl];  // entries of lanes 0 .. nl-1
-      const bool big = nl == 1 && total_staged > kProfStage;
+      const bool big = nl == 1 && total_staged > A.stage;
       if (!big) {
         // ---- which pair each staged entry belongs to (lane-serial fill)
         if (lane < nl)
@@ -189,8 +189,13 @@ __global__ __launch_bounds__(256) void k_profile_inv(ProfileArgs A) {
   if (k > 0) A.inv1[(int64_t)lo * (A.L1 + 1) + A.map1[t]] = k;
 }
 
-hipError_t launch_profile_posterior(const ProfileArgs& a, hipStream_t st) {
-  if (a.L1 <= 0) return hipSuccess;
+hipError_t launch_profile_posterior(const ProfileArgs& a_in, hipStream_t st) {
+  if (a_in.L1 <= 0) return hipSuccess;
+  ProfileArgs a = a_in;
+  // test hook: a smaller stage reaches the partial-run and long-row branches
+  // with small profiles (MLP_PROFILE_STAGE, 1..kProfStage)
+  a.stage = kProfStage;
+  if (const char* e = getenv("MLP_PROFILE_STAGE")) a.stage = std::max(1, std::min(kProfStage, atoi(e)));
   hipLaunchKernelGGL(k_profile_inv, dim3((unsigned)((a.map1_len + 255) / 256)), dim3(256), 0, st, a);
   // column ranges per row: only rows too few to give every CU a wave are
   // split (at C3 refinement, one range per row measured fastest: 376 ms of

@@ -423,23 +423,23 @@ def _pair(n, a, b):
     return a * n - a * (a + 1) // 2 + (b - a - 1)
 
 
-@pytest.mark.parametrize('seed', [81, 82])
-def test_profile_posterior_vs_restatement(seed):
+def _profile_case(seed, n, L, sub, A, B, env=None):
     """mlp_profile_posterior (QuickProbs' buildPosterior on the GPU) against a
     plain restatement of ParallelProbabilisticModel.cpp:301-430 over the same
     relaxed sparse set: weights in double cast to float, terms in (i, j, row,
     entry) order, w * v then +=; bit-exact."""
     rng = np.random.default_rng(seed)
-    n = 9
-    seqs = [x for _, x in synth.family(n, 70, 0.5, seed=seed)]
+    seqs = [x for _, x in synth.family(n, L, sub, seed=seed)]
     fam = Family(seqs)
     fam.posteriors(PID_QP, 0.0)
     w = rng.uniform(0.01, 0.3, n).astype(np.float32)
     fam.relax_qp(2, w)
-    # dense views of every ordered block
-    dense = {}
+    need = set(A) | set(B)
+    dense = {}  # dense views of the ordered blocks the profiles use
     for a in range(n):
         for b in range(a + 1, n):
+            if not ((a in A and b in B) or (a in B and b in A)):
+                continue
             rp, c, v = fam.sparse(_pair(n, a, b))
             rows = [[] for _ in range(len(seqs[a]) + 1)]
             trows = [[] for _ in range(len(seqs[b]) + 1)]
@@ -449,12 +449,21 @@ def test_profile_posterior_vs_restatement(seed):
                     trows[int(c[e])].append((i, float(v[e])))
             dense[(a, b)] = rows
             dense[(b, a)] = trows
-    A, B = [0, 3, 5, 8], [1, 2, 6]
+    assert need
     L1 = max(len(seqs[k]) for k in A) + 9
     L2 = max(len(seqs[k]) for k in B) + 5
     mA = [_gapped(rng, seqs[k], L1)[1] for k in A]
     mB = [_gapped(rng, seqs[k], L2)[1] for k in B]
-    got = fam.profile_posterior(w, A, mA, L1, B, mB, L2)
+    old = {k: os.environ.get(k) for k in (env or {})}
+    try:
+        os.environ.update(env or {})
+        got = fam.profile_posterior(w, A, mA, L1, B, mB, L2)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
     ref = np.zeros((L1 + 1, L2 + 1), np.float32)
     total = 0.0
     for a in A:
@@ -471,6 +480,31 @@ def test_profile_posterior_vs_restatement(seed):
                     ref[r, c] = np.float32(ref[r, c] + np.float32(wf * np.float32(v)))
     np.testing.assert_array_equal(got, ref)
     fam.close()
+
+
+@pytest.mark.parametrize('seed', [81, 82])
+def test_profile_posterior_vs_restatement(seed):
+    _profile_case(seed, 9, 70, 0.5, [0, 3, 5, 8], [1, 2, 6])
+
+
+@pytest.mark.parametrize('stage,split', [('8', None), ('24', '3'), ('1', '2'), (None, '5')])
+def test_profile_posterior_stage_branches(stage, split):
+    """k_profile_post's rarer paths on small profiles: a stage smaller than
+    one row (the piecewise long-row branch), runs cut short by the stage
+    (fewer than 64 pairs), and forced column ranges per row."""
+    env = {}
+    if stage:
+        env['MLP_PROFILE_STAGE'] = stage
+    if split:
+        env['MLP_PROFILE_SPLIT'] = split
+    _profile_case(83, 9, 70, 0.7, [0, 3, 5, 8], [1, 2, 6], env)
+
+
+def test_profile_posterior_many_sequences():
+    """More than 64 sequences in profile A: the column compaction runs in
+    several 64-sequence chunks (and with a small stage, partial runs)."""
+    _profile_case(84, 72, 30, 0.5, list(range(0, 72, 1))[:66], [66, 68, 71])
+    _profile_case(85, 72, 30, 0.5, list(range(3, 72))[:67], [0, 1], {'MLP_PROFILE_STAGE': '40'})
 
 
 # ---- npdoAlign's pair body (MLP_PID_NPDO: ArrangePosteriorProbs,
