@@ -1,4 +1,4 @@
-// Allocation timing probe: hipMalloc of CHUNK_GB chunks until TOTAL_GB, each
+// Allocation timing probe (tools/probe/alloc_chunks CHUNK_GB TOTAL_GB): hipMalloc of CHUNK_GB chunks until TOTAL_GB, each
 // followed by a hipMemset, timed separately (fresh process).
 #include <hip/hip_runtime.h>
 #include <chrono>
