@@ -193,6 +193,19 @@ int mlp_profile_posterior_cpnp(mlp_ctx *ctx, const int32_t *seq_weights, int n1,
  * returned here and valid until the next mlp_profile_posterior* call. */
 const float *mlp_profile_result(const mlp_ctx *ctx);
 
+/* The profile posterior left on the device: with mlp_profile_defer(ctx, 1)
+ * the mlp_profile_posterior* calls (out = NULL) skip the copy back (and
+ * mlp_profile_result returns NULL); then
+ *   mlp_profile_mea: the MEA alignment of that matrix (ComputeAlignment,
+ *     ProbabilisticModel.h:804-864, ChooseBestOfThree ScoreType.h:347-366;
+ *     QuickProbs' computeAlignment is the same recurrence), bit-identical
+ *     score and path, computed on the device; path = 'B'/'X'/'Y' in forward
+ *     order, capacity L1 + L2 bytes;
+ *   mlp_profile_gather: vals[k] = matrix[cells[k]] (row-major (L2 + 1)). */
+int mlp_profile_defer(mlp_ctx *ctx, int on);
+int mlp_profile_mea(mlp_ctx *ctx, char *path, int32_t *path_len, float *score);
+int mlp_profile_gather(mlp_ctx *ctx, int64_t n, const int64_t *cells, float *vals);
+
 /* Evaluation only (not a drop-in path): the consistency transform of the
  * output pairs (x, y), x in xs, y in ys, x < y, as dense 16x16 block
  * products on the fp32 matrix cores (v_mfma_f32_16x16x4_f32), from the

@@ -293,6 +293,48 @@ int main(int argc, char** argv) {
       check(ctx, rc, "profile posterior");
       return mlp_profile_result(ctx);
     });
+    // Profile posterior and MEA both on the device (mlp_profile_mea): only
+    // the path (and the few cells a refinement scores) come back.  Opt-in:
+    // the device MEA is a chain of dependent steps (8 waves over 64-row
+    // strips) and measured slower than the host's at C3 (QuickProbs
+    // refinement: 1.52 ms a call against ~1 ms), so by default
+    // (MLP_MEA_GPU_MIN unset) every MEA runs on the host.
+    static const int64_t mea_min = getenv("MLP_MEA_GPU_MIN") ? atoll(getenv("MLP_MEA_GPU_MIN")) : INT64_MAX;
+    cpnp::set_mea_backend([&](const cpnp::Profile& a, const cpnp::Profile& b, const int* w,
+                              const std::vector<int64_t>* cells, std::vector<float>* vals, std::string& path,
+                              float* score) -> bool {
+      if (mlp_ctx_is_host(ctx) || mea_min == INT64_MAX) return false;
+      const int L1 = a[0].length(), L2 = b[0].length();
+      if ((int64_t)L1 * L2 < mea_min) return false;
+      auto fill = [](const cpnp::Profile& p, std::vector<int32_t>& lab, std::vector<int32_t>& map) {
+        lab.clear();
+        map.clear();
+        for (const Row& r : p) {
+          lab.push_back(r.label);
+          map.push_back(0);
+          for (int c = 1; c <= r.length(); c++)
+            if (r.data[c] != '-') map.push_back(c);
+        }
+      };
+      fill(a, lab1, map1);
+      fill(b, lab2, map2);
+      check(ctx, mlp_profile_defer(ctx, 1), "profile posterior");
+      const int rc = mlp_profile_posterior_cpnp(ctx, w, (int)a.size(), lab1.data(), L1, map1.data(), (int)b.size(),
+                                                lab2.data(), L2, map2.data(), nullptr);
+      if (rc == MLP_ERR_STATE) {   // a profile wider than an LDS row: the host computes it
+        check(ctx, mlp_profile_defer(ctx, 0), "profile posterior");
+        return false;
+      }
+      check(ctx, rc, "profile posterior");
+      if (cells && !cells->empty())
+        check(ctx, mlp_profile_gather(ctx, (int64_t)cells->size(), cells->data(), vals->data()), "profile posterior");
+      path.resize((size_t)L1 + L2);
+      int32_t n = 0;
+      check(ctx, mlp_profile_mea(ctx, &path[0], &n, score), "MEA");
+      path.resize(n);
+      check(ctx, mlp_profile_defer(ctx, 0), "profile posterior");
+      return true;
+    });
     if (progressive) {
       aln = cpnp::progressive_alignment(seqs, sp, tree, pid, opt);
       stage("progressive + refinement");
@@ -302,6 +344,13 @@ int main(int argc, char** argv) {
       aln = cpnp::np_refinement(std::move(aln), sp, D, opt);
       stage("refinement");
     }
+  }
+  if (getenv("MLP_CLI_TIMES")) {
+    double tp, tm;
+    int64_t nc, nd;
+    cpnp::profile_times(&tp, &tm, &nc, &nd);
+    fprintf(stderr, "[host] profile posteriors %.3f s (%lld calls, %lld on the GPU), MEA %.3f s\n", tp, (long long)nc,
+            (long long)nd, tm);
   }
   mlp_ctx_destroy(ctx);
   stage("context teardown");

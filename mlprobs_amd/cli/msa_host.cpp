@@ -1,6 +1,8 @@
 // msa_host.cpp -- see msa_host.h.
 #include "msa_host.h"
 
+#include <chrono>
+
 #include <stdio.h>
 #include <stdlib.h>
 
@@ -293,10 +295,54 @@ static ProfileBackend& profile_backend() {
 }
 void set_profile_backend(ProfileBackend fn) { profile_backend() = std::move(fn); }
 
+// time split of the profile stages (MLP_CLI_TIMES)
+static double g_t_post = 0, g_t_mea = 0;
+static int64_t g_n_post = 0, g_n_dev = 0;
+static double wall() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
+void profile_times(double* post, double* mea, int64_t* calls, int64_t* device_calls) {
+  *post = g_t_post;
+  *mea = g_t_mea;
+  *calls = g_n_post;
+  *device_calls = g_n_dev;
+}
+
+static MeaBackend& mea_backend() {
+  static MeaBackend fn;
+  return fn;
+}
+void set_mea_backend(MeaBackend fn) { mea_backend() = std::move(fn); }
+
+bool device_mea(const Profile& a, const Profile& b, const int* weights, float cutoff,
+                const std::vector<int64_t>* cells, std::vector<float>* vals, std::string& path, float* score) {
+  if (!mea_backend() || cutoff != 0.f) return false;
+  const double t0 = wall();
+  const bool ok = mea_backend()(a, b, weights, cells, vals, path, score);
+  if (ok) {
+    g_t_mea += wall() - t0;
+    g_n_post++;
+    g_n_dev++;
+  }
+  return ok;
+}
+
+static const float* profile_posterior_impl(const Profile& a, const Profile& b, const SparseSet& sp,
+                                           const int* weights, float cutoff);
 const float* profile_posterior(const Profile& a, const Profile& b, const SparseSet& sp, const int* weights,
                                float cutoff) {
+  const double t0 = wall();
+  const float* p = profile_posterior_impl(a, b, sp, weights, cutoff);
+  g_t_post += wall() - t0;
+  g_n_post++;
+  return p;
+}
+
+static const float* profile_posterior_impl(const Profile& a, const Profile& b, const SparseSet& sp,
+                                           const int* weights, float cutoff) {
   if (profile_backend() && cutoff == 0.f)
-    if (const float* p = profile_backend()(a, b, weights)) return p;
+    if (const float* p = profile_backend()(a, b, weights)) {
+      g_n_dev++;
+      return p;
+    }
   // reused, kept all zero between calls: only the cells the previous call
   // wrote are cleared (fresh pages, or a full fill, cost more than the adds)
   static thread_local std::vector<float> buf;
@@ -383,6 +429,13 @@ std::string mea_path_tiled(int len1, int len2, const float* post, float* score) 
 }
 
 std::string mea_path(int len1, int len2, const float* post, float* score) {
+  const double t0 = wall();
+  std::string r = mea_path_dispatch(len1, len2, post, score);
+  g_t_mea += wall() - t0;
+  return r;
+}
+
+std::string mea_path_dispatch(int len1, int len2, const float* post, float* score) {
   // the tiled form pays ~20 parallel regions per call: only for very large
   // matrices (measured: 1100 x 1100 on 16 threads of the GPU box is slower
   // tiled once the thread wake-ups are counted)
@@ -493,9 +546,12 @@ static Profile process_tree(const GuideTree& t, int node, const std::vector<Row>
   Profile left = process_tree(t, nd.left, seqs, sp, opt);
   Profile right = process_tree(t, nd.right, seqs, sp, opt);
   // AlignAlignments (MSA.cpp:1410-1474) with the tree weights
-  const float* post = profile_posterior(left, right, sp, t.weights.data(), opt.cutoff);
+  std::string path;
   float sc;
-  const std::string path = mea_path(left[0].length(), right[0].length(), post, &sc);
+  if (!device_mea(left, right, t.weights.data(), opt.cutoff, nullptr, nullptr, path, &sc)) {
+    const float* post = profile_posterior(left, right, sp, t.weights.data(), opt.cutoff);
+    path = mea_path(left[0].length(), right[0].length(), post, &sc);
+  }
   return merge(left, right, path, !opt.align_order);
 }
 
@@ -554,12 +610,12 @@ static int refine_once(Profile& aln, const SparseSet& sp, const Options& opt) {
   }
   if (one.empty() || two.empty()) return 2;
   const Profile g1 = project(aln, one), g2 = project(aln, two);
-  const float* post = profile_posterior(g1, g2, sp, nullptr, opt.cutoff);
-  // accuracy of the current alignment
+  // accuracy of the current alignment: the posterior at the columns both
+  // groups occupy, summed in column order
   const int L = aln[0].length();
   const int W2 = g2[0].length() + 1;
+  std::vector<int64_t> cells;
   int i1 = 0, i2 = 0;
-  float before = 0;
   for (int i = 1; i <= L; i++) {
     bool f1 = false, f2 = false;
     for (int k : one)
@@ -568,10 +624,18 @@ static int refine_once(Profile& aln, const SparseSet& sp, const Options& opt) {
     for (int k : two)
       if (aln[k].data[i] != '-') { f2 = true; break; }
     if (f2) i2++;
-    if (f1 && f2) before += post[(size_t)i1 * W2 + i2];
+    if (f1 && f2) cells.push_back((int64_t)i1 * W2 + i2);
   }
+  std::vector<float> vals(cells.size());
   float after;
-  const std::string path = mea_path(g1[0].length(), g2[0].length(), post, &after);
+  std::string path;
+  if (!device_mea(g1, g2, nullptr, opt.cutoff, &cells, &vals, path, &after)) {
+    const float* post = profile_posterior(g1, g2, sp, nullptr, opt.cutoff);
+    for (size_t k = 0; k < cells.size(); k++) vals[k] = post[cells[k]];
+    path = mea_path(g1[0].length(), g2[0].length(), post, &after);
+  }
+  float before = 0;
+  for (float v : vals) before += v;
   aln = merge(g1, g2, path, false);
   return before == after ? 1 : 0;
 }

@@ -82,6 +82,17 @@ void set_profile_backend(ProfileBackend fn);
 const float* profile_posterior(const Profile& a, const Profile& b, const SparseSet& sp, const int* weights,
                                float cutoff);
 
+// The profile posterior and its MEA both on the device (the matrix never
+// comes back): fills `path` and `score` and, when `cells` is given, `vals`
+// with the matrix at those row-major indices; false = use the host path.
+using MeaBackend = std::function<bool(const Profile& a, const Profile& b, const int* weights,
+                                      const std::vector<int64_t>* cells, std::vector<float>* vals,
+                                      std::string& path, float* score)>;
+void set_mea_backend(MeaBackend fn);
+// device_mea through the backend when set and the cutoff is 0 (timed with the MEA)
+bool device_mea(const Profile& a, const Profile& b, const int* weights, float cutoff,
+                const std::vector<int64_t>* cells, std::vector<float>* vals, std::string& path, float* score);
+
 // MEA alignment of two profiles (ProbabilisticModel.h:804-864): the path
 // ('B', 'X', 'Y') and its score.
 std::string mea_path(int len1, int len2, const std::vector<float>& post, float* score);
@@ -89,6 +100,9 @@ std::string mea_path(int len1, int len2, const float* post, float* score);  // (
 // the two evaluations mea_path chooses between (tiled: anti-diagonals of
 // 128 x 128 tiles in parallel, for large matrices); identical results
 std::string mea_path_serial(int len1, int len2, const float* post, float* score);
+std::string mea_path_dispatch(int len1, int len2, const float* post, float* score);  // untimed
+// accumulated seconds of profile posteriors and MEA, calls (MLP_CLI_TIMES)
+void profile_times(double* post, double* mea, int64_t* calls, int64_t* device_calls);
 std::string mea_path_tiled(int len1, int len2, const float* post, float* score);
 
 // Profile merge along a path (Sequence.h AddGaps) and helpers.

@@ -552,8 +552,11 @@ static std::vector<std::set<int>> find_similar(std::vector<std::vector<float>> d
 // profile posterior, MEA, merge, SortByLabel unless -a
 static Profile align_profiles(const Profile& a, const Profile& b, const SparseSet& sp, const Options& opt,
                               float* score) {
-  const float* post = profile_posterior(a, b, sp, nullptr, opt.cutoff);
-  const std::string path = mea_path(a[0].length(), b[0].length(), post, score);
+  std::string path;
+  if (!device_mea(a, b, nullptr, opt.cutoff, nullptr, nullptr, path, score)) {
+    const float* post = profile_posterior(a, b, sp, nullptr, opt.cutoff);
+    path = mea_path(a[0].length(), b[0].length(), post, score);
+  }
   return merge(a, b, path, !opt.align_order);
 }
 

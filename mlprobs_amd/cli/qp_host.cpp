@@ -341,16 +341,21 @@ double now() { return omp_get_wtime(); }
 Profile align_alignments(const std::vector<float>& w, const Profile& A, const Profile& B, const PosteriorBackend& be,
                          std::vector<float>& post, int threads) {
   const double t0 = now();
-  const float* P = be.device ? be.device(w, A, B) : nullptr;
-  if (!P) {
-    build_posterior(w, A, B, be.host_sparse(), post, threads);
-    P = post.data();
-  }
-  const double t1 = now();
   float score;
-  const std::string path = cpnp::mea_path(A[0].length(), B[0].length(), P, &score);
-  g_t_post += t1 - t0;
-  g_t_mea += now() - t1;
+  std::string path;
+  if (be.device_mea && be.device_mea(w, A, B, path, &score)) {
+    g_t_mea += now() - t0;
+  } else {
+    const float* P = be.device ? be.device(w, A, B) : nullptr;
+    if (!P) {
+      build_posterior(w, A, B, be.host_sparse(), post, threads);
+      P = post.data();
+    }
+    const double t1 = now();
+    path = cpnp::mea_path(A[0].length(), B[0].length(), P, &score);
+    g_t_post += t1 - t0;
+    g_t_mea += now() - t1;
+  }
   g_n_terms += (int64_t)A.size() * (int64_t)B.size();
   Profile r;
   r.reserve(A.size() + B.size());

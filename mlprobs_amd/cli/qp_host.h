@@ -87,6 +87,10 @@ struct PosteriorBackend {
   // returns the dense (L1 + 1) x (L2 + 1) matrix (valid until the next call)
   // or nullptr to use the host path
   std::function<const float*(const std::vector<float>& w, const Profile& A, const Profile& B)> device;
+  // the posterior and its MEA on the device: path and score, or false
+  std::function<bool(const std::vector<float>& w, const Profile& A, const Profile& B, std::string& path,
+                     float* score)>
+      device_mea;
   std::function<const Sparse&()> host_sparse;
 };
 

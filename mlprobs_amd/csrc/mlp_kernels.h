@@ -358,6 +358,17 @@ struct ProfileArgs {
   int stage;                 // staged entries per run (<= the LDS stage; set by launch_profile_posterior)
 };
 size_t profile_lds(int L2);
+// MEA of the dense profile posterior (profile.hip): choices 2 bits per cell
+// (0 D, 1 L, 2 U), row stride (L2 + 4) / 4 bytes; rows 1..L1, columns 1..L2
+struct MeaArgs {
+  const float* post;         // (L1 + 1) x (L2 + 1)
+  int L1, L2;
+  uint8_t* tb;
+  float* score;              // [0]: the MEA score
+};
+hipError_t launch_profile_mea(const MeaArgs& a, hipStream_t st);
+size_t profile_mea_lds(int L2);  // LDS of k_profile_mea (at most 160 KB: L2 up to ~4600)
+hipError_t launch_profile_gather(const float* post, const int64_t* cells, int64_t n, float* out, hipStream_t st);
 hipError_t launch_profile_posterior(const ProfileArgs& a, hipStream_t st);
 hipError_t launch_transpose(const TransposeArgs& a, hipStream_t st);
 hipError_t launch_relax_tasks(const RelaxArgs& a, hipStream_t st);

@@ -88,6 +88,12 @@ struct mlp_ctx {
   float* h_prof_out = nullptr;
   size_t h_prof_out_bytes = 0;
   double prof_t[2] = {0, 0};  // host preparation, device round trip (MLP_PROFILE_TIMES)
+  // the last profile posterior's matrix on the device (mlp_profile_defer / _mea / _gather)
+  bool prof_defer = false;
+  float* prof_dout = nullptr;
+  int prof_L1 = 0, prof_L2 = 0;
+  uint8_t* h_mea = nullptr;           // pinned: MEA choices + score
+  size_t h_mea_bytes = 0;
   std::vector<float> dist, mea;
   std::vector<int64_t> nnz;
   // Viterbi family test (per pair, pair order)
@@ -101,7 +107,7 @@ struct mlp_ctx {
   size_t scratch_budget = 0;
   // relaxation buffers
   DevBuf r_trowptr, r_tcols, r_tvals, r_raw, r_newrp, r_newcols, r_newvals, r_tasks_p, r_tasks_r,
-      r_pairs, r_nnz, r_newoff, r_img, r_imgoff, r_tiles, r_nwords, r_weights, r_seldist, r_profile;
+      r_pairs, r_nnz, r_newoff, r_img, r_imgoff, r_tiles, r_nwords, r_weights, r_seldist, r_profile, r_mea;
   // comm
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
@@ -410,7 +416,7 @@ void mlp_ctx_destroy(mlp_ctx* c) {
   DevBuf* bufs[] = {&c->scratch, &c->scratch2, &c->r_trowptr, &c->r_tcols, &c->r_tvals, &c->r_raw, &c->r_newrp,
                     &c->r_newcols, &c->r_newvals, &c->r_tasks_p, &c->r_tasks_r, &c->r_pairs,
                     &c->r_nnz, &c->r_newoff, &c->r_img, &c->r_imgoff, &c->r_tiles, &c->r_nwords, &c->r_weights,
-                    &c->r_seldist, &c->r_profile};
+                    &c->r_seldist, &c->r_profile, &c->r_mea};
   for (DevBuf* b : bufs)
     if (b->p) hipFree(b->p);
   if (c->comm) ncclCommDestroy(c->comm);
@@ -420,6 +426,7 @@ void mlp_ctx_destroy(mlp_ctx* c) {
             c->prof_t[1]);
   if (c->h_prof_in) hipHostFree(c->h_prof_in);
   if (c->h_prof_out) hipHostFree(c->h_prof_out);
+  if (c->h_mea) hipHostFree(c->h_mea);
   hipStreamDestroy(c->stream);
   hipStreamDestroy(c->stream2);
   if (c->side.st) {
@@ -1265,6 +1272,9 @@ static int profile_posterior(mlp_ctx* c, const std::vector<float>& w, int n1, co
     return MLP_ERR_STATE;
   }
   hipSetDevice(c->device);
+  // a deferred call may still be reading the pinned input staging
+  if (c->prof_defer) HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->prof_dout = nullptr;
   int rc;
   if ((rc = ensure_transposes(c))) return rc;
   const auto tp0 = std::chrono::steady_clock::now();
@@ -1371,6 +1381,13 @@ static int profile_posterior(mlp_ctx* c, const std::vector<float>& w, int n1, co
   pa.w = d_w;
   pa.out = d_out;
   HIPCHK(c, launch_profile_posterior(pa, c->stream));
+  c->prof_dout = d_out;
+  c->prof_L1 = L1;
+  c->prof_L2 = L2;
+  if (c->prof_defer && !out) {  // stays on the device for mlp_profile_mea / _gather
+    c->prof_t[1] += std::chrono::duration<double>(std::chrono::steady_clock::now() - tp1).count();
+    return MLP_OK;
+  }
   HIPCHK(c, hipMemcpyAsync(c->h_prof_out, d_out, b_out, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->prof_t[1] += std::chrono::duration<double>(std::chrono::steady_clock::now() - tp1).count();
@@ -1380,7 +1397,126 @@ static int profile_posterior(mlp_ctx* c, const std::vector<float>& w, int n1, co
 
 extern "C" {
 
-const float* mlp_profile_result(const mlp_ctx* c) { return c ? c->h_prof_out : nullptr; }
+const float* mlp_profile_result(const mlp_ctx* c) { return c && !c->prof_defer ? c->h_prof_out : nullptr; }
+
+int mlp_profile_defer(mlp_ctx* c, int on) {
+  if (!c) return MLP_ERR_ARG;
+  if (c->host) return MLP_ERR_STATE;
+  c->prof_defer = on != 0;
+  return MLP_OK;
+}
+
+int mlp_profile_mea(mlp_ctx* c, char* path, int32_t* path_len, float* score) {
+  if (!c || !path || !path_len) return MLP_ERR_ARG;
+  if (c->host || !c->prof_dout) return MLP_ERR_STATE;
+  const auto tp = std::chrono::steady_clock::now();
+  const int L1 = c->prof_L1, L2 = c->prof_L2, Wq = (L2 + 4) / 4;
+  const size_t tb_bytes = (size_t)(L1 + 1) * Wq, all = ((tb_bytes + 15) & ~(size_t)15) + 16;
+  int rc;
+  hipSetDevice(c->device);
+  if ((rc = ensure(c, c->r_mea, all))) return rc;
+  if (c->h_mea_bytes < all) {
+    if (c->h_mea) hipHostFree(c->h_mea);
+    c->h_mea = nullptr;
+    c->h_mea_bytes = 0;
+    if (hipHostMalloc((void**)&c->h_mea, all * 2, hipHostMallocDefault) != hipSuccess) return MLP_ERR_MEMORY;
+    c->h_mea_bytes = all * 2;
+  }
+  if (profile_mea_lds(L2) > 160 * 1024 || (L1 + 63) / 64 > 256) {
+    // too wide for the kernel's LDS strip: the matrix comes back and the
+    // same recurrence runs here (ProbabilisticModel.h:804-864)
+    const size_t b_out = (size_t)(L1 + 1) * (L2 + 1) * 4;
+    std::vector<float> post((size_t)(L1 + 1) * (L2 + 1));
+    HIPCHK(c, hipMemcpyAsync(post.data(), c->prof_dout, b_out, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const int W2 = L2 + 1;
+    std::vector<float> rows(2 * (size_t)W2, 0.f);
+    std::vector<uint8_t> ch((size_t)(L1 + 1) * W2, 1);
+    float* oldr = rows.data();
+    float* newr = rows.data() + W2;
+    for (int i = 1; i <= L1; i++) {
+      newr[0] = 0;
+      ch[(size_t)i * W2] = 2;
+      for (int j = 1; j <= L2; j++) {
+        const float x1 = post[(size_t)i * W2 + j] + oldr[j - 1], x2 = newr[j - 1], x3 = oldr[j];
+        float v;
+        uint8_t b;
+        if (x1 >= x2) {
+          if (x1 >= x3) { v = x1; b = 0; } else { v = x3; b = 2; }
+        } else if (x2 >= x3) {
+          v = x2; b = 1;
+        } else {
+          v = x3; b = 2;
+        }
+        newr[j] = v;
+        ch[(size_t)i * W2 + j] = b;
+      }
+      std::swap(oldr, newr);
+    }
+    if (score) *score = oldr[L2];
+    int r = L1, col = L2, k = 0;
+    while (r != 0 || col != 0) {
+      const int b = r == 0 ? 1 : col == 0 ? 2 : ch[(size_t)r * W2 + col];
+      if (b == 1) { col--; path[k++] = 'Y'; }
+      else if (b == 2) { r--; path[k++] = 'X'; }
+      else { r--; col--; path[k++] = 'B'; }
+    }
+    std::reverse(path, path + k);
+    *path_len = k;
+    return MLP_OK;
+  }
+  MeaArgs m;
+  m.post = c->prof_dout;
+  m.L1 = L1;
+  m.L2 = L2;
+  m.tb = (uint8_t*)c->r_mea.p;
+  m.score = (float*)((uint8_t*)c->r_mea.p + all - 16);
+  HIPCHK(c, launch_profile_mea(m, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->h_mea, c->r_mea.p, all, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  const uint8_t* tb = c->h_mea;
+  if (score) memcpy(score, c->h_mea + all - 16, 4);
+  // traceback (ProbabilisticModel.h:846-858): row 0 moves left, column 0 up
+  int r = L1, col = L2, k = 0;
+  while (r != 0 || col != 0) {
+    const int b = r == 0 ? 1 : col == 0 ? 2 : (tb[(size_t)r * Wq + (col >> 2)] >> (2 * (col & 3))) & 3;
+    if (b == 1) {
+      col--;
+      path[k++] = 'Y';
+    } else if (b == 2) {
+      r--;
+      path[k++] = 'X';
+    } else {
+      r--;
+      col--;
+      path[k++] = 'B';
+    }
+  }
+  std::reverse(path, path + k);
+  *path_len = k;
+  c->prof_t[1] += std::chrono::duration<double>(std::chrono::steady_clock::now() - tp).count();
+  return MLP_OK;
+}
+
+int mlp_profile_gather(mlp_ctx* c, int64_t n, const int64_t* cells, float* vals) {
+  if (!c || n < 0 || (n && (!cells || !vals))) return MLP_ERR_ARG;
+  if (c->host || !c->prof_dout) return MLP_ERR_STATE;
+  if (!n) return MLP_OK;
+  const int64_t lim = (int64_t)(c->prof_L1 + 1) * (c->prof_L2 + 1);
+  for (int64_t k = 0; k < n; k++)
+    if (cells[k] < 0 || cells[k] >= lim) return MLP_ERR_ARG;
+  hipSetDevice(c->device);
+  int rc;
+  if ((rc = ensure(c, c->r_mea, (size_t)n * 12 + 64))) return rc;
+  int64_t* d_cells = (int64_t*)c->r_mea.p;
+  float* d_vals = (float*)(d_cells + n);
+  HIPCHK(c, hipMemcpyAsync(d_cells, cells, (size_t)n * 8, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, launch_profile_gather(c->prof_dout, d_cells, n, d_vals, c->stream));
+  HIPCHK(c, hipMemcpyAsync(vals, d_vals, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return MLP_OK;
+}
+
 
 int mlp_pair_results(mlp_ctx* c, int64_t p0, int64_t p1, float* dist, float* mea, int64_t* nnz) {
   if (!c || p0 < 0 || p1 > c->P || p0 > p1) return MLP_ERR_ARG;

@@ -29,6 +29,7 @@
 #include <algorithm>
 
 #include "mlp_kernels.h"
+#include "mlp_numerics.h"
 
 namespace mlp {
 
@@ -173,6 +174,135 @@ __global__ __launch_bounds__(64) void k_profile_post(ProfileArgs A) {
   wave_sync();
   float* o = A.out + (int64_t)r * W2;
   for (int c = c0 + lane; c < c1; c += 64) o[c] = acc[c - c0];
+}
+
+// MEA of a dense (L1 + 1) x (L2 + 1) posterior (ProbabilisticModel.h:804-864,
+// ChooseBestOfThree ScoreType.h:347-366; QuickProbs' computeAlignment is the
+// same recurrence): one wave, rows in strips of 64 lanes, lane r on row
+// 64 s + r + 1 at column j = t - r + 1 of step t (an anti-diagonal
+// wavefront).  up = the upper lane's value of the previous step (DPP shift;
+// lane 0 reads the previous strip's last row, kept in LDS), diagonal = the
+// previous step's up, left = own previous value: every cell adds and compares
+// exactly as the serial loop does, so scores and choices are the reference's
+// bit for bit.  The choices go out as 2 bits per cell (0 D, 1 L, 2 U) for
+// the host to trace back.
+// Several waves: wave w takes strips w, w + W, ...; a strip starts 3
+// intervals (96 steps) after the one above it, so every value its lane 0
+// reads from that strip's last row (kept in a two-slot LDS ring) was
+// written at least one 32-step interval earlier, and all waves meet at a
+// barrier after every interval.  Strip s starts at interval
+// g_s = max(3 s, g_{s-W} + NI) (NI intervals per strip).  The posterior of
+// the next interval is loaded into registers during this one.
+constexpr int kMeaWaves = 8;  // 2 waves per SIMD: 256 VGPRs for the two 32-step register queues
+constexpr int kMeaIv = 32;  // steps per interval
+size_t profile_mea_lds(int L2) { return (size_t)2 * (L2 + 5) * 4 + 4 * 256 + 64; }
+__global__ __launch_bounds__(64 * kMeaWaves) void k_profile_mea(MeaArgs A) {
+  extern __shared__ __align__(16) uint8_t mea_smem[];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, W = blockDim.x >> 6;
+  const int L1 = A.L1, L2 = A.L2, W2 = L2 + 1, Wq = (W2 + 3) >> 2, RS = L2 + 5;
+  float* ring = (float*)mea_smem;                    // 2 x RS: last rows of strips s (slot s & 1)
+  int* g = (int*)(mea_smem + (size_t)2 * RS * 4);     // strip start intervals (<= 256 strips)
+  const int nstrips = (L1 + 63) >> 6;
+  const int NI = (L2 + 63 + kMeaIv - 1) / kMeaIv;
+  for (int k = threadIdx.x; k < 2 * RS; k += blockDim.x) ring[k] = 0.f;  // row 0 (slot 1 for strip 0)
+  if (threadIdx.x == 0) {
+    for (int s = 0; s < nstrips; ++s) g[s] = max(3 * s, s >= W ? g[s - W] + NI : 0);
+  }
+  __syncthreads();
+  const int end = g[nstrips - 1] + NI;
+  int m = 0;                    // this wave's current strip: w + m W
+  int s = w, gs = s < nstrips ? g[s] : end;
+  float left = 0.f, vprev = 0.f, upprev = 0.f, rowend = 0.f, pv = 0.f, lr = 0.f;
+  uint32_t bits = 0;
+  float cur[kMeaIv], nxt[kMeaIv];
+  int i = 0;
+  const float* prow = A.post;
+  uint8_t* trow = A.tb;
+  auto load = [&](int t0, float* dst) {  // posterior of steps t0 .. t0 + 31 of this lane's row
+#pragma unroll
+    for (int u = 0; u < kMeaIv; ++u) dst[u] = prow[min(max(t0 + u - lane + 1, 1), L2)];
+  };
+  for (int q = 0; q < end; ++q) {
+    if (s < nstrips && q == gs + NI) {  // strip done: score, next strip of this wave
+      if (i == L1) A.score[0] = rowend;
+      s += W;
+      gs = s < nstrips ? g[s] : end;
+    }
+    if (s < nstrips && q >= gs) {
+      const int t0 = (q - gs) * kMeaIv;
+      float* up_row = ring + (size_t)((s + 1) & 1) * RS;  // strip s - 1's last row
+      float* my_row = ring + (size_t)(s & 1) * RS;
+      if (t0 == 0) {  // strip start
+        i = 64 * s + lane + 1;
+        const int ii = min(i, L1);
+        prow = A.post + (size_t)ii * W2;
+        trow = A.tb + (size_t)ii * Wq;
+        left = vprev = upprev = rowend = 0.f;
+        bits = 0;
+        load(0, cur);
+        lr = up_row[1 <= L2 ? 1 : L2];
+      } else {
+#pragma unroll
+        for (int u = 0; u < kMeaIv; ++u) cur[u] = nxt[u];
+      }
+      load(t0 + kMeaIv, nxt);
+      const bool live = i <= L1;
+#pragma unroll
+      for (int u = 0; u < kMeaIv; ++u) {
+        const int t = t0 + u;
+        const int j = t - lane + 1;
+        const bool valid = j >= 1 && j <= L2;
+        const float lr_next = up_row[min(t + 2, L2)];
+        const float up = mlp_shr1(vprev, lr);
+        const float diag = upprev;
+        const float x1 = cur[u] + diag, x2 = left, x3 = up;
+        float v;
+        uint32_t b;
+        if (x1 >= x2) {
+          if (x1 >= x3) { v = x1; b = 0; } else { v = x3; b = 2; }
+        } else if (x2 >= x3) {
+          v = x2; b = 1;
+        } else {
+          v = x3; b = 2;
+        }
+        v = valid ? v : 0.f;
+        left = valid ? v : left;
+        bits |= valid ? b << (2 * (j & 3)) : 0u;
+        if (valid && live && ((j & 3) == 3 || j == L2)) trow[j >> 2] = (uint8_t)bits;
+        bits = (j & 3) == 3 ? 0u : bits;
+        my_row[lane == 63 && valid ? j : W2 + (lane & 3)] = v;
+        rowend = j == L2 ? v : rowend;
+        vprev = v;
+        upprev = up;
+        lr = lr_next;
+      }
+      (void)pv;
+    }
+    __syncthreads();
+  }
+  if (s < nstrips && i == L1) A.score[0] = rowend;
+}
+
+__global__ __launch_bounds__(256) void k_profile_gather(const float* post, const int64_t* cells, int64_t n,
+                                                       float* out) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < n) out[k] = post[cells[k]];
+}
+hipError_t launch_profile_gather(const float* post, const int64_t* cells, int64_t n, float* out, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_profile_gather, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, post, cells, n, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_profile_mea(const MeaArgs& a, hipStream_t st) {
+  if (a.L1 <= 0 || a.L2 <= 0) return hipSuccess;
+  const size_t lds = profile_mea_lds(a.L2);
+  const int nstrips = (a.L1 + 63) / 64;
+  if (lds > 160 * 1024 || nstrips > 256) return hipErrorInvalidValue;
+  if (lds > 64 * 1024)
+    (void)hipFuncSetAttribute((const void*)k_profile_mea, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(k_profile_mea, dim3(1), dim3(64 * std::min(kMeaWaves, nstrips)), lds, st, a);
+  return hipGetLastError();
 }
 
 // inv1[i][map1_i[k]] = k: the column -> residue map of profile A, one

@@ -96,6 +96,9 @@ def lib():
         L.mlp_shard_count.argtypes = [P]
         L.mlp_relax_shard_plan.argtypes = [C.c_int, I32P, I64P, C.c_int, I64P]
         L.mlp_relax_blockmfma_eval.argtypes = [P, C.c_int, I32P, C.c_int, I32P, C.c_void_p]
+        L.mlp_profile_defer.argtypes = [P, C.c_int]
+        L.mlp_profile_mea.argtypes = [P, C.c_char_p, C.POINTER(C.c_int32), C.POINTER(C.c_float)]
+        L.mlp_profile_gather.argtypes = [P, C.c_int64, I64P, F32P]
         _LIB = L
     return _LIB
 
@@ -107,7 +110,8 @@ EXPORTED = ['mlp_ctx_create', 'mlp_ctx_destroy', 'mlp_last_error', 'mlp_set_scra
             'mlp_viterbi_path', 'mlp_model_adjustment', 'mlp_family_features', 'mlp_comm_unique_id', 'mlp_comm_init',
             'mlp_shard_range', 'mlp_shard_plan', 'mlp_gather_layout', 'mlp_allgather', 'mlp_synchronize', 'mlp_profile',
             'mlp_kernel_times', 'mlp_profile_reset', 'mlp_ctx_create_mask', 'mlp_set_shards', 'mlp_shard_count',
-            'mlp_relax_shard_plan', 'mlp_ctx_create_host', 'mlp_ctx_is_host', 'mlp_relax_blockmfma_eval']
+            'mlp_relax_shard_plan', 'mlp_ctx_create_host', 'mlp_ctx_is_host', 'mlp_relax_blockmfma_eval',
+            'mlp_profile_defer', 'mlp_profile_mea', 'mlp_profile_gather']
 
 
 def shard_plan(lens, nranks, rank):
@@ -284,6 +288,25 @@ class Family:
         self._chk(self._L.mlp_profile_posterior(self._ctx, w, len(l1), l1, int(L1), m1, len(l2), l2, int(L2), m2,
                                                 out))
         return out.reshape(L1 + 1, L2 + 1)
+
+    def profile_defer(self, on):
+        """Leave the next profile posteriors on the device (mlp_profile_defer)."""
+        self._chk(self._L.mlp_profile_defer(self._ctx, int(bool(on))))
+
+    def profile_mea(self, L1, L2):
+        """MEA path ('B'/'X'/'Y') and score of the last profile posterior,
+        on the device (mlp_profile_mea)."""
+        buf = C.create_string_buffer(L1 + L2 + 1)
+        n = C.c_int32(0)
+        sc = C.c_float(0)
+        self._chk(self._L.mlp_profile_mea(self._ctx, buf, C.byref(n), C.byref(sc)))
+        return buf.raw[:n.value].decode(), np.float32(sc.value)
+
+    def profile_gather(self, cells):
+        c = np.ascontiguousarray(cells, np.int64)
+        out = np.empty(len(c), np.float32)
+        self._chk(self._L.mlp_profile_gather(self._ctx, len(c), c, out))
+        return out
 
     def relax_blockmfma_eval(self, xs, ys):
         """Dense-block MFMA evaluation of one consistency round's transform

@@ -39,11 +39,18 @@ def test_cli_progressive(name, flags, suffix):
 
 @pytest.mark.parametrize('name', ['bb11028', 'div12', 'sim8'])
 @pytest.mark.parametrize('flags,suffix', [((), 'p_0'), (('-p', '1'), 'p_1'), (('-p', '1', '-ir', '0'), 'p_1_ir_0')])
-def test_cli_profile_posterior_on_gpu(name, flags, suffix):
+@pytest.mark.parametrize('mea', ['host', 'device'])
+def test_cli_profile_posterior_on_gpu(name, flags, suffix, mea):
     """Every progressive merge and refinement pass through the GPU's
     BuildPosterior (MLP_PROFILE_GPU_MIN=1: no host fallback for small
-    profile pairs): still the reference's bytes."""
+    profile pairs), its MEA on the host or on the device
+    (MLP_MEA_GPU_MIN=0: mlp_profile_mea for every merge): still the
+    reference's bytes."""
     env = dict(ENV, MLP_PROFILE_GPU_MIN='1', MLP_SRAND_TIME='1700000000')
+    if mea == 'device':
+        env['MLP_MEA_GPU_MIN'] = '0'
+    else:
+        env['MLP_MEA_GPU_MIN'] = str(1 << 40)
     r = subprocess.run([BIN, *(flags or ('-p', '0')), os.path.join(GOLDEN, 'cli', f'{name}.fa')], capture_output=True,
                        text=True, timeout=300, env=env)
     assert r.returncode == 0 and r.stderr == '', r.stderr
@@ -93,10 +100,14 @@ QP_BIN = os.path.join(ROOT, 'mlprobs_amd', 'cli', 'quickprobs')
 
 @pytest.mark.parametrize('name,args', [('bb11028', []), ('bb11028', ['-c', '0']), ('bb11028', ['-c', '1', '-r', '5']),
                                        ('div12', []), ('div12', ['-c', '0']), ('sim8', []),
-                                       ('sim8', ['-c', '3', '-r', '50']), ('qp_div60', []), ('qp_big210', [])])
+                                       ('sim8', ['-c', '3', '-r', '50']), ('qp_div60', []), ('qp_big210', []),
+                                       ('div12', ['mea']), ('qp_div60', ['mea']), ('qp_big210', ['mea'])])
 def test_quickprobs_cli(name, args):
+    env = ENV
+    if args == ['mea']:  # every MEA on the device (mlp_profile_mea)
+        args, env = [], dict(ENV, MLP_MEA_DEVICE='1')
     r = subprocess.run([QP_BIN, *args, os.path.join(GOLDEN, 'cli', f'{name}.fa')], capture_output=True, text=True,
-                       timeout=300, env=ENV)
+                       timeout=300, env=env)
     assert r.returncode == 0 and r.stderr == '', r.stderr
     tag = 'qp_' + name.replace('qp_', '') + ''.join('_' + a.strip('-') for a in args)
     with open(os.path.join(GOLDEN, 'cli', f'{tag}.out')) as fh:

@@ -423,7 +423,7 @@ def _pair(n, a, b):
     return a * n - a * (a + 1) // 2 + (b - a - 1)
 
 
-def _profile_case(seed, n, L, sub, A, B, env=None):
+def _profile_case(seed, n, L, sub, A, B, env=None, mea=True):
     """mlp_profile_posterior (QuickProbs' buildPosterior on the GPU) against a
     plain restatement of ParallelProbabilisticModel.cpp:301-430 over the same
     relaxed sparse set: weights in double cast to float, terms in (i, j, row,
@@ -479,7 +479,52 @@ def _profile_case(seed, n, L, sub, A, B, env=None):
                     c = mB[jb][col]
                     ref[r, c] = np.float32(ref[r, c] + np.float32(wf * np.float32(v)))
     np.testing.assert_array_equal(got, ref)
+    if mea:
+        # the same matrix left on the device: MEA there, and a gather
+        fam.profile_defer(True)
+        fam.profile_posterior(w, A, mA, L1, B, mB, L2)
+        path, score = fam.profile_mea(L1, L2)
+        rpath, rscore = _mea_ref(ref)
+        assert path == rpath and score == rscore, (score, rscore)
+        cells = np.array([0, L2 + 2, (L1 + 1) * (L2 + 1) - 1, 3 * (L2 + 1) + 5], np.int64)
+        np.testing.assert_array_equal(fam.profile_gather(cells), ref.reshape(-1)[cells])
+        fam.profile_defer(False)
     fam.close()
+
+
+def _mea_ref(post):
+    """ComputeAlignment (ProbabilisticModel.h:804-864) in float32, serially."""
+    L1, L2 = post.shape[0] - 1, post.shape[1] - 1
+    old = np.zeros(L2 + 1, np.float32)
+    tb = np.zeros((L1 + 1, L2 + 1), np.int8)
+    for i in range(1, L1 + 1):
+        new = np.zeros(L2 + 1, np.float32)
+        for j in range(1, L2 + 1):
+            x1 = np.float32(post[i, j] + old[j - 1])
+            x2, x3 = new[j - 1], old[j]
+            if x1 >= x2:
+                v, b = (x1, 0) if x1 >= x3 else (x3, 2)
+            elif x2 >= x3:
+                v, b = x2, 1
+            else:
+                v, b = x3, 2
+            new[j] = v
+            tb[i, j] = b
+        old = new
+    r, c, out = L1, L2, []
+    while r or c:
+        b = 1 if r == 0 else 2 if c == 0 else tb[r, c]
+        if b == 1:
+            c -= 1
+            out.append('Y')
+        elif b == 2:
+            r -= 1
+            out.append('X')
+        else:
+            r -= 1
+            c -= 1
+            out.append('B')
+    return ''.join(reversed(out)), old[L2]
 
 
 @pytest.mark.parametrize('seed', [81, 82])
@@ -498,6 +543,11 @@ def test_profile_posterior_stage_branches(stage, split):
     if split:
         env['MLP_PROFILE_SPLIT'] = split
     _profile_case(83, 9, 70, 0.7, [0, 3, 5, 8], [1, 2, 6], env)
+
+
+def test_profile_mea_multi_strip():
+    """Device MEA over profiles of ~190 x ~185 columns (three 64-row strips)."""
+    _profile_case(86, 12, 180, 0.5, [0, 2, 4, 7, 9], [1, 3, 11])
 
 
 def test_profile_posterior_many_sequences():
