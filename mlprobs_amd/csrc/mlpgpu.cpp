@@ -2284,6 +2284,8 @@ static int relax_one(mlp_ctx* c, const QpRelax& qp, bool last) {
     const int n = c->n;
     const bool exact = !tasks_only && n <= 2048;
     const int64_t kSmallCells = 8 * (int64_t)kRelaxThreads;  // 8 slots: the 64-VGPR budget of 8 waves per SIMD
+    // z's per tile whose images may exceed the staging area (staged in passes)
+    const int max_over = getenv("MLP_RELAX_SPLIT_Z") ? atoi(getenv("MLP_RELAX_SPLIT_Z")) : n / 16;
     std::vector<int32_t> isz;  // image bytes of P(s, z), s's residues as rows: isz[s * n + z]
     if (exact) {
       isz.assign((size_t)n * n, 0);
@@ -2322,14 +2324,19 @@ static int relax_one(mlp_ctx* c, const QpRelax& qp, bool last) {
         t.bound = t.cells = t.peak = 0;
       };
       // LDS need of tile t with output x added
-      auto need_with = [&](const Cur& t, int x) -> int64_t {
+      // LDS need of tile t with output x added, and the z's where it exceeds `lim`
+      auto need_with = [&](const Cur& t, int x, int64_t lim, int* over) -> int64_t {
+        *over = 0;
         if (!exact) return t.bound + maxI[x] + maxI[yy];
         const int32_t* ix = &isz[(size_t)x * n];
         int64_t m = 0;
-        if (t.cnt)
-          for (int z = 0; z < n; z++) m = std::max(m, t.sum[z] + ix[z]);
-        else
-          for (int z = 0; z < n; z++) m = std::max<int64_t>(m, (int64_t)iy[z] + ix[z]);
+        int o = 0;
+        for (int z = 0; z < n; z++) {
+          const int64_t v = (t.cnt ? t.sum[z] : (int64_t)iy[z]) + ix[z];
+          m = std::max(m, v);
+          o += v > lim;
+        }
+        *over = o;
         return m;
       };
       for (int x = 0; x < yy; x++) {
@@ -2341,7 +2348,8 @@ static int relax_one(mlp_ctx* c, const QpRelax& qp, bool last) {
         int64_t alone = 0;
         if (!tasks_only && !big[x] && !big[yy] && tile_relax_slots(nz)) {
           const Cur empty{};
-          alone = need_with(empty, x);
+          int unused;
+          alone = need_with(empty, x, budget, &unused);
           k = alone <= small_budget && nz <= kSmallCells ? 0 : alone <= budget ? 1 : -1;
         }
         if (k < 0) {
@@ -2352,11 +2360,15 @@ static int relax_one(mlp_ctx* c, const QpRelax& qp, bool last) {
           continue;
         }
         Cur& t = cur[k];
-        int64_t nd = t.cnt ? need_with(t, x) : alone;
-        if (t.cnt && (t.cnt == tmax || nd > lim[k] || !tile_relax_slots(t.cells + nz) ||
-                      (k == 0 && t.cells + nz > kSmallCells))) {
+        // a tile may exceed its staging area on a few z's (outliers: the
+        // kernel stages those z's outputs in passes), never on one output
+        int over = 0;
+        int64_t nd = t.cnt ? need_with(t, x, lim[k], &over) : alone;
+        if (t.cnt && (t.cnt == tmax || (exact ? over > max_over : nd > lim[k]) ||
+                      !tile_relax_slots(t.cells + nz) || (k == 0 && t.cells + nz > kSmallCells))) {
           flush(k);
           nd = alone;
+          over = 0;
         }
         if (exact) {
           const int32_t* ix = &isz[(size_t)x * n];
@@ -2368,7 +2380,7 @@ static int relax_one(mlp_ctx* c, const QpRelax& qp, bool last) {
         t.cnt++;
         t.bound += maxI[x];
         t.cells += nz;
-        t.peak = nd;
+        t.peak = over ? lim[k] : nd;   // split z's: the staging area is the class bound
       }
       flush(0);
       flush(1);

@@ -492,8 +492,24 @@ __global__ __launch_bounds__(kRelaxThreads, KP == 5 && kRelaxThreads == 1024 ? 8
             }
           }
           if (any) {
-            e0 = make_uint4((uint32_t)(A.img_off[qc] >> 4), (uint32_t)nzc,
-                            (uint32_t)((A.img_off[qc + 1] - A.img_off[qc]) >> 4), (uint32_t)A.lens[z]);
+            // outputs in passes over this z when their images and C exceed
+            // the staging area (greedy in output order; the host keeps each
+            // output with C within it): pass of output t in bits 2t, 2t+1,
+            // passes - 1 in bits 8-9 of e0.w
+            const uint32_t cC = (uint32_t)((A.img_off[qc + 1] - A.img_off[qc]) >> 4);
+            const uint32_t capc = (uint32_t)A.cap >> 4;
+            uint32_t used = cC, grp = 0, gsel = 0;
+#pragma unroll
+            for (int t = 0; t < TM; ++t) {
+              if (na[t] == 0) continue;
+              if (used + ac[t] > capc && used > cC) {
+                ++grp;
+                used = cC;
+              }
+              used += ac[t];
+              gsel |= grp << (2 * t);
+            }
+            e0 = make_uint4((uint32_t)(A.img_off[qc] >> 4), (uint32_t)nzc, cC, gsel | grp << 8);
             e1 = make_uint4(ao[0], ao[1], ao[2], ao[3]);
             e2 = make_uint4(na[0], na[1], na[2], na[3]);
             e3 = make_uint4(ac[0], ac[1], ac[2], ac[3]);
@@ -529,20 +545,34 @@ __global__ __launch_bounds__(kRelaxThreads, KP == 5 && kRelaxThreads == 1024 ? 8
   // next scheduled z (uniform across the workgroup); returns false when done
   uint4 nC, nAo, nNa, nAc;  // the staged-next z's entry
   float4 nW = make_float4(1.f, 1.f, 1.f, 1.f);  // its QuickProbs weights
+  int zpass = 0;  // pass of the current z (several when its images exceed the staging area)
   auto next = [&]() -> bool {
     for (;;) {
-      if (++zpos == kRelaxZChunk) {
-        zbase += kRelaxZChunk;
-        if (zbase >= n) return false;
-        zpos = 0;
-        fill();
+      if (zpos >= 0 && zpass < (int)((nC.w >> 8) & 3) && nC.y) {
+        ++zpass;  // the same z again, the next subset of outputs
+      } else {
+        zpass = 0;
+        if (++zpos == kRelaxZChunk) {
+          zbase += kRelaxZChunk;
+          if (zbase >= n) return false;
+          zpos = 0;
+          fill();
+        }
+        if (zbase + zpos >= n) return false;
+        nC = rfl(ztab[4 * zpos]);
       }
-      if (zbase + zpos >= n) return false;
-      nC = rfl(ztab[4 * zpos]);
       if (nC.y) {
         nAo = rfl(ztab[4 * zpos + 1]);
         nNa = rfl(ztab[4 * zpos + 2]);
         nAc = rfl(ztab[4 * zpos + 3]);
+        if (nC.w >> 8) {  // keep this pass's outputs only
+          const uint32_t g = nC.w;
+          const uint32_t p = (uint32_t)zpass;
+          if (((g >> 0) & 3) != p) { nNa.x = 0; nAc.x = 0; }
+          if (((g >> 2) & 3) != p) { nNa.y = 0; nAc.y = 0; }
+          if (((g >> 4) & 3) != p) { nNa.z = 0; nAc.z = 0; }
+          if (((g >> 6) & 3) != p) { nNa.w = 0; nAc.w = 0; }
+        }
         if constexpr (QP) {
           const float4 w4 = wtab[zpos];
           const uint4 u = rfl(make_uint4(__float_as_uint(w4.x), __float_as_uint(w4.y), __float_as_uint(w4.z),

@@ -256,8 +256,11 @@ def _relax_both_paths(seqs, pid, iters, tag):
         refs.append(cur)
     # tiled kernel with up to 4 outputs per tile, one output per tile, the
     # large-prefetch instantiation, and the row-task kernel
+    # and tiles over a 48 KB staging area whose oversize z's are staged in
+    # passes over subsets of the outputs (MLP_RELAX_SPLIT_Z: no limit)
     modes = [{'MLP_RELAX': 'pairs'}, {'MLP_RELAX': 'pairs', 'MLP_RELAX_TILE': '1'},
-             {'MLP_RELAX': 'pairs', 'MLP_RELAX_KP': '9'}, {'MLP_RELAX': 'tasks'}]
+             {'MLP_RELAX': 'pairs', 'MLP_RELAX_KP': '9'}, {'MLP_RELAX': 'tasks'},
+             {'MLP_RELAX_LDS_KB': '48', 'MLP_RELAX_SPLIT_Z': '100000'}]
     for env in modes:
         os.environ.update(env)
         try:
