@@ -2,6 +2,9 @@
 #include "msa_host.h"
 
 #include <chrono>
+#include <atomic>
+#include <thread>
+#include <omp.h>
 
 #include <stdio.h>
 #include <stdlib.h>
@@ -362,55 +365,94 @@ std::string mea_path(int len1, int len2, const std::vector<float>& post, float* 
   return mea_path(len1, len2, post.data(), score);
 }
 
-// The same recurrence over 128 x 128 tiles, one anti-diagonal of tiles at a
-// time in parallel (every cell still sees exactly its three neighbours'
-// final values, so the result is the serial one bit for bit).
-std::string mea_path_tiled(int len1, int len2, const float* post, float* score) {
+std::string mea_path(int len1, int len2, const float* post, float* score) {
+  const double t0 = wall();
+  std::string r = mea_path_dispatch(len1, len2, post, score);
+  g_t_mea += wall() - t0;
+  return r;
+}
+
+std::string mea_path_dispatch(int len1, int len2, const float* post, float* score) {
+  // one parallel region per call, threads pipelined over 64-row bands, for
+  // matrices large enough to pay for the thread wake-up (MLP_MEA_WAVE_MIN
+  // cells; 0 = always serial).  Measured on the GPU box (16 cores): C2 -p 1
+  // refinement MEA 0.66 -> 0.38 s (profiles of several thousand columns),
+  // but ~1000 x 1000 (QuickProbs C3 refinement) 0.62 -> 0.86 s with every
+  // call threaded, hence the 2.5e6-cell floor.
+  static const int64_t wave_min = getenv("MLP_MEA_WAVE_MIN") ? atoll(getenv("MLP_MEA_WAVE_MIN")) : 2500000;
+  if (wave_min > 0 && (int64_t)len1 * len2 >= wave_min && len1 >= 128 && omp_get_max_threads() > 1)
+    return mea_path_wave(len1, len2, post, score);
+  return mea_path_serial(len1, len2, post, score);
+}
+
+// The same recurrence with threads pipelined over bands of 64 rows: band b
+// goes to thread b mod T, which walks it in 256-column tiles, each tile
+// started once the band above has finished that tile's columns (an atomic
+// count of finished columns per band, spun on).  Every cell still sees its
+// three neighbours' final values: the serial result bit for bit.
+std::string mea_path_wave(int len1, int len2, const float* post, float* score) {
   const int W2 = len2 + 1;
-  constexpr int T = 128;
-  static thread_local std::vector<float> V;  // reused: first touches cost more than the DP
+  constexpr int RB = 64, CB = 256;
+  static thread_local std::vector<float> V;
   static thread_local std::vector<char> tb;
   if (V.size() < (size_t)(len1 + 1) * W2) {
     V.resize((size_t)(len1 + 1) * W2);
     tb.resize((size_t)(len1 + 1) * W2);
   }
-  float* Vp = V.data();  // (the parallel region's threads have their own thread_locals)
+  float* Vp = V.data();
   char* tbp = tb.data();
   for (int j = 0; j <= len2; j++) {
     Vp[j] = 0;
     tbp[j] = 'L';
   }
-  for (int i = 1; i <= len1; i++) {
-    Vp[(size_t)i * W2] = 0;
-    tbp[(size_t)i * W2] = 'U';
-  }
-  const int ti_n = (len1 + T - 1) / T, tj_n = (len2 + T - 1) / T;
-  for (int d = 0; d < ti_n + tj_n - 1; d++) {
-    const int lo = std::max(0, d - (tj_n - 1)), hi = std::min(d, ti_n - 1);
-#pragma omp parallel for schedule(static) if (hi - lo >= 2)
-    for (int ti = lo; ti <= hi; ti++) {
-      const int tj = d - ti;
-      const int i0 = 1 + ti * T, i1 = std::min(len1, i0 + T - 1);
-      const int j0 = 1 + tj * T, j1 = std::min(len2, j0 + T - 1);
+  const int nb = (len1 + RB - 1) / RB;
+  std::vector<std::atomic<int>> done(nb + 1);
+  for (auto& d : done) d.store(0, std::memory_order_relaxed);
+  done[0].store(len2 + 1, std::memory_order_relaxed);  // row 0: complete
+  const int T = std::max(1, std::min({omp_get_max_threads(), 16, nb}));
+#pragma omp parallel num_threads(T)
+  {
+    const int t = omp_get_thread_num(), nt = omp_get_num_threads();
+    for (int b = t; b < nb; b += nt) {
+      const int i0 = 1 + b * RB, i1 = std::min(len1, i0 + RB - 1);
       for (int i = i0; i <= i1; i++) {
-        const float* pr = post + (size_t)i * W2;
-        float* cur = Vp + (size_t)i * W2;
-        const float* up = cur - W2;
-        char* t = tbp + (size_t)i * W2;
-        for (int j = j0; j <= j1; j++) {
-          const float x1 = pr[j] + up[j - 1], x2 = cur[j - 1], x3 = up[j];
-          float v;
-          char b;
-          if (x1 >= x2) {
-            if (x1 >= x3) { v = x1; b = 'D'; } else { v = x3; b = 'U'; }
-          } else if (x2 >= x3) {
-            v = x2; b = 'L';
+        Vp[(size_t)i * W2] = 0;
+        tbp[(size_t)i * W2] = 'U';
+      }
+      for (int j0 = 1; j0 <= len2; j0 += CB) {
+        const int j1 = std::min(len2, j0 + CB - 1);
+        // the band above must have finished columns .. j1
+        // spin briefly, then yield: the CPU may be shared (parallel test runs)
+        for (int spins = 0; done[b].load(std::memory_order_acquire) < j1 + 1; spins++) {
+          if (spins < 2000) {
+#if defined(__x86_64__)
+            __builtin_ia32_pause();
+#endif
           } else {
-            v = x3; b = 'U';
+            std::this_thread::yield();
           }
-          cur[j] = v;
-          t[j] = b;
         }
+        for (int i = i0; i <= i1; i++) {
+          const float* pr = post + (size_t)i * W2;
+          float* cur = Vp + (size_t)i * W2;
+          const float* up = cur - W2;
+          char* tr = tbp + (size_t)i * W2;
+          for (int j = j0; j <= j1; j++) {
+            const float x1 = pr[j] + up[j - 1], x2 = cur[j - 1], x3 = up[j];
+            float v;
+            char c;
+            if (x1 >= x2) {
+              if (x1 >= x3) { v = x1; c = 'D'; } else { v = x3; c = 'U'; }
+            } else if (x2 >= x3) {
+              v = x2; c = 'L';
+            } else {
+              v = x3; c = 'U';
+            }
+            cur[j] = v;
+            tr[j] = c;
+          }
+        }
+        done[b + 1].store(j1 + 1, std::memory_order_release);
       }
     }
   }
@@ -426,21 +468,6 @@ std::string mea_path_tiled(int len1, int len2, const float* post, float* score) 
   }
   std::reverse(path.begin(), path.end());
   return path;
-}
-
-std::string mea_path(int len1, int len2, const float* post, float* score) {
-  const double t0 = wall();
-  std::string r = mea_path_dispatch(len1, len2, post, score);
-  g_t_mea += wall() - t0;
-  return r;
-}
-
-std::string mea_path_dispatch(int len1, int len2, const float* post, float* score) {
-  // the tiled form pays ~20 parallel regions per call: only for very large
-  // matrices (measured: 1100 x 1100 on 16 threads of the GPU box is slower
-  // tiled once the thread wake-ups are counted)
-  if ((int64_t)len1 * len2 >= (int64_t)2048 * 2048) return mea_path_tiled(len1, len2, post, score);
-  return mea_path_serial(len1, len2, post, score);
 }
 
 std::string mea_path_serial(int len1, int len2, const float* post, float* score) {

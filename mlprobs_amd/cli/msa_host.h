@@ -97,13 +97,13 @@ bool device_mea(const Profile& a, const Profile& b, const int* weights, float cu
 // ('B', 'X', 'Y') and its score.
 std::string mea_path(int len1, int len2, const std::vector<float>& post, float* score);
 std::string mea_path(int len1, int len2, const float* post, float* score);  // (len1 + 1) x (len2 + 1) row-major
-// the two evaluations mea_path chooses between (tiled: anti-diagonals of
-// 128 x 128 tiles in parallel, for large matrices); identical results
+// the two evaluations mea_path chooses between (wave: threads pipelined
+// over 64-row bands, for large matrices); identical results
 std::string mea_path_serial(int len1, int len2, const float* post, float* score);
 std::string mea_path_dispatch(int len1, int len2, const float* post, float* score);  // untimed
+std::string mea_path_wave(int len1, int len2, const float* post, float* score);  // threads over 64-row bands
 // accumulated seconds of profile posteriors and MEA, calls (MLP_CLI_TIMES)
 void profile_times(double* post, double* mea, int64_t* calls, int64_t* device_calls);
-std::string mea_path_tiled(int len1, int len2, const float* post, float* score);
 
 // Profile merge along a path (Sequence.h AddGaps) and helpers.
 Profile merge(const Profile& a, const Profile& b, const std::string& path, bool sort_by_label);

@@ -333,7 +333,7 @@ Seq add_gaps(const Seq& s, const std::string& path, char id) {
 }
 
 // time split of the host stages (MLP_CLI_TIMES)
-double g_t_post = 0, g_t_mea = 0;
+double g_t_post = 0, g_t_mea = 0, g_t_merge = 0, g_t_update = 0, g_t_split = 0;
 int64_t g_n_terms = 0;
 double now() { return omp_get_wtime(); }
 
@@ -357,12 +357,15 @@ Profile align_alignments(const std::vector<float>& w, const Profile& A, const Pr
     g_t_mea += now() - t1;
   }
   g_n_terms += (int64_t)A.size() * (int64_t)B.size();
-  Profile r;
-  r.reserve(A.size() + B.size());
-  for (const Seq& s : A) r.push_back(add_gaps(s, path, 'X'));
-  for (const Seq& s : B) r.push_back(add_gaps(s, path, 'Y'));
+  const double t2 = now();
+  Profile r(A.size() + B.size());
+  const int na = (int)A.size(), nr = (int)r.size();
+  const int nt = (int64_t)nr * (int64_t)path.size() > 200000 ? std::max(1, threads) : 1;
+#pragma omp parallel for num_threads(nt) schedule(static)
+  for (int k = 0; k < nr; k++) r[k] = k < na ? add_gaps(A[k], path, 'X') : add_gaps(B[k - na], path, 'Y');
   // MultiSequence::SortByLabel (the labels are distinct)
   std::sort(r.begin(), r.end(), [](const Seq& a, const Seq& b) { return a.sort_label < b.sort_label; });
+  g_t_merge += now() - t2;
   return r;
 }
 
@@ -377,28 +380,35 @@ Profile process_tree(const Tree& T, int node, const std::vector<Seq>& seqs, cons
 }
 
 // MultiSequence::extractSubset (QP/Alignment/DataStructures/MultiSequence.cpp:407-464)
-Profile extract_subset(const Profile& aln, const std::set<int>& idx) {
+Profile extract_subset(const Profile& aln, const std::set<int>& idx, int threads) {
   const int L = aln[*idx.begin()].length();
+  const std::vector<int> rows(idx.begin(), idx.end());
+  const int nt = (int64_t)rows.size() * L > 200000 ? std::max(1, threads) : 1;
   std::vector<char> keep(L + 1, 0);
-  for (int i : idx) {
-    const char* d = aln[i].data.data();
-    for (int c = 1; c <= L; c++) keep[c] |= d[c] != '-';
+  // columns not gapped in every selected row (column blocks in parallel)
+#pragma omp parallel for num_threads(nt) schedule(static)
+  for (int c0 = 1; c0 <= L; c0 += 256) {
+    const int c1 = std::min(L, c0 + 255);
+    for (int i : rows) {
+      const char* d = aln[i].data.data();
+      for (int c = c0; c <= c1; c++) keep[c] |= d[c] != '-';
+    }
   }
-  std::vector<int> cols;  // columns not gapped in every selected row
+  std::vector<int> cols;
   for (int c = 1; c <= L; c++)
     if (keep[c]) cols.push_back(c);
-  Profile r;
-  r.reserve(idx.size());
-  for (int i : idx) {
-    Seq s;
-    s.header = aln[i].header;
-    s.sort_label = aln[i].sort_label;
-    s.label = aln[i].label;
+  Profile r(rows.size());
+#pragma omp parallel for num_threads(nt) schedule(static)
+  for (int k = 0; k < (int)rows.size(); k++) {
+    const Seq& src = aln[rows[k]];
+    Seq& s = r[k];
+    s.header = src.header;
+    s.sort_label = src.sort_label;
+    s.label = src.label;
     s.data.resize(cols.size() + 1);
     s.data[0] = '@';
-    const char* d = aln[i].data.data();
-    for (size_t k = 0; k < cols.size(); k++) s.data[k + 1] = d[cols[k]];
-    r.push_back(std::move(s));
+    const char* d = src.data.data();
+    for (size_t q = 0; q < cols.size(); q++) s.data[q + 1] = d[cols[q]];
   }
   return r;
 }
@@ -425,15 +435,20 @@ struct ColumnRefiner {
   // updateColumnScores (ColumnRefinement.cpp:120-174): resize keeps the
   // previous call's (sorted, filtered) entries at the front, and the gap
   // counts are added onto them.
-  void update(const Profile& aln) {
+  void update(const Profile& aln, int threads) {
     const int n = (int)aln.size(), L = aln[0].length();
     scores.resize(L, std::pair<int, float>(0, 0));
     // gap counts per column; adding them at once equals adding 1.0f per gap
-    // (integers below 2^24 are exact in float)
+    // (integers below 2^24 are exact in float); column blocks in parallel
     std::vector<int> gaps(L, 0);
-    for (int i = 0; i < n; i++) {
-      const char* d = aln[i].data.data() + 1;
-      for (int c = 0; c < L; c++) gaps[c] += d[c] == '-';
+    const int nt = (int64_t)n * L > 200000 ? std::max(1, threads) : 1;
+#pragma omp parallel for num_threads(nt) schedule(static)
+    for (int c0 = 0; c0 < L; c0 += 256) {
+      const int c1 = std::min(L, c0 + 256);
+      for (int i = 0; i < n; i++) {
+        const char* d = aln[i].data.data() + 1;
+        for (int c = c0; c < c1; c++) gaps[c] += d[c] == '-';
+      }
     }
     for (int c = 0; c < (int)scores.size(); c++) {
       scores[c].first = c;
@@ -478,11 +493,14 @@ Profile construct_and_refine(const std::vector<Seq>& seqs, const PosteriorBacken
   const int iters = opt.refinement > 0 ? opt.refinement : (n > 200 ? 200 : 30);
   ColumnRefiner cr;
   cr.cfg_iterations = opt.refinement;
-  cr.update(aln);  // initialise (ColumnRefinement.cpp:64-80)
+  cr.update(aln, threads);  // initialise (ColumnRefinement.cpp:64-80)
   const bool prepared = cr.hi() > 0;
   for (int it = 0; it < iters && prepared; it++) {
     // split (ColumnRefinement.cpp:94-118)
-    cr.update(aln);
+    double tu = now();
+    cr.update(aln, threads);
+    g_t_update += now() - tu;
+    tu = now();
     const int hi = cr.hi();
     if (hi <= 0) continue;
     const int rnd = det_uniform(cr.engine, 0, hi - 1);
@@ -490,13 +508,16 @@ Profile construct_and_refine(const std::vector<Seq>& seqs, const PosteriorBacken
     std::set<int> g1, g2;
     for (int i = 0; i < n; i++) (aln[i].data[col + 1] == '-' ? g1 : g2).insert(i);
     if (g1.empty() || g2.empty()) continue;
-    const Profile p1 = extract_subset(aln, g1), p2 = extract_subset(aln, g2);
+    const Profile p1 = extract_subset(aln, g1, threads), p2 = extract_subset(aln, g2, threads);
+    g_t_split += now() - tu;
     Profile cand = align_alignments(w, p1, p2, be, post, threads);
     if (aln[0].length() >= cand[0].length()) aln = std::move(cand);  // checkAcceptance (length)
   }
   if (getenv("MLP_CLI_TIMES"))
-    fprintf(stderr, "[host] profile posteriors %.3f s (%lld sequence pairs), MEA %.3f s, %d refinement passes\n",
-            g_t_post, (long long)g_n_terms, g_t_mea, iters);
+    fprintf(stderr,
+            "[host] profile posteriors %.3f s (%lld sequence pairs), MEA %.3f s, merges %.3f s, column scores "
+            "%.3f s, splits %.3f s, %d refinement passes\n",
+            g_t_post, (long long)g_n_terms, g_t_mea, g_t_merge, g_t_update, g_t_split, iters);
   return aln;
 }
 

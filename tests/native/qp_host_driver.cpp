@@ -27,7 +27,7 @@ static void rd(FILE* f, T* p, size_t n) {
 
 int main(int argc, char** argv) {
   if (argc < 3) return 2;
-  if (!strcmp(argv[1], "mea") && argc == 5) {  // tiled vs serial MEA on a random matrix
+  if (!strcmp(argv[1], "mea") && argc == 5) {  // threaded (wave) vs serial MEA on a random matrix
     const int L1 = atoi(argv[3]), L2 = atoi(argv[4]);
     std::mt19937 g((unsigned)atoi(argv[2]));
     std::uniform_real_distribution<float> u(0.f, 1.f);
@@ -35,7 +35,7 @@ int main(int argc, char** argv) {
     for (float& x : post) x = u(g) < 0.9f ? 0.f : u(g);  // sparse-ish, with ties
     float s1 = 0, s2 = 0;
     const std::string a = cpnp::mea_path_serial(L1, L2, post.data(), &s1);
-    const std::string b = cpnp::mea_path_tiled(L1, L2, post.data(), &s2);
+    const std::string b = cpnp::mea_path_wave(L1, L2, post.data(), &s2);
     printf("%s\n", (a == b && s1 == s2) ? "same" : "DIFF");
     return 0;
   }

@@ -109,8 +109,9 @@ def test_quickprobs_host_vs_reference_cli(qdriver, tmp_path, name, args):
 
 
 @pytest.mark.parametrize('seed,L1,L2', [(1, 700, 650), (2, 129, 2100), (3, 1500, 257)])
-def test_mea_tiled_equals_serial(qdriver, seed, L1, L2):
-    """The tiled parallel MEA (large profiles) against the serial recurrence
-    (ProbabilisticModel::computeAlignment): same path and score."""
+def test_mea_wave_equals_serial(qdriver, seed, L1, L2):
+    """The threaded MEA (bands of 64 rows pipelined over threads, for large
+    profiles) against the serial recurrence (ProbabilisticModel::
+    computeAlignment): same path and score."""
     out = subprocess.run([qdriver, 'mea', str(seed), str(L1), str(L2)], capture_output=True, text=True, check=True)
     assert out.stdout.strip() == 'same'
