@@ -95,6 +95,11 @@ static void check(mlp_ctx* ctx, int rc, const char* what) {
 }
 
 int main(int argc, char** argv) {
+  // idle OpenMP threads sleep instead of spinning between the short parallel
+  // regions of the host stages: spinning threads burn a CPU quota the
+  // serial stages in between need (a cgroup-limited host throttles the
+  // whole process).  An explicit setting in the environment wins.
+  setenv("OMP_WAIT_POLICY", "passive", 0);
   stage(nullptr);  // start the stage clock
   if (argc < 2) {
     usage();

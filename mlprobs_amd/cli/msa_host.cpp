@@ -520,48 +520,57 @@ static Row add_gaps(const Row& r, const std::string& path, char id) {   // Seque
   o.header = r.header;
   o.label = r.label;
   o.sort_label = r.sort_label;
-  o.data.reserve(path.size() + 1);
-  o.data = "@";
-  size_t k = 1;
-  for (char c : path) {
-    if (c == 'B' || c == id) o.data += r.data[k++];
-    else o.data += '-';
-  }
+  o.data.assign(path.size() + 1, '-');
+  o.data[0] = '@';
+  const char* src = r.data.data() + 1;
+  char* dst = &o.data[1];
+  for (size_t c = 0; c < path.size(); c++)
+    if (path[c] == 'B' || path[c] == id) dst[c] = *src++;
   return o;
 }
 
+// threads for a profile of n rows x L columns (data movement only; small
+// profiles stay serial)
+static int row_threads(size_t n, size_t L) { return n * L > 200000 ? std::max(1, std::min(16, omp_get_max_threads())) : 1; }
+
 Profile merge(const Profile& a, const Profile& b, const std::string& path, bool sort_by_label) {
-  Profile out;
-  out.reserve(a.size() + b.size());
-  for (const Row& r : a) out.push_back(add_gaps(r, path, 'X'));
-  for (const Row& r : b) out.push_back(add_gaps(r, path, 'Y'));
-  if (sort_by_label) {   // MultiSequence::SortByLabel: O(n^2) swap sort
-    for (size_t i = 0; i + 1 < out.size(); i++)
-      for (size_t j = i + 1; j < out.size(); j++)
-        if (out[i].sort_label > out[j].sort_label) std::swap(out[i], out[j]);
-  }
+  const int na = (int)a.size(), nr = (int)(a.size() + b.size());
+  Profile out(nr);
+#pragma omp parallel for num_threads(row_threads(nr, path.size())) schedule(static)
+  for (int k = 0; k < nr; k++) out[k] = k < na ? add_gaps(a[k], path, 'X') : add_gaps(b[k - na], path, 'Y');
+  // MultiSequence::SortByLabel (a swap sort; the labels are distinct, so any
+  // sort gives its order)
+  if (sort_by_label)
+    std::sort(out.begin(), out.end(), [](const Row& x, const Row& y) { return x.sort_label < y.sort_label; });
   return out;
 }
-
-// MultiSequence::Project (MultiSequence.h:662-734)
 Profile project(const Profile& p, const std::set<int>& idx) {
-  const int L = p[*idx.begin()].length();
-  std::vector<int> keep;
-  for (int i = 1; i <= L; i++) {
-    bool found = false;
-    for (int k : idx)
-      if (p[k].data[i] != '-') { found = true; break; }
-    if (found) keep.push_back(i);
+  const std::vector<int> rows(idx.begin(), idx.end());
+  const int L = p[rows[0]].length();
+  const int nt = row_threads(rows.size(), (size_t)L);
+  std::vector<char> has(L + 1, 0);
+#pragma omp parallel for num_threads(nt) schedule(static)
+  for (int c0 = 1; c0 <= L; c0 += 256) {
+    const int c1 = std::min(L, c0 + 255);
+    for (int k : rows) {
+      const char* d = p[k].data.data();
+      for (int i = c0; i <= c1; i++) has[i] |= d[i] != '-';
+    }
   }
-  Profile out;
-  for (int k : idx) {
-    Row r;
-    r.header = p[k].header;
-    r.label = p[k].label;
-    r.sort_label = p[k].sort_label;
-    r.data = "@";
-    for (int i : keep) r.data += p[k].data[i];
-    out.push_back(std::move(r));
+  std::vector<int> keep;
+  for (int i = 1; i <= L; i++)
+    if (has[i]) keep.push_back(i);
+  Profile out(rows.size());
+#pragma omp parallel for num_threads(nt) schedule(static)
+  for (int q = 0; q < (int)rows.size(); q++) {
+    const Row& src = p[rows[q]];
+    Row& r = out[q];
+    r.header = src.header;
+    r.label = src.label;
+    r.sort_label = src.sort_label;
+    r.data.resize(keep.size() + 1);
+    r.data[0] = '@';
+    for (size_t c = 0; c < keep.size(); c++) r.data[c + 1] = src.data[keep[c]];
   }
   return out;
 }

@@ -90,6 +90,11 @@ static bool parse_int(const std::string& s, long long* v) {
 }
 
 int main(int argc, char** argv) {
+  // idle OpenMP threads sleep instead of spinning between the short parallel
+  // regions of the host stages: spinning threads burn a CPU quota the
+  // serial stages in between need (a cgroup-limited host throttles the
+  // whole process).  An explicit setting in the environment wins.
+  setenv("OMP_WAIT_POLICY", "passive", 0);
   stage(nullptr);  // start the stage clock
   std::vector<std::string> args(argv + 1, argv + argc), rest;
   std::string outname;
