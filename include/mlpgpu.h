@@ -65,8 +65,10 @@ int mlp_ctx_is_host(const mlp_ctx *ctx);
  * posteriors balanced by DP cells (mlp_shard_plan), consistency rounds by
  * estimated multiply-adds (mlp_relax_shard_plan); the shards' sparse sets are
  * gathered over xGMI (peer copies) into this context's store, and the whole
- * store goes back to every shard before each relaxation round.  Results are
- * bit-identical to one device.  Everything else runs on the first device. */
+ * store goes back to every shard before each relaxation round.  With 2-4
+ * virtual shards on one GPU the results are bit-identical to one device
+ * (tests/test_gpu_shards.py); runs over several physical GPUs are untested
+ * (no multi-GPU box here).  Everything else runs on the first device. */
 int mlp_ctx_create_mask(uint64_t device_mask, mlp_ctx **out);
 /* Number of shards (0: one per device of the mask when the family is large
  * enough; k > 0: always k, spread round-robin over the mask's devices --

@@ -2185,6 +2185,17 @@ static int relax_one(mlp_ctx* c, const QpRelax& qp, bool last) {
   }
   const int64_t nout = r1 - r0;
   int rc;
+  // MLP_RELAX_LOG=1: wall time of the round's phases on stderr (each mark
+  // drains the stream first, so the phases do not overlap while logging)
+  static const bool rlog = getenv("MLP_RELAX_LOG") != nullptr;
+  auto rl_t = std::chrono::steady_clock::now();
+  auto mark = [&](const char* what) {
+    if (!rlog) return;
+    hipStreamSynchronize(c->stream);
+    const auto t = std::chrono::steady_clock::now();
+    fprintf(stderr, "[relax] %-22s %8.2f ms\n", what, std::chrono::duration<double, std::milli>(t - rl_t).count());
+    rl_t = t;
+  };
   {
     const int64_t total = c->store_total;
     if ((rc = ensure(c, c->r_trowptr, sizeof(int32_t) * c->trp_off[c->P]))) return rc;
@@ -2199,6 +2210,7 @@ static int relax_one(mlp_ctx* c, const QpRelax& qp, bool last) {
     std::vector<int64_t> allp(c->P);
     std::iota(allp.begin(), allp.end(), 0);
     HIPCHK(c, hipMemcpyAsync(c->r_pairs.p, allp.data(), sizeof(int64_t) * c->P, hipMemcpyHostToDevice, c->stream));
+    mark("buffers");
     TransposeArgs ta;
     ta.n = c->n;
     ta.lens = c->d_len;
@@ -2218,6 +2230,7 @@ static int relax_one(mlp_ctx* c, const QpRelax& qp, bool last) {
       Timer t(c, KTRANS, total);
       HIPCHK(c, launch_transpose(ta, c->stream));
     }
+    mark("transpose");
     // Tiled path (k_relax_tile) for every output pair whose blocks fit the
     // LDS tile; the row-task kernel for the rest (MLP_RELAX=tasks: all).
     int64_t LDS_MAX = 160 * 1024 / kRelaxGroupsPerCU;
@@ -2254,6 +2267,7 @@ static int relax_one(mlp_ctx* c, const QpRelax& qp, bool last) {
                                c->stream));
       HIPCHK(c, hipStreamSynchronize(c->stream));
     }
+    mark("pack count");
     // record offsets; per sequence the largest image with its residues as
     // rows (the A_t = P(x, .) and C = P(y, .) roles)
     std::vector<int64_t> img_off(2 * c->P + 1, 0), maxI(c->n, 0);
@@ -2395,6 +2409,7 @@ static int relax_one(mlp_ctx* c, const QpRelax& qp, bool last) {
         });
       for (auto& t : th) t.join();
     }
+    mark("plan");
     // per class: tiles ordered by (first x, y) for the XCD-aware grid order
     std::vector<int32_t> tiles;
     std::vector<int64_t> tp;
@@ -2435,6 +2450,7 @@ static int relax_one(mlp_ctx* c, const QpRelax& qp, bool last) {
       Timer t(c, KTRANS, total);
       HIPCHK(c, launch_pack(pk, c->stream));
     }
+    mark("order, images");
     const int64_t nt = (int64_t)tp.size();
     if (getenv("MLP_PLAN_LOG")) {
       int64_t mx = 0;
@@ -2510,6 +2526,7 @@ static int relax_one(mlp_ctx* c, const QpRelax& qp, bool last) {
         HIPCHK(c, hipStreamWaitEvent(c->stream, c->side.join, 0));
       }
     }
+    mark("relax kernels");
     // filter: count, host scan, write
     std::vector<int64_t> outp(nout);
     std::iota(outp.begin(), outp.end(), r0);
@@ -2551,6 +2568,7 @@ static int relax_one(mlp_ctx* c, const QpRelax& qp, bool last) {
     if ((rc = ensure(c, c->r_newcols, sizeof(uint16_t) * std::max<int64_t>(run, 1)))) return rc;
     if ((rc = ensure(c, c->r_newvals, sizeof(float) * std::max<int64_t>(run, 1)))) return rc;
     HIPCHK(c, hipMemcpyAsync(c->r_newoff.p, noff.data(), sizeof(int64_t) * (c->P + 1), hipMemcpyHostToDevice, c->stream));
+    mark("filter count, scan");
     fa.new_cols = (uint16_t*)c->r_newcols.p;
     fa.new_vals = (float*)c->r_newvals.p;
     fa.write = 1;
@@ -2577,6 +2595,7 @@ static int relax_one(mlp_ctx* c, const QpRelax& qp, bool last) {
     c->store_total = run; ++c->store_ver;
     HIPCHK(c, hipMemcpyAsync(c->d_ent_off, c->ent_off.data(), sizeof(int64_t) * (c->P + 1), hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    mark("filter write, swap");
   }
   return MLP_OK;
 }
