@@ -2295,11 +2295,20 @@ static int relax_one(mlp_ctx* c, const QpRelax& qp, bool last) {
     const int64_t budget = std::min<int64_t>(LDS_MAX - zs, tile_relax_max_cap()) & ~(int64_t)15;
     int64_t small_budget = std::min<int64_t>(budget, (80 * 1024 - zs) & ~(int64_t)15);
     if (LDS_MAX < 160 * 1024 || getenv("MLP_RELAX_ONECLASS")) small_budget = 0;  // tuning hooks
+    if (const char* e = getenv("MLP_RELAX_SMALL_KB"))  // test hook: a small staging area for the small class
+      small_budget = std::min(budget, std::max<int64_t>(64, (int64_t)atoi(e) * 1024 - zs)) & ~(int64_t)15;
     const int n = c->n;
     const bool exact = !tasks_only && n <= 2048;
     const int64_t kSmallCells = 8 * (int64_t)kRelaxThreads;  // 8 slots: the 64-VGPR budget of 8 waves per SIMD
     // z's per tile whose images may exceed the staging area (staged in passes)
     const int max_over = getenv("MLP_RELAX_SPLIT_Z") ? atoi(getenv("MLP_RELAX_SPLIT_Z")) : n / 16;
+    // z's on which a small-class output's image may not fit beside C even
+    // alone (the kernel reads that image in place from HBM on those z's);
+    // 0: such outputs go to the one-workgroup class.  No limit by default: at
+    // C3 round 1 every output has such z's, and the small class with images
+    // read in place runs 1.32 s against 1.60 s for the one-workgroup class
+    // (limits of 8 / 32 z's: 1.60 / 1.55 s)
+    const int max_glob = getenv("MLP_RELAX_GLOBAL_Z") ? atoi(getenv("MLP_RELAX_GLOBAL_Z")) : n;
     std::vector<int32_t> isz;  // image bytes of P(s, z), s's residues as rows: isz[s * n + z]
     if (exact) {
       isz.assign((size_t)n * n, 0);
@@ -2317,6 +2326,7 @@ static int relax_one(mlp_ctx* c, const QpRelax& qp, bool last) {
       std::vector<int32_t> tr;
     };
     std::vector<YPlan> yplans(n);
+    std::atomic<int64_t> n_hbm_outputs{0};  // small-class outputs whose image is read from HBM on some z
     auto plan_y = [&](int yy) {
       YPlan& Y = yplans[yy];
       struct Cur {
@@ -2360,11 +2370,28 @@ static int relax_one(mlp_ctx* c, const QpRelax& qp, bool last) {
         if (nz == 0) continue;  // empty mask: the filter writes an empty block
         int k = -1;
         int64_t alone = 0;
+        int alone_over = 0;  // small class: z's where the output alone exceeds the staging area
         if (!tasks_only && !big[x] && !big[yy] && tile_relax_slots(nz)) {
           const Cur empty{};
           int unused;
           alone = need_with(empty, x, budget, &unused);
           k = alone <= small_budget && nz <= kSmallCells ? 0 : alone <= budget ? 1 : -1;
+          if (k == 1 && exact && max_glob > 0 && small_budget > 0 && nz <= kSmallCells) {
+            // the small class (two workgroups per CU) if C fits on every z and
+            // the output's own image fits beside it on all but a few
+            const int32_t* ix = &isz[(size_t)x * n];
+            int ov = 0;
+            bool cfits = true;
+            for (int z = 0; z < n && cfits; z++) {
+              cfits = iy[z] <= small_budget;
+              ov += (int64_t)iy[z] + ix[z] > small_budget;
+            }
+            if (cfits && ov <= max_glob) {
+              k = 0;
+              alone_over = ov;
+              if (ov) n_hbm_outputs.fetch_add(1, std::memory_order_relaxed);
+            }
+          }
         }
         if (k < 0) {
           for (int g = 1; g <= c->lens[x]; g += 64) {
@@ -2376,13 +2403,13 @@ static int relax_one(mlp_ctx* c, const QpRelax& qp, bool last) {
         Cur& t = cur[k];
         // a tile may exceed its staging area on a few z's (outliers: the
         // kernel stages those z's outputs in passes), never on one output
-        int over = 0;
+        int over = alone_over;
         int64_t nd = t.cnt ? need_with(t, x, lim[k], &over) : alone;
         if (t.cnt && (t.cnt == tmax || (exact ? over > max_over : nd > lim[k]) ||
                       !tile_relax_slots(t.cells + nz) || (k == 0 && t.cells + nz > kSmallCells))) {
           flush(k);
           nd = alone;
-          over = 0;
+          over = alone_over;
         }
         if (exact) {
           const int32_t* ix = &isz[(size_t)x * n];
@@ -2415,14 +2442,26 @@ static int relax_one(mlp_ctx* c, const QpRelax& qp, bool last) {
     std::vector<int64_t> tp;
     std::vector<int32_t> tr;
     int64_t cls_tiles[2] = {0, 0}, cls_cap[2] = {0, 0}, cls_cells[2] = {0, 0};
+    // the small class in two launches: tiles of at most 4 cells per thread
+    // first (fewer registers and no idle slots), then the rest
+    const int64_t kFewCells = 4 * (int64_t)kRelaxThreads;
+    int64_t few_tiles = 0, few_cells = 0;
     for (int k = 0; k < 2; k++) {
       std::vector<std::pair<int, const TileRec*>> order;  // (y, record)
       for (int yy = 1; yy < n; yy++)
         for (const TileRec& r : yplans[yy].recs)
           if (r.cls == k) order.push_back({yy, &r});
-      std::stable_sort(order.begin(), order.end(), [](const auto& u, const auto& v) {
+      std::stable_sort(order.begin(), order.end(), [&](const auto& u, const auto& v) {
+        if (k == 0 && (u.second->cells <= kFewCells) != (v.second->cells <= kFewCells))
+          return u.second->cells <= kFewCells;
         return u.second->x0 != v.second->x0 ? u.second->x0 < v.second->x0 : u.first < v.first;
       });
+      if (k == 0)
+        for (const auto& o : order)
+          if (o.second->cells <= kFewCells) {
+            ++few_tiles;
+            few_cells = std::max(few_cells, o.second->cells);
+          }
       for (const auto& o : order) {
         const std::vector<int32_t>& src = yplans[o.first].ints;
         tiles.insert(tiles.end(), src.begin() + o.second->first, src.begin() + o.second->first + kTileInts);
@@ -2457,10 +2496,10 @@ static int relax_one(mlp_ctx* c, const QpRelax& qp, bool last) {
       for (int i = 0; i < c->n; i++) mx = std::max(mx, maxI[i]);
       fprintf(stderr,
               "relax plan: tiles %lld (cap %lld, cells %lld) + %lld (cap %lld, cells %lld) row tasks %lld budget %lld/%lld "
-              "max image %lld\n",
+              "max image %lld hbm-image outputs %lld\n",
               (long long)cls_tiles[0], (long long)cls_cap[0], (long long)cls_cells[0], (long long)cls_tiles[1],
               (long long)cls_cap[1], (long long)cls_cells[1], (long long)nt, (long long)small_budget, (long long)budget,
-              (long long)mx);
+              (long long)mx, (long long)n_hbm_outputs.load());
     }
     if (mode && !strcmp(mode, "pairs") && nt) {  // test hook: the pair-resident path must cover all
       c->err = "MLP_RELAX=pairs: " + std::to_string(nt) + " row tasks fell back";
@@ -2519,7 +2558,14 @@ static int relax_one(mlp_ctx* c, const QpRelax& qp, bool last) {
       }
       if (cls_tiles[1])
         HIPCHK(c, launch_relax_tiles(pc[1], tile_relax_slots(cls_cells[1]), fork ? c->side.st : c->stream));
-      if (cls_tiles[0]) HIPCHK(c, launch_relax_tiles(pc[0], tile_relax_slots(cls_cells[0]), c->stream));
+      if (cls_tiles[0]) {
+        TileRelaxArgs a = pc[0], b = pc[0];
+        a.ntiles = few_tiles;
+        b.tiles += few_tiles * kTileInts;
+        b.ntiles = cls_tiles[0] - few_tiles;
+        HIPCHK(c, launch_relax_tiles(a, tile_relax_slots(few_cells), c->stream));
+        HIPCHK(c, launch_relax_tiles(b, tile_relax_slots(cls_cells[0]), c->stream));
+      }
       HIPCHK(c, launch_relax_tasks(ra, c->stream));
       if (fork) {
         HIPCHK(c, hipEventRecord(c->side.join, c->side.st));

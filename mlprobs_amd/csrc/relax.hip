@@ -327,7 +327,7 @@ constexpr int kRelaxZChunk = 128;  // z schedule entries per LDS fill (64 B each
 constexpr int kZEntBytes = 64;
 // LDS: [z schedule][QuickProbs z weights][per-output A bases, weights, weight sums][tile]
 static __host__ __device__ inline size_t relax_tile_off() {
-  return (size_t)kZEntBytes * kRelaxZChunk + 16 * kRelaxZChunk + 16 * kTileMax + 16 + 16 + 16;
+  return (size_t)kZEntBytes * kRelaxZChunk + 16 * kRelaxZChunk + 16 * kTileMax + 16 + 16 + 16 + 8 * kTileMax;
 }
 size_t tile_relax_lds(int cap) { return relax_tile_off() + (size_t)cap + 16; }  // + a word pair read past the last row
 
@@ -390,6 +390,7 @@ __global__ __launch_bounds__(kRelaxThreads, KP == 5 && kRelaxThreads == 1024 ? 8
   float* zw = (float*)(zb + TM);  // per output: this z's weight
   float* zsum = zw + 4;           // per output: 1 + sum of the weights so far (z ascending)
   float* wxy = zsum + 4;          // per output: QuickProbs' W_{x_t y} (ConsistencyStage.cpp:199-203)
+  const uint8_t** gptr = (const uint8_t**)(wxy + 4);  // per output: its image in HBM (read in place this z)
   uint8_t* tileb = lds + relax_tile_off();
   if constexpr (QP) {  // accepted z per output (A_xy)
     int* nacc = (int*)wxy;
@@ -493,15 +494,21 @@ __global__ __launch_bounds__(kRelaxThreads, KP == 5 && kRelaxThreads == 1024 ? 8
           }
           if (any) {
             // outputs in passes over this z when their images and C exceed
-            // the staging area (greedy in output order; the host keeps each
-            // output with C within it): pass of output t in bits 2t, 2t+1,
-            // passes - 1 in bits 8-9 of e0.w
+            // the staging area (greedy in output order): pass of output t in
+            // bits 2t, 2t+1, passes - 1 in bits 8-9 of e0.w; an output whose
+            // image does not fit beside C even alone is not staged (bit 12 + t:
+            // its cells read the image from HBM; small-class tiles only)
             const uint32_t cC = (uint32_t)((A.img_off[qc + 1] - A.img_off[qc]) >> 4);
             const uint32_t capc = (uint32_t)A.cap >> 4;
-            uint32_t used = cC, grp = 0, gsel = 0;
+            uint32_t used = cC, grp = 0, gsel = 0, gmask = 0;
 #pragma unroll
             for (int t = 0; t < TM; ++t) {
               if (na[t] == 0) continue;
+              if (cC + ac[t] > capc) {  // not staged: its cells read the image in HBM (pass 0)
+                gmask |= 1u << t;
+                ac[t] = 0;
+                continue;
+              }
               if (used + ac[t] > capc && used > cC) {
                 ++grp;
                 used = cC;
@@ -509,7 +516,7 @@ __global__ __launch_bounds__(kRelaxThreads, KP == 5 && kRelaxThreads == 1024 ? 8
               used += ac[t];
               gsel |= grp << (2 * t);
             }
-            e0 = make_uint4((uint32_t)(A.img_off[qc] >> 4), (uint32_t)nzc, cC, gsel | grp << 8);
+            e0 = make_uint4((uint32_t)(A.img_off[qc] >> 4), (uint32_t)nzc, cC, gsel | grp << 8 | gmask << 12);
             e1 = make_uint4(ao[0], ao[1], ao[2], ao[3]);
             e2 = make_uint4(na[0], na[1], na[2], na[3]);
             e3 = make_uint4(ac[0], ac[1], ac[2], ac[3]);
@@ -565,7 +572,7 @@ __global__ __launch_bounds__(kRelaxThreads, KP == 5 && kRelaxThreads == 1024 ? 8
         nAo = rfl(ztab[4 * zpos + 1]);
         nNa = rfl(ztab[4 * zpos + 2]);
         nAc = rfl(ztab[4 * zpos + 3]);
-        if (nC.w >> 8) {  // keep this pass's outputs only
+        if ((nC.w >> 8) & 3) {  // keep this pass's outputs only
           const uint32_t g = nC.w;
           const uint32_t p = (uint32_t)zpass;
           if (((g >> 0) & 3) != p) { nNa.x = 0; nAc.x = 0; }
@@ -638,15 +645,20 @@ __global__ __launch_bounds__(kRelaxThreads, KP == 5 && kRelaxThreads == 1024 ? 8
     }
     const uint32_t cbase = (uint32_t)(relax_tile_off() + 16 * (size_t)sg[TM]);
     const int nzC = (int)nC.y;
+    const uint32_t gmz = (nC.w >> 12) & 15;  // this z's outputs read in HBM
     if (tid == 0) {
       zw[0] = nW.x; zw[1] = nW.y; zw[2] = nW.z; zw[3] = nW.w;
       const uint32_t na_[TM] = {nNa.x, nNa.y, nNa.z, nNa.w};
+      const uint32_t ao_[TM] = {nAo.x, nAo.y, nAo.z, nAo.w};
 #pragma unroll
       for (int t = 0; t < TM; ++t) {
-        const uint32_t ab = (uint32_t)(relax_tile_off() + 16 * (size_t)sg[t]);
+        // in HBM (bit 12 + t): offsets from the image's own start
+        const bool g = (nC.w >> (12 + t)) & 1;
+        const uint32_t ab = g ? 0u : (uint32_t)(relax_tile_off() + 16 * (size_t)sg[t]);
         const uint32_t ho = ab + (uint32_t)mlp_align16(4 * (int64_t)na_[t]);
         zb[t] = make_int4((int)ab, (int)ho, (int)(ho + (uint32_t)mlp_align16(4 * (int64_t)(Lxt[t] + 1))),
                           (int)na_[t]);
+        gptr[t] = A.img + 16 * (uint64_t)ao_[t];
       }
     }
 #ifdef MLP_RELAX_TIMING
@@ -669,70 +681,80 @@ __global__ __launch_bounds__(kRelaxThreads, KP == 5 && kRelaxThreads == 1024 ? 8
     const uint64_t tc0 = clock64();
 #endif
 #ifndef MLP_RELAX_NOCOMPUTE  // (timing experiment: staging only)
-    {
-      const float* Cvals = (const float*)(lds + cbase);
-      const uint32_t* Chdr = (const uint32_t*)(lds + cbase + (uint32_t)mlp_align16(4 * (int64_t)nzC));
-      const uint2* Cwords = (const uint2*)((const uint8_t*)Chdr + (uint32_t)mlp_align16(4 * (int64_t)(Ly + 1)));
-      // row headers of slot s + 1 are read while slot s intersects
-      auto headers = [&](uint32_t cl, int4& z4, uint32_t& ha, uint32_t& hc) {
-        z4 = zb[cl >> 26];
-        ha = z4.w ? ((const uint32_t*)(lds + z4.y))[cl & 0x1fff] : 0u;  // nw 0: no words
-        hc = Chdr[(cl >> 13) & 0x1fff];
-      };
-      uint32_t cl = cel[0];
-      asm volatile("" : "+v"(cl));
-      int4 z4;
-      uint32_t ha, hc;
-      headers(cl, z4, ha, hc);
-#pragma unroll
-      for (int s = 0; s < SL; ++s) {
-        uint32_t cl1 = 0, ha1 = 0, hc1 = 0;
-        int4 z41 = make_int4(0, 0, 0, 0);
-        if (s + 1 < SL) {
-          cl1 = cel[s + 1];
-          // re-derive the cells' offsets every z: hoisting them out of the z
-          // loop would hold ~4 more registers per slot
-          asm volatile("" : "+v"(cl1));
-          headers(cl1, z41, ha1, hc1);
-        }
-        if (cl != 0) {
-          const int a0 = (int)((ha >> 16) & 0xff), c0 = (int)((hc >> 16) & 0xff);
-          const int we = min(a0 + (int)(ha >> 24), c0 + (int)(hc >> 24));
-          const uint2* pa = (const uint2*)(lds + z4.z) + ((int)(ha & 0xffff) - a0);
-          const uint2* pc = Cwords + ((int)(hc & 0xffff) - c0);
-          const float* Avals = (const float*)(lds + z4.x);
-          const float wk = QP ? zw[cl >> 26] : 1.0f;  // weight * XZ * ZY (ConsistencyStage.cpp:284)
-          float ac = acc[s];
-          // two words per step (the second masked off past the overlap)
-          for (int w = max(a0, c0); w < we; w += 2) {
-            const uint2 xa0 = pa[w], xa1 = pa[w + 1], xc0 = pc[w], xc1 = pc[w + 1];
-            uint32_t m0 = xa0.x & xc0.x;
-            uint32_t m1 = w + 1 < we ? xa1.x & xc1.x : 0u;
-            while (m0) {  // common columns k, ascending
-              const uint32_t bit = 1u << __builtin_ctz(m0);
-              m0 ^= bit;
-              const float va = QP ? wk * Avals[xa0.y + __popc(xa0.x & (bit - 1u))]
-                                  : Avals[xa0.y + __popc(xa0.x & (bit - 1u))];
-              const float vc = Cvals[xc0.y + __popc(xc0.x & (bit - 1u))];
-              ac += va * vc;
-            }
-            while (m1) {
-              const uint32_t bit = 1u << __builtin_ctz(m1);
-              m1 ^= bit;
-              const float va = QP ? wk * Avals[xa1.y + __popc(xa1.x & (bit - 1u))]
-                                  : Avals[xa1.y + __popc(xa1.x & (bit - 1u))];
-              const float vc = Cvals[xc1.y + __popc(xc1.x & (bit - 1u))];
-              ac += va * vc;
-            }
-          }
-          acc[s] = ac;
-        }
-        cl = cl1;
-        z4 = z41;
-        ha = ha1;
-        hc = hc1;
-      }
+    // the cell loop, twice: with every image in LDS, and (GA) for a z where
+    // some output image is read in place from HBM (generic loads)
+#define MLP_CELLS(GA) \
+    {                                                                                                            \
+      const float* Cvals = (const float*)(lds + cbase);                                                          \
+      const uint32_t* Chdr = (const uint32_t*)(lds + cbase + (uint32_t)mlp_align16(4 * (int64_t)nzC));           \
+      const uint2* Cwords = (const uint2*)((const uint8_t*)Chdr + (uint32_t)mlp_align16(4 * (int64_t)(Ly + 1))); \
+      /* row headers of slot s + 1 are read while slot s intersects */                                           \
+      /* GA: outputs of this z may be read in HBM (generic pointers) */                                          \
+      auto headers = [&](uint32_t cl, int4& z4, uint32_t& ha, uint32_t& hc, const uint8_t*& ab) {                \
+        z4 = zb[cl >> 26];                                                                                       \
+        ab = (GA) && ((gmz >> (cl >> 26)) & 1) ? gptr[cl >> 26] : (const uint8_t*)lds;                           \
+        ha = z4.w ? ((const uint32_t*)(ab + z4.y))[cl & 0x1fff] : 0u;  /* nw 0: no words */                      \
+        hc = Chdr[(cl >> 13) & 0x1fff];                                                                          \
+      };                                                                                                         \
+      uint32_t cl = cel[0];                                                                                      \
+      asm volatile("" : "+v"(cl));                                                                               \
+      int4 z4;                                                                                                   \
+      uint32_t ha, hc;                                                                                           \
+      const uint8_t* ab;                                                                                         \
+      headers(cl, z4, ha, hc, ab);                                                                               \
+_Pragma("unroll")                                                                                         \
+      for (int s = 0; s < SL; ++s) {                                                                             \
+        uint32_t cl1 = 0, ha1 = 0, hc1 = 0;                                                                      \
+        int4 z41 = make_int4(0, 0, 0, 0);                                                                        \
+        const uint8_t* ab1 = lds;                                                                                \
+        if (s + 1 < SL) {                                                                                        \
+          cl1 = cel[s + 1];                                                                                      \
+          /* re-derive the cells' offsets every z: hoisting them out of the z */                                 \
+          /* loop would hold ~4 more registers per slot */                                                       \
+          asm volatile("" : "+v"(cl1));                                                                          \
+          headers(cl1, z41, ha1, hc1, ab1);                                                                      \
+        }                                                                                                        \
+        if (cl != 0) {                                                                                           \
+          const int a0 = (int)((ha >> 16) & 0xff), c0 = (int)((hc >> 16) & 0xff);                                \
+          const int we = min(a0 + (int)(ha >> 24), c0 + (int)(hc >> 24));                                        \
+          const uint2* pa = (const uint2*)(ab + z4.z) + ((int)(ha & 0xffff) - a0);                               \
+          const uint2* pc = Cwords + ((int)(hc & 0xffff) - c0);                                                  \
+          const float* Avals = (const float*)(ab + z4.x);                                                        \
+          const float wk = QP ? zw[cl >> 26] : 1.0f;  /* weight * XZ * ZY (ConsistencyStage.cpp:284) */          \
+          float ac = acc[s];                                                                                     \
+          /* two words per step (the second masked off past the overlap) */                                      \
+          for (int w = max(a0, c0); w < we; w += 2) {                                                            \
+            const uint2 xa0 = pa[w], xa1 = pa[w + 1], xc0 = pc[w], xc1 = pc[w + 1];                              \
+            uint32_t m0 = xa0.x & xc0.x;                                                                         \
+            uint32_t m1 = w + 1 < we ? xa1.x & xc1.x : 0u;                                                       \
+            while (m0) {  /* common columns k, ascending */                                                      \
+              const uint32_t bit = 1u << __builtin_ctz(m0);                                                      \
+              m0 ^= bit;                                                                                         \
+              const float va = QP ? wk * Avals[xa0.y + __popc(xa0.x & (bit - 1u))]                               \
+                                  : Avals[xa0.y + __popc(xa0.x & (bit - 1u))];                                   \
+              const float vc = Cvals[xc0.y + __popc(xc0.x & (bit - 1u))];                                        \
+              ac += va * vc;                                                                                     \
+            }                                                                                                    \
+            while (m1) {                                                                                         \
+              const uint32_t bit = 1u << __builtin_ctz(m1);                                                      \
+              m1 ^= bit;                                                                                         \
+              const float va = QP ? wk * Avals[xa1.y + __popc(xa1.x & (bit - 1u))]                               \
+                                  : Avals[xa1.y + __popc(xa1.x & (bit - 1u))];                                   \
+              const float vc = Cvals[xc1.y + __popc(xc1.x & (bit - 1u))];                                        \
+              ac += va * vc;                                                                                     \
+            }                                                                                                    \
+          }                                                                                                      \
+          acc[s] = ac;                                                                                           \
+        }                                                                                                        \
+        cl = cl1;                                                                                                \
+        z4 = z41;                                                                                                \
+        ha = ha1;                                                                                                \
+        hc = hc1;                                                                                                \
+        ab = ab1;                                                                                                \
+      }                                                                                                          \
     }
+    if (gmz) MLP_CELLS(true) else MLP_CELLS(false)
+#undef MLP_CELLS
 #endif
 #ifdef MLP_RELAX_TIMING
     {

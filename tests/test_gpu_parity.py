@@ -241,6 +241,14 @@ def test_family_features_cli_golden(name):
     fam.close()
 
 
+# small-class tiles (two workgroups per CU) whose staging area is too small
+# for some outputs' images beside C: those are read in place from HBM on those
+# z's (with and without passes over output subsets on the others)
+_HBM_IMAGE_MODES = [{'MLP_RELAX': 'pairs', 'MLP_RELAX_SMALL_KB': '14', 'MLP_RELAX_GLOBAL_Z': '100000'},
+                    {'MLP_RELAX': 'pairs', 'MLP_RELAX_SMALL_KB': '16', 'MLP_RELAX_GLOBAL_Z': '100000',
+                     'MLP_RELAX_SPLIT_Z': '100000'}]
+
+
 def _relax_both_paths(seqs, pid, iters, tag):
     """Tiled and row-task relaxation vs the oracle, bit-exact, `iters` rounds."""
     n = len(seqs)
@@ -257,10 +265,12 @@ def _relax_both_paths(seqs, pid, iters, tag):
     # tiled kernel with up to 4 outputs per tile, one output per tile, the
     # large-prefetch instantiation, and the row-task kernel
     # and tiles over a 48 KB staging area whose oversize z's are staged in
-    # passes over subsets of the outputs (MLP_RELAX_SPLIT_Z: no limit)
+    # passes over subsets of the outputs (MLP_RELAX_SPLIT_Z: no limit), and
+    # small-class tiles over a tiny staging area, whose outputs' images are
+    # read in place from HBM on the z's where they do not fit beside C
     modes = [{'MLP_RELAX': 'pairs'}, {'MLP_RELAX': 'pairs', 'MLP_RELAX_TILE': '1'},
              {'MLP_RELAX': 'pairs', 'MLP_RELAX_KP': '9'}, {'MLP_RELAX': 'tasks'},
-             {'MLP_RELAX_LDS_KB': '48', 'MLP_RELAX_SPLIT_Z': '100000'}]
+             {'MLP_RELAX_LDS_KB': '48', 'MLP_RELAX_SPLIT_Z': '100000'}] + _HBM_IMAGE_MODES
     for env in modes:
         os.environ.update(env)
         try:
@@ -289,6 +299,40 @@ def test_relax_pair_path_ragged():
 def test_relax_pair_path_similar():
     seqs = [x for _, x in synth.family(30, 200, 0.2, seed=43)]
     _relax_both_paths(seqs, 3, 3, 'similar')
+
+
+def test_relax_hbm_images_exercised(capfd):
+    """Small-class tiles whose outputs' images are read in place from HBM on
+    the z's where they do not fit beside C (relax.hip, bit 12 + t of the z
+    schedule): the plan log must show such outputs for some staging size, and
+    one round must equal the oracle's bit for bit."""
+    seqs = _ragged_family(24, 1, 400, 42)
+    n = len(seqs)
+    fam = Family(seqs)
+    fam.posteriors(1, 0.132548)
+    rp, eo, cols, vals = [a.copy() for a in fam.export()]
+    cur = [fam.sparse(k) for k in range(n * (n - 1) // 2)]
+    ref = orc.relax([len(x) for x in seqs], [(r.astype(np.int32), c.astype(np.int32), v) for r, c, v in cur])
+    seen = 0
+    for kb in (14, 16, 20, 24, 32):
+        env = {'MLP_RELAX': 'pairs', 'MLP_RELAX_SMALL_KB': str(kb), 'MLP_RELAX_GLOBAL_Z': '100000',
+               'MLP_PLAN_LOG': '1'}
+        os.environ.update(env)
+        try:
+            fam.import_csr(rp, eo, cols, vals)
+            fam.relax(1)
+            fam.synchronize()
+            for k in range(len(ref)):
+                csr_equal(ref[k], fam.sparse(k), f'hbm {kb} KB p{k}')
+        finally:
+            for key in env:
+                del os.environ[key]
+        err = capfd.readouterr().err
+        got = [int(l.split('hbm-image outputs')[1]) for l in err.splitlines() if 'hbm-image outputs' in l]
+        assert got, err
+        seen += sum(got)
+    fam.close()
+    assert seen > 0
 
 
 def test_relax_blockmfma_eval():
@@ -352,7 +396,7 @@ def test_qp_ragged_chains():
 
 # ---- QuickProbs consistency (QP/Alignment/Multiple/ConsistencyStage.cpp:90-258)
 _RELAX_MODES = [{'MLP_RELAX': 'pairs'}, {'MLP_RELAX': 'pairs', 'MLP_RELAX_TILE': '1'},
-                {'MLP_RELAX': 'pairs', 'MLP_RELAX_KP': '9'}, {'MLP_RELAX': 'tasks'}]
+                {'MLP_RELAX': 'pairs', 'MLP_RELAX_KP': '9'}, {'MLP_RELAX': 'tasks'}] + _HBM_IMAGE_MODES
 
 
 def _import(fam, csrs):
