@@ -2442,26 +2442,27 @@ static int relax_one(mlp_ctx* c, const QpRelax& qp, bool last) {
     std::vector<int64_t> tp;
     std::vector<int32_t> tr;
     int64_t cls_tiles[2] = {0, 0}, cls_cap[2] = {0, 0}, cls_cells[2] = {0, 0};
-    // the small class in two launches: tiles of at most 4 cells per thread
-    // first (fewer registers and no idle slots), then the rest
-    const int64_t kFewCells = 4 * (int64_t)kRelaxThreads;
-    int64_t few_tiles = 0, few_cells = 0;
+    // the small class in one launch per slot count (cells per thread): fewer
+    // registers and idle slots than one launch sized for its largest tile
+    std::vector<std::pair<int, int64_t>> small_groups;  // (slots, tiles), in launch order
     for (int k = 0; k < 2; k++) {
       std::vector<std::pair<int, const TileRec*>> order;  // (y, record)
       for (int yy = 1; yy < n; yy++)
         for (const TileRec& r : yplans[yy].recs)
           if (r.cls == k) order.push_back({yy, &r});
       std::stable_sort(order.begin(), order.end(), [&](const auto& u, const auto& v) {
-        if (k == 0 && (u.second->cells <= kFewCells) != (v.second->cells <= kFewCells))
-          return u.second->cells <= kFewCells;
+        if (k == 0) {
+          const int su = tile_relax_slots(u.second->cells), sv = tile_relax_slots(v.second->cells);
+          if (su != sv) return su < sv;
+        }
         return u.second->x0 != v.second->x0 ? u.second->x0 < v.second->x0 : u.first < v.first;
       });
       if (k == 0)
-        for (const auto& o : order)
-          if (o.second->cells <= kFewCells) {
-            ++few_tiles;
-            few_cells = std::max(few_cells, o.second->cells);
-          }
+        for (const auto& o : order) {
+          const int sl = tile_relax_slots(o.second->cells);
+          if (small_groups.empty() || small_groups.back().first != sl) small_groups.push_back({sl, 0});
+          small_groups.back().second++;
+        }
       for (const auto& o : order) {
         const std::vector<int32_t>& src = yplans[o.first].ints;
         tiles.insert(tiles.end(), src.begin() + o.second->first, src.begin() + o.second->first + kTileInts);
@@ -2558,13 +2559,13 @@ static int relax_one(mlp_ctx* c, const QpRelax& qp, bool last) {
       }
       if (cls_tiles[1])
         HIPCHK(c, launch_relax_tiles(pc[1], tile_relax_slots(cls_cells[1]), fork ? c->side.st : c->stream));
-      if (cls_tiles[0]) {
-        TileRelaxArgs a = pc[0], b = pc[0];
-        a.ntiles = few_tiles;
-        b.tiles += few_tiles * kTileInts;
-        b.ntiles = cls_tiles[0] - few_tiles;
-        HIPCHK(c, launch_relax_tiles(a, tile_relax_slots(few_cells), c->stream));
-        HIPCHK(c, launch_relax_tiles(b, tile_relax_slots(cls_cells[0]), c->stream));
+      int64_t first = 0;
+      for (const auto& g : small_groups) {
+        TileRelaxArgs a = pc[0];
+        a.tiles += first * kTileInts;
+        a.ntiles = g.second;
+        HIPCHK(c, launch_relax_tiles(a, g.first, c->stream));
+        first += g.second;
       }
       HIPCHK(c, launch_relax_tasks(ra, c->stream));
       if (fork) {

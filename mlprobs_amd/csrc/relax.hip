@@ -342,7 +342,7 @@ int tile_relax_max_cap() { return 9 * kRelaxThreads * 16; }
 
 int tile_relax_slots(int64_t cells) {
   const int64_t per = (cells + kRelaxThreads - 1) / kRelaxThreads;
-  for (int sl : {4, 8, 12})
+  for (int sl : {4, 6, 8, 12})
     if (per <= sl) return sl;
   if (kRelaxThreads < 1024 && per <= 16) return 16;
   return 0;
@@ -822,6 +822,7 @@ static hipError_t launch_tiles_kp(const TileRelaxArgs& a, int slots, size_t lds,
     hipLaunchKernelGGL((k_relax_tile<KP, SL, QP>), grid, block, lds, st, a);                \
     break;
     MLP_RELAX_CASE(4)
+    MLP_RELAX_CASE(6)
     MLP_RELAX_CASE(8)
     MLP_RELAX_CASE(12)
 #if MLP_RELAX_THREADS < 1024
