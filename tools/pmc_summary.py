@@ -78,6 +78,7 @@ GROUPS = {'forward': ('k_forward',), 'backward': ('k_backward', 'k_fold_totals')
 def groups(o, d):
     """Per bench kernel group: bytes and VALU instructions per pair-cell."""
     cells = None
+    nnz_in = None  # relaxation round 1 input entries (bench --relax 1)
     for log in ('p1.log', 'p2.log', 'p3.log', 'stats.log'):
         f = os.path.join(d, log)
         if not os.path.exists(f):
@@ -86,6 +87,8 @@ def groups(o, d):
             if line.startswith('{"metric"'):
                 b = json.loads(line)
                 cells = b['config']['pair_cells'] * (b['steps'] + b['warmup'])
+                if b.get('relax') and b['relax']['rounds'] == 1:
+                    nnz_in = b['relax']['per_round'][0]['nnz_in']
         if cells:
             break
     out = {'_source': os.path.basename(os.path.normpath(d)), '_pair_cells': cells,
@@ -101,6 +104,15 @@ def groups(o, d):
         out[g] = {'kernels': ks, 'read_bytes_per_cell': rd / cells, 'write_bytes_per_cell': wr / cells,
                   'traffic_bytes_per_cell': (rd + wr) / cells, 'valu_insts_per_cell': vi / cells,
                   'profiled_ms': ns / 1e6}
+    # the consistency round's tile and row-task kernels, per input entry
+    ks = [k for k in o if k.startswith('k_relax') and not k.startswith('k_relax_blockmfma')]
+    if ks and nnz_in:
+        rd = sum(o[k].get('fetch_bytes_per_launch_x2', 0) * o[k].get('calls', 1) for k in ks)
+        wr = sum(o[k].get('write_bytes_per_launch', 0) * o[k].get('calls', 1) for k in ks)
+        out['relax'] = {'kernels': ks, 'nnz_in': nnz_in, 'read_bytes_per_nnz_in': rd / nnz_in,
+                        'write_bytes_per_nnz_in': wr / nnz_in, 'traffic_bytes_per_nnz_in': (rd + wr) / nnz_in,
+                        'valu_insts_per_nnz_in': sum(o[k].get('SQ_INSTS_VALU', 0) for k in ks) / nnz_in,
+                        'profiled_ms': sum(o[k]['total_ns'] for k in ks) / 1e6}
     return out
 
 
