@@ -52,8 +52,11 @@ int mlp_ctx_create(int device, mlp_ctx **out);
  * the reference's own operation order, the partition function in x87 long
  * double like the reference.  Covers the C_P_NP_Aln entry points
  * (mlp_viterbi / mlp_model_adjustment / mlp_family_features, mlp_posteriors
- * with pid 0-4 and MLP_PID_NPDO, mlp_relax, the CSR calls); the QuickProbs
- * and profile-posterior calls return MLP_ERR_STATE. */
+ * with pid 0-4 and MLP_PID_NPDO, mlp_relax, the CSR calls) and QuickProbs'
+ * posterior and consistency stages (mlp_posteriors with MLP_PID_QP,
+ * mlp_relax_qp / mlp_relax_qp_selective, QuickProbs' plain double partition
+ * function); the profile-posterior calls return MLP_ERR_STATE (callers fall
+ * back to their host restatement). */
 int mlp_ctx_create_host(mlp_ctx **out);
 /* 1 for a host context. */
 int mlp_ctx_is_host(const mlp_ctx *ctx);

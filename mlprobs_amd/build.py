@@ -48,8 +48,22 @@ def build(force=False, verbose=False, variant=None, defines=()):
         return LIB
     os.makedirs(LIBDIR, exist_ok=True)
     extra = os.environ.get('MLP_EXTRA_FLAGS', '').split() if variant else []  # experiment copies only
-    cmd = [HIPCC] + FLAGS + extra + ['-D' + d for d in defines] + ['-shared', '-I', os.path.join(ROOT, 'include')]
-    cmd += [os.path.join(CSRC, f) for f in SOURCES] + ['-lrccl', '-o', out + '.tmp']
+    # one object per source, compiled concurrently (the kernels are
+    # independent translation units), then one link
+    objdir = os.path.join(HERE, '_build', variant or 'default')
+    os.makedirs(objdir, exist_ok=True)
+    base = [HIPCC] + FLAGS + extra + ['-D' + d for d in defines] + ['-I', os.path.join(ROOT, 'include')]
+    procs, objs = [], []
+    for f in SOURCES:
+        obj = os.path.join(objdir, f + '.o')
+        objs.append(obj)
+        cmd = base + ['-c', os.path.join(CSRC, f), '-o', obj]
+        if verbose:
+            print(' '.join(cmd))
+        procs.append(subprocess.Popen(cmd))
+    if any(p.wait() != 0 for p in procs):
+        raise subprocess.CalledProcessError(1, 'hipcc -c')
+    cmd = [HIPCC, '--offload-arch=gfx950', '-shared', '-fPIC'] + objs + ['-lrccl', '-o', out + '.tmp']
     if verbose:
         print(' '.join(cmd))
     subprocess.check_call(cmd)

@@ -94,12 +94,19 @@ static void check(mlp_ctx* ctx, int rc, const char* what) {
   if (rc != MLP_OK) fail(std::string("ERROR: ") + what + ": " + (ctx ? mlp_last_error(ctx) : "no context"));
 }
 
+// Device 0 by default.  MLP_DEVICES=<mask> (bit k = HIP device k, e.g. 0xff)
+// opts in to one context over several GPUs, which shards families of >= 1e9
+// pair-cells over them (mlp_ctx_create_mask); that path is verified with
+// virtual shards on one GPU only, so it is not the default.
+static int open_device(mlp_ctx** ctx) {
+  if (const char* m = getenv("MLP_DEVICES")) {
+    const unsigned long long mask = strtoull(m, nullptr, 0);
+    if (mask) return mlp_ctx_create_mask(mask, ctx);
+  }
+  return mlp_ctx_create(0, ctx);
+}
+
 int main(int argc, char** argv) {
-  // idle OpenMP threads sleep instead of spinning between the short parallel
-  // regions of the host stages: spinning threads burn a CPU quota the
-  // serial stages in between need (a cgroup-limited host throttles the
-  // whole process).  An explicit setting in the environment wins.
-  setenv("OMP_WAIT_POLICY", "passive", 0);
   stage(nullptr);  // start the stage clock
   if (argc < 2) {
     usage();
@@ -191,8 +198,7 @@ int main(int argc, char** argv) {
     check(nullptr, mlp_ctx_create_host(&ctx), "host context");
     stage("host context");
   } else {
-    // every visible GPU: families of >= 1e9 pair-cells are sharded over them
-    check(nullptr, mlp_ctx_create_mask(~0ull, &ctx), "device");
+    check(nullptr, open_device(&ctx), "device");
     stage("device init");
     // one family per process: a moderate batch scratch.  A fresh process's
     // allocation waits for the driver to clear memory the previous process

@@ -89,12 +89,19 @@ static bool parse_int(const std::string& s, long long* v) {
   return true;
 }
 
+// Device 0 by default.  MLP_DEVICES=<mask> (bit k = HIP device k, e.g. 0xff)
+// opts in to one context over several GPUs, which shards families of >= 1e9
+// pair-cells over them (mlp_ctx_create_mask); that path is verified with
+// virtual shards on one GPU only, so it is not the default.
+static int open_device(mlp_ctx** ctx) {
+  if (const char* m = getenv("MLP_DEVICES")) {
+    const unsigned long long mask = strtoull(m, nullptr, 0);
+    if (mask) return mlp_ctx_create_mask(mask, ctx);
+  }
+  return mlp_ctx_create(0, ctx);
+}
+
 int main(int argc, char** argv) {
-  // idle OpenMP threads sleep instead of spinning between the short parallel
-  // regions of the host stages: spinning threads burn a CPU quota the
-  // serial stages in between need (a cgroup-limited host throttles the
-  // whole process).  An explicit setting in the environment wins.
-  setenv("OMP_WAIT_POLICY", "passive", 0);
   stage(nullptr);  // start the stage clock
   std::vector<std::string> args(argv + 1, argv + argc), rest;
   std::string outname;
@@ -153,14 +160,27 @@ int main(int argc, char** argv) {
     } else {
       mlp_ctx* ctx = nullptr;
       stage("parse");
-      // every visible GPU: families of >= 1e9 pair-cells are sharded over them
-      check(nullptr, mlp_ctx_create_mask(~0ull, &ctx), "device");
-      stage("device init");
-      // one family per process: a 16 GB batch scratch.  A fresh process's
-      // allocation waits for the driver to clear memory the previous process
-      // released: measured at C3 (512 x 400) 0.82 s posteriors at 16 GB vs
-      // 6.9-7.2 s at 64 GB, 1.16 s at 8 GB
-      if (!getenv("MLP_SCRATCH_GB")) check(ctx, mlp_set_scratch(ctx, 16ull << 30), "device");
+      // Small families (MLProbs realigns one column region per call) run on
+      // the host context: the same stages bit for bit on host threads, no
+      // HIP runtime start-up (0.14-0.22 s per process); above
+      // MLP_HOST_MAX_CELLS pair-cells (default 4e6, 0: always the GPU) the GPU.
+      double pair_cells = 0;
+      for (size_t a = 0; a < seqs.size(); a++)
+        for (size_t b = a + 1; b < seqs.size(); b++)
+          pair_cells += (double)(seqs[a].length() + 1) * (double)(seqs[b].length() + 1);
+      const double host_max = getenv("MLP_HOST_MAX_CELLS") ? atof(getenv("MLP_HOST_MAX_CELLS")) : 4e6;
+      if (pair_cells <= host_max) {
+        check(nullptr, mlp_ctx_create_host(&ctx), "host context");
+        stage("host context");
+      } else {
+        check(nullptr, open_device(&ctx), "device");
+        stage("device init");
+        // one family per process: a 16 GB batch scratch.  A fresh process's
+        // allocation waits for the driver to clear memory the previous process
+        // released: measured at C3 (512 x 400) 0.82 s posteriors at 16 GB vs
+        // 6.9-7.2 s at 64 GB, 1.16 s at 8 GB
+        if (!getenv("MLP_SCRATCH_GB")) check(ctx, mlp_set_scratch(ctx, 16ull << 30), "device");
+      }
       std::string res;
       std::vector<int64_t> off(1, 0);
       for (const qph::Seq& s : seqs) {

@@ -7,6 +7,8 @@
 //   SparseMatrix.h:55-98, 205-248          sparse matrix, stable transpose
 //   MSA.cpp:946-1025, 1670-1753            pid branches, RMS merge orders, distances
 //   MSA.cpp:1172-1360                      DoRelaxation / Relax / Relax1
+//   QP/Alignment/Multiple/PosteriorStage.cpp:123-196, PartitionFunction.cpp:71-291,
+//   ConsistencyStage.cpp:133-300           QuickProbs' posterior and consistency stages
 // All of it is plain host C++ (no HIP call), compiled without FMA
 // contraction like the reference's scalar SSE build.
 #include "host_backend.h"
@@ -368,6 +370,84 @@ float mea_score(int L1, int L2, const std::vector<float>& P, int* nb) {
   return o[L2];
 }
 
+// QuickProbs' PartitionFunction::computeForward / computeReverse
+// (QP/Alignment/Multiple/PartitionFunction.cpp:71-156, 185-289): plain double,
+// Zm over (L1 + 1) x (L2 + 1) rows of seq1, two-row Ze / Zf buffers; the
+// posterior keeps values in [0.001, 1] (PartitionFunction.cpp:262-266).
+void posterior_pf_qp(const mlp::Tables& T, const mlp::ModelScalars& ms, const PairSeqs& q, std::vector<float>& P) {
+  const int L1 = q.L1, L2 = q.L2, lda = L2 + 1;
+  const double go = ms.pf_open, ge = ms.pf_ext, tgo = 1.0, tge = 1.0;  // terminal gaps: exp(beta * 0)
+  // T.sub is [seq2 letter][seq1 letter]
+  auto score = [&](char c1, char c2) { return T.sub[lc(c2) * 26 + lc(c1)]; };
+  static thread_local std::vector<double> Zm, buf;
+  Zm.assign((size_t)(L1 + 1) * lda, 0.0);
+  buf.assign(10 * (size_t)lda, 0.0);
+  double* Ze = buf.data();            // rows 0 / 1 at Ze, Ze + lda
+  double* Zf = buf.data() + 2 * lda;
+  double zz = 0;
+  Zm[0] = 1.0;
+  Zf[0] = Ze[0] = 0;
+  Zf[lda] = Zm[0] * tgo;
+  Ze[1] = Zm[0] * tgo;
+  for (int j = 2; j <= L2; j++) Ze[j] = Ze[j - 1] * tge;
+  for (int i = 1; i <= L1; i++) {
+    for (int j = 1; j <= L2; j++) {
+      const double sc = score(q.s1[i - 1], q.s2[j - 1]);
+      double open0 = go, extend0 = ge, open1 = go, extend1 = ge;
+      if (i == L1) { open0 = tgo; extend0 = tge; }
+      if (j == L2) { open1 = tgo; extend1 = tge; }
+      Ze[lda + j] = Zm[(size_t)i * lda + j - 1] * open0 + Ze[lda + j - 1] * extend0;
+      Zf[lda + j] = Zm[(size_t)(i - 1) * lda + j] * open1 + Zf[j] * extend1;
+      Zm[(size_t)i * lda + j] = (Zm[(size_t)(i - 1) * lda + j - 1] + Ze[j - 1] + Zf[j - 1]) * sc;
+      zz = Zm[(size_t)i * lda + j] + Ze[lda + j] + Zf[lda + j];
+    }
+    for (int t = 0; t <= L2; t++) {
+      Ze[t] = Ze[lda + t];
+      Ze[lda + t] = 0;
+      Zf[t] = Zf[lda + t];
+      Zf[lda + t] = 0;
+    }
+    Zf[lda] = 1;
+  }
+  Zm[0] = zz;
+  double* Rm = buf.data() + 4 * lda;
+  double* Re = buf.data() + 6 * lda;
+  double* Rf = buf.data() + 8 * lda;
+  P.assign((size_t)(L1 + 1) * lda, 0.0f);
+  Rm[lda + L2] = 1;
+  Re[L2] = Rf[L2] = 0;
+  Rf[lda + L2] = Rm[lda + L2] * tgo;
+  Re[L2 - 1] = Rm[lda + L2] * tgo;
+  for (int j = L2 - 2; j >= 0; j--) Re[j] = Re[j + 1] * tge;
+  for (int i = L1 - 1; i >= 0; i--) {
+    for (int j = L2 - 1; j >= 0; j--) {
+      const double sc = score(q.s1[i], q.s2[j]);
+      double open0 = go, extend0 = ge, open1 = go, extend1 = ge;
+      if (i == 0) { open0 = tgo; extend0 = tge; }
+      if (j == 0) { open1 = tgo; extend1 = tge; }
+      Rf[lda + j] = Rm[lda + j] * open1 + Rf[j] * extend1;
+      Re[lda + j] = Rm[j + 1] * open0 + Re[lda + j + 1] * extend0;
+      Rm[j] = (Rm[lda + j + 1] + Rf[j + 1] + Re[j + 1]) * sc;
+      double tv = Zm[(size_t)(i + 1) * lda + j + 1] * Rm[j];
+      tv /= (sc * Zm[0]);
+      const float prob = (float)tv;
+      if (prob <= 1 && prob >= 0.001) P[(size_t)(i + 1) * lda + j + 1] = prob;
+    }
+    for (int t = 0; t <= L2; t++) {
+      Re[t] = Re[lda + t];
+      Re[lda + t] = 0;
+      Rf[t] = Rf[lda + t];
+      Rf[lda + t] = 0;
+      Rm[lda + t] = Rm[t];
+      Rm[t] = 0;
+    }
+    Rf[L2] = 1;
+  }
+  P[0] = 0;
+}
+
+inline float fixed16(float v) { return (float)(uint32_t)(uint16_t)(v * 65535.0f) / 65535.0f; }
+
 }  // namespace
 
 int threads_for(int64_t units) {
@@ -529,7 +609,76 @@ int posteriors(const mlp::Tables& T, const mlp::ModelScalars& ms, const FamilyVi
   return 0;
 }
 
-void relax(const FamilyView& f, const std::vector<int64_t>& rp_off, Store& st, int64_t* nnz) {
+void qp_posteriors(const mlp::Tables& T, const mlp::ModelScalars& ms, const FamilyView& f, int64_t p0, int64_t p1,
+                   float cutoff, const std::vector<int64_t>& rp_off, Store& st, float* dist, float* mea,
+                   int64_t* nnz) {
+  const int64_t np = p1 - p0;
+  std::vector<std::vector<uint16_t>> pc(np);
+  std::vector<std::vector<float>> pv(np);
+  parallel_for(np, threads_for(np), [&](int64_t k) {
+    const int64_t p = p0 + k;
+    const int a = f.pa[p], b = f.pb[p];
+    PairSeqs q{(const char*)f.res + f.offs[a], (const char*)f.res + f.offs[b], f.lens[a], f.lens[b]};
+    const int W = q.L2 + 1;
+    static thread_local std::vector<float> F, B, ph, pf, oldr, newr;
+    posterior_pf_qp(T, ms, q, pf);
+    forward5(T, ms, q, F);
+    backward5(T, ms, q, B);
+    posterior_hmm(T, ms, q, true, F, B, ph);
+    // combineMatrices (PosteriorStage.cpp:160-196): the RMS in place of ph,
+    // the MEA value recurrence over two rows
+    oldr.assign(W, 0.f);
+    newr.assign(W, 0.f);
+    for (int i = 0; i <= q.L1; i++) {
+      for (int j = 0; j <= q.L2; j++) {
+        const size_t c = (size_t)i * W + j;
+        if (i == 0 || j == 0) {
+          ph[c] = 0;
+          newr[j] = 0;
+        } else {
+          const float v1 = ph[c], v2 = pf[c];
+          ph[c] = sqrtf((v1 * v1 + v2 * v2) * 0.5f);
+          const float x = ph[c] + oldr[j - 1], y = newr[j - 1], z = oldr[j];
+          newr[j] = x >= y ? (x >= z ? x : z) : (y >= z ? y : z);
+        }
+      }
+      std::swap(oldr, newr);
+    }
+    const float total = oldr[q.L2];
+    mea[p] = total;
+    dist[p] = 1.0f - total / (float)std::min(q.L1, q.L2);
+    int32_t* rp = st.rowptr.data() + rp_off[p];
+    rp[0] = rp[1] = 0;
+    std::vector<uint16_t>& cc = pc[k];
+    std::vector<float>& vv = pv[k];
+    cc.clear();
+    vv.clear();
+    for (int i = 1; i <= q.L1; i++) {
+      const float* row = ph.data() + (size_t)i * W;
+      for (int j = 1; j <= q.L2; j++)
+        if (row[j] >= cutoff) {
+          cc.push_back((uint16_t)j);
+          vv.push_back(fixed16(row[j]));
+        }
+      rp[i + 1] = (int32_t)cc.size();
+    }
+  });
+  int64_t run = st.ent_off[p0];
+  for (int64_t k = 0; k < np; k++) {
+    st.ent_off[p0 + k] = run;
+    nnz[p0 + k] = (int64_t)pc[k].size();
+    run += (int64_t)pc[k].size();
+  }
+  st.ent_off[p1] = run;
+  st.cols.resize(run);
+  st.vals.resize(run);
+  for (int64_t k = 0; k < np; k++) {
+    std::copy(pc[k].begin(), pc[k].end(), st.cols.begin() + st.ent_off[p0 + k]);
+    std::copy(pv[k].begin(), pv[k].end(), st.vals.begin() + st.ent_off[p0 + k]);
+  }
+}
+
+void relax(const FamilyView& f, const std::vector<int64_t>& rp_off, Store& st, int64_t* nnz, const QpRelaxHost* qp) {
   const int n = f.n;
   const int64_t P = (int64_t)n * (n - 1) / 2;
   auto pidx = [&](int a, int b) { return (int64_t)a * n - (int64_t)a * (a + 1) / 2 + (b - a - 1); };
@@ -583,31 +732,54 @@ void relax(const FamilyView& f, const std::vector<int64_t>& rp_off, Store& st, i
     post.assign((size_t)(Lx + 1) * W, 0.f);
     for (int i = 1; i <= Lx; i++)
       for (int32_t e = rp[i]; e < rp[i + 1]; e++) post[(size_t)i * W + cx[e]] = vx[e];
-    for (float& v : post) v += v;
+    // QuickProbs: z accepted by the selectivity filter (ConsistencyStage.cpp:
+    // 180-203), its weight w_z / W_xy, the weight sum in z order
+    auto accept = [&](int z) {
+      if (!qp->seldist) return true;
+      const float dx = qp->seldist[(size_t)x * n + z], dy = qp->seldist[(size_t)y * n + z];
+      return (dx > dy ? dx : dy) <= qp->selectivity;
+    };
+    float wxy = 0.f, sumw = 1.0f;
+    if (qp) {
+      int accepted = 0;
+      for (int z = 0; z < n; z++) accepted += z != x && z != y && accept(z);
+      wxy = 1.0f + (qp->selfweight - 1.0f) * (float)accepted / qp->selectivity;
+      wxy *= qp->weights[x] + qp->weights[y];
+    } else {
+      for (float& v : post) v += v;   // z = x and z = y (CPNP/MSA.cpp:1211-1213)
+    }
     // z ascending; Relax / Relax1 / transposed Relax all add, per cell, the
     // terms of z's k in ascending order
     for (int z = 0; z < n; z++) {
       if (z == x || z == y) continue;
+      float wz = 1.0f;
+      if (qp) {
+        if (!accept(z)) continue;
+        wz = qp->weights[z] / wxy;
+        sumw += wz;
+      }
       for (int i = 1; i <= Lx; i++) {
         const Row A = row_of(x, z, i);
         float* base = post.data() + (size_t)i * W;
         for (int32_t u = A.b; u < A.e; u++) {
           const Row Bk = row_of(z, y, A.c[u]);
-          const float a = A.v[u];
+          const float a = qp ? wz * A.v[u] : A.v[u];   // weight * XZ * ZY (ConsistencyStage.cpp:294)
           for (int32_t w = Bk.b; w < Bk.e; w++) base[Bk.c[w]] += a * Bk.v[w];
         }
       }
     }
-    for (float& v : post) v /= (float)n;
-    // mask to the old pattern, then SparseMatrix at 0.01
+    const float div = qp ? sumw : (float)n;
+    for (float& v : post) v /= div;
+    // mask to the old pattern, then SparseMatrix at the cutoff
+    const float cut = qp ? qp->cutoff : kCutoff;
     int32_t* out = nrp.data() + rp_off[p];
     out[0] = out[1] = 0;
     for (int i = 1; i <= Lx; i++) {
       for (int32_t e = rp[i]; e < rp[i + 1]; e++) {
         const float v = post[(size_t)i * W + cx[e]];
-        if (v >= kCutoff) {
+        if (v >= cut) {
           nc[p].push_back(cx[e]);
-          nv[p].push_back(v);
+          nv[p].push_back(qp ? fixed16(v) : v);
         }
       }
       out[i + 1] = (int32_t)nc[p].size();

@@ -56,7 +56,32 @@ int posteriors(const mlp::Tables& T, const mlp::ModelScalars& ms, const FamilyVi
                int64_t p0, int64_t p1, const std::vector<int64_t>& rp_off, Store& st, float* dist, float* mea,
                int64_t* nnz, std::string& err);
 
-// One MSA::DoRelaxation round (CPNP/MSA.cpp:1172-1360) over every pair.
-void relax(const FamilyView& f, const std::vector<int64_t>& rp_off, Store& st, int64_t* nnz);
+// QuickProbs' posterior stage (PosteriorStage::computePairwise +
+// combineMatrices, QP/Alignment/Multiple/PosteriorStage.cpp:123-196) for pairs
+// [p0, p1): the 5-state posterior above, QuickProbs' double partition
+// function (PartitionFunction.cpp:71-291; T.sub / ms.pf_* from the QuickProbs
+// tables), RMS of the two fused with the MEA score, distance
+// 1 - score / min(L1, L2), entries >= `cutoff` as 16-bit fixed point read back
+// as q / 65535 (PackedSparseMatrix, SparseEntry.h:31-32).
+void qp_posteriors(const mlp::Tables& T, const mlp::ModelScalars& ms, const FamilyView& f, int64_t p0, int64_t p1,
+                   float cutoff, const std::vector<int64_t>& rp_off, Store& st, float* dist, float* mea,
+                   int64_t* nnz);
+
+// QuickProbs' consistency round instead of C_P_NP_Aln's (ConsistencyStage::
+// doRelaxation, QP/Alignment/Multiple/ConsistencyStage.cpp:133-266): z
+// accepted iff max(seldist[x][z], seldist[y][z]) <= selectivity (NULL: all),
+// P' = (P + sum_z w_z P_xz P_zy) / (1 + sum_z w_z), w_z = weights[z] / W_xy,
+// W_xy = (1 + (selfweight - 1) A_xy / selectivity)(w_x + w_y); entries >=
+// cutoff kept as 16-bit fixed point.
+struct QpRelaxHost {
+  const float* weights;
+  const float* seldist;
+  float selectivity, selfweight, cutoff;
+};
+
+// One MSA::DoRelaxation round (CPNP/MSA.cpp:1172-1360) over every pair, or
+// QuickProbs' round when qp is given.
+void relax(const FamilyView& f, const std::vector<int64_t>& rp_off, Store& st, int64_t* nnz,
+           const QpRelaxHost* qp = nullptr);
 
 }  // namespace mlph

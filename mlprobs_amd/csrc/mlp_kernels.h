@@ -328,7 +328,9 @@ int tile_relax_prefetch(int cap);              // 16-byte chunks per thread, 0 =
 int tile_relax_slots(int64_t cells);           // cells per thread, 0 = too many
 int tile_relax_max_cap();                      // largest tile the prefetch registers hold
 hipError_t launch_pack(const PackArgs& a, hipStream_t st);
-hipError_t launch_relax_tiles(const TileRelaxArgs& a, int slots, hipStream_t st);
+// one_per_cu: the one-workgroup class (KP = 9 whatever its cap: the KP = 5
+// instance is bounded to 64 VGPRs for two workgroups per CU)
+hipError_t launch_relax_tiles(const TileRelaxArgs& a, int slots, bool one_per_cu, hipStream_t st);
 // dense-block MFMA evaluation of the consistency transform (relax_mfma.hip):
 // res = {kernel s, dense MACs, outputs, max rel err, cells checked, tiles, blocks}
 int relax_blockmfma_eval(int n, const int32_t* lens, const int64_t* rp_off, const int32_t* rowptr,

@@ -924,10 +924,6 @@ static mlph::FamilyView host_view(const mlp_ctx* c) {
 static int host_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
   const bool npdo = (pid & kPidNpdo) != 0;
   pid &= ~kPidNpdo;
-  if (pid == kPidQP) {
-    c->err = "the QuickProbs posterior stage runs on a device context";
-    return MLP_ERR_STATE;
-  }
   if (c->store_p0 == c->store_p1 || p0 != c->store_p1) {  // as the device store: append or restart
     c->store_p0 = c->store_p1 = p0;
     c->store_total = 0; ++c->store_ver;
@@ -937,10 +933,16 @@ static int host_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t
   }
   Tables T;
   ModelScalars ms;
-  build_tables(T, ms, delta);
-  const int rc = mlph::posteriors(T, ms, host_view(c), pid, npdo, p0, p1, c->rp_off, c->hs, c->dist.data(),
-                                  c->mea.data(), c->nnz.data(), c->err);
-  if (rc) return rc == 3 ? MLP_ERR_OVERFLOW : MLP_ERR_STATE;
+  if (pid == kPidQP) {  // QuickProbs' posterior stage (its HMM tables are these; its own PF)
+    build_tables(T, ms, -1.f, true);
+    mlph::qp_posteriors(T, ms, host_view(c), p0, p1, mlp_qp_cutoff, c->rp_off, c->hs, c->dist.data(),
+                        c->mea.data(), c->nnz.data());
+  } else {
+    build_tables(T, ms, delta);
+    const int rc = mlph::posteriors(T, ms, host_view(c), pid, npdo, p0, p1, c->rp_off, c->hs, c->dist.data(),
+                                    c->mea.data(), c->nnz.data(), c->err);
+    if (rc) return rc == 3 ? MLP_ERR_OVERFLOW : MLP_ERR_STATE;
+  }
   for (int64_t p = p0; p <= p1; p++) c->ent_off[p] = c->hs.ent_off[p];
   c->store_p1 = p1;
   c->store_total = c->hs.ent_off[p1];
@@ -1893,22 +1895,33 @@ int mlp_relax_shard_plan(int n, const int32_t* lens, const int64_t* pair_nnz, in
   if (n < 0 || nranks < 1 || !bounds || (n > 0 && (!lens || !pair_nnz))) return MLP_ERR_ARG;
   const int64_t P = (int64_t)n * (n - 1) / 2;
   std::vector<double> cost(std::max<int64_t>(P, 1), 0.0);
-  if (n <= 2048) {
+  if (n <= 1024) {
+    // O(n^3 / 2) multiply-adds (1.5e8 at n = 1024, ~0.1 s serial): rows x
+    // spread over host threads (the split only balances; any x order gives
+    // the same costs)
     std::vector<float> M((size_t)n * n, 0.f);
     for (int a = 0, p = 0; a < n; a++)
       for (int b = a + 1; b < n; b++, p++) M[(size_t)a * n + b] = M[(size_t)b * n + a] = (float)pair_nnz[p];
-    std::vector<double> acc(n);
-    for (int x = 0; x < n; x++) {
-      std::fill(acc.begin(), acc.end(), 0.0);
-      for (int z = 0; z < n; z++) {
-        const double w = M[(size_t)x * n + z] / std::max(1, lens[z]);
-        if (w == 0) continue;
-        const float* mz = &M[(size_t)z * n];
-        for (int y = x + 1; y < n; y++) acc[y] += w * mz[y];
+    std::atomic<int> next(0);
+    auto work = [&]() {
+      std::vector<double> acc(n);
+      for (int x; (x = next.fetch_add(1)) < n;) {
+        std::fill(acc.begin(), acc.end(), 0.0);
+        for (int z = 0; z < n; z++) {
+          const double w = M[(size_t)x * n + z] / std::max(1, lens[z]);
+          if (w == 0) continue;
+          const float* mz = &M[(size_t)z * n];
+          for (int y = x + 1; y < n; y++) acc[y] += w * mz[y];
+        }
+        const int64_t base = pair_index_host(n, x, x + 1);
+        for (int y = x + 1; y < n; y++) cost[base + (y - x - 1)] = acc[y];
       }
-      const int64_t base = pair_index_host(n, x, x + 1);
-      for (int y = x + 1; y < n; y++) cost[base + (y - x - 1)] = acc[y];
-    }
+    };
+    const int nt = n >= 256 ? std::max(1, std::min(16, (int)std::thread::hardware_concurrency())) : 1;
+    std::vector<std::thread> pool;
+    for (int t = 1; t < nt; t++) pool.emplace_back(work);
+    work();
+    for (std::thread& th : pool) th.join();
   } else {  // large families: per-sequence totals only
     std::vector<double> T(n, 0.0);
     for (int a = 0, p = 0; a < n; a++)
@@ -2080,11 +2093,21 @@ int mlp_relax_qp_selective(mlp_ctx* c, int iters, const float* seq_weights, cons
                            float selectivity) {
   if (!c || !seq_weights || !(selectivity > 0)) return MLP_ERR_ARG;
   if (c->n < 2) return MLP_ERR_STATE;
-  if (c->host) {
-    c->err = "QuickProbs' consistency stage runs on a device context";
-    return MLP_ERR_STATE;
-  }
   if (iters < 0) iters = c->n > 50 ? 1 : 2;
+  if (c->host) {
+    if (c->store_p0 != 0 || c->store_p1 != c->P) {
+      c->err = "relaxation needs every pair";
+      return MLP_ERR_STATE;
+    }
+    for (int it = 0; it < iters; it++) {
+      const mlph::QpRelaxHost q{seq_weights, sel_dist, selectivity, 3.0f, it == iters - 1 ? 1e-5f : 0.01f};
+      mlph::relax(host_view(c), c->rp_off, c->hs, c->nnz.data(), &q);
+    }
+    c->ent_off = c->hs.ent_off;
+    c->store_total = c->hs.ent_off[c->P];
+    ++c->store_ver;
+    return MLP_OK;
+  }
   int rc;
   if ((rc = ensure(c, c->r_weights, sizeof(float) * c->n))) return rc;
   HIPCHK(c, hipMemcpyAsync(c->r_weights.p, seq_weights, sizeof(float) * c->n, hipMemcpyHostToDevice, c->stream));
@@ -2558,13 +2581,13 @@ static int relax_one(mlp_ctx* c, const QpRelax& qp, bool last) {
         HIPCHK(c, hipStreamWaitEvent(c->side.st, c->side.fork, 0));
       }
       if (cls_tiles[1])
-        HIPCHK(c, launch_relax_tiles(pc[1], tile_relax_slots(cls_cells[1]), fork ? c->side.st : c->stream));
+        HIPCHK(c, launch_relax_tiles(pc[1], tile_relax_slots(cls_cells[1]), true, fork ? c->side.st : c->stream));
       int64_t first = 0;
       for (const auto& g : small_groups) {
         TileRelaxArgs a = pc[0];
         a.tiles += first * kTileInts;
         a.ntiles = g.second;
-        HIPCHK(c, launch_relax_tiles(a, g.first, c->stream));
+        HIPCHK(c, launch_relax_tiles(a, g.first, false, c->stream));
         first += g.second;
       }
       HIPCHK(c, launch_relax_tasks(ra, c->stream));

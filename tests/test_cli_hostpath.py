@@ -133,3 +133,97 @@ def test_host_context_family_test():
     vm, o_ident, o_delta = orc.model_adjustment(orc.model(0.132548), seqs)
     assert code == vm and np.float32(ident) == np.float32(o_ident) and np.float32(delta) == np.float32(o_delta)
     fam.close()
+
+
+# ---- QuickProbs on the host context (quickprobs drop-in, small families)
+QP_BIN = os.path.join(ROOT, 'mlprobs_amd', 'cli', 'quickprobs')
+
+
+def _qp_expected(seqs, a, b):
+    h, g, p, dist = orc.qp_pair(orc.model(-1.0), seqs[a], seqs[b])
+    rp, cols, q = orc.qp_sparsify(len(seqs[a]), len(seqs[b]), p)
+    return (rp, cols, q.astype(np.float32) / np.float32(65535)), dist
+
+
+@pytest.mark.parametrize('n,L,s,iters,seed,sel', [(9, 140, 0.6, 2, 71, False), (12, 90, 0.7, 3, 73, False),
+                                                  (14, 120, 0.6, 2, 74, True), (6, 60, 0.2, 1, 76, True)])
+def test_host_context_qp_stage_vs_oracle(n, L, s, iters, seed, sel):
+    """QuickProbs' posterior stage and selective consistency rounds on the host
+    context: bit-exact to the oracle's restatement (the GPU twin of this test
+    is test_gpu_parity.py::test_qp_stage_vs_oracle)."""
+    from mlprobs_amd.engine import PID_QP
+    seqs = [x for _, x in synth.family(n, L, s, seed=seed)]
+    rng = np.random.default_rng(seed)
+    w = rng.uniform(1, 30, n).astype(np.float32)
+    seld = None
+    if sel:
+        seld = rng.integers(2, n + 1, (n, n)).astype(np.float32)
+        seld = np.minimum(seld, seld.T)
+        np.fill_diagonal(seld, 0)
+    fam = Family(seqs, host=True)
+    fam.posteriors(PID_QP, 0.0)
+    D = fam.distances()
+    cur, k = [], 0
+    for a in range(n):
+        for b in range(a + 1, n):
+            ref, dist = _qp_expected(seqs, a, b)
+            r, c, v = fam.sparse(k)
+            np.testing.assert_array_equal(r, ref[0])
+            np.testing.assert_array_equal(c.astype(np.int32), ref[1])
+            np.testing.assert_array_equal(v, ref[2])
+            assert D[a, b] == dist
+            cur.append((ref[0].astype(np.int32), ref[1].astype(np.int32), ref[2]))
+            k += 1
+    lens = [len(x) for x in seqs]
+    for it in range(1, iters + 1):
+        cur = orc.relax(lens, cur, qp=(w, 3.0, 1e-5 if it == iters else 0.01, seld, 6.0))
+    fam.relax_qp(iters, w, seld, 6.0)
+    for k in range(len(cur)):
+        r, c, v = fam.sparse(k)
+        np.testing.assert_array_equal(r, cur[k][0])
+        np.testing.assert_array_equal(c.astype(np.int32), cur[k][1])
+        np.testing.assert_array_equal(v, cur[k][2])
+    fam.close()
+
+
+def test_qp_cli_goldens_on_host_path():
+    """The quickprobs binary's host path against the reference QuickProbs CLI
+    (built from source): every golden family under the threshold."""
+    runs = []
+    for name, args in [('bb11028', []), ('bb11028', ['-c', '0']), ('bb11028', ['-c', '1', '-r', '5']),
+                       ('div12', []), ('div12', ['-c', '0']), ('sim8', []), ('sim8', ['-c', '3', '-r', '50']),
+                       ('qp_div60', []), ('qp_big210', [])]:
+        fa = os.path.join(GOLDEN, 'cli', f'{name}.fa')
+        tag = 'qp_' + name.replace('qp_', '') + ''.join('_' + a.strip('-') for a in args)
+        if _cells(fa) <= HOST_MAX:
+            runs.append((fa, args, os.path.join(GOLDEN, 'cli', f'{tag}.out')))
+    for sub in ('real',):
+        d = os.path.join(GOLDEN, sub)
+        for f in sorted(os.listdir(d)):
+            if f.endswith('.qp.out'):
+                fa = os.path.join(d, f[:-len('.qp.out')] + '.fa')
+                if _cells(fa) <= HOST_MAX:
+                    runs.append((fa, [], os.path.join(d, f)))
+    assert len(runs) >= 20, runs
+
+    def one(r):
+        fa, args, gold = r
+        p = subprocess.run([QP_BIN, *args, fa], capture_output=True, timeout=300,
+                           env=dict(os.environ, MLP_HOST_THREADS='2'))
+        with open(gold, 'rb') as fh:
+            return fa, args, p.returncode == 0 and p.stdout == fh.read()
+
+    with ThreadPoolExecutor(4) as ex:
+        bad = [(f, v) for f, v, ok in ex.map(one, runs) if not ok]
+    assert not bad, bad
+
+
+def test_qp_parity_sweep_on_host_path(tmp_path):
+    """tools/parity_sweep.py's quickprobs half on every sweep family up to
+    4e6 pair-cells (972 of the reference's TEST families): byte-identical."""
+    out = tmp_path / 'sweep.txt'
+    subprocess.run([sys.executable, os.path.join(ROOT, 'tools', 'parity_sweep.py'), str(out), '8', 'qp', '4e6'],
+                   check=True, capture_output=True, timeout=1200)
+    text = out.read_text()
+    assert 'qp: 972/972 byte-identical' in text, text
+    assert 'MISMATCH' not in text

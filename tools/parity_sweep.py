@@ -6,7 +6,9 @@ scratch each) and writes a summary and any mismatches to OUT.  TAGS (comma
 list of G, p_0, qp; default all) selects the runs: the c_p_np_aln runs of
 the sweep (G, p_0; at most 2e6 pair-cells) all take the drop-in's host path
 (mlp_ctx_create_host), so `G,p_0` needs no GPU.
-    python tools/parity_sweep.py OUT [workers] [TAGS]
+With MAX_CELLS only families of at most that many pair-cells run (the
+drop-ins' host path: `qp 4e6` runs without a GPU).
+    python tools/parity_sweep.py OUT [workers] [TAGS] [MAX_CELLS]
 """
 import json
 import lzma
@@ -22,16 +24,35 @@ CP = os.path.join(ROOT, 'mlprobs_amd', 'cli', 'c_p_np_aln')
 QP = os.path.join(ROOT, 'mlprobs_amd', 'cli', 'quickprobs')
 
 
+def pair_cells(fa_text):
+    """(L_a + 1)(L_b + 1) summed over pairs, residues as the CLIs count them."""
+    lens, cur = [], None
+    for line in fa_text.splitlines():
+        if line.startswith('>'):
+            if cur is not None:
+                lens.append(cur)
+            cur = 0
+        elif cur is not None:
+            cur += sum(ch.isalpha() for ch in line)
+    if cur is not None:
+        lens.append(cur)
+    tot = sum(lens)
+    return ((tot + len(lens)) ** 2 - sum((L + 1) ** 2 for L in lens)) / 2
+
+
 def main():
     out = sys.argv[1]
     workers = int(sys.argv[2]) if len(sys.argv) > 2 else 8
     tags = sys.argv[3].split(',') if len(sys.argv) > 3 else ['G', 'p_0', 'qp']
+    max_cells = float(sys.argv[4]) if len(sys.argv) > 4 else float('inf')
     with lzma.open(os.path.join(ROOT, 'tests', 'golden', 'sweep.json.xz'), 'rt') as fh:
         fams = json.load(fh)
     env = dict(os.environ, MLP_SCRATCH_GB='8', MLP_HOST_THREADS='2')
     td = tempfile.mkdtemp()
     jobs = []
     for name, e in sorted(fams.items()):
+        if pair_cells(e['fa']) > max_cells:
+            continue
         fa = os.path.join(td, name.replace('/', '_') + '.fa')
         with open(fa, 'wb') as fh:
             fh.write(e['fa'].encode('latin-1'))
