@@ -21,6 +21,7 @@
 
 #include "mlpgpu.h"
 #include "msa_host.h"
+#include "runners.h"
 
 using cpnp::Row;
 
@@ -59,55 +60,13 @@ static bool get_float(const char* s, float* v) {   // MSA::GetFloat (CPNP/MSA.cp
   return true;
 }
 
-// MLP_CLI_TIMES=1 prints stage times to stderr (off by default: the
-// reference is silent on stderr on success).
-static void stage(const char* name) {
-  static const bool on = getenv("MLP_CLI_TIMES") != nullptr;
-  static auto t0 = std::chrono::steady_clock::now();
-  if (!on) return;
-  if (!name) {  // first call, from main: time since the process started (loader, static init)
-    double up = 0, start = 0;
-    if (FILE* f = fopen("/proc/uptime", "r")) { if (fscanf(f, "%lf", &up) != 1) up = 0; fclose(f); }
-    if (FILE* f = fopen("/proc/self/stat", "r")) {
-      char buf[1024];
-      const size_t n = fread(buf, 1, sizeof buf - 1, f);
-      fclose(f);
-      buf[n] = 0;
-      const char* q = strrchr(buf, ')');  // fields after the command name; starttime is field 22
-      for (int k = 2; q && k < 22; k++) q = strchr(q + 1, ' ');
-      if (q) start = strtod(q + 1, nullptr) / (double)sysconf(_SC_CLK_TCK);
-    }
-    std::cerr << "[stage] process start to main " << (up - start) << " s" << std::endl;
-    return;
-  }
-  const auto t1 = std::chrono::steady_clock::now();
-  std::cerr << "[stage] " << name << " " << std::chrono::duration<double>(t1 - t0).count() << " s" << std::endl;
-  t0 = t1;
-}
-
 [[noreturn]] static void fail(const std::string& msg) {
   std::cerr << msg << std::endl;
   exit(1);
 }
 
-static void check(mlp_ctx* ctx, int rc, const char* what) {
-  if (rc != MLP_OK) fail(std::string("ERROR: ") + what + ": " + (ctx ? mlp_last_error(ctx) : "no context"));
-}
-
-// Device 0 by default.  MLP_DEVICES=<mask> (bit k = HIP device k, e.g. 0xff)
-// opts in to one context over several GPUs, which shards families of >= 1e9
-// pair-cells over them (mlp_ctx_create_mask); that path is verified with
-// virtual shards on one GPU only, so it is not the default.
-static int open_device(mlp_ctx** ctx) {
-  if (const char* m = getenv("MLP_DEVICES")) {
-    const unsigned long long mask = strtoull(m, nullptr, 0);
-    if (mask) return mlp_ctx_create_mask(mask, ctx);
-  }
-  return mlp_ctx_create(0, ctx);
-}
-
 int main(int argc, char** argv) {
-  stage(nullptr);  // start the stage clock
+  mlpr::stage(nullptr);  // start the stage clock
   if (argc < 2) {
     usage();
     return 1;
@@ -179,195 +138,13 @@ int main(int argc, char** argv) {
       seqs.push_back(std::move(r));
     }
   }
-  if (seqs.empty()) fail("ERROR: No sequences read.");
-  const int n = (int)seqs.size();
-
-  mlp_ctx* ctx = nullptr;
-  stage("parse");
-  // Small families run on the host (mlp_ctx_create_host: the same stages,
-  // bit for bit, without initialising the GPU runtime, whose start-up and
-  // teardown alone cost 0.2-0.4 s per process); at ~2e7 pair-cells/s on the
-  // host threads, families up to MLP_HOST_MAX_CELLS pair-cells (default 4e6,
-  // 0: always the GPU) finish there before a device would be ready.
-  double pair_cells = 0;
-  for (size_t a = 0; a < seqs.size(); a++)
-    for (size_t b = a + 1; b < seqs.size(); b++)
-      pair_cells += (double)(seqs[a].length() + 1) * (double)(seqs[b].length() + 1);
-  const double host_max = getenv("MLP_HOST_MAX_CELLS") ? atof(getenv("MLP_HOST_MAX_CELLS")) : 4e6;
-  if (pair_cells <= host_max) {
-    check(nullptr, mlp_ctx_create_host(&ctx), "host context");
-    stage("host context");
-  } else {
-    check(nullptr, open_device(&ctx), "device");
-    stage("device init");
-    // one family per process: a moderate batch scratch.  A fresh process's
-    // allocation waits for the driver to clear memory the previous process
-    // released; back to back at C3 (512 x 400) the posterior stage took 1.09 s
-    // at 32 GB, 1.39 s at 16 GB, 7.4-10.5 s at 64 GB
-    if (!getenv("MLP_SCRATCH_GB")) check(ctx, mlp_set_scratch(ctx, 32ull << 30), "device");
+  std::string out, err;
+  const int status = mlpr::run_cpnp(std::move(seqs), just_features, progressive, opt, nullptr, out, err);
+  if (status) {
+    std::cerr << err << std::endl;
+    return status;
   }
-  std::string res;
-  std::vector<int64_t> off(1, 0);
-  for (const Row& r : seqs) {
-    res.append(r.data, 1, std::string::npos);
-    off.push_back((int64_t)res.size());
-  }
-  check(ctx, mlp_family_load(ctx, n, res.data(), off.data()), "family");
-  stage("load");
-
-  if (just_features) {   // CPNP/MSA.cpp:153-166 (theta = 1.0)
-    float f[5];
-    int32_t ints[2];
-    check(ctx, mlp_family_features(ctx, 1.0f, f, ints), "family test");
-    char line[512];
-    snprintf(line, sizeof line, "%f\t%f\t%d\t%d\t%f\t%f\t%f", f[0], f[1], ints[0], ints[1], f[2], f[3], f[4]);
-    std::cout << line << std::endl;
-    mlp_ctx_destroy(ctx);
-    return 0;
-  }
-  cpnp::Profile aln;
-  if (n == 1) {
-    aln.push_back(seqs[0]);
-  } else {
-    // ModelAdjustmentTest (CPNP/MSA.cpp:775-882) -> pid, delta
-    float identity, variance, delta;
-    int32_t code;
-    check(ctx, mlp_model_adjustment(ctx, &identity, &variance, &delta, &code), "family test");
-    stage("family test (Viterbi)");
-    const int pid = code % 10, vpid = code / 10;
-    // pdoAlign (CPNP/MSA.cpp:895-1081): posteriors, distances, tree, consistency;
-    // npdoAlign (CPNP/MSA.cpp:1084-1140): ArrangePosteriorProbs' pair body,
-    // consistency, alignment graph, refinement
-    const int64_t P = mlp_family_npairs(ctx);
-    check(ctx, mlp_posteriors(ctx, progressive ? pid : pid | MLP_PID_NPDO, delta, 0, P), "posteriors");
-    std::vector<float> dist(P);
-    check(ctx, mlp_pair_results(ctx, 0, P, dist.data(), nullptr, nullptr), "results");
-    std::vector<std::vector<float>> D(n, std::vector<float>(n, 0.f));
-    for (int a = 0, p = 0; a < n; a++)
-      for (int b = a + 1; b < n; b++, p++) D[a][b] = D[b][a] = dist[p];
-    stage("posteriors");
-    cpnp::GuideTree tree;
-    if (progressive) {
-      tree = cpnp::build_tree(D, vpid);
-      stage("guide tree");
-    }
-    if (opt.consistency > 0) check(ctx, mlp_relax(ctx, opt.consistency), "consistency");
-    check(ctx, mlp_synchronize(ctx), "consistency");
-    stage("consistency");
-    cpnp::SparseSet sp;
-    sp.n = n;
-    sp.lens.resize(n);
-    for (int k = 0; k < n; k++) sp.lens[k] = seqs[k].length();
-    sp.rp_off.assign(P + 1, 0);
-    for (int a = 0, p = 0; a < n; a++)
-      for (int b = a + 1; b < n; b++, p++) sp.rp_off[p + 1] = sp.rp_off[p] + sp.lens[a] + 2;
-    int64_t total = 0;
-    check(ctx, mlp_csr_total(ctx, &total), "sparse set");
-    sp.row_ptr.resize(sp.rp_off[P]);
-    sp.ent_off.resize(P + 1);
-    sp.cols.resize(std::max<int64_t>(total, 1));
-    sp.vals.resize(std::max<int64_t>(total, 1));
-    check(ctx, mlp_csr_export(ctx, sp.row_ptr.data(), sp.ent_off.data(), sp.cols.data(), sp.vals.data()),
-          "sparse set");
-    stage("sparse set to host");
-    // BuildPosterior of the merges and refinement passes on the GPU
-    // (mlp_profile_posterior_cpnp) once the profile pair holds enough sparse
-    // entries to pay for a device round trip (~0.1-0.2 ms; the host adds
-    // ~5e4 entries in that time); the sparse set stays resident.  After
-    // consistency a divergent family's set is nearly empty (C2: 5e4 entries
-    // over 8128 pairs), a similar family's is not.
-    static const int64_t gpu_min = getenv("MLP_PROFILE_GPU_MIN") ? atoll(getenv("MLP_PROFILE_GPU_MIN")) : 100000;
-    std::vector<int32_t> lab1, lab2, map1, map2;
-    cpnp::set_profile_backend([&](const cpnp::Profile& a, const cpnp::Profile& b, const int* w) -> const float* {
-      int64_t entries = 0;
-      for (const Row& x : a)
-        for (const Row& y : b) {
-          const int64_t p = sp.pair(std::min(x.label, y.label), std::max(x.label, y.label));
-          entries += sp.ent_off[p + 1] - sp.ent_off[p];
-        }
-      if (entries < gpu_min) return nullptr;
-      auto fill = [](const cpnp::Profile& p, std::vector<int32_t>& lab, std::vector<int32_t>& map) {
-        lab.clear();
-        map.clear();
-        for (const Row& r : p) {   // Sequence::GetMapping: 0, then the column of each residue
-          lab.push_back(r.label);
-          map.push_back(0);
-          for (int c = 1; c <= r.length(); c++)
-            if (r.data[c] != '-') map.push_back(c);
-        }
-      };
-      fill(a, lab1, map1);
-      fill(b, lab2, map2);
-      const int rc = mlp_profile_posterior_cpnp(ctx, w, (int)a.size(), lab1.data(), a[0].length(), map1.data(),
-                                                (int)b.size(), lab2.data(), b[0].length(), map2.data(), nullptr);
-      if (rc == MLP_ERR_STATE) return nullptr;   // a profile wider than an LDS row: the host computes it
-      check(ctx, rc, "profile posterior");
-      return mlp_profile_result(ctx);
-    });
-    // Profile posterior and MEA both on the device (mlp_profile_mea): only
-    // the path (and the few cells a refinement scores) come back.  Opt-in:
-    // the device MEA is a chain of dependent steps (8 waves over 64-row
-    // strips) and measured slower than the host's at C3 (QuickProbs
-    // refinement: 1.52 ms a call against ~1 ms), so by default
-    // (MLP_MEA_GPU_MIN unset) every MEA runs on the host.
-    static const int64_t mea_min = getenv("MLP_MEA_GPU_MIN") ? atoll(getenv("MLP_MEA_GPU_MIN")) : INT64_MAX;
-    cpnp::set_mea_backend([&](const cpnp::Profile& a, const cpnp::Profile& b, const int* w,
-                              const std::vector<int64_t>* cells, std::vector<float>* vals, std::string& path,
-                              float* score) -> bool {
-      if (mlp_ctx_is_host(ctx) || mea_min == INT64_MAX) return false;
-      const int L1 = a[0].length(), L2 = b[0].length();
-      if ((int64_t)L1 * L2 < mea_min) return false;
-      auto fill = [](const cpnp::Profile& p, std::vector<int32_t>& lab, std::vector<int32_t>& map) {
-        lab.clear();
-        map.clear();
-        for (const Row& r : p) {
-          lab.push_back(r.label);
-          map.push_back(0);
-          for (int c = 1; c <= r.length(); c++)
-            if (r.data[c] != '-') map.push_back(c);
-        }
-      };
-      fill(a, lab1, map1);
-      fill(b, lab2, map2);
-      check(ctx, mlp_profile_defer(ctx, 1), "profile posterior");
-      const int rc = mlp_profile_posterior_cpnp(ctx, w, (int)a.size(), lab1.data(), L1, map1.data(), (int)b.size(),
-                                                lab2.data(), L2, map2.data(), nullptr);
-      if (rc == MLP_ERR_STATE) {   // a profile wider than an LDS row: the host computes it
-        check(ctx, mlp_profile_defer(ctx, 0), "profile posterior");
-        return false;
-      }
-      check(ctx, rc, "profile posterior");
-      if (cells && !cells->empty())
-        check(ctx, mlp_profile_gather(ctx, (int64_t)cells->size(), cells->data(), vals->data()), "profile posterior");
-      path.resize((size_t)L1 + L2);
-      int32_t n = 0;
-      check(ctx, mlp_profile_mea(ctx, &path[0], &n, score), "MEA");
-      path.resize(n);
-      check(ctx, mlp_profile_defer(ctx, 0), "profile posterior");
-      return true;
-    });
-    if (progressive) {
-      aln = cpnp::progressive_alignment(seqs, sp, tree, pid, opt);
-      stage("progressive + refinement");
-    } else {
-      aln = cpnp::graph_alignment(seqs, sp);
-      stage("alignment graph");
-      aln = cpnp::np_refinement(std::move(aln), sp, D, opt);
-      stage("refinement");
-    }
-  }
-  if (getenv("MLP_CLI_TIMES")) {
-    double tp, tm;
-    int64_t nc, nd;
-    cpnp::profile_times(&tp, &tm, &nc, &nd);
-    fprintf(stderr, "[host] profile posteriors %.3f s (%lld calls, %lld on the GPU), MEA %.3f s\n", tp, (long long)nc,
-            (long long)nd, tm);
-  }
-  mlp_ctx_destroy(ctx);
-  stage("context teardown");
-  std::string out;
-  cpnp::write_mfa(out, aln);
-  if (outname.empty()) {
+  if (outname.empty() || just_features) {   // the -G line always goes to stdout (CPNP/MSA.cpp:163)
     fwrite(out.data(), 1, out.size(), stdout);
   } else {
     FILE* f = fopen(outname.c_str(), "wb");
@@ -375,6 +152,6 @@ int main(int argc, char** argv) {
     fwrite(out.data(), 1, out.size(), f);
     fclose(f);
   }
-  stage("output");
+  mlpr::stage("output");
   return 0;
 }

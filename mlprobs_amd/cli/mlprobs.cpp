@@ -1,0 +1,239 @@
+// mlprobs -- the MLProbs pipeline driver (kuangmeng/MLProbs MLProbs.py) over
+// the MI355X aligners, one process per family:
+//
+//   mlprobs [options] in.fa [out.msa]      (MLProbs.py in.fa out.msa)
+//
+// writes the final MSA to out.msa (default result.msa, MLProbs.py:33) and the
+// reference's "[MAIN STEP]" / "[ELAPSED TIME]" progress on stdout.  The
+// aligners run in-process (pipeline.h, runners.h); options:
+//   --models DIR      forests + normalisation files (default: the
+//                     classifier/ directory next to this binary's package)
+//   --cpnp CMD --quickprobs CMD
+//                     run the stages as external commands instead, exactly
+//                     as MLProbs.py does (the reference CLIs built from
+//                     source: the pipeline's CPU baseline)
+//   --tmp DIR         scratch for the external commands' region files
+//   --trace FILE      a JSON record of the stages (features, classes, column
+//                     scores, regions, per-stage seconds)
+//   -q                no progress lines
+// Exit status 0; 1 where the reference pipeline raises a Python exception
+// (no output written).
+#include <limits.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <unistd.h>
+
+#include <string>
+
+#include "pipeline.h"
+
+static std::string self_dir() {
+  char buf[PATH_MAX];
+  const ssize_t n = readlink("/proc/self/exe", buf, sizeof buf - 1);
+  if (n <= 0) return ".";
+  buf[n] = 0;
+  std::string p(buf);
+  return p.substr(0, p.rfind('/'));
+}
+
+static std::string json_str(const std::string& s) {
+  std::string r = "\"";
+  for (unsigned char c : s) {
+    if (c == '"' || c == '\\') r += '\\', r += (char)c;
+    else if (c < 0x20) {
+      char b[8];
+      snprintf(b, sizeof b, "\\u%04x", c);
+      r += b;
+    } else r += (char)c;
+  }
+  return r + "\"";
+}
+
+static std::string json_num(double v) {
+  char b[40];
+  snprintf(b, sizeof b, "%.17g", v);
+  return b;
+}
+
+static void write_trace(const std::string& path, const mlpp::Trace& tr, const std::string& tools) {
+  std::string j = "{";
+  j += "\"tools\": " + json_str(tools);
+  j += ", \"features_line\": " + json_str(tr.features_line);
+  j += ", \"features1\": [";
+  for (size_t i = 0; i < tr.features1.size(); i++) j += (i ? ", " : "") + json_num(tr.features1[i]);
+  j += "], \"class1\": " + std::to_string(tr.class1);
+  j += ", \"killed_stage\": " + std::to_string(tr.killed_stage);
+  j += ", \"un_sp\": " + json_num(tr.cs.un_sp) + ", \"sd_un_sp\": " + json_num(tr.cs.sd) +
+       ", \"peak_length_ratio\": " + json_num(tr.cs.peak) + ", \"len_seqs\": " + std::to_string(tr.cs.lens) +
+       ", \"len_family\": " + std::to_string(tr.cs.nkeys);
+  j += ", \"col_score\": [";
+  for (size_t i = 0; i < tr.cs.col.size(); i++) j += (i ? ", " : "") + json_num(tr.cs.col[i]);
+  j += "], \"class_region\": " + std::to_string(tr.class_region) + ", \"class_lens\": " + std::to_string(tr.class_lens);
+  j += ", \"regions\": [";
+  for (size_t i = 0; i < tr.regions.size(); i++)
+    j += (i ? ", [" : "[") + std::to_string(tr.regions[i].first) + ", " + std::to_string(tr.regions[i].second) + "]";
+  j += "], \"realigned\": [";
+  for (size_t i = 0; i < tr.realigned.size(); i++) j += (i ? ", " : "") + json_str(tr.realigned[i]);
+  j += "], \"kept_original\": [";
+  for (size_t i = 0; i < tr.kept_original.size(); i++) j += (i ? ", " : "") + std::to_string(tr.kept_original[i]);
+  j += "], \"path\": " + json_str(tr.path) + ", \"quickprobs_calls\": " + std::to_string(tr.quickprobs_calls);
+  j += ", \"times\": {";
+  bool first = true;
+  for (const auto& kv : tr.times) {
+    j += (first ? "" : ", ") + json_str(kv.first) + ": " + json_num(kv.second);
+    first = false;
+  }
+  j += "}}\n";
+  FILE* f = fopen(path.c_str(), "wb");
+  if (f) {
+    fwrite(j.data(), 1, j.size(), f);
+    fclose(f);
+  }
+}
+
+// Stage probes for the tests (tests/test_pipeline.py):
+//   --classify NAME   feature rows (whitespace separated) on stdin -> per row
+//                     "class p_0 .. p_k" (the normalised inputs, as the
+//                     classifiers receive them)
+//   --scores FILE     calculateColScore on FILE's text (one trailing newline
+//                     removed, as getstatusoutput gives it) and getAvgColScore
+//                     on FILE, as JSON
+//   --regions         one score vector per stdin line -> the unreliable
+//                     regions for class_lens 0..3 and the reliable regions,
+//                     one JSON line each
+static int probe(const std::string& mode, const std::string& arg, const std::string& models) {
+  if (mode == "--classify") {
+    mlpp::Forest f;
+    std::string err;
+    if (!f.load(models + "/" + arg + ".forest", err)) {
+      fprintf(stderr, "%s\n", err.c_str());
+      return 1;
+    }
+    char line[1 << 16];
+    while (fgets(line, sizeof line, stdin)) {
+      std::vector<double> x;
+      char* p = line;
+      char* end;
+      for (double v; (v = strtod(p, &end)), end != p; p = end) x.push_back(v);
+      if ((int)x.size() != f.n_features) continue;
+      const std::vector<double> pr = f.predict_proba(x);
+      printf("%.17g", f.predict(x));
+      for (double v : pr) printf(" %.17g", v);
+      printf("\n");
+    }
+    return 0;
+  }
+  if (mode == "--scores") {
+    FILE* fh = fopen(arg.c_str(), "rb");
+    if (!fh) return 1;
+    std::string text;
+    char buf[1 << 16];
+    size_t got;
+    while ((got = fread(buf, 1, sizeof buf, fh)) > 0) text.append(buf, got);
+    fclose(fh);
+    std::string t = text;
+    if (!t.empty() && t.back() == '\n') t.pop_back();
+    const mlpp::ColScores cs = mlpp::column_scores(mlpp::parse_dic(mlpp::split_newline(t)));
+    std::string j = "{\"col_score\": [";
+    for (size_t i = 0; i < cs.col.size(); i++) j += (i ? ", " : "") + json_num(cs.col[i]);
+    j += "], \"un_sp\": " + json_num(cs.un_sp) + ", \"sd_un_sp\": " + json_num(cs.sd) +
+         ", \"peak_length_ratio\": " + json_num(cs.peak) + ", \"len_seqs\": " + std::to_string(cs.lens) +
+         ", \"len_family\": " + std::to_string(cs.nkeys) + ", \"error\": " + (cs.error ? "true" : "false") +
+         ", \"avg_col_score\": " + json_num(mlpp::avg_col_score(text)) + "}\n";
+    fwrite(j.data(), 1, j.size(), stdout);
+    return 0;
+  }
+  if (mode == "--regions") {
+    std::string line;
+    char buf[1 << 16];
+    while (fgets(buf, sizeof buf, stdin)) {
+      line = buf;
+      std::vector<double> col;
+      const char* p = line.c_str();
+      char* end;
+      for (double v; (v = strtod(p, &end)), end != p; p = end) col.push_back(v);
+      auto emit = [](const std::vector<std::pair<int64_t, int64_t>>& r) {
+        std::string s = "[";
+        for (size_t i = 0; i < r.size(); i++)
+          s += (i ? ", [" : "[") + std::to_string(r[i].first) + ", " + std::to_string(r[i].second) + "]";
+        return s + "]";
+      };
+      std::string j = "{\"unreliable\": {";
+      for (int cl = 0; cl < 4; cl++)
+        j += (cl ? ", \"" : "\"") + std::to_string(cl) + "\": " + emit(mlpp::unreliable_regions(col, 1.2, 0.0, cl));
+      j += "}, \"reliable\": " + emit(mlpp::reliable_regions(col, 2.0, 0, 0)) + "}\n";
+      fwrite(j.data(), 1, j.size(), stdout);
+    }
+    return 0;
+  }
+  return 2;
+}
+
+int main(int argc, char** argv) {
+  std::string models = self_dir() + "/../classifier", cpnp_cmd, qp_cmd, tmp = "/tmp", trace;
+  bool verbose = true;
+  std::vector<std::string> pos;
+  for (int i = 1; i < argc; i++) {
+    const std::string a = argv[i];
+    auto val = [&]() -> std::string {
+      if (i + 1 >= argc) {
+        fprintf(stderr, "mlprobs: %s needs a value\n", a.c_str());
+        exit(2);
+      }
+      return argv[++i];
+    };
+    if (a == "--models") models = val();
+    else if (a == "--cpnp") cpnp_cmd = val();
+    else if (a == "--quickprobs") qp_cmd = val();
+    else if (a == "--tmp") tmp = val();
+    else if (a == "--trace") trace = val();
+    else if (a == "-q") verbose = false;
+    else if (a == "--classify" || a == "--scores") {
+      const std::string v = val();
+      return probe(a, v, models);
+    } else if (a == "--regions") return probe(a, "", models);
+    else if (a == "-h" || a == "--help") {
+      printf("usage: mlprobs [--models DIR] [--cpnp CMD --quickprobs CMD] [--tmp DIR] [--trace FILE] [-q] in.fa [out.msa]\n");
+      return 0;
+    } else pos.push_back(a);
+  }
+  if (pos.empty()) {
+    fprintf(stderr, "usage: mlprobs [options] in.fa [out.msa]\n");
+    return 2;
+  }
+  const std::string in = pos[0], out = pos.size() > 1 ? pos[1] : "result.msa";
+  mlpp::Models M;
+  std::string err;
+  if (!M.load(models, err)) {
+    fprintf(stderr, "mlprobs: %s\n", err.c_str());
+    return 1;
+  }
+  mlpr::Session session;
+  std::unique_ptr<mlpp::Tools> tools;
+  if (!cpnp_cmd.empty() || !qp_cmd.empty()) {
+    if (cpnp_cmd.empty() || qp_cmd.empty()) {
+      fprintf(stderr, "mlprobs: --cpnp and --quickprobs go together\n");
+      return 2;
+    }
+    tools = mlpp::external_tools(cpnp_cmd, qp_cmd, tmp);
+  } else {
+    tools = mlpp::in_process_tools(&session);
+  }
+  std::string result;
+  mlpp::Trace tr;
+  const bool ok = mlpp::run_pipeline(in, *tools, M, result, tr, err, verbose);
+  if (!trace.empty()) write_trace(trace, tr, tools->name());
+  if (!ok) {
+    fprintf(stderr, "mlprobs: %s\n", err.c_str());
+    return 1;
+  }
+  FILE* f = fopen(out.c_str(), "wb");
+  if (!f) {
+    fprintf(stderr, "mlprobs: cannot write %s\n", out.c_str());
+    return 1;
+  }
+  fwrite(result.data(), 1, result.size(), f);
+  fclose(f);
+  return 0;
+}

@@ -1,10 +1,12 @@
 // msa_host.cpp -- see msa_host.h.
 #include "msa_host.h"
 
+#include <stdexcept>
+
 #include <chrono>
 #include <atomic>
 #include <thread>
-#include <omp.h>
+#include "pool.h"
 
 #include <stdio.h>
 #include <stdlib.h>
@@ -144,10 +146,8 @@ GuideTree build_tree(std::vector<std::vector<float>> dist, int varianceid) {
         }
       }
     }
-    if (bi < 0) {
-      fprintf(stderr, "OOPS: Error occurred while constructing the cluster tree\n\n");
-      exit(-1);
-    }
+    if (bi < 0)   // the reference prints this and exits with -1 (the CLI does, from the exception)
+      throw std::runtime_error("OOPS: Error occurred while constructing the cluster tree\n");
     const int mi = active[bi], mj = active[bj];
     const float half = best * 0.5f;
     GuideTree::Node& par = t.nodes[node];
@@ -380,7 +380,7 @@ std::string mea_path_dispatch(int len1, int len2, const float* post, float* scor
   // but ~1000 x 1000 (QuickProbs C3 refinement) 0.62 -> 0.86 s with every
   // call threaded, hence the 2.5e6-cell floor.
   static const int64_t wave_min = getenv("MLP_MEA_WAVE_MIN") ? atoll(getenv("MLP_MEA_WAVE_MIN")) : 2500000;
-  if (wave_min > 0 && (int64_t)len1 * len2 >= wave_min && len1 >= 128 && omp_get_max_threads() > 1)
+  if (wave_min > 0 && (int64_t)len1 * len2 >= wave_min && len1 >= 128 && mlpr::host_threads() > 1)
     return mea_path_wave(len1, len2, post, score);
   return mea_path_serial(len1, len2, post, score);
 }
@@ -409,10 +409,8 @@ std::string mea_path_wave(int len1, int len2, const float* post, float* score) {
   std::vector<std::atomic<int>> done(nb + 1);
   for (auto& d : done) d.store(0, std::memory_order_relaxed);
   done[0].store(len2 + 1, std::memory_order_relaxed);  // row 0: complete
-  const int T = std::max(1, std::min({omp_get_max_threads(), 16, nb}));
-#pragma omp parallel num_threads(T)
-  {
-    const int t = omp_get_thread_num(), nt = omp_get_num_threads();
+  const int T = std::max(1, std::min({mlpr::host_threads(), 16, nb}));
+  mlpr::parallel(T, [&](int t, int nt) {
     for (int b = t; b < nb; b += nt) {
       const int i0 = 1 + b * RB, i1 = std::min(len1, i0 + RB - 1);
       for (int i = i0; i <= i1; i++) {
@@ -455,7 +453,7 @@ std::string mea_path_wave(int len1, int len2, const float* post, float* score) {
         done[b + 1].store(j1 + 1, std::memory_order_release);
       }
     }
-  }
+  });
   if (score) *score = Vp[(size_t)len1 * W2 + len2];
   std::string path;
   int r = len1, c = len2;
@@ -531,13 +529,13 @@ static Row add_gaps(const Row& r, const std::string& path, char id) {   // Seque
 
 // threads for a profile of n rows x L columns (data movement only; small
 // profiles stay serial)
-static int row_threads(size_t n, size_t L) { return n * L > 200000 ? std::max(1, std::min(16, omp_get_max_threads())) : 1; }
+static int row_threads(size_t n, size_t L) { return n * L > 200000 ? mlpr::host_threads() : 1; }
 
 Profile merge(const Profile& a, const Profile& b, const std::string& path, bool sort_by_label) {
   const int na = (int)a.size(), nr = (int)(a.size() + b.size());
   Profile out(nr);
-#pragma omp parallel for num_threads(row_threads(nr, path.size())) schedule(static)
-  for (int k = 0; k < nr; k++) out[k] = k < na ? add_gaps(a[k], path, 'X') : add_gaps(b[k - na], path, 'Y');
+  mlpr::parallel_for(nr, row_threads(nr, path.size()),
+                     [&](int64_t k) { out[k] = k < na ? add_gaps(a[k], path, 'X') : add_gaps(b[k - na], path, 'Y'); });
   // MultiSequence::SortByLabel (a swap sort; the labels are distinct, so any
   // sort gives its order)
   if (sort_by_label)
@@ -549,20 +547,18 @@ Profile project(const Profile& p, const std::set<int>& idx) {
   const int L = p[rows[0]].length();
   const int nt = row_threads(rows.size(), (size_t)L);
   std::vector<char> has(L + 1, 0);
-#pragma omp parallel for num_threads(nt) schedule(static)
-  for (int c0 = 1; c0 <= L; c0 += 256) {
-    const int c1 = std::min(L, c0 + 255);
+  mlpr::parallel_for((L + 255) / 256, nt, [&](int64_t blk) {
+    const int c0 = 1 + 256 * (int)blk, c1 = std::min(L, c0 + 255);
     for (int k : rows) {
       const char* d = p[k].data.data();
       for (int i = c0; i <= c1; i++) has[i] |= d[i] != '-';
     }
-  }
+  });
   std::vector<int> keep;
   for (int i = 1; i <= L; i++)
     if (has[i]) keep.push_back(i);
   Profile out(rows.size());
-#pragma omp parallel for num_threads(nt) schedule(static)
-  for (int q = 0; q < (int)rows.size(); q++) {
+  mlpr::parallel_for((int64_t)rows.size(), nt, [&](int64_t q) {
     const Row& src = p[rows[q]];
     Row& r = out[q];
     r.header = src.header;
@@ -571,7 +567,7 @@ Profile project(const Profile& p, const std::set<int>& idx) {
     r.data.resize(keep.size() + 1);
     r.data[0] = '@';
     for (size_t c = 0; c < keep.size(); c++) r.data[c + 1] = src.data[keep[c]];
-  }
+  });
   return out;
 }
 

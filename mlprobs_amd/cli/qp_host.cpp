@@ -2,7 +2,7 @@
 #include "qp_host.h"
 
 #include <math.h>
-#include <omp.h>
+#include <chrono>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -15,6 +15,7 @@
 #include <stdexcept>
 
 #include "msa_host.h"  // cpnp::mea_path: QuickProbs' computeAlignment is the same MEA recurrence
+#include "pool.h"
 
 namespace qph {
 
@@ -30,6 +31,10 @@ bool load_fasta(const std::string& path, std::vector<Seq>& seqs, std::string& ou
   size_t got;
   while ((got = fread(tmp, 1, sizeof tmp, f)) > 0) buf.append(tmp, got);
   fclose(f);
+  return load_fasta_text(buf, seqs, out_msg, err);
+}
+
+bool load_fasta_text(const std::string& buf, std::vector<Seq>& seqs, std::string& out_msg, std::string& err) {
   // std::istream::getline(buffer, MAX_LINE_LENGTH = 10000) semantics
   // (SequenceIO.h:64): a line of 10000+ characters stores its first 9999 and
   // fails the stream, which ends the read; a final unterminated line counts.
@@ -124,8 +129,7 @@ void Sparse::build_views() {
   trow_ptr.assign(P > 0 ? trp_off[P] : 1, 0);
   tcols.resize(cols.size());
   tvals.resize(vals.size());
-#pragma omp parallel for schedule(dynamic)
-  for (int64_t p = 0; p < P; p++) {
+  mlpr::parallel_for_dynamic(P, mlpr::host_threads(), [&](int64_t p) {
     int a = 0;
     int64_t q = p;
     while (q >= n - 1 - a) { q -= n - 1 - a; ++a; }
@@ -151,7 +155,7 @@ void Sparse::build_views() {
         tc[k] = (uint16_t)i;
         tv[k] = v[e];
       }
-  }
+  });
   for (int a = 0, p = 0; a < n; a++)
     for (int b = a + 1; b < n; b++, p++) {
       blocks[(size_t)a * n + b] = Block{row_ptr.data() + rp_off[p], cols.data() + ent_off[p], vals.data() + ent_off[p]};
@@ -288,9 +292,7 @@ void build_posterior(const std::vector<float>& w, const Profile& A, const Profil
   for (size_t i = 0; i < A.size(); i++) mapping(A[i], m1[i]);
   for (size_t j = 0; j < B.size(); j++) mapping(B[j], m2[j]);
   const int nt = std::max(1, std::min(threads, L1 / 16));
-#pragma omp parallel num_threads(nt)
-  {
-    const int t = omp_get_thread_num(), T = omp_get_num_threads();
+  mlpr::parallel(nt, [&](int t, int T) {
     const int r0 = 1 + (int)((int64_t)L1 * t / T), r1 = 1 + (int)((int64_t)L1 * (t + 1) / T);  // dense rows [r0, r1)
     std::fill(post.begin() + (size_t)r0 * W2, post.begin() + (size_t)r1 * W2, 0.f);
     for (size_t i = 0; i < A.size(); i++) {
@@ -314,7 +316,7 @@ void build_posterior(const std::vector<float>& w, const Profile& A, const Profil
         }
       }
     }
-  }
+  });
 }
 
 // Sequence::AddGaps (Sequence.cpp:67-92)
@@ -335,7 +337,7 @@ Seq add_gaps(const Seq& s, const std::string& path, char id) {
 // time split of the host stages (MLP_CLI_TIMES)
 double g_t_post = 0, g_t_mea = 0, g_t_merge = 0, g_t_update = 0, g_t_split = 0;
 int64_t g_n_terms = 0;
-double now() { return omp_get_wtime(); }
+double now() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
 
 // ConstructionStage::alignAlignments (ConstructionStage.cpp:86-126)
 Profile align_alignments(const std::vector<float>& w, const Profile& A, const Profile& B, const PosteriorBackend& be,
@@ -361,8 +363,7 @@ Profile align_alignments(const std::vector<float>& w, const Profile& A, const Pr
   Profile r(A.size() + B.size());
   const int na = (int)A.size(), nr = (int)r.size();
   const int nt = (int64_t)nr * (int64_t)path.size() > 200000 ? std::max(1, threads) : 1;
-#pragma omp parallel for num_threads(nt) schedule(static)
-  for (int k = 0; k < nr; k++) r[k] = k < na ? add_gaps(A[k], path, 'X') : add_gaps(B[k - na], path, 'Y');
+  mlpr::parallel_for(nr, nt, [&](int64_t k) { r[k] = k < na ? add_gaps(A[k], path, 'X') : add_gaps(B[k - na], path, 'Y'); });
   // MultiSequence::SortByLabel (the labels are distinct)
   std::sort(r.begin(), r.end(), [](const Seq& a, const Seq& b) { return a.sort_label < b.sort_label; });
   g_t_merge += now() - t2;
@@ -386,20 +387,18 @@ Profile extract_subset(const Profile& aln, const std::set<int>& idx, int threads
   const int nt = (int64_t)rows.size() * L > 200000 ? std::max(1, threads) : 1;
   std::vector<char> keep(L + 1, 0);
   // columns not gapped in every selected row (column blocks in parallel)
-#pragma omp parallel for num_threads(nt) schedule(static)
-  for (int c0 = 1; c0 <= L; c0 += 256) {
-    const int c1 = std::min(L, c0 + 255);
+  mlpr::parallel_for((L + 255) / 256, nt, [&](int64_t blk) {
+    const int c0 = 1 + 256 * (int)blk, c1 = std::min(L, c0 + 255);
     for (int i : rows) {
       const char* d = aln[i].data.data();
       for (int c = c0; c <= c1; c++) keep[c] |= d[c] != '-';
     }
-  }
+  });
   std::vector<int> cols;
   for (int c = 1; c <= L; c++)
     if (keep[c]) cols.push_back(c);
   Profile r(rows.size());
-#pragma omp parallel for num_threads(nt) schedule(static)
-  for (int k = 0; k < (int)rows.size(); k++) {
+  mlpr::parallel_for((int64_t)rows.size(), nt, [&](int64_t k) {
     const Seq& src = aln[rows[k]];
     Seq& s = r[k];
     s.header = src.header;
@@ -409,7 +408,7 @@ Profile extract_subset(const Profile& aln, const std::set<int>& idx, int threads
     s.data[0] = '@';
     const char* d = src.data.data();
     for (size_t q = 0; q < cols.size(); q++) s.data[q + 1] = d[cols[q]];
-  }
+  });
   return r;
 }
 
@@ -442,14 +441,13 @@ struct ColumnRefiner {
     // (integers below 2^24 are exact in float); column blocks in parallel
     std::vector<int> gaps(L, 0);
     const int nt = (int64_t)n * L > 200000 ? std::max(1, threads) : 1;
-#pragma omp parallel for num_threads(nt) schedule(static)
-    for (int c0 = 0; c0 < L; c0 += 256) {
-      const int c1 = std::min(L, c0 + 256);
+    mlpr::parallel_for((L + 255) / 256, nt, [&](int64_t blk) {
+      const int c0 = 256 * (int)blk, c1 = std::min(L, c0 + 256);
       for (int i = 0; i < n; i++) {
         const char* d = aln[i].data.data() + 1;
         for (int c = c0; c < c1; c++) gaps[c] += d[c] == '-';
       }
-    }
+    });
     for (int c = 0; c < (int)scores.size(); c++) {
       scores[c].first = c;
       scores[c].second += (float)gaps[c];

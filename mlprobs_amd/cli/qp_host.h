@@ -33,6 +33,8 @@ using Profile = std::vector<Seq>;
 // on stdout by the reference, one line per illegal character) and `err`
 // (the exception text).
 bool load_fasta(const std::string& path, std::vector<Seq>& seqs, std::string& out_msg, std::string& err);
+// the same on the file's bytes
+bool load_fasta_text(const std::string& text, std::vector<Seq>& seqs, std::string& out_msg, std::string& err);
 
 // SequenceIO::saveFasta (SequenceIO.cpp:176-199): 60 columns.
 void write_fasta(std::string& out, const Profile& p);

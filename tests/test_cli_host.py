@@ -24,9 +24,10 @@ CLI = os.path.join(ROOT, 'mlprobs_amd', 'cli')
 @pytest.fixture(scope='module')
 def driver(tmp_path_factory):
     out = str(tmp_path_factory.mktemp('drv') / 'host_driver')
-    subprocess.check_call(['g++', '-O2', '-std=c++17', '-ffp-contract=off', '-fopenmp', '-I', CLI,
+    subprocess.check_call(['g++', '-O2', '-std=c++17', '-ffp-contract=off', '-pthread', '-I', CLI,
                            os.path.join(ROOT, 'tests', 'native', 'host_driver.cpp'),
-                           os.path.join(CLI, 'msa_host.cpp'), os.path.join(CLI, 'np_host.cpp'), '-o', out])
+                           os.path.join(CLI, 'msa_host.cpp'), os.path.join(CLI, 'np_host.cpp'),
+                           os.path.join(CLI, 'pool.cpp'), '-o', out])
     return out
 
 

@@ -1,0 +1,193 @@
+"""The MLProbs pipeline driver (mlprobs_amd/cli/mlprobs: MLProbs.py and
+utils/*.py restated in C++) on the CPU.
+
+Pinned against tests/golden/pipeline/, made by tests/golden/gen_pipeline.py
+from the reference's own utils/*.py modules driving the reference CLIs built
+from source:
+  * every stage of 24 TEST/ox + TEST/sabre families (the -G line, classifier
+    inputs and decisions, column scores, regions, realigned regions) and the
+    final MSA bytes, with the aligners in-process on the host path;
+  * the same families with the stages run as external commands (the
+    reference CLIs), i.e. the orchestration alone against the reference's;
+  * calculateColScore / getAvgColScore on 18 published MLProbs outputs and
+    both region detectors on 60 score vectors, exact to the last bit.
+The forests: the C++ evaluator against tests/forest_ref.py, and both against
+scikit-learn's own predict_proba over the same exported arrays (the 0.21.3
+pickles cannot be loaded here: the classifier stage is "parity unpinned"
+against the original model objects).
+"""
+import json
+import os
+import subprocess
+import tempfile
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import pytest
+
+import forest_ref
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, 'mlprobs_amd', 'cli', 'mlprobs')
+FIX = os.path.join(ROOT, 'tests', 'golden', 'pipeline')
+REF_CP = os.path.join(ROOT, 'oracle', '_ref', 'c_p_np_aln_ft')
+REF_QP = os.path.join(ROOT, 'oracle', '_ref', 'quickprobs')
+FIXED_TIME = '1700000000'
+ENV = dict(os.environ, MLP_SRAND_TIME=FIXED_TIME, MLP_HOST_THREADS='2', OMP_NUM_THREADS='2')
+
+
+def families():
+    with open(os.path.join(FIX, 'manifest.json')) as fh:
+        return [f['tag'] for f in json.load(fh)['families']]
+
+
+def load(tag):
+    with open(os.path.join(FIX, f'{tag}.json')) as fh:
+        return json.load(fh)
+
+
+def run_pipeline(tag, tmp, extra=(), env=ENV):
+    out = os.path.join(tmp, f'{tag}.msa')
+    trace = os.path.join(tmp, f'{tag}.trace.json')
+    r = subprocess.run([BIN, '-q', '--trace', trace, *extra, os.path.join(FIX, f'{tag}.fa'), out],
+                       capture_output=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr.decode()
+    with open(out, encoding='latin-1') as fh:
+        res = fh.read()
+    with open(trace) as fh:
+        return res, json.load(fh)
+
+
+def check_trace(rec, tr, tag):
+    assert tr['features_line'] == rec['features_line'], tag
+    assert tr['features1'] == rec['features1'], tag
+    assert tr['class1'] == rec['class1'], tag
+    assert tr['killed_stage'] == rec['killed_stage'], tag
+    assert tr['col_score'] == rec['col_score'], tag
+    for k in ('un_sp', 'sd_un_sp', 'peak_length_ratio', 'len_seqs', 'len_family', 'class_region', 'class_lens'):
+        assert tr[k] == rec[k], (tag, k, tr[k], rec[k])
+    assert tr['regions'] == rec['regions'], tag
+    realigned = sorted(f for f in rec['region_files'] if f.endswith('.unreliable'))
+    if tr['path'].endswith('whole-family'):
+        realigned = []
+    assert sorted(tr['realigned']) == realigned, tag
+
+
+@pytest.mark.parametrize('tag', families())
+def test_pipeline_host_path(tag, tmp_path):
+    """mlprobs with both aligners in-process (host context: every family here
+    is under 4e6 pair-cells): every stage and the final bytes."""
+    rec = load(tag)
+    res, tr = run_pipeline(tag, str(tmp_path))
+    check_trace(rec, tr, tag)
+    assert res == rec['final'], tag
+
+
+@pytest.mark.skipif(not (os.path.exists(REF_CP) and os.path.exists(REF_QP)),
+                    reason='reference CLIs not built (oracle/_ref)')
+def test_pipeline_external_reference_clis(tmp_path):
+    """The orchestration alone: mlprobs driving the reference CLIs built from
+    source as external commands reproduces the reference pipeline's output."""
+    cp = f'env REF_FIXED_TIME={FIXED_TIME} taskset -c 0 {REF_CP}'
+    qp = f'{REF_QP} -t 1'
+
+    def one(tag):
+        rec = load(tag)
+        res, tr = run_pipeline(tag, str(tmp_path), ['--cpnp', cp, '--quickprobs', qp, '--tmp', str(tmp_path)])
+        check_trace(rec, tr, tag)
+        return tag, res == rec['final']
+
+    with ThreadPoolExecutor(4) as ex:
+        bad = [t for t, ok in ex.map(one, families()) if not ok]
+    assert not bad, bad
+
+
+def test_column_scores_fixture(tmp_path):
+    with open(os.path.join(FIX, 'scores.json')) as fh:
+        fx = json.load(fh)
+    assert len(fx['msas']) >= 15
+    for m in fx['msas']:
+        p = tmp_path / 'msa.txt'
+        p.write_bytes(m['text'].encode('latin-1'))
+        r = subprocess.run([BIN, '--scores', str(p)], capture_output=True, timeout=60, check=True)
+        got = json.loads(r.stdout)
+        assert got['col_score'] == m['col_score'], m['name']
+        for k in ('un_sp', 'sd_un_sp', 'peak_length_ratio', 'len_seqs', 'len_family', 'avg_col_score'):
+            assert got[k] == m[k], (m['name'], k, got[k], m[k])
+
+
+def test_region_detectors_fixture():
+    with open(os.path.join(FIX, 'scores.json')) as fh:
+        fx = json.load(fh)
+    lines = ''.join(' '.join(repr(v) for v in r['col_score']) + '\n' for r in fx['regions'])
+    r = subprocess.run([BIN, '--regions'], input=lines.encode(), capture_output=True, timeout=60, check=True)
+    got = [json.loads(x) for x in r.stdout.decode().splitlines()]
+    assert len(got) == len(fx['regions'])
+    for g, want in zip(got, fx['regions']):
+        assert g['unreliable'] == want['unreliable']
+        assert g['reliable'] == want['reliable']
+
+
+def _sklearn_forest(f):
+    """A scikit-learn RandomForestClassifier holding the exported arrays
+    (leaf values as class fractions, as scikit-learn >= 1.4 stores them)."""
+    from sklearn.ensemble import RandomForestClassifier
+    from sklearn.tree import DecisionTreeClassifier, _tree
+    nf, classes = f['n_features'], f['classes']
+    k = len(classes)
+    ests = []
+    for left, right, feat, thr, val in f['trees']:
+        n = len(left)
+        t = _tree.Tree(nf, np.array([k], dtype=np.intp), 1)
+        nodes = np.zeros(n, dtype=_tree.NODE_DTYPE)
+        nodes['left_child'], nodes['right_child'] = left, right
+        nodes['feature'] = np.where(left == -1, -2, feat)
+        nodes['threshold'] = np.where(left == -1, -2.0, thr)
+        nodes['n_node_samples'], nodes['weighted_n_node_samples'] = 1, 1.0
+        depth = np.zeros(n, int)
+        for i in range(n):
+            if left[i] != -1:
+                depth[left[i]] = depth[right[i]] = depth[i] + 1
+        s = val.sum(axis=1, keepdims=True)
+        s[s == 0] = 1
+        t.__setstate__({'max_depth': int(depth.max()), 'node_count': n, 'nodes': nodes,
+                        'values': (val / s).reshape(n, 1, k).copy()})
+        d = DecisionTreeClassifier()
+        d.tree_, d.n_classes_, d.classes_, d.n_outputs_, d.n_features_in_ = t, k, classes, 1, nf
+        ests.append(d)
+    clf = RandomForestClassifier(n_estimators=len(ests))
+    clf.estimators_, clf.classes_, clf.n_classes_, clf.n_outputs_, clf.n_features_in_ = ests, classes, k, 1, nf
+    return clf
+
+
+def _samples(f, n, seed):
+    """Uniform inputs plus inputs sitting exactly on split thresholds (after
+    the float32 cast the classifiers apply)."""
+    rng = np.random.default_rng(seed)
+    nf = f['n_features']
+    X = rng.uniform(-0.2, 1.2, (n, nf))
+    thr = np.concatenate([t[3][t[0] != -1] for t in f['trees']])
+    feat = np.concatenate([t[2][t[0] != -1] for t in f['trees']])
+    Xb = rng.uniform(-0.2, 1.2, (n, nf))
+    idx = rng.integers(0, len(thr), n)
+    Xb[np.arange(n), feat[idx]] = thr[idx].astype(np.float32)
+    return np.concatenate([X, Xb])
+
+
+@pytest.mark.parametrize('name', ['branch', 'regions', 'seq_lens'])
+def test_forest_evaluators(name):
+    f = forest_ref.load_forest(name)
+    X = _samples(f, 1500, 11)
+    want = np.array([forest_ref.predict_proba(f, x) for x in X])
+    want_cls = f['classes'][np.argmax(want, axis=1)]
+    rows = ''.join(' '.join(repr(float(v)) for v in x) + '\n' for x in X)
+    r = subprocess.run([BIN, '--classify', name], input=rows.encode(), capture_output=True, timeout=120, check=True)
+    got = np.array([[float(v) for v in line.split()] for line in r.stdout.decode().splitlines()])
+    np.testing.assert_array_equal(got[:, 0], want_cls)
+    np.testing.assert_array_equal(got[:, 1:], want)
+    try:
+        clf = _sklearn_forest(f)
+    except ImportError:
+        pytest.skip('scikit-learn not importable')
+    np.testing.assert_array_equal(clf.predict_proba(X), want)
+    np.testing.assert_array_equal(clf.predict(X), want_cls)

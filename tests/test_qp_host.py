@@ -33,9 +33,10 @@ def golden_name(name, args):
 @pytest.fixture(scope='module')
 def qdriver(tmp_path_factory):
     out = str(tmp_path_factory.mktemp('qdrv') / 'qp_host_driver')
-    subprocess.check_call(['g++', '-O2', '-std=c++17', '-ffp-contract=off', '-fopenmp', '-I', CLI,
+    subprocess.check_call(['g++', '-O2', '-std=c++17', '-ffp-contract=off', '-pthread', '-I', CLI,
                            os.path.join(ROOT, 'tests', 'native', 'qp_host_driver.cpp'),
-                           os.path.join(CLI, 'qp_host.cpp'), os.path.join(CLI, 'msa_host.cpp'), '-o', out])
+                           os.path.join(CLI, 'qp_host.cpp'), os.path.join(CLI, 'msa_host.cpp'),
+                           os.path.join(CLI, 'pool.cpp'), '-o', out])
     return out
 
 
