@@ -55,6 +55,7 @@ def parse():
     ap.add_argument('--no-e2e', action='store_true',
                     help='skip the end-to-end c_p_np_aln / quickprobs family timings')
     ap.add_argument('--no-qp', action='store_true', help='skip the QuickProbs posterior/consistency timings')
+    ap.add_argument('--e2e-runs', type=int, default=3, help='fresh-process runs per end-to-end leg')
     return ap.parse_args()
 
 
@@ -273,40 +274,144 @@ def relax_leg(fam, args, n, lens, total_cells):
     return res
 
 
+# ---- MSA readouts: MLProbs' own SP score and TC
+_ALPHA = 'ARNDCQEGHILKMFPSTWYV'
+_BLOSUM62 = np.array([
+    [4, -1, -2, -2, 0, -1, -1, 0, -2, -1, -1, -1, -1, -2, -1, 1, 0, -3, -2, 0],
+    [-1, 5, 0, -2, -3, 1, 0, -2, 0, -3, -2, 2, -1, -3, -2, -1, -1, -3, -2, -3],
+    [-2, 0, 6, 1, -3, 0, 0, 0, 1, -3, -3, 0, -2, -3, -2, 1, 0, -4, -2, -3],
+    [-2, -2, 1, 6, -3, 0, 2, -1, -1, -3, -4, -1, -3, -3, -1, 0, -1, -4, -3, -3],
+    [0, -3, -3, -3, 9, -3, -4, -3, -3, -1, -1, -3, -1, -2, -3, -1, -1, -2, -2, -1],
+    [-1, 1, 0, 0, -3, 5, 2, -2, 0, -3, -2, 1, 0, -3, -1, 0, -1, -2, -1, -2],
+    [-1, 0, 0, 2, -4, 2, 5, -2, 0, -3, -3, 1, -2, -3, -1, 0, -1, -3, -2, -2],
+    [0, -2, 0, -1, -3, -2, -2, 6, -2, -4, -4, -2, -3, -3, -2, 0, -2, -2, -3, -3],
+    [-2, 0, 1, -1, -3, 0, 0, -2, 8, -3, -3, -1, -2, -1, -2, -1, -2, -2, 2, -3],
+    [-1, -3, -3, -3, -1, -3, -3, -4, -3, 4, 2, -3, 1, 0, -3, -2, -1, -3, -1, 3],
+    [-1, -2, -3, -4, -1, -2, -3, -4, -3, 2, 4, -2, 2, 0, -3, -2, -1, -2, -1, 1],
+    [-1, 2, 0, -1, -3, 1, 1, -2, -1, -3, -2, 5, -1, -3, -1, 0, -1, -3, -2, -2],
+    [-1, -1, -2, -3, -1, 0, -2, -3, -2, 1, 2, -1, 5, 0, -2, -1, -1, -1, -1, 1],
+    [-2, -3, -3, -3, -2, -3, -3, -3, -1, 0, 0, -3, 0, 6, -4, -2, -2, 1, 3, -1],
+    [-1, -2, -2, -1, -3, -1, -1, -2, -2, -3, -3, -1, -2, -4, 7, -1, -1, -4, -3, -2],
+    [1, -1, 1, 0, -1, 0, 0, 0, -1, -2, -2, 0, -1, -2, -1, 4, 1, -3, -2, -2],
+    [0, -1, 0, -1, -1, -1, -1, -2, -2, -1, -1, -1, -1, -2, -1, 1, 5, -2, -2, 0],
+    [-3, -3, -4, -4, -2, -2, -3, -2, -2, -3, -2, -3, -1, 1, -4, -3, -2, 11, 2, -3],
+    [-2, -2, -2, -3, -2, -1, -2, -3, 2, -1, -1, -2, -1, 3, -3, -2, -2, 2, 7, -1],
+    [0, -3, -3, -3, -1, -2, -2, -3, -3, 3, 1, -2, 1, -1, -2, -2, 0, -3, -1, 4]], np.int64)
+
+
+def msa_rows(text):
+    """Header line -> row, as MLProbs' utils parse an MSA (later duplicates win)."""
+    rows, key = {}, None
+    for line in text.splitlines():
+        if line.startswith('>'):
+            key = line
+            rows[key] = ''
+        elif key is not None:
+            rows[key] += line.replace('\r', '')
+    return rows
+
+
+def sp_score(text):
+    """MLProbs' un_sp (utils/calculate_column_scores.py:37-82): the mean over
+    columns of the BLOSUM62 sum of pairs / (N (N - 1) / 2), gaps and
+    non-standard letters scoring 0; exact integer pair sums per column."""
+    rows = msa_rows(text)
+    if len(rows) < 2:
+        return None
+    L = min(len(r) for r in rows.values())
+    idx = np.full(256, 20, np.int64)
+    for k, c in enumerate(_ALPHA):
+        idx[ord(c)] = k
+    A = np.stack([idx[np.frombuffer(r[:L].encode('latin-1'), np.uint8)] for r in rows.values()])
+    cnt = np.zeros((L, 21), np.int64)
+    for k in range(21):
+        cnt[:, k] = (A == k).sum(0)
+    c = cnt[:, :20]
+    pair = np.einsum('la,ab,lb->l', c, _BLOSUM62, c) - (c * np.diag(_BLOSUM62)).sum(1)
+    n = len(rows)
+    col = (pair // 2) / (n * (n - 1) / 2)
+    return sum(col.tolist()) / L if L else 0.0   # summed in column order, like the reference
+
+
+def tc_score(text, ref_text):
+    """Total-column score: the fraction of `text`'s columns that are also
+    columns of `ref_text`, a column being the tuple (per shared header) of the
+    residue index each row has there (-1 = gap)."""
+    a, b = msa_rows(text), msa_rows(ref_text)
+    keys = sorted(set(a) & set(b))
+    if not keys:
+        return None
+
+    def columns(rows):
+        cols = []
+        mats = []
+        for k in keys:
+            r = np.frombuffer(rows[k].encode('latin-1'), np.uint8)
+            res = (r != ord('-')) & (r != ord('.'))
+            mats.append(np.where(res, np.cumsum(res) - 1, -1))
+        L = min(len(m) for m in mats)
+        M = np.stack([m[:L] for m in mats])
+        for j in range(L):
+            if (M[:, j] >= 0).any():
+                cols.append(M[:, j].tobytes())
+        return cols
+
+    ca, cb = columns(a), set(columns(b))
+    return sum(c in cb for c in ca) / max(len(ca), 1)
+
+
+def _stages(stderr):
+    st = {}
+    for line in stderr.splitlines():
+        if line.startswith('[stage] '):
+            name, sec = line[8:].rsplit(' ', 2)[0], line.rsplit(' ', 2)[1]
+            st[name] = float(sec)
+    return st
+
+
 def e2e_families(args):
     """End-to-end seconds per family of the c_p_np_aln drop-in (-p 0: family
     test, posteriors, guide tree, 2 consistency rounds, progressive alignment,
     refinement; -p 1: family test, posteriors, 2 consistency rounds, alignment
-    graph, refinement), one fresh process per run, wall clock around the
-    process; two runs each, the faster reported (either may wait seconds for
-    the driver to clear memory an earlier process released: all runs are
-    listed in runs_s, the stage split is the reported run's); stage
-    times from MLP_CLI_TIMES."""
+    graph, refinement), one fresh process per run (as MLProbs starts them),
+    wall clock around the process; three runs each, every run listed with
+    the median and the maximum (a process can wait for the driver to clear
+    memory an earlier process released); the stage split is the median run's
+    (MLP_CLI_TIMES).  The -p 0 outputs are compared in the run with the
+    reference CLI's own output on the same family (tests/golden/config), with
+    MLProbs' SP score (un_sp) and TC against it."""
     from mlprobs_amd import synth
     cli = os.path.join(ROOT, 'mlprobs_amd', 'cli', 'c_p_np_aln')
     if not os.path.exists(cli):
         return None
     res = {}
-    for tag, n, L in (('C2 128x256', 128, 256), (f'C3 {args.n}x{args.len}', args.n, args.len)):
+    for tag, n, L, gold in (('C2 128x256', 128, 256, 'c2_128x256_s11'),
+                            (f'C3 {args.n}x{args.len}', args.n, args.len, f'c3_{args.n}x{args.len}_s{args.seed}')):
         for mode in ('0', '1'):
             with tempfile.TemporaryDirectory() as td:
                 fa = os.path.join(td, 'fam.fa')
                 synth.write_fasta(fa, synth.family(n, L, args.s, seed=args.seed))
                 runs = []
-                for _ in range(2):  # the first process may wait for memory an earlier one released
+                for _ in range(args.e2e_runs):
                     t0 = time.perf_counter()
                     r = subprocess.run([cli, '-p', mode, fa], capture_output=True, text=True, timeout=600,
                                        env=dict(os.environ, MLP_CLI_TIMES='1'))
                     runs.append((time.perf_counter() - t0, r))
-            dt, r = min(runs, key=lambda x: x[0])
-            log(f'e2e {tag} -p {mode}: {runs[0][0]:.2f} s, {runs[1][0]:.2f} s (exit {r.returncode})')
-            stages = {}
-            for line in r.stderr.splitlines():
-                if line.startswith('[stage] '):
-                    name, sec = line[8:].rsplit(' ', 2)[0], line.rsplit(' ', 2)[1]
-                    stages[name] = float(sec)
-            res[tag if mode == '0' else f'{tag} -p 1'] = {'seconds': dt, 'runs_s': [x[0] for x in runs],
-                                                          'exit': r.returncode, 'stages_s': stages}
+            order = sorted(range(len(runs)), key=lambda k: runs[k][0])
+            med_dt, r = runs[order[len(order) // 2]]
+            log(f'e2e {tag} -p {mode}: ' + ', '.join(f'{x[0]:.2f}' for x in runs) + f' s (exit {r.returncode})')
+            rec = {'median_s': med_dt, 'max_s': max(x[0] for x in runs), 'runs_s': [x[0] for x in runs],
+                   'exit': r.returncode, 'stages_s': _stages(r.stderr)}
+            g = os.path.join(ROOT, 'tests', 'golden', 'config', f'{gold}.p_0.out')
+            if mode == '0' and os.path.exists(g) and args.s == 0.7:
+                with open(g) as fh:
+                    ref = fh.read()
+                rec['reference_output'] = {'identical': all(x[1].stdout == ref for x in runs),
+                                           'sp_ours': sp_score(r.stdout), 'sp_reference': sp_score(ref),
+                                           'tc_vs_reference': tc_score(r.stdout, ref),
+                                           'reference': f'tests/golden/config/{gold}.p_0.out (reference CLI, '
+                                                        'single thread)'}
+            res[tag if mode == '0' else f'{tag} -p 1'] = rec
     qp = os.path.join(ROOT, 'mlprobs_amd', 'cli', 'quickprobs')
     ref = os.path.join(ROOT, 'oracle', '_ref', 'quickprobs')
     if os.path.exists(qp):
@@ -318,17 +423,17 @@ def e2e_families(args):
             with tempfile.TemporaryDirectory() as td:
                 fa = os.path.join(td, 'fam.fa')
                 synth.write_fasta(fa, synth.family(n, L, args.s, seed=args.seed))
-                t0 = time.perf_counter()
-                r = subprocess.run([qp, fa], capture_output=True, text=True, timeout=600,
-                                   env=dict(os.environ, MLP_CLI_TIMES='1'))
-                dt = time.perf_counter() - t0
-                stages = {}
-                for line in r.stderr.splitlines():
-                    if line.startswith('[stage] '):
-                        name, sec = line[8:].rsplit(' ', 2)[0], line.rsplit(' ', 2)[1]
-                        stages[name] = float(sec)
-                res[tag] = {'seconds': dt, 'exit': r.returncode, 'stages_s': stages}
-                log(f'e2e {tag}: {dt:.2f} s (exit {r.returncode})')
+                runs = []
+                for _ in range(args.e2e_runs):
+                    t0 = time.perf_counter()
+                    r = subprocess.run([qp, fa], capture_output=True, text=True, timeout=600,
+                                       env=dict(os.environ, MLP_CLI_TIMES='1'))
+                    runs.append((time.perf_counter() - t0, r))
+                order = sorted(range(len(runs)), key=lambda k: runs[k][0])
+                dt, r = runs[order[len(order) // 2]]
+                res[tag] = {'median_s': dt, 'max_s': max(x[0] for x in runs), 'runs_s': [x[0] for x in runs],
+                            'exit': r.returncode, 'stages_s': _stages(r.stderr)}
+                log(f'e2e {tag}: ' + ', '.join(f'{x[0]:.2f}' for x in runs) + f' s (exit {r.returncode})')
                 if n <= 128 and os.path.exists(ref) and not args.no_cpu:
                     t0 = time.perf_counter()
                     rr = subprocess.run([ref, '-t', str(args.cpu_threads), fa], capture_output=True, text=True,
@@ -338,31 +443,56 @@ def e2e_families(args):
     return res
 
 
-def c5_families(args):
-    """C5-style end-to-end seconds per family (BASELINE.json configs[4]: the
-    reference's TEST/ox + TEST/sabre families) for the C_P_NP_Aln calls
-    MLProbs.py makes per family -- the `-G` feature line, then the MSA
-    (`-p 0`) -- one fresh process each, as MLProbs runs them: the drop-in
-    (small families take its host path, larger ones the GPU) against the
-    reference CLI built from source (oracle/_ref/c_p_np_aln, OpenMP with
-    --cpu-threads threads; its default of every host core oversubscribes the
-    box's CPU share), on every 15th family of tests/golden/sweep.json.xz,
-    with the outputs compared to the reference's stored ones.  The classifier
-    and the QuickProbs region realignment of MLProbs.py are not part of
-    this drop-in."""
+def hbm_stream():
+    """The on-box HBM bandwidth (tools/probe/hbm_stream: 16-byte read, write
+    and copy kernels over 8 GiB, best of 10): the measured peak each roofline
+    is also quoted against."""
+    probe = os.path.join(ROOT, 'tools', 'probe', 'hbm_stream')
+    if not os.path.exists(probe):
+        return None
+    r = subprocess.run([probe, '8', '10'], capture_output=True, text=True, timeout=120)
+    if r.returncode != 0:
+        return {'error': r.stderr[-300:]}
+    s = json.loads(r.stdout.strip().splitlines()[-1])
+    s['peak_GBps'] = max(s['read_gbps'], s['write_gbps'], s['copy_gbps'])
+    log(f"hbm stream: read {s['read_gbps']:.0f} write {s['write_gbps']:.0f} copy {s['copy_gbps']:.0f} GB/s")
+    return s
+
+
+def c5_pipeline(args):
+    """C5 (BASELINE.json configs[4]): the whole MLProbs pipeline per family
+    -- features, classifier 1, c_p_np_aln -p 0|1, column scores, classifiers
+    3/2, region split, quickprobs on every region kept if not worse, combine,
+    fallbacks -- as `mlprobs_amd/cli/mlprobs`, one process per family (as
+    MLProbs.py runs), aligners in-process (host context for small families,
+    one device context otherwise), on every 15th TEST/ox + TEST/sabre family
+    of tests/golden/sweep.json.xz (50).  Baseline: the same orchestration
+    driving the reference CLIs built from source as external commands,
+    exactly as MLProbs.py spawns them (c_p_np_aln with its own thread count
+    and passive OpenMP waits, quickprobs -t --cpu-threads); the reference's
+    Python orchestration itself (not on the box) is not in that time, so the
+    baseline is a lower bound of the reference pipeline's.  Readouts: MLProbs'
+    SP score (un_sp) of each final MSA and TC against the published MLProbs
+    output of the family (output4evaluation/, tests/golden/c5_published.json.xz),
+    and whether the two pipelines' outputs are identical (the reference's
+    multi-threaded quickprobs and time-seeded -p 1 make this informative
+    only; byte parity at every stage is pinned by tests/test_pipeline.py)."""
     import lzma
-    cli = os.path.join(ROOT, 'mlprobs_amd', 'cli', 'c_p_np_aln')
-    ref = os.path.join(ROOT, 'oracle', '_ref', 'c_p_np_aln')
-    if not os.path.exists(cli):
+    bin_ = os.path.join(ROOT, 'mlprobs_amd', 'cli', 'mlprobs')
+    ref_cp = os.path.join(ROOT, 'oracle', '_ref', 'c_p_np_aln')
+    ref_qp = os.path.join(ROOT, 'oracle', '_ref', 'quickprobs')
+    if not os.path.exists(bin_):
         return None
     with lzma.open(os.path.join(ROOT, 'tests', 'golden', 'sweep.json.xz'), 'rt') as fh:
         fams = json.load(fh)
+    pub_path = os.path.join(ROOT, 'tests', 'golden', 'c5_published.json.xz')
+    pub = {}
+    if os.path.exists(pub_path):
+        with lzma.open(pub_path, 'rt') as fh:
+            pub = json.load(fh)
     names = [k for k in sorted(fams) if k.split('/')[0] in ('ox', 'sabre') and 'p_0' in fams[k]][::15]
-    ours, theirs, same, host = [], [], 0, 0
-    # the reference sets omp_set_num_threads(omp_get_num_procs()) itself
-    # (CPNP/MSA.cpp:146-151): on the GPU box that is every core of the node
-    # under a 16-core quota, and GOMP's spinning idle threads then stall a
-    # small family for ~23 s; passive waiting does not change its output
+    ours, theirs, same, host, calls, paths = [], [], 0, 0, 0, {}
+    sp_o, sp_r, sp_p, tc_o, tc_r, fails = [], [], [], [], [], 0
     env_ref = dict(os.environ, OMP_NUM_THREADS=str(args.cpu_threads), OMP_WAIT_POLICY='passive')
     with tempfile.TemporaryDirectory() as td:
         for k, name in enumerate(names):
@@ -372,25 +502,58 @@ def c5_families(args):
             fa = os.path.join(td, 'f.fa')
             with open(fa, 'wb') as fh:
                 fh.write(e['fa'].encode('latin-1'))
+            out, trace = os.path.join(td, 'o.msa'), os.path.join(td, 't.json')
             t0 = time.perf_counter()
-            g = subprocess.run([cli, '-G', fa], capture_output=True, timeout=300)
-            m = subprocess.run([cli, '-p', '0', fa], capture_output=True, timeout=300)
+            r = subprocess.run([bin_, '-q', '--trace', trace, fa, out], capture_output=True, timeout=600)
             ours.append(time.perf_counter() - t0)
-            same += (g.stdout.decode('latin-1') == e['G'][1]) and (m.stdout.decode('latin-1') == e['p_0'][1])
+            if r.returncode != 0:
+                fails += 1
+                continue
+            with open(out, encoding='latin-1') as fh:
+                mine = fh.read()
+            with open(trace) as fh:
+                tr = json.load(fh)
+            calls += tr['quickprobs_calls']
+            paths[tr['path']] = paths.get(tr['path'], 0) + 1
             host += e['cells'] <= 4e6
-            if os.path.exists(ref) and not args.no_cpu:
+            sp_o.append(sp_score(mine))
+            if name in pub:
+                sp_p.append(sp_score(pub[name]))
+                tc_o.append(tc_score(mine, pub[name]))
+            if os.path.exists(ref_cp) and os.path.exists(ref_qp) and not args.no_cpu:
+                out2 = os.path.join(td, 'r.msa')
                 t0 = time.perf_counter()
-                subprocess.run([ref, '-G', fa], capture_output=True, timeout=120, env=env_ref)
-                subprocess.run([ref, '-p', '0', fa], capture_output=True, timeout=120, env=env_ref)
+                subprocess.run([bin_, '-q', '--cpnp', ref_cp, '--quickprobs', f'{ref_qp} -t {args.cpu_threads}',
+                                '--tmp', td, fa, out2], capture_output=True, timeout=600, env=env_ref)
                 theirs.append(time.perf_counter() - t0)
-    res = {'families': len(names), 'sample': 'every 15th TEST/ox + TEST/sabre family of tests/golden/sweep.json.xz',
-           'calls': '-G then -p 0, one process each', 'host_path_families': host,
-           'identical_outputs': same, 'drop_in_s_per_family': {'median': float(np.median(ours)),
-                                                                 'mean': float(np.mean(ours))}}
+                with open(out2, encoding='latin-1') as fh:
+                    refo = fh.read()
+                same += refo == mine
+                sp_r.append(sp_score(refo))
+                if name in pub:
+                    tc_r.append(tc_score(refo, pub[name]))
+
+    def mean(v):
+        v = [x for x in v if x is not None]
+        return float(np.mean(v)) if v else None
+
+    res = {'families': len(names), 'failed': fails,
+           'sample': 'every 15th TEST/ox + TEST/sabre family of tests/golden/sweep.json.xz',
+           'pipeline': 'mlprobs (MLProbs.py + utils/*.py restated in C++, aligners in-process)',
+           'host_path_families': host, 'quickprobs_region_calls': calls, 'paths': paths,
+           's_per_family': {'median': float(np.median(ours)), 'mean': float(np.mean(ours)), 'max': float(np.max(ours))},
+           'sp_un_sp_mean': mean(sp_o), 'published_sp_un_sp_mean': mean(sp_p),
+           'tc_vs_published_mean': mean(tc_o)}
     if theirs:
-        res['reference_s_per_family'] = {'median': float(np.median(theirs)), 'mean': float(np.mean(theirs)),
-                                         'threads': 'omp_get_num_procs() (its own setting), OMP_WAIT_POLICY=passive'}
+        res['reference_clis_s_per_family'] = {
+            'median': float(np.median(theirs)), 'mean': float(np.mean(theirs)),
+            'how': 'the same orchestration driving oracle/_ref/c_p_np_aln (its own thread count, passive OpenMP '
+                   f'waits) and oracle/_ref/quickprobs -t {args.cpu_threads} as external commands'}
         res['speedup_median'] = float(np.median(theirs)) / float(np.median(ours))
+        res['speedup_mean'] = float(np.mean(theirs)) / float(np.mean(ours))
+        res['identical_to_reference_clis'] = same
+        res['reference_clis_sp_un_sp_mean'] = mean(sp_r)
+        res['reference_clis_tc_vs_published_mean'] = mean(tc_r)
     return res
 
 
@@ -448,8 +611,9 @@ def main():
     # end-to-end family timings first, on an idle device (a process that
     # follows a large release waits for the driver to clear that memory)
     log('start')
+    stream = hbm_stream() if world == 1 else None
     e2e = e2e_families(args) if (not args.no_e2e and world == 1) else None
-    c5 = c5_families(args) if (not args.no_e2e and world == 1 and rank == 0) else None
+    c5 = c5_pipeline(args) if (not args.no_e2e and world == 1 and rank == 0) else None
     if args.relax < 0:
         args.relax = 4 if world == 1 else 0
     fam_in = synth.family(args.n, args.len, args.s, seed=args.seed)
@@ -568,12 +732,21 @@ def main():
         }
         if cpu:
             out['speedup_vs_cpu'] = value / cpu['value']
+        if stream and 'peak_GBps' in stream:
+            mp = stream['peak_GBps']
+            out['hbm_stream'] = stream
+            out['roofline']['peak_measured'] = mp
+            out['roofline']['frac_of_measured'] = achieved / mp
+            out['stage_roofline']['frac_of_measured'] = value * STAGE_BYTES / 1e9 / mp
+            if relax_info:
+                relax_info['roofline']['peak_measured'] = mp
+                relax_info['roofline']['frac_of_measured'] = relax_info['roofline']['achieved'] / mp
         if relax_info:
             out['relax'] = relax_info
         if e2e is not None:
             out['e2e'] = e2e
         if c5 is not None:
-            out['c5_families'] = c5
+            out['c5_pipeline'] = c5
         if qp_info is not None:
             out['quickprobs'] = qp_info
         print(json.dumps(out))
