@@ -56,6 +56,7 @@ def parse():
                     help='skip the end-to-end c_p_np_aln / quickprobs family timings')
     ap.add_argument('--no-qp', action='store_true', help='skip the QuickProbs posterior/consistency timings')
     ap.add_argument('--e2e-runs', type=int, default=3, help='fresh-process runs per end-to-end leg')
+    ap.add_argument('--no-shards', action='store_true', help='skip the 8-virtual-shard all-gather timing')
     return ap.parse_args()
 
 
@@ -443,6 +444,37 @@ def e2e_families(args):
     return res
 
 
+def shard_gather(args, seqs):
+    """SURVEY.md section 8e on one GPU: the C3 posterior stage and one
+    consistency round with 8 virtual shards (mlp_set_shards; real N > 1 GPUs
+    are unmeasured here), timing the all-gathers of the sparse set (every
+    shard pulls every other shard's block on its own copy streams, the parent
+    takes the full store) -- device-to-device copies here, peer copies over
+    xGMI on a multi-GPU box."""
+    from mlprobs_amd.engine import Family
+    fam = Family(seqs, shards=8)
+    fam.profile(True)
+    t0 = time.perf_counter()
+    fam.posteriors(args.pid, args.delta)
+    fam.synchronize()
+    t_post = time.perf_counter() - t0
+    kt = fam.kernel_times()['allgather']
+    rp, eo, cols, vals = fam.export()
+    store_bytes = int(eo[-1]) * 6 + rp.nbytes
+    res = {'shards': 8, 'posterior_stage_s': t_post, 'gather_ms': kt['ms'], 'store_bytes': store_bytes,
+           'bytes_moved': 9 * store_bytes,
+           'note': '8 destinations x the whole store + the parent\'s copy; virtual shards share one GPU'}
+    fam.profile(True)
+    t0 = time.perf_counter()
+    fam.relax(1)
+    fam.synchronize()
+    res['relax_round_s'] = time.perf_counter() - t0
+    res['relax_gather_ms'] = fam.kernel_times()['allgather']['ms'] - kt['ms']
+    fam.close()
+    log(f"shards: posteriors {t_post:.2f} s (gather {kt['ms']:.1f} ms), relax round {res['relax_round_s']:.2f} s")
+    return res
+
+
 def hbm_stream():
     """The on-box HBM bandwidth (tools/probe/hbm_stream: 16-byte read, write
     and copy kernels over 8 GiB, best of 10): the measured peak each roofline
@@ -689,6 +721,10 @@ def main():
                     'insts_per_cell': g['valu_insts_per_cell']}
     log('quickprobs stage')
     qp_info = quickprobs_stage(fam, fam_in, total_cells, args) if (world == 1 and not args.no_qp) else None
+    shards_info = None
+    if world == 1 and not args.no_shards:
+        log('virtual shards')
+        shards_info = shard_gather(args, seqs)
     out = None
     if rank == 0:
         cpu, parity = None, None
@@ -749,6 +785,8 @@ def main():
             out['c5_pipeline'] = c5
         if qp_info is not None:
             out['quickprobs'] = qp_info
+        if shards_info is not None:
+            out['virtual_shards'] = shards_info
         print(json.dumps(out))
     fam.close()
     if world > 1:

@@ -117,6 +117,11 @@ struct mlp_ctx {
   int shards_req = 0;                // 0: one per device when the family is large enough
   std::vector<mlp_ctx*> shards;
   int64_t rel_r0 = -1, rel_r1 = -1;  // a shard's output-pair range for one relaxation round
+  // all-gather (allgather_shards): the incoming store, copy streams (one per
+  // source shard) and the parent store version every shard holds in full
+  DevBuf ag_cols, ag_vals;
+  std::vector<hipStream_t> cst;
+  uint64_t shards_full_ver = ~0ull;
   // profiling
   bool profile = false;
   double kms[MLP_NKERNELS] = {0};
@@ -416,7 +421,7 @@ void mlp_ctx_destroy(mlp_ctx* c) {
   DevBuf* bufs[] = {&c->scratch, &c->scratch2, &c->r_trowptr, &c->r_tcols, &c->r_tvals, &c->r_raw, &c->r_newrp,
                     &c->r_newcols, &c->r_newvals, &c->r_tasks_p, &c->r_tasks_r, &c->r_pairs,
                     &c->r_nnz, &c->r_newoff, &c->r_img, &c->r_imgoff, &c->r_tiles, &c->r_nwords, &c->r_weights,
-                    &c->r_seldist, &c->r_profile, &c->r_mea};
+                    &c->r_seldist, &c->r_profile, &c->r_mea, &c->ag_cols, &c->ag_vals};
   for (DevBuf* b : bufs)
     if (b->p) hipFree(b->p);
   if (c->comm) ncclCommDestroy(c->comm);
@@ -427,6 +432,7 @@ void mlp_ctx_destroy(mlp_ctx* c) {
   if (c->h_prof_in) hipHostFree(c->h_prof_in);
   if (c->h_prof_out) hipHostFree(c->h_prof_out);
   if (c->h_mea) hipHostFree(c->h_mea);
+  for (hipStream_t st : c->cst) hipStreamDestroy(st);
   hipStreamDestroy(c->stream);
   hipStreamDestroy(c->stream2);
   if (c->side.st) {
@@ -449,6 +455,7 @@ int mlp_family_load(mlp_ctx* c, int n, const char* residues, const int64_t* offs
   if (!c || n < 1 || !residues || !offsets) return MLP_ERR_ARG;
   for (mlp_ctx* ch : c->shards) mlp_ctx_destroy(ch);  // re-created for the new family when needed
   c->shards.clear();
+  c->shards_full_ver = ~0ull;
   if (!c->host) hipSetDevice(c->device);
   c->n = n;
   c->lens.assign(n, 0);
@@ -782,16 +789,28 @@ static int shard_count(mlp_ctx* c) {
   return cells >= kShardMinCells ? (int)devs.size() : 1;
 }
 
-static hipError_t copy_from(mlp_ctx* dst, void* d, const mlp_ctx* src, const void* s, size_t bytes) {
+// MLP_FORCE_PEER=1 (test hook): peer copies even between contexts on one
+// device, so virtual shards exercise the xGMI branch
+static bool force_peer() {
+  const char* e = getenv("MLP_FORCE_PEER");
+  return e && atoi(e) > 0;
+}
+
+static hipError_t copy_on(hipStream_t st, mlp_ctx* dst, void* d, const mlp_ctx* src, const void* s, size_t bytes) {
   if (!bytes) return hipSuccess;
-  if (dst->device == src->device) return hipMemcpyAsync(d, s, bytes, hipMemcpyDeviceToDevice, dst->stream);
-  return hipMemcpyPeerAsync(d, dst->device, s, src->device, bytes, dst->stream);
+  if (dst->device == src->device && !force_peer()) return hipMemcpyAsync(d, s, bytes, hipMemcpyDeviceToDevice, st);
+  return hipMemcpyPeerAsync(d, dst->device, s, src->device, bytes, st);
+}
+
+static hipError_t copy_from(mlp_ctx* dst, void* d, const mlp_ctx* src, const void* s, size_t bytes) {
+  return copy_on(dst->stream, dst, d, src, s, bytes);
 }
 
 static int ensure_shards(mlp_ctx* c, int S) {
   if ((int)c->shards.size() == S) return MLP_OK;
   for (mlp_ctx* ch : c->shards) mlp_ctx_destroy(ch);
   c->shards.clear();
+  c->shards_full_ver = ~0ull;  // new shards hold no store yet
   std::vector<int> devs = mask_devices(c->dev_mask);
   if (devs.empty()) devs.push_back(c->device);
   std::vector<int> per(devs.size(), 0);
@@ -846,55 +865,6 @@ static int run_shards(mlp_ctx* c, F fn) {
   return MLP_OK;
 }
 
-// The shards hold consecutive pair ranges tiling [0, P), entries from 0:
-// concatenate them into the parent's canonical store.
-static int gather_shards(mlp_ctx* c) {
-  const int S = (int)c->shards.size();
-  std::vector<int64_t> ebase(S + 1, 0);
-  for (int s = 0; s < S; s++) {
-    const mlp_ctx* ch = c->shards[s];
-    if (ch->store_p0 != (s ? c->shards[s - 1]->store_p1 : 0)) {
-      c->err = "shard ranges do not tile the pair range";
-      return MLP_ERR_STATE;
-    }
-    ebase[s + 1] = ebase[s] + ch->store_total;
-  }
-  if (c->shards[S - 1]->store_p1 != c->P) {
-    c->err = "shard ranges do not tile the pair range";
-    return MLP_ERR_STATE;
-  }
-  hipSetDevice(c->device);
-  const int64_t total = ebase[S];
-  int rc;
-  if ((rc = grow_store(c, total, 0))) return rc;
-  {
-    Timer tm(c, KGATHER, 0);
-    for (int s = 0; s < S; s++) {
-      mlp_ctx* ch = c->shards[s];
-      const int64_t p0 = ch->store_p0, p1 = ch->store_p1;
-      HIPCHK(c, copy_from(c, c->d_cols + ebase[s], ch, ch->d_cols, sizeof(uint16_t) * ch->store_total));
-      HIPCHK(c, copy_from(c, c->d_vals + ebase[s], ch, ch->d_vals, sizeof(float) * ch->store_total));
-      HIPCHK(c, copy_from(c, c->d_rowptr + c->rp_off[p0], ch, ch->d_rowptr + c->rp_off[p0],
-                          sizeof(int32_t) * (c->rp_off[p1] - c->rp_off[p0])));
-      for (int64_t p = p0; p < p1; p++) {
-        c->dist[p] = ch->dist[p];
-        c->mea[p] = ch->mea[p];
-        c->nnz[p] = ch->nnz[p];
-        c->ent_off[p] = ebase[s] + ch->ent_off[p] - ch->ent_off[p0];
-      }
-    }
-  }
-  c->ent_off[c->P] = total;
-  HIPCHK(c, hipMemcpyAsync(c->d_ent_off, c->ent_off.data(), sizeof(int64_t) * (c->P + 1), hipMemcpyHostToDevice,
-                           c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
-  c->store_p0 = 0;
-  c->store_p1 = c->P;
-  c->store_total = total;
-  ++c->store_ver;
-  return MLP_OK;
-}
-
 // The parent's whole store onto one shard (before a relaxation round).
 static int broadcast_store(mlp_ctx* c, mlp_ctx* ch) {
   int rc;
@@ -913,6 +883,123 @@ static int broadcast_store(mlp_ctx* c, mlp_ctx* ch) {
   ch->store_p1 = c->P;
   ch->store_total = c->store_total;
   ++ch->store_ver;
+  return MLP_OK;
+}
+
+// All-gather of the shards' blocks: after the
+// posteriors or a relaxation round every shard holds the entries of its own
+// contiguous pair range; each shard then pulls every other shard's block
+// into place concurrently, one copy stream per source (xGMI peer copies
+// between GPUs: all of a device's links at once, instead of the parent's
+// serial gather followed by a whole-store broadcast), and the parent takes
+// the full store from the shard on its own device.  Per-pair scalars and
+// entry offsets are assembled on the host.
+static int allgather_shards(mlp_ctx* c) {
+  const int S = (int)c->shards.size();
+  std::vector<int64_t> ebase(S + 1, 0);
+  for (int s = 0; s < S; s++) {
+    const mlp_ctx* ch = c->shards[s];
+    if (ch->store_p0 != (s ? c->shards[s - 1]->store_p1 : 0)) {
+      c->err = "shard ranges do not tile the pair range";
+      return MLP_ERR_STATE;
+    }
+    ebase[s + 1] = ebase[s] + ch->store_total;
+  }
+  if (c->shards[S - 1]->store_p1 != c->P) {
+    c->err = "shard ranges do not tile the pair range";
+    return MLP_ERR_STATE;
+  }
+  const int64_t total = ebase[S];
+  const auto t0 = std::chrono::steady_clock::now();
+  // global offsets and scalars (host)
+  for (int s = 0; s < S; s++) {
+    const mlp_ctx* ch = c->shards[s];
+    for (int64_t p = ch->store_p0; p < ch->store_p1; p++) {
+      c->dist[p] = ch->dist[p];
+      c->mea[p] = ch->mea[p];
+      c->nnz[p] = ch->nnz[p];
+      c->ent_off[p] = ebase[s] + ch->ent_off[p] - ch->ent_off[ch->store_p0];
+    }
+  }
+  c->ent_off[c->P] = total;
+  struct Src { const mlp_ctx* ch; const uint16_t* cols; const float* vals; const int32_t* rp; int64_t p0, p1, n; };
+  std::vector<Src> src(S);
+  for (int s = 0; s < S; s++) {
+    const mlp_ctx* ch = c->shards[s];
+    src[s] = {ch, ch->d_cols, ch->d_vals, ch->d_rowptr, ch->store_p0, ch->store_p1, ch->store_total};
+  }
+  // phase 1: every destination pulls every block (sources stay untouched)
+  int rc = run_shards(c, [&](mlp_ctx* ch, int s) -> int {
+    int r;
+    if ((r = ensure(ch, ch->ag_cols, sizeof(uint16_t) * std::max<int64_t>(total, 1)))) return r;
+    if ((r = ensure(ch, ch->ag_vals, sizeof(float) * std::max<int64_t>(total, 1)))) return r;
+    while ((int)ch->cst.size() < S) {
+      hipStream_t st;
+      HIPCHK(ch, hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+      ch->cst.push_back(st);
+    }
+    for (int q = 0; q < S; q++) {
+      const Src& b = src[q];
+      hipStream_t st = ch->cst[q];
+      HIPCHK(ch, copy_on(st, ch, (uint16_t*)ch->ag_cols.p + ebase[q], b.ch, b.cols, sizeof(uint16_t) * b.n));
+      HIPCHK(ch, copy_on(st, ch, (float*)ch->ag_vals.p + ebase[q], b.ch, b.vals, sizeof(float) * b.n));
+      if (q != s)  // row pointers of the block, in place (disjoint pair ranges)
+        HIPCHK(ch, copy_on(st, ch, ch->d_rowptr + c->rp_off[b.p0], b.ch, b.rp + c->rp_off[b.p0],
+                           sizeof(int32_t) * (c->rp_off[b.p1] - c->rp_off[b.p0])));
+    }
+    for (int q = 0; q < S; q++) HIPCHK(ch, hipStreamSynchronize(ch->cst[q]));
+    return MLP_OK;
+  });
+  if (rc) return rc;
+  // phase 2: swap the gathered store in
+  rc = run_shards(c, [&](mlp_ctx* ch, int) -> int {
+    uint16_t* oc = ch->d_cols;
+    float* ov = ch->d_vals;
+    const int64_t ocap = ch->ent_cap;
+    ch->d_cols = (uint16_t*)ch->ag_cols.p;
+    ch->d_vals = (float*)ch->ag_vals.p;
+    ch->ent_cap = (int64_t)std::min(ch->ag_cols.bytes / sizeof(uint16_t), ch->ag_vals.bytes / sizeof(float));
+    ch->ag_cols.p = oc;
+    ch->ag_cols.bytes = sizeof(uint16_t) * (size_t)ocap;
+    ch->ag_vals.p = ov;
+    ch->ag_vals.bytes = sizeof(float) * (size_t)ocap;
+    ch->ent_off = c->ent_off;
+    ch->nnz = c->nnz;
+    ch->dist = c->dist;
+    ch->mea = c->mea;
+    HIPCHK(ch, hipMemcpyAsync(ch->d_ent_off, ch->ent_off.data(), sizeof(int64_t) * (c->P + 1), hipMemcpyHostToDevice,
+                              ch->stream));
+    HIPCHK(ch, hipStreamSynchronize(ch->stream));
+    ch->store_p0 = 0;
+    ch->store_p1 = c->P;
+    ch->store_total = total;
+    ++ch->store_ver;
+    return MLP_OK;
+  });
+  if (rc) return rc;
+  // the parent: one copy of the full store from the shard on its device
+  int home = 0;
+  for (int s = 0; s < S; s++)
+    if (c->shards[s]->device == c->device) { home = s; break; }
+  const mlp_ctx* h = c->shards[home];
+  hipSetDevice(c->device);
+  if ((rc = grow_store(c, total, 0))) return rc;
+  HIPCHK(c, copy_from(c, c->d_cols, h, h->d_cols, sizeof(uint16_t) * total));
+  HIPCHK(c, copy_from(c, c->d_vals, h, h->d_vals, sizeof(float) * total));
+  HIPCHK(c, copy_from(c, c->d_rowptr, h, h->d_rowptr, sizeof(int32_t) * c->rp_off[c->P]));
+  HIPCHK(c, hipMemcpyAsync(c->d_ent_off, c->ent_off.data(), sizeof(int64_t) * (c->P + 1), hipMemcpyHostToDevice,
+                           c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->store_p0 = 0;
+  c->store_p1 = c->P;
+  c->store_total = total;
+  ++c->store_ver;
+  c->shards_full_ver = c->store_ver;
+  if (c->profile) {
+    c->kms[KGATHER] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    c->klaunch[KGATHER] += 1;
+    c->kcells[KGATHER] += total;
+  }
   return MLP_OK;
 }
 
@@ -957,7 +1044,7 @@ static int sharded_posteriors(mlp_ctx* c, int pid, float delta, int S) {
   for (int s = 0; s < S; s++) mlp_shard_plan(c->n, c->lens.data(), S, s, &b[s], &e[s]);
   if ((rc = run_shards(c, [&](mlp_ctx* ch, int s) { return mlp_posteriors(ch, pid, delta, b[s], e[s]); })))
     return rc;
-  return gather_shards(c);
+  return allgather_shards(c);
 }
 extern "C" {
 
@@ -2155,9 +2242,12 @@ static int sharded_relax(mlp_ctx* c, int iters, const QpRelax& qp, const float* 
   for (int it = 0; it < iters; it++) {
     std::vector<int64_t> bounds;
     relax_bounds(c, S, bounds);
+    // the shards hold the parent's store from the last all-gather; a store
+    // that came another way (an unsharded stage, mlp_csr_import) is sent out
+    const bool send = c->shards_full_ver != c->store_ver;
     if ((rc = run_shards(c, [&](mlp_ctx* ch, int s) -> int {
           int r;
-          if ((r = broadcast_store(c, ch))) return r;
+          if (send && (r = broadcast_store(c, ch))) return r;
           ch->rel_r0 = bounds[s];
           ch->rel_r1 = bounds[s + 1];
           r = relax_one(ch, q[s], it == iters - 1);
@@ -2165,7 +2255,7 @@ static int sharded_relax(mlp_ctx* c, int iters, const QpRelax& qp, const float* 
           return r;
         })))
       return rc;
-    if ((rc = gather_shards(c))) return rc;
+    if ((rc = allgather_shards(c))) return rc;
   }
   return MLP_OK;
 }

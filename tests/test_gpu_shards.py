@@ -59,3 +59,38 @@ def test_virtual_shards_quickprobs(k):
     _same(one, many, 'quickprobs')
     one.close()
     many.close()
+
+
+@pytest.mark.parametrize('k', [2, 8])
+def test_virtual_shards_forced_peer_copies(k, monkeypatch):
+    """MLP_FORCE_PEER=1: the all-gather's copies take the hipMemcpyPeerAsync
+    branch even between shards of one device (the xGMI path of a real
+    multi-GPU box)."""
+    monkeypatch.setenv('MLP_FORCE_PEER', '1')
+    seqs = [s for _, s in synth.family(40, 150, 0.7, seed=93)]
+    one = Family(seqs)
+    many = Family(seqs, shards=k)
+    one.posteriors(0, 0.132548)
+    many.posteriors(0, 0.132548)
+    _same(one, many, f'k={k} peer posteriors')
+    one.relax(2)
+    many.relax(2)
+    _same(one, many, f'k={k} peer relax x2')
+    one.close()
+    many.close()
+
+
+def test_virtual_shards_imported_store():
+    """A store the shards never saw (mlp_csr_import) is sent out before the
+    first sharded round, then all-gathered after each."""
+    seqs = [s for _, s in synth.family(36, 140, 0.7, seed=94)]
+    one = Family(seqs)
+    one.posteriors(0, 0.132548)
+    many = Family(seqs, shards=3)
+    many.import_csr(*one.export())
+    one.relax(1)
+    many.relax(1)
+    for x, y in zip(one.export(), many.export()):
+        np.testing.assert_array_equal(x, y)
+    one.close()
+    many.close()
