@@ -723,6 +723,10 @@ def main():
     qp_info = quickprobs_stage(fam, fam_in, total_cells, args) if (world == 1 and not args.no_qp) else None
     shards_info = None
     if world == 1 and not args.no_shards:
+        # the main context's batch scratch (45% of the device) goes first: the
+        # 8 shard contexts need their own
+        fam.close()
+        fam = None
         log('virtual shards')
         shards_info = shard_gather(args, seqs)
     out = None
@@ -788,7 +792,8 @@ def main():
         if shards_info is not None:
             out['virtual_shards'] = shards_info
         print(json.dumps(out))
-    fam.close()
+    if fam is not None:
+        fam.close()
     if world > 1:
         dist.destroy_process_group()
 
