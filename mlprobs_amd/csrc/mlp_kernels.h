@@ -74,7 +74,7 @@ struct PairMeta {
   const int32_t* pb;       // seq index of column sequence (seq2)
   const int32_t* row0;     // first stacked row of the pair in its chain
   const int32_t* chain;    // chain of the pair
-  const int64_t* rm_off;   // base of the pair's row-major local-chain region
+  const int64_t* rm_off;   // base of the pair's chunk maxima (L1 x ceil(L2 / 64) floats)
   const int64_t* ell_row;  // first ELL row of the pair (rows 1..L1)
 };
 
@@ -112,8 +112,12 @@ struct Scratch {
   float* fl;               // local fwd M, then f+b
   double* zm;              // PF forward Zm (packed with frame)
   float* pg;               // PF posterior
-  float* chf;              // row-major local fwd M   (chain for total)
-  float* chb;              // row-major local bwd M + emission
+  float* bl;               // step-diagonal: local bwd M (the merge adds fl + bl)
+  // local-model chain totals (k_local_totals): per pair (rows 1..L1, chunks
+  // of 64 columns, row-major from rm_off) the largest chain element of each
+  // chunk, forward (f_M) and backward (b_M + emission), written by the sweeps
+  float* cmf;
+  float* cmb;
   float* bnd5;             // chain boundary row: 5 floats per column
   float* bndl;             // 3 floats per column
   double* bndz;            // 3 doubles per column
@@ -166,8 +170,10 @@ hipError_t launch_forward(int models, const ModelScalars& ms, const Tables* tab,
 hipError_t launch_backward(int models, const ModelScalars& ms, const Tables* tab, SeqSet seqs,
                            PairMeta pm, ChainMeta cm, PairRec* rec, Scratch sc, int64_t nchains,
                            int lds_seq, int64_t npairs, hipStream_t st, const SideStream* side);
-hipError_t launch_local_totals(SeqSet seqs, PairMeta pm, PairRec* rec, Scratch sc, int64_t npairs,
-                               hipStream_t st);
+hipError_t launch_local_totals(const ModelScalars& ms, const Tables* tab, SeqSet seqs, PairMeta pm, ChainMeta cm,
+                               PairRec* rec, Scratch sc, int64_t npairs, hipStream_t st);
+// chunk maxima per pair row (columns 1..L2 in chunks of 64)
+__host__ __device__ constexpr int local_chunks(int L2) { return (L2 + 63) >> 6; }
 hipError_t launch_fold_totals(const ModelScalars& ms, const Tables* tab, SeqSet seqs, PairMeta pm,
                               PairRec* rec, int64_t npairs, hipStream_t st);
 hipError_t launch_merge(int models, int pid, const ModelScalars& ms, SeqSet seqs, PairMeta pm,

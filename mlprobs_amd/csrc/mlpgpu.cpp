@@ -679,7 +679,7 @@ static void plan_chains(const mlp_ctx* c, int64_t p, int64_t q, ChainPlan& P) {
       P.rm[s] = P.rm_total;
       P.ell[s] = P.ell_rows;
       row0 += L1 + 1;
-      P.rm_total += (int64_t)L1 * ((L2 + 3) & ~3);
+      P.rm_total += (int64_t)L1 * local_chunks(L2);
       P.ell_rows += L1;
     }
   }
@@ -1069,10 +1069,13 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
   const int models = model_set_for_pid(pid);
   SeqSet seqs{c->d_res, c->d_off, c->d_len};
 
+  // step-diagonal bytes per slot of the models this pid runs: f5 (5-state),
+  // fl + bl (local), zm + pg (partition function)
+  const int slot_bytes = ((models & kHmm5) ? 4 : 0) + ((models & kLocal) ? 8 : 0) + ((models & kPF) ? 12 : 0);
   auto pair_bytes = [&](int64_t q) {
     const int L1 = c->lens[c->pa[q]], L2 = c->lens[c->pb[q]];
-    const int64_t rmc = (int64_t)L1 * ((L2 + 3) & ~3);
-    return (size_t)(pair_slots_bound(c, q) * 20 + rmc * 8) +
+    const int64_t rmc = (models & kLocal) ? (int64_t)L1 * local_chunks(L2) : 0;
+    return (size_t)(pair_slots_bound(c, q) * slot_bytes + rmc * 8) +
            (size_t)pair_width_bound(c, q) * (5 * 4 + 3 * 4 + 3 * 8 + 4 + 4 + 4) +
            (size_t)L1 * (kEll * 6 + 4) + kPerSlotMeta;
   };
@@ -1176,9 +1179,12 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
     const int64_t np = P.np, nch = P.nch;
     // ---- carve scratch
     Carver cv;
-    const size_t o_f5 = cv.take(P.cells * 4), o_fl = cv.take(P.cells * 4), o_pg = cv.take(P.cells * 4),
-                 o_zm = cv.take(P.cells * 8), o_chf = cv.take(P.rm_total * 4), o_chb = cv.take(P.rm_total * 4),
-                 o_b5 = cv.take(P.bnd * 20), o_bl = cv.take(P.bnd * 12), o_bz = cv.take(P.bnd * 24),
+    const bool h5 = models & kHmm5, lo = models & kLocal, pf = models & kPF;
+    const size_t o_f5 = cv.take(h5 ? P.cells * 4 : 0), o_fl = cv.take(lo ? P.cells * 4 : 0),
+                 o_bl = cv.take(lo ? P.cells * 4 : 0), o_pg = cv.take(pf ? P.cells * 4 : 0),
+                 o_zm = cv.take(pf ? P.cells * 8 : 0), o_cmf = cv.take(lo ? P.rm_total * 4 : 0),
+                 o_cmb = cv.take(lo ? P.rm_total * 4 : 0),
+                 o_b5 = cv.take(P.bnd * 20), o_bnl = cv.take(P.bnd * 12), o_bz = cv.take(P.bnd * 24),
                  o_be = cv.take(P.bnd * 4), o_bm = cv.take(P.bnd * 4), o_bc = cv.take(P.bnd * 4), o_ec = cv.take(P.ell_rows * kEll * 2),
                  o_ev = cv.take(P.ell_rows * kEll * 4), o_en = cv.take(P.ell_rows * 4),
                  o_entb = cv.take(np * 8), o_rpb = cv.take(np * 8), o_rec = cv.take(np * sizeof(PairRec));
@@ -1195,10 +1201,11 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
     sc.fl = (float*)(base + o_fl);
     sc.pg = (float*)(base + o_pg);
     sc.zm = (double*)(base + o_zm);
-    sc.chf = (float*)(base + o_chf);
-    sc.chb = (float*)(base + o_chb);
+    sc.bl = (float*)(base + o_bl);
+    sc.cmf = (float*)(base + o_cmf);
+    sc.cmb = (float*)(base + o_cmb);
     sc.bnd5 = (float*)(base + o_b5);
-    sc.bndl = (float*)(base + o_bl);
+    sc.bndl = (float*)(base + o_bnl);
     sc.bndz = (double*)(base + o_bz);
     sc.bnde = (int32_t*)(base + o_be);
     sc.bndm = (float*)(base + o_bm);
@@ -1224,7 +1231,7 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
     }
     if (models & kLocal) {
       Timer t(c, KTOT, bcells, st);
-      HIPCHK(c, launch_local_totals(seqs, pm, d_rec, sc, np, st));
+      HIPCHK(c, launch_local_totals(ms, c->d_tables, seqs, pm, cm, d_rec, sc, np, st));
     }
     {
       Timer t(c, KMERGE, bcells, st);

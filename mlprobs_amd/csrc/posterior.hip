@@ -68,6 +68,27 @@ __device__ __forceinline__ void pf_rescale(double& m, double& e, double& f, int&
     ++E;
   }
 }
+// Frame changes are rare (a pair's values cross 2^200 a few times at most),
+// so both frame steps run as wave-uniform branches around the common case:
+// with all three neighbour frames equal pf_align does nothing (E = ea), and
+// pf_rescale acts only past 2^200.  The per-lane code inside is unchanged,
+// so every value rounds as before; the compiler no longer if-converts the
+// ldexp blocks into always-executed selects.
+__device__ __forceinline__ bool wave_none(bool p) { return __ballot(p) == 0; }
+__device__ __forceinline__ int pf_align_fast(double& a0, double& a1, double& a2, int ea,
+                                             double& b0, double& b1, double& b2, int eb,
+                                             double& c0, double& c1, double& c2, int ec) {
+  if (wave_none(ea != eb || eb != ec)) return ea;
+  return pf_align(a0, a1, a2, ea, b0, b1, b2, eb, c0, c1, c2, ec);
+}
+__device__ __forceinline__ void pf_rescale_fast(double& m, double& e, double& f, int& E) {
+  const double mx = fmax(fmax(m, e), f);
+  if (wave_none(mx > MLP_PF_HUGE)) return;
+  if (mx > MLP_PF_HUGE) {
+    m = ldexp(m, -MLP_PF_STEP); e = ldexp(e, -MLP_PF_STEP); f = ldexp(f, -MLP_PF_STEP);
+    ++E;
+  }
+}
 
 // =====================================================================
 // Forward sweep: 5-state forward, local forward, PF forward Zm.
@@ -101,8 +122,7 @@ __global__ __launch_bounds__(256, SweepWaves<M>::fwd) void k_forward(ModelScalar
   for (int k = 0; k < 5; ++k) L5[k] = U5[k] = D5[k] = LZ;
 #pragma unroll
   for (int k = 0; k < 3; ++k) LL[k] = UL[k] = DL[k] = LZ;
-  // row-major chain staging; unused slots stay LOG_ZERO, a no-op in the chain
-  float cb0 = LZ, cb1 = LZ, cb2 = LZ, cb3 = LZ;
+  float cmx = LZ;   // running maximum of the local chain elements in the current 64-column chunk
   BoundaryChunks<M> bc;
   const int nseg = (W + 63) >> 6;
 
@@ -212,23 +232,12 @@ __global__ __launch_bounds__(256, SweepWaves<M>::fwd) void k_forward(ModelScalar
             sc.bndl[(bo + j) * 3 + 1] = Cx;
             sc.bndl[(bo + j) * 3 + 2] = Cy;
           }
-          // row-major chain copy of interior M values (CPNP/ProbabilisticModel.h:438-447)
-#ifdef MLP_EXP_NOCHAIN  // timing experiment only (wrong totals): no row-major chain stores
-          if (false) {
-#else
+          // the chain total's input (CPNP/ProbabilisticModel.h:438-447): the
+          // largest f_M of each 64-column chunk of the row, for
+          // k_local_totals' exact skip test
           if (act && i >= 1 && j >= 1) {
-#endif
-            const int qq = (j - 1) & 3;
-            cb0 = qq == 0 ? Cm : cb0;
-            cb1 = qq == 1 ? Cm : cb1;
-            cb2 = qq == 2 ? Cm : cb2;
-            cb3 = qq == 3 ? Cm : cb3;
-            if (qq == 3 || j == L2) {
-              const int Wp = (L2 + 3) & ~3;
-              *reinterpret_cast<float4*>(sc.chf + c.rm + (int64_t)(i - 1) * Wp + ((j - 1) & ~3)) =
-                  make_float4(cb0, cb1, cb2, cb3);
-              cb0 = cb1 = cb2 = cb3 = LZ;
-            }
+            cmx = ((j - 1) & 63) == 0 ? Cm : fmaxf(cmx, Cm);
+            if ((j & 63) == 0 || j == L2) sc.cmf[c.rm + (int64_t)(i - 1) * local_chunks(L2) + ((j - 1) >> 6)] = cmx;
           }
           LL[0] = Cm; LL[1] = Cx; LL[2] = Cy;
         }
@@ -246,14 +255,14 @@ __global__ __launch_bounds__(256, SweepWaves<M>::fwd) void k_forward(ModelScalar
             // align copies: U becomes the next column's D with its own frame
             double uZm = UZm, uZe = UZe, uZf = UZf, dZm = DZm, dZe = DZe, dZf = DZf;
             double lZm = LZm, lZe = LZe, lZf = LZf;
-            E = pf_align(uZm, uZe, uZf, Ue, dZm, dZe, dZf, De, lZm, lZe, lZf, Le);
+            E = pf_align_fast(uZm, uZe, uZf, Ue, dZm, dZe, dZf, De, lZm, lZe, lZf, Le);
             const double o0 = (j == L2) ? 1.0 : pfo, e0 = (j == L2) ? 1.0 : pfe;
             const double o1 = (i == L1) ? 1.0 : pfo, e1 = (i == L1) ? 1.0 : pfe;
             Ze = uZm * o0 + uZe * e0;
             Zf = lZm * o1 + lZf * e1;
             // QuickProbs' Ze/Zf are ours transposed (QP/PartitionFunction.cpp:128-130)
             Zm = ((M & kQP) != 0 ? (dZm + dZf) + dZe : (dZm + dZe) + dZf) * score;
-            pf_rescale(Zm, Ze, Zf, E);
+            pf_rescale_fast(Zm, Ze, Zf, E);
           }
           sc.zm[idx] = mlp_pf_pack(Zm, E);
           if (act) {
@@ -279,8 +288,8 @@ __global__ __launch_bounds__(256, SweepWaves<M>::fwd) void k_forward(ModelScalar
 }
 
 // =====================================================================
-// Backward sweep (reverse step order): 5-state f+b (in place), local f+b
-// and chain, PF posterior.
+// Backward sweep (reverse step order): 5-state f+b (in place), local b
+// and the chunk maxima of its chain, PF posterior.
 // =====================================================================
 template <int M>
 __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScalars ms, const Tables* __restrict__ tab,
@@ -312,20 +321,19 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
   for (int k = 0; k < 5; ++k) R5[k] = N5[k] = G5[k] = LZ;
 #pragma unroll
   for (int k = 0; k < 3; ++k) RL[k] = NL[k] = GL[k] = LZ;
-  float cb0 = LZ, cb1 = LZ, cb2 = LZ, cb3 = LZ;
+  float cmx = LZ;   // running maximum of the local chain elements in the current 64-column chunk
   BoundaryChunks<M> bc;
   const int nseg = (W + 63) >> 6;
-  // the step-t loads of f5 / fl / zm are issued kPrefetch steps earlier into
+  // the step-t loads of f5 / zm are issued kPrefetch steps earlier into
   // fixed registers: slot u serves steps t0 - u (segments hold whole groups
   // of kPrefetch steps); every slot was written by the forward sweep, values
   // of idle cells are never used
-  float q5[kPrefetch] = {}, ql[kPrefetch] = {};
+  float q5[kPrefetch] = {};
   double qz[kPrefetch] = {};
 #pragma unroll
   for (int k = 0; k < kPrefetch; ++k) {
     const int64_t at = base + (int64_t)(top - k) * 64;
     if constexpr ((M & kHmm5) != 0) q5[k] = sc.f5[at];
-    if constexpr ((M & kLocal) != 0) ql[k] = sc.fl[at];
     if constexpr ((M & kPF) != 0) qz[k] = sc.zm[at];
   }
 
@@ -354,7 +362,7 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
         const int i = c.i, j = c.j, L1 = c.L1, L2 = c.L2;
         const bool act = c.q >= 0 && j <= L2;
         const bool in_i = i < L1, in_j = j < L2;
-        const float f5v = q5[u], flv = ql[u];
+        const float f5v = q5[u];
         const double zmv = qz[u];
         const int c1 = c.c1, c1n = c.c1n;
         const int c2 = C.seq[c.ca];        // residue j   (0 at j = 0 and past L2)
@@ -432,31 +440,18 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
             Bm = mlp_log_add_t(Bm, RL[2] + ms.lt[0][2] - rt1, lk);
             By = mlp_log_add_t(By, RL[2] + ms.lt[2][2] - rt1, lk);
           }
-          sc.fl[idx] = flv + Bm;
+          sc.bl[idx] = Bm;   // f + b is formed by the merge (the same float add)
           if (lane == 0) {
             sc.bndl[(bo + j) * 3 + 0] = Bm;
             sc.bndl[(bo + j) * 3 + 1] = Bx;
             sc.bndl[(bo + j) * 3 + 2] = By;
           }
           // chain element (CPNP/ProbabilisticModel.h:444-445); columns descend,
-          // so a group of 4 is complete at its first column
-#ifdef MLP_EXP_NOCHAIN
-          if (false) {
-#else
+          // so a chunk starts at its top column and ends at 64c + 1
           if (act && i >= 1 && j >= 1) {
-#endif
             const float e = Bm + T_.match[c1 * 26 + c2] - ins1 - T_.ins[c2] - two_rt1;
-            const int qq = (j - 1) & 3;
-            cb0 = qq == 0 ? e : cb0;
-            cb1 = qq == 1 ? e : cb1;
-            cb2 = qq == 2 ? e : cb2;
-            cb3 = qq == 3 ? e : cb3;
-            if (qq == 0) {
-              const int Wp = (L2 + 3) & ~3;
-              *reinterpret_cast<float4*>(sc.chb + c.rm + (int64_t)(i - 1) * Wp + (j - 1)) =
-                  make_float4(cb0, cb1, cb2, cb3);
-              cb0 = cb1 = cb2 = cb3 = LZ;
-            }
+            cmx = ((j & 63) == 0 || j == L2) ? e : fmaxf(cmx, e);
+            if (((j - 1) & 63) == 0) sc.cmb[c.rm + (int64_t)(i - 1) * local_chunks(L2) + ((j - 1) >> 6)] = cmx;
           }
           RL[0] = Bm; RL[1] = Bx; RL[2] = By;
         }
@@ -483,11 +478,11 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
             }
             if (j == 1) { o0 = 1.0; e0 = 1.0; }
             if (i == 1) { o1 = 1.0; e1 = 1.0; }
-            E = pf_align(nZm, nZe, nZf, ne, rZm, rZe, rZf, re, gZm, gZe, gZf, ge);
+            E = pf_align_fast(nZm, nZe, nZf, ne, rZm, rZe, rZf, re, gZm, gZe, gZf, ge);
             Zf = rZm * o1 + rZf * e1;
             Ze = nZm * o0 + nZe * e0;
             Zm = ((M & kQP) != 0 ? (gZm + gZe) + gZf : (gZm + gZf) + gZe) * score;  // QP/PartitionFunction.cpp:260
-            pf_rescale(Zm, Ze, Zf, E);
+            pf_rescale_fast(Zm, Ze, Zf, E);
             if (act) {
               int ef;
               const double zf = mlp_pf_unpack(zmv, &ef);
@@ -510,7 +505,6 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
         // (a loop-carried copy of a pending load would drain vmcnt)
         const int64_t at = base + (int64_t)max(t - kPrefetch, -1) * 64;
         if constexpr ((M & kHmm5) != 0) q5[u] = sc.f5[at];
-        if constexpr ((M & kLocal) != 0) ql[u] = sc.fl[at];
         if constexpr ((M & kPF) != 0) qz[u] = sc.zm[at];
         cursor_prev(c, C, T_.ins);
       }
@@ -559,12 +553,12 @@ __global__ __launch_bounds__(256, MLP_MERGE_WAVES) void k_merge(ModelScalars ms,
   constexpr int QD = 8;
   // fixed-register load queue: slot u serves steps t0 + u (segments hold
   // whole groups of QD steps); values of idle cells are never used
-  float q5[QD] = {}, ql[QD] = {}, qg[QD] = {};
+  float q5[QD] = {}, ql[QD] = {}, qb[QD] = {}, qg[QD] = {};
 #pragma unroll
   for (int k = 0; k < QD; ++k) {
     const int64_t at = base + (int64_t)k * 64;
     if constexpr ((M & kHmm5) != 0) q5[k] = sc.f5[at];
-    if constexpr ((M & kLocal) != 0) ql[k] = sc.fl[at];
+    if constexpr ((M & kLocal) != 0) { ql[k] = sc.fl[at]; qb[k] = sc.bl[at]; }
     if constexpr ((M & kPF) != 0) qg[k] = sc.pg[at];
   }
   const int nseg = (W + 63) >> 6;
@@ -588,7 +582,9 @@ __global__ __launch_bounds__(256, MLP_MERGE_WAVES) void k_merge(ModelScalars ms,
       for (int u = 0; u < QD; ++u) {
         const int t = t0 + u;
         const int i = c.i, j = c.j, L1 = c.L1, L2 = c.L2;
-        const float f5v = q5[u], flv = ql[u], pgv = qg[u];
+        // local f + b (CPNP/ProbabilisticModel.h:484): the same float add the
+        // backward sweep used to do in place
+        const float f5v = q5[u], flv = ql[u] + qb[u], pgv = qg[u];
         Dv = Uv;
         Uv = take_bnd ? mlp_shr1(Lv, readlane_f(bch, t - t_lo)) : mlp_shr1z(Lv);
         if constexpr (NP) {
@@ -661,7 +657,7 @@ __global__ __launch_bounds__(256, MLP_MERGE_WAVES) void k_merge(ModelScalars ms,
         // refill slot u once its value is dead (see k_backward)
         const int64_t at = base + (int64_t)min(t + QD, last) * 64;
         if constexpr ((M & kHmm5) != 0) q5[u] = sc.f5[at];
-        if constexpr ((M & kLocal) != 0) ql[u] = sc.fl[at];
+        if constexpr ((M & kLocal) != 0) { ql[u] = sc.fl[at]; qb[u] = sc.bl[at]; }
         if constexpr ((M & kPF) != 0) qg[u] = sc.pg[at];
         cursor_next(c, C, noins);
       }

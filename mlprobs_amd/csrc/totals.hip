@@ -23,166 +23,89 @@ static inline dim3 wave_grid(int64_t n) {
 // =====================================================================
 // Local-model totals: the reference sums LOG_PLUS_EQUALS over all interior
 // cells in row-major order (CPNP/ProbabilisticModel.h:435-450), a single
-// non-associative chain, for the forward and the backward half.
+// non-associative chain, for the forward half (f_M) and the backward half
+// (b_M + emission).
 //
-// Rows are padded to a multiple of 4 with LOG_ZERO, a no-op element.  An
-// element x changes the running value acc only if acc - x < 7.5: otherwise
-// LOG_ADD returns acc unchanged (CPNP/ScoreType.h:279-285), so skipping it is
-// exact; acc never decreases, so a skipped element stays skippable.
+// An element x changes the running value acc only if acc - x < 7.5:
+// otherwise LOG_ADD returns acc unchanged (CPNP/ScoreType.h:279-285), so
+// skipping it is exact; acc never decreases, so a skipped element stays
+// skippable.  The sweeps leave, per pair row and 64-column chunk, the
+// largest chain element of the chunk (Scratch::cmf / cmb); a chunk with
+// acc - max >= 7.5 holds no element that can change acc (fl(acc - x) >=
+// fl(acc - max) for x <= max) and is skipped whole.  At C3 about 0.5% of the
+// forward chunks and 0.07% of the backward ones are not skippable; only
+// those are read, 64 elements gathered from the step-diagonal f_M / b_M
+// (their addresses from the chain layout), and folded exactly in order.
+// One wave per pair; acc is wave-uniform.
 // =====================================================================
-// Variant (default): 8 pairs per wave, 8 lanes per pair.  Chunks of 64
-// elements per chain (8 per lane, two float4 loads); candidates of each
-// chain (elements with acc - x < 7.5, acc = chain value at the chunk start)
-// are compacted in order into LDS, then lanes 0..15 fold the 16 chains of the
-// wave in parallel.  The candidate list is a superset of the elements that
-// change acc: LOG_ADD(acc, x) for acc - x >= 7.5 returns acc exactly, so
-// folding every listed element reproduces the reference's serial chain.
-#ifndef MLP_TOT_PAIRS
-#define MLP_TOT_PAIRS 8
-#endif
-constexpr int kTotPairs = MLP_TOT_PAIRS;   // pairs per wave
-constexpr int kTotLP = 64 / kTotPairs;      // lanes per pair
-constexpr int kTotEL = 64 / kTotLP;         // elements per lane per 64-element chunk (float4 pieces: >= 4)
-static_assert(kTotEL >= 4 && kTotEL % 4 == 0, "MLP_TOT_PAIRS must be 4, 8 or 16");
-__global__ __launch_bounds__(256) void k_local_totals_multi(SeqSet sq, PairMeta pm, PairRec* __restrict__ rec,
-                                                            Scratch sc, int64_t npairs) {
-  __shared__ float4 lk[kLookupRows];
-  __shared__ float list[kWavesPerBlock][2 * kTotPairs][64];
-  if (threadIdx.x == 0) mlp_lookup_table(lk);
-  __syncthreads();
-  const int lane = threadIdx.x & 63;
-  const int w = threadIdx.x >> 6;
-  const int g = lane / kTotLP, sub = lane % kTotLP;
-  const int64_t p = ((int64_t)blockIdx.x * kWavesPerBlock + w) * kTotPairs + g;
-  int64_t ne = 0, base = 0;
-  if (p < npairs) {
-    const int L1 = sq.len[pm.pa[p]], L2 = sq.len[pm.pb[p]];
-    ne = (int64_t)L1 * ((L2 + 3) & ~3);
-    base = pm.rm_off[p];
-  }
-  int64_t emax = ne;
-  for (int off = 32; off >= kTotLP; off >>= 1) emax = max(emax, (int64_t)__shfl_xor(emax, off));
-  const float* __restrict__ cf = sc.chf + base;
-  const float* __restrict__ cb = sc.chb + base;
-  // chain c = 2g (forward) / 2g+1 (backward) is folded on lane c
+template <bool BWD>
+__device__ __forceinline__ float local_chain_fold(const float* __restrict__ cmx, const float* __restrict__ vals,
+                                                  int L1, int L2, int row0, int W, int64_t cell_off,
+                                                  const uint8_t* s1, const uint8_t* s2, const float* match,
+                                                  const float* ins, float two_rt1, const float4* lk, int lane) {
+  const int nch = local_chunks(L2);
+  const int64_t n = (int64_t)L1 * nch;
   float acc = LZ;
-  float nf[kTotEL], nb[kTotEL];
-  auto load = [&](int64_t e0, float* f, float* b) {
-    const int64_t e = e0 + sub * kTotEL;   // ne is a multiple of 4: float4 pieces are all-in or all-out
-#pragma unroll
-    for (int h = 0; h < kTotEL / 4; ++h) {
-      float4 vf = make_float4(LZ, LZ, LZ, LZ), vb = vf;
-      if (e + 4 * h < ne) {
-        vf = *reinterpret_cast<const float4*>(cf + e + 4 * h);
-        vb = *reinterpret_cast<const float4*>(cb + e + 4 * h);
+  for (int64_t k0 = 0; k0 < n; k0 += 64) {
+    const int64_t kk = k0 + lane;
+    const float mx = kk < n ? cmx[kk] : LZ;
+    uint64_t live = __ballot(kk < n && !(acc - mx >= 7.5f));
+    while (live) {
+      const int64_t ck = k0 + __builtin_ctzll(live);
+      const int i = (int)(ck / nch) + 1, cidx = (int)(ck % nch);
+      const int j = 64 * cidx + 1 + lane;   // this lane's column of the chunk
+      float x = LZ;
+      const bool in = j <= L2;
+      if (in) {
+        const int g = row0 + i, r = g & 63;
+        const int64_t tau = (int64_t)W * (g >> 6) + r + j;
+        const float v = vals[cell_off + (tau + 1) * 64 + r];
+        if constexpr (BWD) {
+          // CPNP/ProbabilisticModel.h:444-445, the backward sweep's expression
+          const int c1 = s1[i - 1], c2 = s2[j - 1];
+          x = v + match[c1 * 26 + c2] - ins[c1] - ins[c2] - two_rt1;
+        } else {
+          x = v;
+        }
       }
-      f[4 * h + 0] = vf.x; f[4 * h + 1] = vf.y; f[4 * h + 2] = vf.z; f[4 * h + 3] = vf.w;
-      b[4 * h + 0] = vb.x; b[4 * h + 1] = vb.y; b[4 * h + 2] = vb.z; b[4 * h + 3] = vb.w;
+      // the chunk's elements in column order; candidates only (exact)
+      uint64_t m = __ballot(in && !(acc - x >= 7.5f));
+      while (m) {
+        const float v = readlane_f(x, __builtin_ctzll(m));
+        acc = mlp_log_add_t(acc, v, lk);
+        m &= m - 1;
+        m &= __ballot(!(acc - x >= 7.5f));
+      }
+      live &= live - 1;
+      live &= __ballot(!(acc - mx >= 7.5f));
     }
-  };
-  // two chunks in flight: HBM latency exceeds one chunk's fold
-  float nf2[kTotEL], nb2[kTotEL];
-  load(0, nf, nb);
-  load(64, nf2, nb2);
-  // exclusive prefix of a per-lane count over the kTotLP lanes of its group
-  auto group_scan = [&](int c) {
-    int x = c;
-#pragma unroll
-    for (int d = 1; d < kTotLP; d <<= 1) {
-      const int y = __shfl_up(x, d, kTotLP);
-      x += (sub >= d) ? y : 0;
-    }
-    return x - c;
-  };
-  auto chunk = [&](int64_t e0, float* xf, float* xb) {
-    const float af = __shfl(acc, 2 * g), ab = __shfl(acc, 2 * g + 1);
-    const int64_t e = e0 + sub * kTotEL;
-    unsigned ff = 0, fb = 0;
-#pragma unroll
-    for (int k = 0; k < kTotEL; ++k) {
-      const bool in = e + k < ne;
-      ff |= (in && !(af - xf[k] >= 7.5f)) ? (1u << k) : 0u;
-      fb |= (in && !(ab - xb[k] >= 7.5f)) ? (1u << k) : 0u;
-    }
-    const int cf_n = __popc(ff), cb_n = __popc(fb);
-    int pf = group_scan(cf_n), pb = group_scan(cb_n);
-    float* lf = list[w][2 * g];
-    float* lb = list[w][2 * g + 1];
-#pragma unroll
-    for (int k = 0; k < kTotEL; ++k) {
-      if (ff & (1u << k)) lf[pf++] = xf[k];
-      if (fb & (1u << k)) lb[pb++] = xb[k];
-    }
-    // totals per chain: last lane of the group holds the inclusive sums
-    const int tot_f = __shfl(pf, g * kTotLP + kTotLP - 1), tot_b = __shfl(pb, g * kTotLP + kTotLP - 1);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // chain `lane` (< 16) folds its list; count from its group's last lane
-    const int cnt_f = __shfl(tot_f, (lane >> 1) * kTotLP), cnt_b = __shfl(tot_b, (lane >> 1) * kTotLP);
-    const int cnt = lane < 2 * kTotPairs ? ((lane & 1) ? cnt_b : cnt_f) : 0;
-    const float* my = list[w][lane & (2 * kTotPairs - 1)];
-    for (int k = 0; __any(k < cnt); ++k) {
-      if (k < cnt) acc = mlp_log_add_t(acc, my[k], lk);
-    }
-    __builtin_amdgcn_wave_barrier();
-  };
-  for (int64_t e0 = 0; e0 < emax; e0 += 128) {
-    float xf[kTotEL], xb[kTotEL];
-#pragma unroll
-    for (int k = 0; k < kTotEL; ++k) { xf[k] = nf[k]; xb[k] = nb[k]; }
-    if (e0 + 128 < emax) load(e0 + 128, nf, nb);
-    chunk(e0, xf, xb);
-    if (e0 + 64 >= emax) break;
-#pragma unroll
-    for (int k = 0; k < kTotEL; ++k) { xf[k] = nf2[k]; xb[k] = nb2[k]; }
-    if (e0 + 192 < emax) load(e0 + 192, nf2, nb2);
-    chunk(e0 + 64, xf, xb);
   }
-  const float tf = __shfl(acc, 2 * g), tb = __shfl(acc, 2 * g + 1);
-  if (p < npairs && sub == 0) {
-    rec[p].tfl = tf;
-    rec[p].tbl = tb;
-  }
+  return acc;
 }
 
-// Variant: one wave per pair, candidates folded serially (see above).
-__global__ __launch_bounds__(256) void k_local_totals_wave(SeqSet sq, PairMeta pm, PairRec* __restrict__ rec,
-                                                           Scratch sc, int64_t npairs) {
+__global__ __launch_bounds__(256) void k_local_totals(ModelScalars ms, const Tables* __restrict__ tab, SeqSet sq,
+                                                      PairMeta pm, ChainMeta cm, PairRec* __restrict__ rec,
+                                                      Scratch sc, int64_t npairs) {
   __shared__ float4 lk[kLookupRows];
+  __shared__ float match[26 * 26], ins[26];
   if (threadIdx.x == 0) mlp_lookup_table(lk);
+  for (int k = threadIdx.x; k < 26 * 26; k += blockDim.x) match[k] = tab->match[k];
+  if (threadIdx.x < 26) ins[threadIdx.x] = tab->ins[threadIdx.x];
   __syncthreads();
   const int64_t p = wave_index();
   if (p >= npairs) return;
   const int lane = threadIdx.x & 63;
   const int L1 = sq.len[pm.pa[p]], L2 = sq.len[pm.pb[p]];
-  const int64_t ne = (int64_t)L1 * ((L2 + 3) & ~3);
-  const float* __restrict__ cf = sc.chf + pm.rm_off[p];
-  const float* __restrict__ cbk = sc.chb + pm.rm_off[p];
-  // lane 0 carries the forward chain, lane 1 the backward chain: one LOG_ADD
-  // sequence advances both (LOG_ADD(acc, LOG_ZERO) == acc keeps an idle
-  // chain unchanged)
-  float acc = LZ;
-  float tf = LZ, tb = LZ;   // wave-uniform copies
-  float xf = LZ, xb = LZ;
-  if (lane < ne) { xf = cf[lane]; xb = cbk[lane]; }
-  for (int64_t c0 = 0; c0 < ne; c0 += 64) {
-    const float cxf = xf, cxb = xb;
-    const int64_t nx = c0 + 64 + lane;
-    xf = LZ; xb = LZ;
-    if (nx < ne) { xf = cf[nx]; xb = cbk[nx]; }   // prefetch next chunk
-    uint64_t mf = __ballot(!(tf - cxf >= 7.5f));
-    uint64_t mb = __ballot(!(tb - cxb >= 7.5f));
-    while (mf | mb) {
-      const float vf = mf ? readlane_f(cxf, __builtin_ctzll(mf)) : LZ;
-      const float vb = mb ? readlane_f(cxb, __builtin_ctzll(mb)) : LZ;
-      acc = mlp_log_add_t(acc, lane == 0 ? vf : vb, lk);
-      tf = readlane_f(acc, 0);
-      tb = readlane_f(acc, 1);
-      if (mf) mf = (mf & (mf - 1)) & __ballot(!(tf - cxf >= 7.5f));
-      if (mb) mb = (mb & (mb - 1)) & __ballot(!(tb - cxb >= 7.5f));
-    }
-  }
+  const int h = pm.chain[p];
+  const int W = cm.width[h], row0 = pm.row0[p];
+  const int64_t cell_off = cm.cell_off[h];
+  const uint8_t* s1 = sq.res + sq.off[pm.pa[p]];
+  const uint8_t* s2 = sq.res + sq.off[pm.pb[p]];
+  const int64_t rm = pm.rm_off[p];
+  const float tf = local_chain_fold<false>(sc.cmf + rm, sc.fl, L1, L2, row0, W, cell_off, s1, s2, match, ins,
+                                           2 * ms.rt1, lk, lane);
+  const float tb = local_chain_fold<true>(sc.cmb + rm, sc.bl, L1, L2, row0, W, cell_off, s1, s2, match, ins,
+                                          2 * ms.rt1, lk, lane);
   if (lane == 0) {
     rec[p].tfl = tf;
     rec[p].tbl = tb;
@@ -253,15 +176,11 @@ __global__ void k_fold_totals(ModelScalars ms, SeqSet sq, PairMeta pm, PairRec* 
 }
 
 // ------------------------------------------------------------ launchers
-hipError_t launch_local_totals(SeqSet seqs, PairMeta pm, PairRec* rec, Scratch sc, int64_t npairs,
-                               hipStream_t st) {
+hipError_t launch_local_totals(const ModelScalars& ms, const Tables* tab, SeqSet seqs, PairMeta pm, ChainMeta cm,
+                               PairRec* rec, Scratch sc, int64_t npairs, hipStream_t st) {
   if (npairs <= 0) return hipSuccess;
-  const char* v = getenv("MLP_TOTALS");
-  if (v && v[0] == 'w')
-    hipLaunchKernelGGL(k_local_totals_wave, wave_grid(npairs), dim3(64 * kWavesPerBlock), 0, st, seqs, pm, rec, sc, npairs);
-  else
-    hipLaunchKernelGGL(k_local_totals_multi, dim3((unsigned)((npairs + kTotPairs * kWavesPerBlock - 1) / (kTotPairs * kWavesPerBlock))),
-                       dim3(64 * kWavesPerBlock), 0, st, seqs, pm, rec, sc, npairs);
+  hipLaunchKernelGGL(k_local_totals, wave_grid(npairs), dim3(64 * kWavesPerBlock), 0, st, ms, tab, seqs, pm, cm, rec,
+                     sc, npairs);
   return hipGetLastError();
 }
 

@@ -12,6 +12,6 @@ mkdir -p $O
 timeout -k 10 900 python3 bench.py "$@" > $O/bench.log 2>&1 || { tail -30 $O/bench.log; exit 1; }
 grep '^{"metric"' $O/bench.log | tail -1 > $O/bench.json
 grep '^\[bench' $O/bench.log
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o stats -- python3 bench.py --no-e2e "$@" \
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o stats -- python3 bench.py --no-e2e --no-shards "$@" \
     > $O/prof_bench.log 2>&1 || { tail -30 $O/prof_bench.log; exit 1; }
 grep '^{"metric"' $O/prof_bench.log | tail -1 > $O/prof_bench.json
