@@ -469,7 +469,7 @@ def shard_gather(args, seqs):
     fam.relax(1)
     fam.synchronize()
     res['relax_round_s'] = time.perf_counter() - t0
-    res['relax_gather_ms'] = fam.kernel_times()['allgather']['ms'] - kt['ms']
+    res['relax_gather_ms'] = fam.kernel_times()['allgather']['ms']  # counters reset before the round
     fam.close()
     log(f"shards: posteriors {t_post:.2f} s (gather {kt['ms']:.1f} ms), relax round {res['relax_round_s']:.2f} s")
     return res

@@ -102,6 +102,9 @@ std::string mea_path(int len1, int len2, const float* post, float* score);  // (
 std::string mea_path_serial(int len1, int len2, const float* post, float* score);
 std::string mea_path_dispatch(int len1, int len2, const float* post, float* score);  // untimed
 std::string mea_path_wave(int len1, int len2, const float* post, float* score);  // threads over 64-row bands
+// SIMD lanes over rows (8: AVX2, 16: AVX-512; 0: none), MLP_MEA_SIMD overrides
+int mea_simd_lanes();
+std::string mea_path_simd(int len1, int len2, const float* post, float* score, int lanes);
 // accumulated seconds of profile posteriors and MEA, calls (MLP_CLI_TIMES)
 void profile_times(double* post, double* mea, int64_t* calls, int64_t* device_calls);
 

@@ -39,6 +39,7 @@ namespace {
 struct DevBuf {
   void* p = nullptr;
   size_t bytes = 0;
+  bool lent = false;  // carved from the idle batch scratch (ensure_tmp), not owned
 };
 
 enum KernelId { KFWD = 0, KBWD, KTOT, KMERGE, KCOMPACT, KRELAX, KTRANS, KFILTER, KGATHER, KVITERBI };
@@ -106,6 +107,8 @@ struct mlp_ctx {
   DevBuf scratch, scratch2;        // batch scratch of the two posterior streams
   size_t scratch_budget = 0;
   // relaxation buffers
+  bool arena_on = false;               // relax_one: temporaries come from the batch scratch
+  size_t arena_off = 0;
   DevBuf r_trowptr, r_tcols, r_tvals, r_raw, r_newrp, r_newcols, r_newvals, r_tasks_p, r_tasks_r,
       r_pairs, r_nnz, r_newoff, r_img, r_imgoff, r_tiles, r_nwords, r_weights, r_seldist, r_profile, r_mea;
   // comm
@@ -154,6 +157,11 @@ struct mlp_ctx {
   } while (0)
 
 static int ensure(mlp_ctx* c, DevBuf& b, size_t bytes) {
+  if (b.lent) {  // a lent buffer is only valid inside the round that carved it
+    b.p = nullptr;
+    b.bytes = 0;
+    b.lent = false;
+  }
   if (b.bytes >= bytes) return MLP_OK;
   if (b.p) hipFree(b.p);
   b.p = nullptr;
@@ -166,6 +174,25 @@ static int ensure(mlp_ctx* c, DevBuf& b, size_t bytes) {
   }
   b.bytes = want;
   return MLP_OK;
+}
+
+// A relaxation round's temporaries (transposes, images, tiles, raw values,
+// the filtered entries) carved from the posterior stage's batch scratch,
+// idle between posterior stages: at C3 ~10 GB fewer bytes per process (a
+// fresh process's allocations wait while the driver clears what earlier
+// processes released).  Valid until the round ends; without scratch room
+// the buffer is an owned allocation as before.
+static int ensure_tmp(mlp_ctx* c, DevBuf& b, size_t bytes) {
+  const size_t need = (std::max<size_t>(bytes, 256) + 255) & ~(size_t)255;
+  if (c->arena_on && c->scratch.p && c->arena_off + need <= c->scratch.bytes) {
+    if (b.p && !b.lent) hipFree(b.p);
+    b.p = (char*)c->scratch.p + c->arena_off;
+    b.bytes = need;
+    b.lent = true;
+    c->arena_off += need;
+    return MLP_OK;
+  }
+  return ensure(c, b, bytes);
 }
 
 template <class T>
@@ -423,7 +450,7 @@ void mlp_ctx_destroy(mlp_ctx* c) {
                     &c->r_nnz, &c->r_newoff, &c->r_img, &c->r_imgoff, &c->r_tiles, &c->r_nwords, &c->r_weights,
                     &c->r_seldist, &c->r_profile, &c->r_mea, &c->ag_cols, &c->ag_vals};
   for (DevBuf* b : bufs)
-    if (b->p) hipFree(b->p);
+    if (b->p && !b->lent) hipFree(b->p);
   if (c->comm) ncclCommDestroy(c->comm);
   for (hipEvent_t e : c->evpool) hipEventDestroy(e);
   if (getenv("MLP_PROFILE_TIMES") && (c->prof_t[0] > 0 || c->prof_t[1] > 0))
@@ -1118,7 +1145,7 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
     hipStream_t st = streams[B.slot];
     HIPCHK(c, hipStreamSynchronize(st));
     const int64_t np = B.np;
-#if defined(MLP_EXP_NOCHAIN) || defined(MLP_EXP_CONSTLK)
+#if defined(MLP_EXP_NOCHAIN) || defined(MLP_EXP_CONSTLK) || defined(MLP_EXP_TOT_NOFWD) || defined(MLP_EXP_TOT_NOBWD)
     for (int64_t s = 0; s < np; s++) B.rec[s].flags = 0;  // timing experiments: results are not meaningful
 #endif
     for (int64_t s = 0; s < np; s++) {
@@ -2293,6 +2320,16 @@ static int relax_one(mlp_ctx* c, const QpRelax& qp, bool last) {
     return MLP_ERR_STATE;
   }
   hipSetDevice(c->device);
+  HIPCHK(c, hipStreamSynchronize(c->stream2));  // the batch scratch is idle: its temporaries come from there
+  c->arena_on = true;
+  c->arena_off = 0;
+  struct ArenaOff {
+    mlp_ctx* c;
+    ~ArenaOff() {
+      c->arena_on = false;
+      c->tr_ver = ~0ull;  // the lent transposes are gone after the round
+    }
+  } arena_guard{c};
   int64_t r0 = 0, r1 = c->P;
   if (c->rel_r0 >= 0) {
     r0 = c->rel_r0;
@@ -2318,13 +2355,13 @@ static int relax_one(mlp_ctx* c, const QpRelax& qp, bool last) {
   };
   {
     const int64_t total = c->store_total;
-    if ((rc = ensure(c, c->r_trowptr, sizeof(int32_t) * c->trp_off[c->P]))) return rc;
-    if ((rc = ensure(c, c->r_tcols, sizeof(uint16_t) * std::max<int64_t>(total, 1)))) return rc;
-    if ((rc = ensure(c, c->r_tvals, sizeof(float) * std::max<int64_t>(total, 1)))) return rc;
-    if ((rc = ensure(c, c->r_raw, sizeof(float) * std::max<int64_t>(total, 1)))) return rc;
-    if ((rc = ensure(c, c->r_pairs, sizeof(int64_t) * std::max<int64_t>(c->P, 1)))) return rc;
-    if ((rc = ensure(c, c->r_nnz, sizeof(int64_t) * std::max<int64_t>(c->P, 1)))) return rc;
-    if ((rc = ensure(c, c->r_newoff, sizeof(int64_t) * (c->P + 1)))) return rc;
+    if ((rc = ensure_tmp(c, c->r_trowptr, sizeof(int32_t) * c->trp_off[c->P]))) return rc;
+    if ((rc = ensure_tmp(c, c->r_tcols, sizeof(uint16_t) * std::max<int64_t>(total, 1)))) return rc;
+    if ((rc = ensure_tmp(c, c->r_tvals, sizeof(float) * std::max<int64_t>(total, 1)))) return rc;
+    if ((rc = ensure_tmp(c, c->r_raw, sizeof(float) * std::max<int64_t>(total, 1)))) return rc;
+    if ((rc = ensure_tmp(c, c->r_pairs, sizeof(int64_t) * std::max<int64_t>(c->P, 1)))) return rc;
+    if ((rc = ensure_tmp(c, c->r_nnz, sizeof(int64_t) * std::max<int64_t>(c->P, 1)))) return rc;
+    if ((rc = ensure_tmp(c, c->r_newoff, sizeof(int64_t) * (c->P + 1)))) return rc;
     if ((rc = ensure(c, c->r_newrp, sizeof(int32_t) * c->rp_off[c->P]))) return rc;
     // all pairs are transposed (every rank reads every block)
     std::vector<int64_t> allp(c->P);
@@ -2360,7 +2397,7 @@ static int relax_one(mlp_ctx* c, const QpRelax& qp, bool last) {
     const int tmax = tenv ? std::max(1, std::min(kTileMax, atoi(tenv))) : kTileMax;
     bool tasks_only = (mode && !strcmp(mode, "tasks")) || c->max_len > 8000 || c->P >= (1LL << 31);
     std::vector<int32_t> nwords(2 * c->P, 0);
-    if ((rc = ensure(c, c->r_nwords, sizeof(int32_t) * std::max<int64_t>(2 * c->P, 1)))) return rc;
+    if ((rc = ensure_tmp(c, c->r_nwords, sizeof(int32_t) * std::max<int64_t>(2 * c->P, 1)))) return rc;
     PackArgs pk;
     pk.n = c->n;
     pk.lens = c->d_len;
@@ -2597,9 +2634,9 @@ static int relax_one(mlp_ctx* c, const QpRelax& qp, bool last) {
     }
     const int64_t ntiles = cls_tiles[0] + cls_tiles[1];
     if (ntiles) {
-      if ((rc = ensure(c, c->r_img, std::max<int64_t>(img_off[2 * c->P], 16)))) return rc;
-      if ((rc = ensure(c, c->r_imgoff, sizeof(int64_t) * (2 * c->P + 1)))) return rc;
-      if ((rc = ensure(c, c->r_tiles, sizeof(int32_t) * tiles.size()))) return rc;
+      if ((rc = ensure_tmp(c, c->r_img, std::max<int64_t>(img_off[2 * c->P], 16)))) return rc;
+      if ((rc = ensure_tmp(c, c->r_imgoff, sizeof(int64_t) * (2 * c->P + 1)))) return rc;
+      if ((rc = ensure_tmp(c, c->r_tiles, sizeof(int32_t) * tiles.size()))) return rc;
       HIPCHK(c, hipMemcpyAsync(c->r_imgoff.p, img_off.data(), sizeof(int64_t) * (2 * c->P + 1),
                                hipMemcpyHostToDevice, c->stream));
       HIPCHK(c, hipMemcpyAsync(c->r_tiles.p, tiles.data(), sizeof(int32_t) * tiles.size(), hipMemcpyHostToDevice,
@@ -2626,8 +2663,8 @@ static int relax_one(mlp_ctx* c, const QpRelax& qp, bool last) {
       c->err = "MLP_RELAX=pairs: " + std::to_string(nt) + " row tasks fell back";
       return MLP_ERR_STATE;
     }
-    if ((rc = ensure(c, c->r_tasks_p, sizeof(int64_t) * std::max<int64_t>(nt, 1)))) return rc;
-    if ((rc = ensure(c, c->r_tasks_r, sizeof(int32_t) * std::max<int64_t>(nt, 1)))) return rc;
+    if ((rc = ensure_tmp(c, c->r_tasks_p, sizeof(int64_t) * std::max<int64_t>(nt, 1)))) return rc;
+    if ((rc = ensure_tmp(c, c->r_tasks_r, sizeof(int32_t) * std::max<int64_t>(nt, 1)))) return rc;
     if (nt) {
       HIPCHK(c, hipMemcpyAsync(c->r_tasks_p.p, tp.data(), sizeof(int64_t) * nt, hipMemcpyHostToDevice, c->stream));
       HIPCHK(c, hipMemcpyAsync(c->r_tasks_r.p, tr.data(), sizeof(int32_t) * nt, hipMemcpyHostToDevice, c->stream));
@@ -2732,8 +2769,8 @@ static int relax_one(mlp_ctx* c, const QpRelax& qp, bool last) {
       noff[r0 + k] = run;
       run += pn[k];
     }
-    if ((rc = ensure(c, c->r_newcols, sizeof(uint16_t) * std::max<int64_t>(run, 1)))) return rc;
-    if ((rc = ensure(c, c->r_newvals, sizeof(float) * std::max<int64_t>(run, 1)))) return rc;
+    if ((rc = ensure_tmp(c, c->r_newcols, sizeof(uint16_t) * std::max<int64_t>(run, 1)))) return rc;
+    if ((rc = ensure_tmp(c, c->r_newvals, sizeof(float) * std::max<int64_t>(run, 1)))) return rc;
     HIPCHK(c, hipMemcpyAsync(c->r_newoff.p, noff.data(), sizeof(int64_t) * (c->P + 1), hipMemcpyHostToDevice, c->stream));
     mark("filter count, scan");
     fa.new_cols = (uint16_t*)c->r_newcols.p;

@@ -28,32 +28,45 @@ static inline dim3 wave_grid(int64_t n) {
 //
 // An element x changes the running value acc only if acc - x < 7.5:
 // otherwise LOG_ADD returns acc unchanged (CPNP/ScoreType.h:279-285), so
-// skipping it is exact; acc never decreases, so a skipped element stays
-// skippable.  The sweeps leave, per pair row and 64-column chunk, the
-// largest chain element of the chunk (Scratch::cmf / cmb); a chunk with
-// acc - max >= 7.5 holds no element that can change acc (fl(acc - x) >=
-// fl(acc - max) for x <= max) and is skipped whole.  At C3 about 0.5% of the
-// forward chunks and 0.07% of the backward ones are not skippable; only
-// those are read, 64 elements gathered from the step-diagonal f_M / b_M
-// (their addresses from the chain layout), and folded exactly in order.
+// skipping it is exact.  LOG_ADD(acc, x) >= max(acc, x) (the LOOKUP cubic
+// lies >= 4.4e-4 above d on every float d in [0, 7.5), checked exhaustively),
+// so acc is at least every element before it in the chain: an element with
+// bound - x >= 7.5, bound = the largest element before it, is skipped exactly
+// (fl(acc - x) >= fl(bound - x) for acc >= bound).
+//
+// Forward (about one row in 1.5 holds a candidate chunk, ~10 candidates a
+// row at C3): the wave streams the pair's f_M strip by strip in its
+// step-diagonal layout (one coalesced 256-B slab per step, lane r holding row
+// 64 S + r in column order), the bound being the larger of the rows before
+// (prefix maximum of the sweeps' per-chunk maxima, Scratch::cmf) and the row
+// so far; each lane lists its row's candidates in LDS and the strip's rows
+// are then folded in order.  A row with more than kRowList candidates (the
+// first rows of a pair) is folded chunk by chunk from HBM instead.
+// Backward (0.1% of the chunks hold a candidate): chunks whose maximum
+// (Scratch::cmb) passes the test against acc are gathered and folded.
 // One wave per pair; acc is wave-uniform.
 // =====================================================================
+constexpr int kRowList = 16;
+constexpr int kListPitch = 65;  // LDS row pitch of a wave's candidate lists (bank-conflict free)
+
+// Fold chunks [kb, ke) of a chain (row-major chunk index (i - 1) * nch + c)
+// whose maximum passes the test against acc, elements gathered from the
+// step-diagonal array.
 template <bool BWD>
-__device__ __forceinline__ float local_chain_fold(const float* __restrict__ cmx, const float* __restrict__ vals,
-                                                  int L1, int L2, int row0, int W, int64_t cell_off,
-                                                  const uint8_t* s1, const uint8_t* s2, const float* match,
-                                                  const float* ins, float two_rt1, const float4* lk, int lane) {
+__device__ __forceinline__ float fold_chunks(float acc, int64_t kb, int64_t ke, const float* __restrict__ cmx,
+                                             const float* __restrict__ vals, int L2, int row0, int W,
+                                             int64_t cell_off, const uint8_t* s1, const uint8_t* s2,
+                                             const float* match, const float* ins, float two_rt1,
+                                             const float4* lk, int lane) {
   const int nch = local_chunks(L2);
-  const int64_t n = (int64_t)L1 * nch;
-  float acc = LZ;
-  for (int64_t k0 = 0; k0 < n; k0 += 64) {
+  for (int64_t k0 = kb; k0 < ke; k0 += 64) {
     const int64_t kk = k0 + lane;
-    const float mx = kk < n ? cmx[kk] : LZ;
-    uint64_t live = __ballot(kk < n && !(acc - mx >= 7.5f));
+    const float mx = kk < ke ? cmx[kk] : LZ;
+    uint64_t live = __ballot(kk < ke && !(acc - mx >= 7.5f));
     while (live) {
       const int64_t ck = k0 + __builtin_ctzll(live);
       const int i = (int)(ck / nch) + 1, cidx = (int)(ck % nch);
-      const int j = 64 * cidx + 1 + lane;   // this lane's column of the chunk
+      const int j = 64 * cidx + 1 + lane;  // this lane's column of the chunk
       float x = LZ;
       const bool in = j <= L2;
       if (in) {
@@ -83,11 +96,72 @@ __device__ __forceinline__ float local_chain_fold(const float* __restrict__ cmx,
   return acc;
 }
 
+__device__ __forceinline__ float local_fwd_fold(const float* __restrict__ cmf, const float* __restrict__ fl, int L1,
+                                                int L2, int row0, int W, int64_t cell_off, const float4* lk,
+                                                float* lst, int lane) {
+  const int nch = local_chunks(L2);
+  float acc = LZ, carry = LZ;  // carry: the largest element of the pair's rows before strip S
+  const int S0 = (row0 + 1) >> 6, S1 = (row0 + L1) >> 6;
+  const int tend = L2 + 63;  // steps of a strip: lane r holds column t - r at step t
+  for (int S = S0; S <= S1; ++S) {
+    const int i = 64 * S + lane - row0;  // this lane's pair row
+    const bool row_in = i >= 1 && i <= L1;
+    float rmx = LZ;
+    if (row_in)
+      for (int c = 0; c < nch; ++c) rmx = fmaxf(rmx, cmf[(int64_t)(i - 1) * nch + c]);
+    float incl = rmx;  // inclusive prefix maximum over the strip's rows
+    for (int off = 1; off < 64; off <<= 1) {
+      const float y = __shfl_up(incl, off);
+      if (lane >= off) incl = fmaxf(incl, y);
+    }
+    float before = __shfl_up(incl, 1);
+    if (lane == 0) before = LZ;
+    float run = fmaxf(carry, before);
+    carry = fmaxf(carry, readlane_f(incl, 63));
+    int cnt = 0;
+    const float* slab = fl + cell_off + ((int64_t)W * S + 1) * 64 + lane;  // + t * 64: step W S + t
+    for (int t0 = 1; t0 <= tend; t0 += 8) {
+      float x[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) x[u] = (t0 + u <= tend) ? slab[(int64_t)(t0 + u) * 64] : LZ;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int j = t0 + u - lane;
+        if (row_in && j >= 1 && j <= L2) {
+          if (!(run - x[u] >= 7.5f)) {
+            if (cnt < kRowList) lst[cnt * kListPitch + lane] = x[u];
+            ++cnt;
+          }
+          run = fmaxf(run, x[u]);
+        }
+      }
+    }
+    // the strip's rows in order
+    for (int r = 0; r < 64; ++r) {
+      const int n = __builtin_amdgcn_readlane(cnt, r);
+      if (n == 0) continue;
+      if (n <= kRowList) {
+        const float xv = lane < n ? lst[lane * kListPitch + r] : LZ;
+        for (int k = 0; k < n; ++k) {
+          const float v = readlane_f(xv, k);
+          if (!(acc - v >= 7.5f)) acc = mlp_log_add_t(acc, v, lk);
+        }
+      } else {
+        const int ir = 64 * S + r - row0;
+        acc = fold_chunks<false>(acc, (int64_t)(ir - 1) * nch, (int64_t)ir * nch, cmf, fl, L2, row0, W, cell_off,
+                                 nullptr, nullptr, nullptr, nullptr, 0.f, lk, lane);
+      }
+    }
+  }
+  return acc;
+}
+
 __global__ __launch_bounds__(256) void k_local_totals(ModelScalars ms, const Tables* __restrict__ tab, SeqSet sq,
                                                       PairMeta pm, ChainMeta cm, PairRec* __restrict__ rec,
                                                       Scratch sc, int64_t npairs) {
   __shared__ float4 lk[kLookupRows];
   __shared__ float match[26 * 26], ins[26];
+  __shared__ float lists[kWavesPerBlock][kRowList * kListPitch];
   if (threadIdx.x == 0) mlp_lookup_table(lk);
   for (int k = threadIdx.x; k < 26 * 26; k += blockDim.x) match[k] = tab->match[k];
   if (threadIdx.x < 26) ins[threadIdx.x] = tab->ins[threadIdx.x];
@@ -102,10 +176,18 @@ __global__ __launch_bounds__(256) void k_local_totals(ModelScalars ms, const Tab
   const uint8_t* s1 = sq.res + sq.off[pm.pa[p]];
   const uint8_t* s2 = sq.res + sq.off[pm.pb[p]];
   const int64_t rm = pm.rm_off[p];
-  const float tf = local_chain_fold<false>(sc.cmf + rm, sc.fl, L1, L2, row0, W, cell_off, s1, s2, match, ins,
-                                           2 * ms.rt1, lk, lane);
-  const float tb = local_chain_fold<true>(sc.cmb + rm, sc.bl, L1, L2, row0, W, cell_off, s1, s2, match, ins,
-                                          2 * ms.rt1, lk, lane);
+#ifdef MLP_EXP_TOT_NOFWD  // timing experiments (wrong results): one half of the fold only
+  const float tf = 0.f;
+#else
+  const float tf = local_fwd_fold(sc.cmf + rm, sc.fl, L1, L2, row0, W, cell_off, lk,
+                                  lists[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)], lane);
+#endif
+#ifdef MLP_EXP_TOT_NOBWD
+  const float tb = 0.f;
+#else
+  const float tb = fold_chunks<true>(LZ, 0, (int64_t)L1 * local_chunks(L2), sc.cmb + rm, sc.bl, L2, row0, W,
+                                     cell_off, s1, s2, match, ins, 2 * ms.rt1, lk, lane);
+#endif
   if (lane == 0) {
     rec[p].tfl = tf;
     rec[p].tbl = tb;
