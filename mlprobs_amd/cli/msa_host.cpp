@@ -471,64 +471,119 @@ __attribute__((target("avx2"))) std::string mea_simd8(int len1, int len2, const 
   return mea_trace(len1, len2, N, T, tbm.data());
 }
 
-__attribute__((target("avx512f,avx512bw,avx512vl"))) std::string mea_simd16(int len1, int len2, const float* post,
-                                                                             float* score) {
-  constexpr int N = 16;
-  const int W2 = len2 + 1;
-  const int ns = (len1 + N - 1) / N;
-  const int T = len2 + N;
-  std::vector<float> rowA(W2, 0.f), rowB(W2, 0.f);
-  float* above = rowA.data();
-  float* below = rowB.data();
-  std::vector<uint8_t> tbm((size_t)ns * T * (N / 4));
+// 16 lanes (AVX-512), strips pipelined over host threads: strip s goes to
+// thread s mod T and runs in chunks of steps, each chunk started once strip
+// s - 1 has finished the columns its lane 0 reads (a per-strip count of
+// finished columns, spun on).  Every cell sees its neighbours' final values:
+// the serial result bit for bit, for any T.
+struct Mea16 {
+  int len1, len2, W2, ns, TS;
+  const float* post;
+  float* rows;
+  uint8_t* tbm;
+  std::atomic<int>* done;
+};
+
+__attribute__((target("avx512f,avx512bw,avx512vl"))) void mea16_strips(const Mea16& m, int th, int nth) {
+  constexpr int N = 16, CHUNK = 256;
+  const int len1 = m.len1, len2 = m.len2, W2 = m.W2, TS = m.TS;
+  const float* post = m.post;
   const __m512i shl = _mm512_setr_epi32(0, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14);
   const __m512i lane = _mm512_setr_epi32(0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
   const __m512 zero = _mm512_setzero_ps();
   alignas(64) float vout[N];
-  for (int s = 0; s < ns; s++) {
+  for (int s = th; s < m.ns; s += nth) {
     const int i0 = 1 + s * N;
     const int nr = std::min(N, len1 - i0 + 1);
     alignas(64) int32_t ix[N];
     for (int r = 0; r < N; r++) ix[r] = (i0 + std::min(r, nr - 1)) * W2 - r;
     const __m512i idx = _mm512_load_si512((const void*)ix);
-    __m512 p1 = zero, p2 = zero;
-    uint8_t* tbs = tbm.data() + (size_t)s * T * (N / 4);
-    for (int t = 1; t < T; t++) {
-      const __m512 up = _mm512_mask_blend_ps(1, _mm512_permutexvar_ps(shl, p1), _mm512_set1_ps(above[std::min(t, len2)]));
-      const __m512 ul =
-          _mm512_mask_blend_ps(1, _mm512_permutexvar_ps(shl, p2), _mm512_set1_ps(above[std::min(t - 1, len2)]));
-      __m512 pr;
-      if (t >= N && t <= len2) {
-        pr = _mm512_i32gather_ps(idx, post + t, 4);
-      } else {
-        const __m512i j = _mm512_sub_epi32(_mm512_set1_epi32(t), lane);
-        const __mmask16 live = _mm512_cmpgt_epi32_mask(j, _mm512_setzero_si512()) &
-                               _mm512_cmpgt_epi32_mask(_mm512_set1_epi32(len2 + 1), j);
-        pr = _mm512_mask_i32gather_ps(zero, live, idx, post + t, 4);
-      }
-      const __m512 x1 = _mm512_add_ps(pr, ul), x2 = p1, x3 = up;
-      const __mmask16 m12 = _mm512_cmp_ps_mask(x1, x2, _CMP_GE_OQ), m13 = _mm512_cmp_ps_mask(x1, x3, _CMP_GE_OQ),
-                      m23 = _mm512_cmp_ps_mask(x2, x3, _CMP_GE_OQ);
-      const __mmask16 d = m12 & m13, l = (__mmask16)(~m12 & m23);
-      __m512 v = _mm512_mask_blend_ps(d, _mm512_mask_blend_ps(l, x3, x2), x1);
-      if (t < N) v = _mm512_maskz_mov_ps(_mm512_cmpgt_epi32_mask(_mm512_set1_epi32(t), lane), v);
-      tbs[(size_t)t * 4] = (uint8_t)d;
-      tbs[(size_t)t * 4 + 1] = (uint8_t)(d >> 8);
-      tbs[(size_t)t * 4 + 2] = (uint8_t)l;
-      tbs[(size_t)t * 4 + 3] = (uint8_t)(l >> 8);
-      const int jl = t - (nr - 1);
-      if (jl >= 1 && jl <= len2) {
-        _mm512_store_ps(vout, v);
-        below[jl] = vout[nr - 1];
-      }
-      p2 = p1;
-      p1 = v;
-    }
+    const float* above = m.rows + (size_t)s * W2;
+    float* below = m.rows + (size_t)(s + 1) * W2;
     below[0] = 0.f;
-    std::swap(above, below);
+    __m512 p1 = zero, p2 = zero;
+    uint8_t* tbs = m.tbm + (size_t)s * TS * (N / 4);
+    for (int c0 = 1; c0 < TS; c0 += CHUNK) {
+      const int c1 = std::min(TS, c0 + CHUNK);
+      // lane 0 reads the row above through column min(c1 - 1, len2)
+      const int need = std::min(c1 - 1, len2) + 1;
+      for (int spins = 0; m.done[s].load(std::memory_order_acquire) < need; spins++) {
+        if (spins < 4000) {
+          _mm_pause();
+        } else {
+          std::this_thread::yield();
+        }
+      }
+      for (int t = c0; t < c1; t++) {
+        const __m512 up =
+            _mm512_mask_blend_ps(1, _mm512_permutexvar_ps(shl, p1), _mm512_set1_ps(above[std::min(t, len2)]));
+        const __m512 ul =
+            _mm512_mask_blend_ps(1, _mm512_permutexvar_ps(shl, p2), _mm512_set1_ps(above[std::min(t - 1, len2)]));
+        __m512 pr;
+        if (t >= N && t <= len2) {
+          pr = _mm512_i32gather_ps(idx, post + t, 4);
+        } else {
+          const __m512i j = _mm512_sub_epi32(_mm512_set1_epi32(t), lane);
+          const __mmask16 live = _mm512_cmpgt_epi32_mask(j, _mm512_setzero_si512()) &
+                                 _mm512_cmpgt_epi32_mask(_mm512_set1_epi32(len2 + 1), j);
+          pr = _mm512_mask_i32gather_ps(zero, live, idx, post + t, 4);
+        }
+        const __m512 x1 = _mm512_add_ps(pr, ul), x2 = p1, x3 = up;
+        const __mmask16 m12 = _mm512_cmp_ps_mask(x1, x2, _CMP_GE_OQ), m13 = _mm512_cmp_ps_mask(x1, x3, _CMP_GE_OQ),
+                        m23 = _mm512_cmp_ps_mask(x2, x3, _CMP_GE_OQ);
+        const __mmask16 d = m12 & m13, l = (__mmask16)(~m12 & m23);
+        __m512 v = _mm512_mask_blend_ps(d, _mm512_mask_blend_ps(l, x3, x2), x1);
+        if (t < N) v = _mm512_maskz_mov_ps(_mm512_cmpgt_epi32_mask(_mm512_set1_epi32(t), lane), v);
+        tbs[(size_t)t * 4] = (uint8_t)d;
+        tbs[(size_t)t * 4 + 1] = (uint8_t)(d >> 8);
+        tbs[(size_t)t * 4 + 2] = (uint8_t)l;
+        tbs[(size_t)t * 4 + 3] = (uint8_t)(l >> 8);
+        const int jl = t - (nr - 1);
+        if (jl >= 1 && jl <= len2) {
+          _mm512_store_ps(vout, v);
+          below[jl] = vout[nr - 1];
+        }
+        p2 = p1;
+        p1 = v;
+      }
+      // the last row is final through column c1 - 1 - (nr - 1)
+      m.done[s + 1].store(std::min(len2, c1 - nr) + 1, std::memory_order_release);
+    }
+    m.done[s + 1].store(W2, std::memory_order_release);
   }
-  if (score) *score = len1 ? above[len2] : 0.f;
-  return mea_trace(len1, len2, N, T, tbm.data());
+}
+
+// 16 lanes (AVX-512), strips pipelined over host threads: strip s goes to
+// thread s mod T and runs in chunks of steps, each chunk started once strip
+// s - 1 has finished the columns its lane 0 reads (a per-strip count of
+// finished columns, spun on).  Every cell sees its neighbours' final values:
+// the serial result bit for bit, for any T.
+std::string mea_simd16(int len1, int len2, const float* post, float* score, int T) {
+  constexpr int N = 16;
+  Mea16 m;
+  m.len1 = len1;
+  m.len2 = len2;
+  m.W2 = len2 + 1;
+  m.ns = (len1 + N - 1) / N;
+  m.TS = len2 + N;  // steps of a strip: t = 1 .. len2 + N - 1
+  m.post = post;
+  // rows[(s + 1) W2 ..]: the last row of strip s; rows[0 ..]: row 0 (zeros)
+  std::vector<float> rows((size_t)(m.ns + 1) * m.W2, 0.f);
+  std::vector<uint8_t> tbm((size_t)m.ns * m.TS * (N / 4));
+  std::vector<std::atomic<int>> done(m.ns + 1);  // done[s + 1]: leading columns of strip s's last row finished
+  for (auto& d : done) d.store(0, std::memory_order_relaxed);
+  done[0].store(m.W2, std::memory_order_relaxed);
+  m.rows = rows.data();
+  m.tbm = tbm.data();
+  m.done = done.data();
+  T = std::max(1, std::min(T, m.ns));
+  if (T > 1) {
+    mlpr::parallel(T, [&](int th, int nth) { mea16_strips(m, th, nth); });
+  } else {
+    mea16_strips(m, 0, 1);
+  }
+  if (score) *score = len1 ? rows[(size_t)m.ns * m.W2 + len2] : 0.f;
+  return mea_trace(len1, len2, N, m.TS, tbm.data());
 }
 }  // namespace
 
@@ -544,7 +599,12 @@ int mea_simd_lanes() {
 
 std::string mea_path_simd(int len1, int len2, const float* post, float* score, int lanes) {
   if ((int64_t)(len1 + 1) * (len2 + 1) >= (1LL << 31)) return mea_path_serial(len1, len2, post, score);  // 32-bit gathers
-  if (lanes == 16 && __builtin_cpu_supports("avx512f")) return mea_simd16(len1, len2, post, score);
+  if (lanes == 16 && __builtin_cpu_supports("avx512f")) {
+    // threads for matrices that pay for the wake-up (MLP_MEA_THREAD_MIN cells)
+    static const int64_t tmin = getenv("MLP_MEA_THREAD_MIN") ? atoll(getenv("MLP_MEA_THREAD_MIN")) : 1000000;
+    const int T = (int64_t)len1 * len2 >= tmin ? std::min(16, mlpr::host_threads()) : 1;
+    return mea_simd16(len1, len2, post, score, T);
+  }
   if (lanes == 8 && __builtin_cpu_supports("avx2")) return mea_simd8(len1, len2, post, score);
   return mea_path_serial(len1, len2, post, score);
 }

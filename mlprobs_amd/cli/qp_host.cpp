@@ -514,8 +514,8 @@ Profile construct_and_refine(const std::vector<Seq>& seqs, const PosteriorBacken
   if (getenv("MLP_CLI_TIMES"))
     fprintf(stderr,
             "[host] profile posteriors %.3f s (%lld sequence pairs), MEA %.3f s, merges %.3f s, column scores "
-            "%.3f s, splits %.3f s, %d refinement passes\n",
-            g_t_post, (long long)g_n_terms, g_t_mea, g_t_merge, g_t_update, g_t_split, iters);
+            "%.3f s, splits %.3f s, %d refinement passes (MEA SIMD lanes %d)\n",
+            g_t_post, (long long)g_n_terms, g_t_mea, g_t_merge, g_t_update, g_t_split, iters, cpnp::mea_simd_lanes());
   return aln;
 }
 

@@ -96,6 +96,7 @@ __device__ __forceinline__ float fold_chunks(float acc, int64_t kb, int64_t ke, 
   return acc;
 }
 
+template <bool FOLD = true>
 __device__ __forceinline__ float local_fwd_fold(const float* __restrict__ cmf, const float* __restrict__ fl, int L1,
                                                 int L2, int row0, int W, int64_t cell_off, const float4* lk,
                                                 float* lst, int lane) {
@@ -135,6 +136,10 @@ __device__ __forceinline__ float local_fwd_fold(const float* __restrict__ cmf, c
           run = fmaxf(run, x[u]);
         }
       }
+    }
+    if constexpr (!FOLD) {  // timing experiment: streaming only
+      acc = fmaxf(acc, (float)__builtin_amdgcn_readlane(cnt, 5));
+      continue;
     }
     // the strip's rows in order
     for (int r = 0; r < 64; ++r) {
@@ -176,17 +181,24 @@ __global__ __launch_bounds__(256) void k_local_totals(ModelScalars ms, const Tab
   const uint8_t* s1 = sq.res + sq.off[pm.pa[p]];
   const uint8_t* s2 = sq.res + sq.off[pm.pb[p]];
   const int64_t rm = pm.rm_off[p];
-#ifdef MLP_EXP_TOT_NOFWD  // timing experiments (wrong results): one half of the fold only
-  const float tf = 0.f;
-#else
-  const float tf = local_fwd_fold(sc.cmf + rm, sc.fl, L1, L2, row0, W, cell_off, lk,
-                                  lists[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)], lane);
+  float tf = local_fwd_fold(sc.cmf + rm, sc.fl, L1, L2, row0, W, cell_off, lk,
+                            lists[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)], lane);
+  float tb = fold_chunks<true>(LZ, 0, (int64_t)L1 * local_chunks(L2), sc.cmb + rm, sc.bl, L2, row0, W, cell_off, s1,
+                               s2, match, ins, 2 * ms.rt1, lk, lane);
+#ifdef MLP_EXP_TOT_FWD2  // timing experiments: one half of the fold twice (same results)
+  if (local_fwd_fold(sc.cmf + rm, sc.fl, L1, L2, row0, W, cell_off, lk,
+                     lists[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)], lane) == 12345.f)
+    tf = 0.f;
 #endif
-#ifdef MLP_EXP_TOT_NOBWD
-  const float tb = 0.f;
-#else
-  const float tb = fold_chunks<true>(LZ, 0, (int64_t)L1 * local_chunks(L2), sc.cmb + rm, sc.bl, L2, row0, W,
-                                     cell_off, s1, s2, match, ins, 2 * ms.rt1, lk, lane);
+#ifdef MLP_EXP_TOT_STRM2  // the forward streaming pass twice (no second fold)
+  if (local_fwd_fold<false>(sc.cmf + rm, sc.fl, L1, L2, row0, W, cell_off, lk,
+                            lists[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)], lane) == 12345.f)
+    tf = 0.f;
+#endif
+#ifdef MLP_EXP_TOT_BWD2
+  if (fold_chunks<true>(LZ, 0, (int64_t)L1 * local_chunks(L2), sc.cmb + rm, sc.bl, L2, row0, W, cell_off, s1, s2,
+                        match, ins, 2 * ms.rt1, lk, lane) == 12345.f)
+    tb = 0.f;
 #endif
   if (lane == 0) {
     rec[p].tfl = tf;

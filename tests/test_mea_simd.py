@@ -33,10 +33,12 @@ def checker(tmp_path_factory):
     return out
 
 
-@pytest.mark.parametrize('lanes,flag', [(8, 'avx2'), (16, 'avx512bw')])
-def test_mea_simd_matches_serial(checker, lanes, flag):
+@pytest.mark.parametrize('lanes,flag,threads', [(8, 'avx2', 1), (16, 'avx512bw', 1), (16, 'avx512bw', 4)])
+def test_mea_simd_matches_serial(checker, lanes, flag, threads):
+    """threads > 1: the 16-lane strips pipelined over host threads."""
     if not _cpu_has(flag):
         pytest.skip(f'no {flag} on this CPU')
-    r = subprocess.run([checker, str(lanes)], capture_output=True, text=True, timeout=300)
+    env = dict(os.environ, MLP_HOST_THREADS=str(threads), MLP_MEA_THREAD_MIN='1' if threads > 1 else '0')
+    r = subprocess.run([checker, str(lanes)], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.startswith('ok 3000')

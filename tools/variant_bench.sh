@@ -7,7 +7,7 @@ O=gpurun_out/variants
 mkdir -p $O
 for v in "$@"; do
   if [ "$v" = base ]; then unset MLP_LIB_VARIANT; else export MLP_LIB_VARIANT=$v; fi
-  timeout -k 10 300 python3 bench.py --no-cpu --no-e2e --no-qp --relax ${RELAX:-0} --steps 2 --warmup 1 > $O/$v.json 2> $O/$v.err || { tail -5 $O/$v.err; exit 1; }
+  timeout -k 10 300 python3 bench.py --no-cpu --no-e2e --no-qp --relax ${RELAX:-0} --no-shards --steps 2 --warmup 1 > $O/$v.json 2> $O/$v.err || { tail -5 $O/$v.err; exit 1; }
   python3 -c "
 import json,sys; d=json.load(open('$O/$v.json'))
 k=d['kernels_ms_per_step']; r=d.get('relax')
