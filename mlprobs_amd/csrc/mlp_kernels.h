@@ -118,6 +118,11 @@ struct Scratch {
   // chunk, forward (f_M) and backward (b_M + emission), written by the sweeps
   float* cmf;
   float* cmb;
+  // k_local_totals' per-wave candidate lists (64 rows x clist_row floats per
+  // resident wave) and its pair counter (work queue)
+  float* clist;
+  int32_t clist_row;
+  int32_t* tot_next;
   float* bnd5;             // chain boundary row: 5 floats per column
   float* bndl;             // 3 floats per column
   double* bndz;            // 3 doubles per column
@@ -171,9 +176,14 @@ hipError_t launch_backward(int models, const ModelScalars& ms, const Tables* tab
                            PairMeta pm, ChainMeta cm, PairRec* rec, Scratch sc, int64_t nchains,
                            int lds_seq, int64_t npairs, hipStream_t st, const SideStream* side);
 hipError_t launch_local_totals(const ModelScalars& ms, const Tables* tab, SeqSet seqs, PairMeta pm, ChainMeta cm,
-                               PairRec* rec, Scratch sc, int64_t npairs, hipStream_t st);
+                               PairRec* rec, Scratch sc, int64_t npairs, int nwaves, hipStream_t st);
+// resident waves of k_local_totals (persistent: each takes pairs off a counter)
+constexpr int kTotalsWaves = 8192;
 // chunk maxima per pair row (columns 1..L2 in chunks of 64)
 __host__ __device__ constexpr int local_chunks(int L2) { return (L2 + 63) >> 6; }
+#ifdef MLP_EXP_TOT_STATS
+void tot_stats_print();
+#endif
 hipError_t launch_fold_totals(const ModelScalars& ms, const Tables* tab, SeqSet seqs, PairMeta pm,
                               PairRec* rec, int64_t npairs, hipStream_t st);
 hipError_t launch_merge(int models, int pid, const ModelScalars& ms, SeqSet seqs, PairMeta pm,

@@ -138,6 +138,19 @@ struct mlp_ctx {
 };
 
 // ------------------------------------------------------------------ helpers
+#ifdef MLP_EXP_SYNC  // debug variant: drain the device after each posterior-stage launch
+#define EXP_SYNC(name)                                                                        \
+  do {                                                                                        \
+    hipError_t e_ = hipDeviceSynchronize();                                                   \
+    if (e_ != hipSuccess) {                                                                   \
+      c->err = std::string("after ") + (name) + ": " + hipGetErrorString(e_);                 \
+      return MLP_ERR_HIP;                                                                     \
+    }                                                                                         \
+    fprintf(stderr, "[sync] %s ok\n", name);                                                 \
+  } while (0)
+#else
+#define EXP_SYNC(name)
+#endif
 #define HIPCHK(ctx, expr)                                                          \
   do {                                                                             \
     hipError_t e_ = (expr);                                                        \
@@ -1145,7 +1158,7 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
     hipStream_t st = streams[B.slot];
     HIPCHK(c, hipStreamSynchronize(st));
     const int64_t np = B.np;
-#if defined(MLP_EXP_NOCHAIN) || defined(MLP_EXP_CONSTLK) || defined(MLP_EXP_TOT_NOFWD) || defined(MLP_EXP_TOT_NOBWD)
+#if defined(MLP_EXP_NOCHAIN) || defined(MLP_EXP_CONSTLK)
     for (int64_t s = 0; s < np; s++) B.rec[s].flags = 0;  // timing experiments: results are not meaningful
 #endif
     for (int64_t s = 0; s < np; s++) {
@@ -1190,6 +1203,9 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
     }
     c->store_total = run; ++c->store_ver;
     c->store_p1 = B.q;
+#ifdef MLP_EXP_TOT_STATS
+    mlp::tot_stats_print();
+#endif
     return MLP_OK;
   };
   int64_t p = p0;
@@ -1205,12 +1221,21 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
     hipStream_t st = streams[slot];
     const int64_t np = P.np, nch = P.nch;
     // ---- carve scratch
+    // k_local_totals: persistent waves, each with 64 candidate rows of the
+    // batch's widest row (at most ~1 GB of lists)
+    int tot_row = 16;
+    for (int64_t h = 0; h < P.nch; h++) tot_row = std::max(tot_row, P.width[h]);
+    tot_row = (tot_row + 15) & ~15;
+    int tot_waves = (int)std::max<int64_t>(
+        64, std::min<int64_t>({(int64_t)kTotalsWaves, P.np, (int64_t)(1LL << 30) / (64LL * tot_row * 4)}));
+    tot_waves = (tot_waves + kWavesPerBlock - 1) / kWavesPerBlock * kWavesPerBlock;  // whole workgroups
     Carver cv;
     const bool h5 = models & kHmm5, lo = models & kLocal, pf = models & kPF;
     const size_t o_f5 = cv.take(h5 ? P.cells * 4 : 0), o_fl = cv.take(lo ? P.cells * 4 : 0),
                  o_bl = cv.take(lo ? P.cells * 4 : 0), o_pg = cv.take(pf ? P.cells * 4 : 0),
                  o_zm = cv.take(pf ? P.cells * 8 : 0), o_cmf = cv.take(lo ? P.rm_total * 4 : 0),
                  o_cmb = cv.take(lo ? P.rm_total * 4 : 0),
+                 o_tn = cv.take(lo ? 256 : 0), o_cl = cv.take(lo ? (size_t)tot_waves * 64 * tot_row * 4 : 0),
                  o_b5 = cv.take(P.bnd * 20), o_bnl = cv.take(P.bnd * 12), o_bz = cv.take(P.bnd * 24),
                  o_be = cv.take(P.bnd * 4), o_bm = cv.take(P.bnd * 4), o_bc = cv.take(P.bnd * 4), o_ec = cv.take(P.ell_rows * kEll * 2),
                  o_ev = cv.take(P.ell_rows * kEll * 4), o_en = cv.take(P.ell_rows * 4),
@@ -1231,6 +1256,9 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
     sc.bl = (float*)(base + o_bl);
     sc.cmf = (float*)(base + o_cmf);
     sc.cmb = (float*)(base + o_cmb);
+    sc.clist = (float*)(base + o_cl);
+    sc.clist_row = tot_row;
+    sc.tot_next = (int32_t*)(base + o_tn);
     sc.bnd5 = (float*)(base + o_b5);
     sc.bndl = (float*)(base + o_bnl);
     sc.bndz = (double*)(base + o_bz);
@@ -1251,18 +1279,22 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
     {
       Timer t(c, KFWD, bcells, st);
       HIPCHK(c, launch_forward(models, ms, c->d_tables, seqs, pm, cm, d_rec, sc, nch, lds_seq, st, side));
+      EXP_SYNC("forward");
     }
     {
       Timer t(c, KBWD, bcells, st);
       HIPCHK(c, launch_backward(models, ms, c->d_tables, seqs, pm, cm, d_rec, sc, nch, lds_seq, np, st, side));
+      EXP_SYNC("backward");
     }
     if (models & kLocal) {
       Timer t(c, KTOT, bcells, st);
-      HIPCHK(c, launch_local_totals(ms, c->d_tables, seqs, pm, cm, d_rec, sc, np, st));
+      HIPCHK(c, launch_local_totals(ms, c->d_tables, seqs, pm, cm, d_rec, sc, np, tot_waves, st));
+      EXP_SYNC("totals");
     }
     {
       Timer t(c, KMERGE, bcells, st);
       HIPCHK(c, launch_merge(models, pid, ms, seqs, pm, cm, d_rec, sc, nch, lds_seq, st));
+      EXP_SYNC("merge");
     }
     B.live = true;
     B.slot = slot;

@@ -2,6 +2,8 @@
 // sweeps: the exact local-model chain totals, the 5-state backward total fold
 // and the ELL -> canonical CSR compaction (one wave per pair / 8 pairs per
 // wave; no wavefront).
+#include <stdio.h>
+
 #include "mlp_kernels.h"
 #include "mlp_numerics.h"
 
@@ -34,20 +36,21 @@ static inline dim3 wave_grid(int64_t n) {
 // bound - x >= 7.5, bound = the largest element before it, is skipped exactly
 // (fl(acc - x) >= fl(bound - x) for acc >= bound).
 //
-// Forward (about one row in 1.5 holds a candidate chunk, ~10 candidates a
-// row at C3): the wave streams the pair's f_M strip by strip in its
-// step-diagonal layout (one coalesced 256-B slab per step, lane r holding row
-// 64 S + r in column order), the bound being the larger of the rows before
-// (prefix maximum of the sweeps' per-chunk maxima, Scratch::cmf) and the row
-// so far; each lane lists its row's candidates in LDS and the strip's rows
-// are then folded in order.  A row with more than kRowList candidates (the
-// first rows of a pair) is folded chunk by chunk from HBM instead.
+// Forward: the bound is the largest element of the rows before (prefix
+// maximum of the sweeps' per-chunk maxima, Scratch::cmf) and of the row so
+// far.  At C3 (pid 0, the family's delta) the forward chain's values rise
+// along the rows: ~18k of the 160k terms of a pair change acc, ~55k pass the
+// bound (local_fwd_fold).
 // Backward (0.1% of the chunks hold a candidate): chunks whose maximum
 // (Scratch::cmb) passes the test against acc are gathered and folded.
-// One wave per pair; acc is wave-uniform.
 // =====================================================================
-constexpr int kRowList = 16;
-constexpr int kListPitch = 65;  // LDS row pitch of a wave's candidate lists (bank-conflict free)
+#ifdef MLP_EXP_TOT_STATS  // measurement variant: fold work counters, printed per batch on stderr
+__device__ unsigned long long g_totstats[8];
+#define TOT_STAT(k, v) \
+  if (lane == 0) atomicAdd(&g_totstats[k], (unsigned long long)(v))
+#else
+#define TOT_STAT(k, v)
+#endif
 
 // Fold chunks [kb, ke) of a chain (row-major chunk index (i - 1) * nch + c)
 // whose maximum passes the test against acc, elements gathered from the
@@ -64,6 +67,7 @@ __device__ __forceinline__ float fold_chunks(float acc, int64_t kb, int64_t ke, 
     const float mx = kk < ke ? cmx[kk] : LZ;
     uint64_t live = __ballot(kk < ke && !(acc - mx >= 7.5f));
     while (live) {
+      TOT_STAT(BWD ? 4 : 3, 1);
       const int64_t ck = k0 + __builtin_ctzll(live);
       const int i = (int)(ck / nch) + 1, cidx = (int)(ck % nch);
       const int j = 64 * cidx + 1 + lane;  // this lane's column of the chunk
@@ -96,20 +100,31 @@ __device__ __forceinline__ float fold_chunks(float acc, int64_t kb, int64_t ke, 
   return acc;
 }
 
+// Forward chain: stream the pair's f_M strip by strip in its step-diagonal
+// layout (one coalesced 256-B slab per step; lane r holds row 64 S + r in
+// column order), list every element that passes the bound test in the
+// lane's row list (this wave's region of Scratch::clist, one row of
+// clist_row floats per lane: every element fits), then fold the strip's
+// rows in order: per 64 listed elements, a ballot of those that pass the
+// test against acc, the lowest folded, the ballot renewed (the rest of the
+// list stays in order; an element that stopped passing is skipped, exactly).
 template <bool FOLD = true>
 __device__ __forceinline__ float local_fwd_fold(const float* __restrict__ cmf, const float* __restrict__ fl, int L1,
                                                 int L2, int row0, int W, int64_t cell_off, const float4* lk,
-                                                float* lst, int lane) {
+                                                float* __restrict__ region, int row_cap, int lane) {
   const int nch = local_chunks(L2);
   float acc = LZ, carry = LZ;  // carry: the largest element of the pair's rows before strip S
   const int S0 = (row0 + 1) >> 6, S1 = (row0 + L1) >> 6;
   const int tend = L2 + 63;  // steps of a strip: lane r holds column t - r at step t
+  float* mine = region + (int64_t)lane * row_cap;
   for (int S = S0; S <= S1; ++S) {
     const int i = 64 * S + lane - row0;  // this lane's pair row
     const bool row_in = i >= 1 && i <= L1;
     float rmx = LZ;
     if (row_in)
-      for (int c = 0; c < nch; ++c) rmx = fmaxf(rmx, cmf[(int64_t)(i - 1) * nch + c]);
+      for (int c = 0; c < nch; ++c) {
+        rmx = fmaxf(rmx, cmf[(int64_t)(i - 1) * nch + c]);
+      }
     float incl = rmx;  // inclusive prefix maximum over the strip's rows
     for (int off = 1; off < 64; off <<= 1) {
       const float y = __shfl_up(incl, off);
@@ -124,85 +139,91 @@ __device__ __forceinline__ float local_fwd_fold(const float* __restrict__ cmf, c
     for (int t0 = 1; t0 <= tend; t0 += 8) {
       float x[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) x[u] = (t0 + u <= tend) ? slab[(int64_t)(t0 + u) * 64] : LZ;
+      for (int u = 0; u < 8; ++u) {
+        x[u] = (t0 + u <= tend) ? slab[(int64_t)(t0 + u) * 64] : LZ;
+      }
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         const int j = t0 + u - lane;
         if (row_in && j >= 1 && j <= L2) {
           if (!(run - x[u] >= 7.5f)) {
-            if (cnt < kRowList) lst[cnt * kListPitch + lane] = x[u];
-            ++cnt;
+            mine[cnt++] = x[u];
           }
           run = fmaxf(run, x[u]);
         }
       }
     }
+    TOT_STAT(1, cnt);
     if constexpr (!FOLD) {  // timing experiment: streaming only
       acc = fmaxf(acc, (float)__builtin_amdgcn_readlane(cnt, 5));
       continue;
     }
+    // the lists were written by this wave: same-CU visibility
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     // the strip's rows in order
     for (int r = 0; r < 64; ++r) {
       const int n = __builtin_amdgcn_readlane(cnt, r);
-      if (n == 0) continue;
-      if (n <= kRowList) {
-        const float xv = lane < n ? lst[lane * kListPitch + r] : LZ;
-        for (int k = 0; k < n; ++k) {
-          const float v = readlane_f(xv, k);
-          if (!(acc - v >= 7.5f)) acc = mlp_log_add_t(acc, v, lk);
+      const float* lst = region + (int64_t)r * row_cap;
+      for (int k0 = 0; k0 < n; k0 += 64) {
+        const bool in = k0 + lane < n;
+        const float x = in ? lst[k0 + lane] : LZ;
+        uint64_t live = __ballot(in && !(acc - x >= 7.5f));
+        while (live) {
+          const float v = readlane_f(x, __builtin_ctzll(live));
+          acc = mlp_log_add_t(acc, v, lk);
+          TOT_STAT(5, 1);
+          live &= live - 1;
+          live &= __ballot(!(acc - x >= 7.5f));
         }
-      } else {
-        const int ir = 64 * S + r - row0;
-        acc = fold_chunks<false>(acc, (int64_t)(ir - 1) * nch, (int64_t)ir * nch, cmf, fl, L2, row0, W, cell_off,
-                                 nullptr, nullptr, nullptr, nullptr, 0.f, lk, lane);
       }
     }
+    // the next strip's stores must not overtake this strip's list reads
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   }
   return acc;
 }
 
+// Persistent: gridDim.x * 4 waves, each taking pairs off Scratch::tot_next
+// until none is left (every wave reaches the exit).
 __global__ __launch_bounds__(256) void k_local_totals(ModelScalars ms, const Tables* __restrict__ tab, SeqSet sq,
                                                       PairMeta pm, ChainMeta cm, PairRec* __restrict__ rec,
                                                       Scratch sc, int64_t npairs) {
   __shared__ float4 lk[kLookupRows];
   __shared__ float match[26 * 26], ins[26];
-  __shared__ float lists[kWavesPerBlock][kRowList * kListPitch];
   if (threadIdx.x == 0) mlp_lookup_table(lk);
   for (int k = threadIdx.x; k < 26 * 26; k += blockDim.x) match[k] = tab->match[k];
   if (threadIdx.x < 26) ins[threadIdx.x] = tab->ins[threadIdx.x];
   __syncthreads();
-  const int64_t p = wave_index();
-  if (p >= npairs) return;
   const int lane = threadIdx.x & 63;
-  const int L1 = sq.len[pm.pa[p]], L2 = sq.len[pm.pb[p]];
-  const int h = pm.chain[p];
-  const int W = cm.width[h], row0 = pm.row0[p];
-  const int64_t cell_off = cm.cell_off[h];
-  const uint8_t* s1 = sq.res + sq.off[pm.pa[p]];
-  const uint8_t* s2 = sq.res + sq.off[pm.pb[p]];
-  const int64_t rm = pm.rm_off[p];
-  float tf = local_fwd_fold(sc.cmf + rm, sc.fl, L1, L2, row0, W, cell_off, lk,
-                            lists[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)], lane);
-  float tb = fold_chunks<true>(LZ, 0, (int64_t)L1 * local_chunks(L2), sc.cmb + rm, sc.bl, L2, row0, W, cell_off, s1,
-                               s2, match, ins, 2 * ms.rt1, lk, lane);
-#ifdef MLP_EXP_TOT_FWD2  // timing experiments: one half of the fold twice (same results)
-  if (local_fwd_fold(sc.cmf + rm, sc.fl, L1, L2, row0, W, cell_off, lk,
-                     lists[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)], lane) == 12345.f)
-    tf = 0.f;
-#endif
+  float* region = sc.clist + wave_index() * 64 * (int64_t)sc.clist_row;
+
+  // one counter increment per wave, every lane taking part (no divergent
+  // branch around the atomic): lane 0 receives the pair number
+  auto take = [&]() -> int64_t {
+    const int got = atomicAdd(sc.tot_next, lane == 0 ? 1 : 0);
+    return __builtin_amdgcn_readfirstlane(got);
+  };
+  for (int64_t p = take(); p < npairs; p = take()) {
+    const int L1 = sq.len[pm.pa[p]], L2 = sq.len[pm.pb[p]];
+    const int h = pm.chain[p];
+    const int W = cm.width[h], row0 = pm.row0[p];
+    const int64_t cell_off = cm.cell_off[h];
+    const uint8_t* s1 = sq.res + sq.off[pm.pa[p]];
+    const uint8_t* s2 = sq.res + sq.off[pm.pb[p]];
+    const int64_t rm = pm.rm_off[p];
+    float tf = local_fwd_fold(sc.cmf + rm, sc.fl, L1, L2, row0, W, cell_off, lk, region, sc.clist_row, lane);
+    float tb = fold_chunks<true>(LZ, 0, (int64_t)L1 * local_chunks(L2), sc.cmb + rm, sc.bl, L2, row0, W, cell_off, s1,
+                                 s2, match, ins, 2 * ms.rt1, lk, lane);
 #ifdef MLP_EXP_TOT_STRM2  // the forward streaming pass twice (no second fold)
-  if (local_fwd_fold<false>(sc.cmf + rm, sc.fl, L1, L2, row0, W, cell_off, lk,
-                            lists[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)], lane) == 12345.f)
-    tf = 0.f;
+    if (local_fwd_fold<false>(sc.cmf + rm, sc.fl, L1, L2, row0, W, cell_off, lk, region, sc.clist_row, lane) ==
+        12345.f)
+      tf = 0.f;
 #endif
-#ifdef MLP_EXP_TOT_BWD2
-  if (fold_chunks<true>(LZ, 0, (int64_t)L1 * local_chunks(L2), sc.cmb + rm, sc.bl, L2, row0, W, cell_off, s1, s2,
-                        match, ins, 2 * ms.rt1, lk, lane) == 12345.f)
-    tb = 0.f;
-#endif
-  if (lane == 0) {
-    rec[p].tfl = tf;
-    rec[p].tbl = tb;
+    if (lane == 0) {
+      rec[p].tfl = tf;
+      rec[p].tbl = tb;
+    }
   }
 }
 
@@ -269,11 +290,24 @@ __global__ void k_fold_totals(ModelScalars ms, SeqSet sq, PairMeta pm, PairRec* 
   r.b5[0] = tb;  // merge kernel reads the folded backward total here
 }
 
+#ifdef MLP_EXP_TOT_STATS
+void tot_stats_print() {
+  unsigned long long h[8];
+  hipMemcpyFromSymbol(h, HIP_SYMBOL(g_totstats), sizeof(h));
+  fprintf(stderr,
+          "[totals] rows %llu listed %llu overflow rows %llu fwd live chunks %llu bwd live chunks %llu folded %llu "
+          "row max below %llu above %llu\n",
+          h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7]);
+}
+#endif
 // ------------------------------------------------------------ launchers
 hipError_t launch_local_totals(const ModelScalars& ms, const Tables* tab, SeqSet seqs, PairMeta pm, ChainMeta cm,
-                               PairRec* rec, Scratch sc, int64_t npairs, hipStream_t st) {
+                               PairRec* rec, Scratch sc, int64_t npairs, int nwaves, hipStream_t st) {
   if (npairs <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_local_totals, wave_grid(npairs), dim3(64 * kWavesPerBlock), 0, st, ms, tab, seqs, pm, cm, rec,
+  hipError_t e = hipMemsetAsync(sc.tot_next, 0, sizeof(int32_t), st);
+  if (e != hipSuccess) return e;
+  if (nwaves % kWavesPerBlock) return hipErrorInvalidValue;  // every wave owns a list region
+  hipLaunchKernelGGL(k_local_totals, wave_grid(nwaves), dim3(64 * kWavesPerBlock), 0, st, ms, tab, seqs, pm, cm, rec,
                      sc, npairs);
   return hipGetLastError();
 }
