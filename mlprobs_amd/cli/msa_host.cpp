@@ -600,8 +600,10 @@ int mea_simd_lanes() {
 std::string mea_path_simd(int len1, int len2, const float* post, float* score, int lanes) {
   if ((int64_t)(len1 + 1) * (len2 + 1) >= (1LL << 31)) return mea_path_serial(len1, len2, post, score);  // 32-bit gathers
   if (lanes == 16 && __builtin_cpu_supports("avx512f")) {
-    // threads for matrices that pay for the wake-up (MLP_MEA_THREAD_MIN cells)
-    static const int64_t tmin = getenv("MLP_MEA_THREAD_MIN") ? atoll(getenv("MLP_MEA_THREAD_MIN")) : 1000000;
+    // strips over threads only on request (MLP_MEA_THREAD_MIN cells): on the
+    // GPU box (16-core quota) QuickProbs C3's ~4e6-cell refinement MEAs ran
+    // 0.95-1.4 s single-threaded against 1.0-1.8 s threaded (tools/qp_mea_ab.sh)
+    static const int64_t tmin = getenv("MLP_MEA_THREAD_MIN") ? atoll(getenv("MLP_MEA_THREAD_MIN")) : INT64_MAX;
     const int T = (int64_t)len1 * len2 >= tmin ? std::min(16, mlpr::host_threads()) : 1;
     return mea_simd16(len1, len2, post, score, T);
   }

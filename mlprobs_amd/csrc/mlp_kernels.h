@@ -378,14 +378,23 @@ struct ProfileArgs {
 size_t profile_lds(int L2);
 // MEA of the dense profile posterior (profile.hip): choices 2 bits per cell
 // (0 D, 1 L, 2 U), row stride (L2 + 4) / 4 bytes; rows 1..L1, columns 1..L2
+// Device MEA (k_profile_mea): one workgroup per 64-row strip, strips
+// pipelined across CUs through HBM.  Workspace layout (mea_layout): the
+// choices (2 bits a cell, per strip, 16-step block and lane a uint32), each
+// strip's last row, per strip its count of finished columns, the score and
+// an error word (a strip that waited too long for the one above).
+constexpr int kMeaBlk = 16;  // steps per block (one uint32 of choices per lane)
+struct MeaLayout {
+  int nstrips, nblk, rowpitch;
+  size_t o_tb, o_row, o_prog, o_score, o_err, bytes;
+};
+MeaLayout mea_layout(int L1, int L2);
 struct MeaArgs {
   const float* post;         // (L1 + 1) x (L2 + 1)
   int L1, L2;
-  uint8_t* tb;
-  float* score;              // [0]: the MEA score
+  uint8_t* work;             // mea_layout(L1, L2).bytes
 };
 hipError_t launch_profile_mea(const MeaArgs& a, hipStream_t st);
-size_t profile_mea_lds(int L2);  // LDS of k_profile_mea (at most 160 KB: L2 up to ~4600)
 hipError_t launch_profile_gather(const float* post, const int64_t* cells, int64_t n, float* out, hipStream_t st);
 hipError_t launch_profile_posterior(const ProfileArgs& a, hipStream_t st);
 hipError_t launch_transpose(const TransposeArgs& a, hipStream_t st);

@@ -1565,76 +1565,51 @@ int mlp_profile_mea(mlp_ctx* c, char* path, int32_t* path_len, float* score) {
   if (!c || !path || !path_len) return MLP_ERR_ARG;
   if (c->host || !c->prof_dout) return MLP_ERR_STATE;
   const auto tp = std::chrono::steady_clock::now();
-  const int L1 = c->prof_L1, L2 = c->prof_L2, Wq = (L2 + 4) / 4;
-  const size_t tb_bytes = (size_t)(L1 + 1) * Wq, all = ((tb_bytes + 15) & ~(size_t)15) + 16;
+  const int L1 = c->prof_L1, L2 = c->prof_L2;
+  const MeaLayout m = mea_layout(L1, L2);
   int rc;
   hipSetDevice(c->device);
-  if ((rc = ensure(c, c->r_mea, all))) return rc;
-  if (c->h_mea_bytes < all) {
+  if ((rc = ensure(c, c->r_mea, m.bytes))) return rc;
+  const size_t back = m.o_row;  // the choices; the score and error words follow separately
+  if (c->h_mea_bytes < back + 16) {
     if (c->h_mea) hipHostFree(c->h_mea);
     c->h_mea = nullptr;
     c->h_mea_bytes = 0;
-    if (hipHostMalloc((void**)&c->h_mea, all * 2, hipHostMallocDefault) != hipSuccess) return MLP_ERR_MEMORY;
-    c->h_mea_bytes = all * 2;
+    if (hipHostMalloc((void**)&c->h_mea, (back + 16) * 2, hipHostMallocDefault) != hipSuccess) return MLP_ERR_MEMORY;
+    c->h_mea_bytes = (back + 16) * 2;
   }
-  if (profile_mea_lds(L2) > 160 * 1024 || (L1 + 63) / 64 > 256) {
-    // too wide for the kernel's LDS strip: the matrix comes back and the
-    // same recurrence runs here (ProbabilisticModel.h:804-864)
-    const size_t b_out = (size_t)(L1 + 1) * (L2 + 1) * 4;
-    std::vector<float> post((size_t)(L1 + 1) * (L2 + 1));
-    HIPCHK(c, hipMemcpyAsync(post.data(), c->prof_dout, b_out, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    const int W2 = L2 + 1;
-    std::vector<float> rows(2 * (size_t)W2, 0.f);
-    std::vector<uint8_t> ch((size_t)(L1 + 1) * W2, 1);
-    float* oldr = rows.data();
-    float* newr = rows.data() + W2;
-    for (int i = 1; i <= L1; i++) {
-      newr[0] = 0;
-      ch[(size_t)i * W2] = 2;
-      for (int j = 1; j <= L2; j++) {
-        const float x1 = post[(size_t)i * W2 + j] + oldr[j - 1], x2 = newr[j - 1], x3 = oldr[j];
-        float v;
-        uint8_t b;
-        if (x1 >= x2) {
-          if (x1 >= x3) { v = x1; b = 0; } else { v = x3; b = 2; }
-        } else if (x2 >= x3) {
-          v = x2; b = 1;
-        } else {
-          v = x3; b = 2;
-        }
-        newr[j] = v;
-        ch[(size_t)i * W2 + j] = b;
-      }
-      std::swap(oldr, newr);
-    }
-    if (score) *score = oldr[L2];
-    int r = L1, col = L2, k = 0;
-    while (r != 0 || col != 0) {
-      const int b = r == 0 ? 1 : col == 0 ? 2 : ch[(size_t)r * W2 + col];
-      if (b == 1) { col--; path[k++] = 'Y'; }
-      else if (b == 2) { r--; path[k++] = 'X'; }
-      else { r--; col--; path[k++] = 'B'; }
-    }
-    std::reverse(path, path + k);
-    *path_len = k;
-    return MLP_OK;
-  }
-  MeaArgs m;
-  m.post = c->prof_dout;
-  m.L1 = L1;
-  m.L2 = L2;
-  m.tb = (uint8_t*)c->r_mea.p;
-  m.score = (float*)((uint8_t*)c->r_mea.p + all - 16);
-  HIPCHK(c, launch_profile_mea(m, c->stream));
-  HIPCHK(c, hipMemcpyAsync(c->h_mea, c->r_mea.p, all, hipMemcpyDeviceToHost, c->stream));
+  MeaArgs a;
+  a.post = c->prof_dout;
+  a.L1 = L1;
+  a.L2 = L2;
+  a.work = (uint8_t*)c->r_mea.p;
+  HIPCHK(c, launch_profile_mea(a, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->h_mea, c->r_mea.p, back, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->h_mea + back, (uint8_t*)c->r_mea.p + m.o_score, 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->h_mea + back + 4, (uint8_t*)c->r_mea.p + m.o_err, 4, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  const uint8_t* tb = c->h_mea;
-  if (score) memcpy(score, c->h_mea + all - 16, 4);
-  // traceback (ProbabilisticModel.h:846-858): row 0 moves left, column 0 up
+  int err = 0;
+  memcpy(&err, c->h_mea + back + 4, 4);
+  if (err) {
+    c->err = "device MEA: a strip timed out waiting for the one above";
+    return MLP_ERR_HIP;
+  }
+  if (score) memcpy(score, c->h_mea + back, 4);
+  // traceback (ProbabilisticModel.h:846-858): row 0 moves left, column 0 up;
+  // cell (i, j): strip (i - 1) / 64, lane (i - 1) % 64, step j + lane
+  const uint32_t* tbw = (const uint32_t*)c->h_mea;
   int r = L1, col = L2, k = 0;
   while (r != 0 || col != 0) {
-    const int b = r == 0 ? 1 : col == 0 ? 2 : (tb[(size_t)r * Wq + (col >> 2)] >> (2 * (col & 3))) & 3;
+    int b;
+    if (r == 0) {
+      b = 1;
+    } else if (col == 0) {
+      b = 2;
+    } else {
+      const int sr = (r - 1) >> 6, ln = (r - 1) & 63, t = col + ln;
+      const int blk = (t - 1) / kMeaBlk, u = (t - 1) % kMeaBlk;
+      b = (tbw[((size_t)sr * m.nblk + blk) * 64 + ln] >> (2 * u)) & 3;
+    }
     if (b == 1) {
       col--;
       path[k++] = 'Y';

@@ -178,109 +178,114 @@ __global__ __launch_bounds__(64) void k_profile_post(ProfileArgs A) {
 
 // MEA of a dense (L1 + 1) x (L2 + 1) posterior (ProbabilisticModel.h:804-864,
 // ChooseBestOfThree ScoreType.h:347-366; QuickProbs' computeAlignment is the
-// same recurrence): one wave, rows in strips of 64 lanes, lane r on row
-// 64 s + r + 1 at column j = t - r + 1 of step t (an anti-diagonal
-// wavefront).  up = the upper lane's value of the previous step (DPP shift;
-// lane 0 reads the previous strip's last row, kept in LDS), diagonal = the
-// previous step's up, left = own previous value: every cell adds and compares
-// exactly as the serial loop does, so scores and choices are the reference's
-// bit for bit.  The choices go out as 2 bits per cell (0 D, 1 L, 2 U) for
-// the host to trace back.
-// Several waves: wave w takes strips w, w + W, ...; a strip starts 3
-// intervals (96 steps) after the one above it, so every value its lane 0
-// reads from that strip's last row (kept in a two-slot LDS ring) was
-// written at least one 32-step interval earlier, and all waves meet at a
-// barrier after every interval.  Strip s starts at interval
-// g_s = max(3 s, g_{s-W} + NI) (NI intervals per strip).  The posterior of
-// the next interval is loaded into registers during this one.
-constexpr int kMeaWaves = 8;  // 2 waves per SIMD: 256 VGPRs for the two 32-step register queues
-constexpr int kMeaIv = 32;  // steps per interval
-size_t profile_mea_lds(int L2) { return (size_t)2 * (L2 + 5) * 4 + 4 * 256 + 64; }
-__global__ __launch_bounds__(64 * kMeaWaves) void k_profile_mea(MeaArgs A) {
-  extern __shared__ __align__(16) uint8_t mea_smem[];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, W = blockDim.x >> 6;
-  const int L1 = A.L1, L2 = A.L2, W2 = L2 + 1, Wq = (W2 + 3) >> 2, RS = L2 + 5;
-  float* ring = (float*)mea_smem;                    // 2 x RS: last rows of strips s (slot s & 1)
-  int* g = (int*)(mea_smem + (size_t)2 * RS * 4);     // strip start intervals (<= 256 strips)
-  const int nstrips = (L1 + 63) >> 6;
-  const int NI = (L2 + 63 + kMeaIv - 1) / kMeaIv;
-  for (int k = threadIdx.x; k < 2 * RS; k += blockDim.x) ring[k] = 0.f;  // row 0 (slot 1 for strip 0)
-  if (threadIdx.x == 0) {
-    for (int s = 0; s < nstrips; ++s) g[s] = max(3 * s, s >= W ? g[s - W] + NI : 0);
-  }
-  __syncthreads();
-  const int end = g[nstrips - 1] + NI;
-  int m = 0;                    // this wave's current strip: w + m W
-  int s = w, gs = s < nstrips ? g[s] : end;
-  float left = 0.f, vprev = 0.f, upprev = 0.f, rowend = 0.f, pv = 0.f, lr = 0.f;
-  uint32_t bits = 0;
-  float cur[kMeaIv], nxt[kMeaIv];
-  int i = 0;
-  const float* prow = A.post;
-  uint8_t* trow = A.tb;
-  auto load = [&](int t0, float* dst) {  // posterior of steps t0 .. t0 + 31 of this lane's row
-#pragma unroll
-    for (int u = 0; u < kMeaIv; ++u) dst[u] = prow[min(max(t0 + u - lane + 1, 1), L2)];
+// same recurrence).  One workgroup (one wave) per strip of 64 rows: lane r
+// holds row 64 s + r + 1 and is at column j = t - r at step t (a skewed
+// wavefront).  up = the upper lane's value of the previous step (DPP wave
+// shift; lane 0 takes the strip above's last row), diagonal = the previous
+// step's up, left = the lane's own previous value: every cell adds and
+// compares exactly as the serial loop does, so scores and choices are the
+// reference's bit for bit.  The strips run on different CUs at once: strip
+// s's last lane writes its row to HBM and, after every 16-step block,
+// publishes how many columns of it are final (agent-scope release); strip
+// s + 1 waits for the columns its next block reads (acquire) -- a pipeline
+// with ~100 steps of lag per strip instead of one CU doing every strip.
+// Choices: 2 bits per cell (0 D, 1 L, 2 U), one uint32 per lane and block;
+// the host traces back.  A strip that waits implausibly long sets the error
+// word and returns (every wave reaches an exit; the host falls back).
+__device__ __forceinline__ float mea_readlane(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
+MeaLayout mea_layout(int L1, int L2) {
+  MeaLayout m;
+  m.nstrips = (L1 + 63) / 64;
+  m.nblk = (L2 + 63 + kMeaBlk - 1) / kMeaBlk;  // steps 1 .. L2 + 63
+  m.rowpitch = (L2 + 1 + 63) & ~63;
+  size_t o = 0;
+  auto take = [&](size_t n) {
+    const size_t at = o;
+    o += (n + 255) & ~(size_t)255;
+    return at;
   };
-  for (int q = 0; q < end; ++q) {
-    if (s < nstrips && q == gs + NI) {  // strip done: score, next strip of this wave
-      if (i == L1) A.score[0] = rowend;
-      s += W;
-      gs = s < nstrips ? g[s] : end;
-    }
-    if (s < nstrips && q >= gs) {
-      const int t0 = (q - gs) * kMeaIv;
-      float* up_row = ring + (size_t)((s + 1) & 1) * RS;  // strip s - 1's last row
-      float* my_row = ring + (size_t)(s & 1) * RS;
-      if (t0 == 0) {  // strip start
-        i = 64 * s + lane + 1;
-        const int ii = min(i, L1);
-        prow = A.post + (size_t)ii * W2;
-        trow = A.tb + (size_t)ii * Wq;
-        left = vprev = upprev = rowend = 0.f;
-        bits = 0;
-        load(0, cur);
-        lr = up_row[1 <= L2 ? 1 : L2];
-      } else {
+  m.o_tb = take((size_t)m.nstrips * m.nblk * 64 * 4);
+  m.o_row = take((size_t)m.nstrips * m.rowpitch * 4);
+  m.o_prog = take((size_t)m.nstrips * 4);
+  m.o_score = take(4);
+  m.o_err = take(4);
+  m.bytes = o;
+  return m;
+}
+
+__global__ __launch_bounds__(64) void k_profile_mea(MeaArgs A, MeaLayout M) {
+  const int s = blockIdx.x, lane = threadIdx.x;
+  const int L1 = A.L1, L2 = A.L2, W2 = L2 + 1;
+  const int i = 64 * s + 1 + lane;
+  const int nr = min(64, L1 - 64 * s);
+  const float* prow = A.post + (int64_t)min(i, L1) * W2;
+  float* rows = reinterpret_cast<float*>(A.work + M.o_row);
+  const float* above = rows + (int64_t)(s > 0 ? s - 1 : 0) * M.rowpitch;
+  float* below = rows + (int64_t)s * M.rowpitch;
+  int* prog = reinterpret_cast<int*>(A.work + M.o_prog);
+  int* err = reinterpret_cast<int*>(A.work + M.o_err);
+  uint32_t* tbw = reinterpret_cast<uint32_t*>(A.work + M.o_tb) + (int64_t)s * M.nblk * 64;
+  if (lane == 0) below[0] = 0.f;
+  float v = 0.f, upp = 0.f;  // own value and up of the previous step
+  float pv[kMeaBlk], pn[kMeaBlk];
 #pragma unroll
-        for (int u = 0; u < kMeaIv; ++u) cur[u] = nxt[u];
-      }
-      load(t0 + kMeaIv, nxt);
-      const bool live = i <= L1;
-#pragma unroll
-      for (int u = 0; u < kMeaIv; ++u) {
-        const int t = t0 + u;
-        const int j = t - lane + 1;
-        const bool valid = j >= 1 && j <= L2;
-        const float lr_next = up_row[min(t + 2, L2)];
-        const float up = mlp_shr1(vprev, lr);
-        const float diag = upprev;
-        const float x1 = cur[u] + diag, x2 = left, x3 = up;
-        float v;
-        uint32_t b;
-        if (x1 >= x2) {
-          if (x1 >= x3) { v = x1; b = 0; } else { v = x3; b = 2; }
-        } else if (x2 >= x3) {
-          v = x2; b = 1;
-        } else {
-          v = x3; b = 2;
+  for (int u = 0; u < kMeaBlk; ++u) pv[u] = prow[min(max(1 + u - lane, 0), L2)];
+  for (int b = 0; b < M.nblk; ++b) {
+    const int t0 = kMeaBlk * b + 1;
+    // the row above through column min(t0 + 15, L2)
+    float ab = 0.f;
+    if (s > 0) {
+      const int need = min(t0 + kMeaBlk - 1, L2);
+      int spins = 0;
+      for (;;) {
+        const int have = __builtin_amdgcn_readfirstlane(
+            __hip_atomic_load(prog + s - 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT));
+        if (have >= need) break;
+        if (++spins > (1 << 22)) {  // ~seconds: give up (the host falls back)
+          if (lane == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          return;
         }
-        v = valid ? v : 0.f;
-        left = valid ? v : left;
-        bits |= valid ? b << (2 * (j & 3)) : 0u;
-        if (valid && live && ((j & 3) == 3 || j == L2)) trow[j >> 2] = (uint8_t)bits;
-        bits = (j & 3) == 3 ? 0u : bits;
-        my_row[lane == 63 && valid ? j : W2 + (lane & 3)] = v;
-        rowend = j == L2 ? v : rowend;
-        vprev = v;
-        upprev = up;
-        lr = lr_next;
+        __builtin_amdgcn_s_sleep(1);
       }
-      (void)pv;
+      ab = above[min(t0 + lane, L2)];  // lanes 0..15: above[t0 + u]
     }
-    __syncthreads();
+    // the next block's posterior
+#pragma unroll
+    for (int u = 0; u < kMeaBlk; ++u) pn[u] = prow[min(max(t0 + kMeaBlk + u - lane, 0), L2)];
+    uint32_t bits = 0;
+#pragma unroll
+    for (int u = 0; u < kMeaBlk; ++u) {
+      const int j = t0 + u - lane;
+      const float up = mlp_shr1(v, mea_readlane(ab, u));
+      const float x1 = ((j >= 1 && j <= L2) ? pv[u] : 0.f) + upp, x2 = v, x3 = up;
+      float nv;
+      uint32_t c;
+      if (x1 >= x2) {
+        if (x1 >= x3) { nv = x1; c = 0; } else { nv = x3; c = 2; }
+      } else if (x2 >= x3) {
+        nv = x2; c = 1;
+      } else {
+        nv = x3; c = 2;
+      }
+      nv = j >= 1 ? nv : 0.f;  // column 0 (and the lanes not started yet)
+      bits |= c << (2 * u);
+      if (lane == nr - 1 && j >= 1 && j <= L2) {
+        below[j] = nv;
+        if (s == M.nstrips - 1 && j == L2) *reinterpret_cast<float*>(A.work + M.o_score) = nv;
+      }
+      upp = up;
+      v = nv;
+    }
+    tbw[(int64_t)b * 64 + lane] = bits;
+#pragma unroll
+    for (int u = 0; u < kMeaBlk; ++u) pv[u] = pn[u];
+    // the last row is final through column t0 + 15 - (nr - 1)
+    if (lane == 0)
+      __hip_atomic_store(prog + s, min(L2, t0 + kMeaBlk - 1 - (nr - 1)), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   }
-  if (s < nstrips && i == L1) A.score[0] = rowend;
 }
 
 __global__ __launch_bounds__(256) void k_profile_gather(const float* post, const int64_t* cells, int64_t n,
@@ -296,12 +301,10 @@ hipError_t launch_profile_gather(const float* post, const int64_t* cells, int64_
 
 hipError_t launch_profile_mea(const MeaArgs& a, hipStream_t st) {
   if (a.L1 <= 0 || a.L2 <= 0) return hipSuccess;
-  const size_t lds = profile_mea_lds(a.L2);
-  const int nstrips = (a.L1 + 63) / 64;
-  if (lds > 160 * 1024 || nstrips > 256) return hipErrorInvalidValue;
-  if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute((const void*)k_profile_mea, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL(k_profile_mea, dim3(1), dim3(64 * std::min(kMeaWaves, nstrips)), lds, st, a);
+  const MeaLayout m = mea_layout(a.L1, a.L2);
+  hipError_t e = hipMemsetAsync(a.work + m.o_prog, 0, m.o_err + 4 - m.o_prog, st);  // progress, score, error
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_profile_mea, dim3((unsigned)m.nstrips), dim3(64), 0, st, a, m);
   return hipGetLastError();
 }
 
