@@ -167,6 +167,12 @@ inline int model_set_for_pid(int pid) {
 struct SideStream {
   hipStream_t st;
   hipEvent_t fork, join;
+  // join_mode 0: each sweep joins the side stream before it returns.  1: the
+  // backward sweep records the join but does not wait (the caller waits
+  // before the merge), so the local totals, which need only the fp32 sweep,
+  // run beside the fp64 backward.  2: per-model chains -- neither sweep forks
+  // or joins after the forward's fork; the caller joins before the merge.
+  int join_mode;
 };
 // launchers (posterior.hip).  lds_seq: chain_lds_pack(max seq_bytes, max members).
 hipError_t launch_forward(int models, const ModelScalars& ms, const Tables* tab, SeqSet seqs,

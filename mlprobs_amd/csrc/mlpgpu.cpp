@@ -394,6 +394,8 @@ int mlp_ctx_create(int device, mlp_ctx** out) {
     delete c;
     return MLP_ERR_HIP;
   }
+  // MLP_JOIN: experiment hook for SideStream::join_mode (mlp_kernels.h)
+  c->side.join_mode = getenv("MLP_JOIN") ? atoi(getenv("MLP_JOIN")) : 0;
   if (hipMalloc((void**)&c->d_tables, sizeof(Tables)) != hipSuccess) {
     delete c;
     return MLP_ERR_MEMORY;
@@ -1291,6 +1293,7 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
       HIPCHK(c, launch_local_totals(ms, c->d_tables, seqs, pm, cm, d_rec, sc, np, tot_waves, st));
       EXP_SYNC("totals");
     }
+    if (side && side->join_mode != 0) HIPCHK(c, hipStreamWaitEvent(st, side->join, 0));  // deferred join
     {
       Timer t(c, KMERGE, bcells, st);
       HIPCHK(c, launch_merge(models, pid, ms, seqs, pm, cm, d_rec, sc, nch, lds_seq, st));

@@ -685,7 +685,7 @@ static bool fuse_models() {
   return v == 1;
 }
 
-template <template <int> class K>
+template <template <int> class K, bool kFwd>
 static hipError_t launch_sweep(int models, const ModelScalars& ms, const Tables* tab, SeqSet seqs,
                                PairMeta pm, ChainMeta cm, PairRec* rec, Scratch sc, int64_t nchains,
                                int lds_seq, hipStream_t st, const SideStream* side) {
@@ -702,12 +702,18 @@ static hipError_t launch_sweep(int models, const ModelScalars& ms, const Tables*
       return hipSuccess;
     }
     hipError_t e;
-    if ((e = hipEventRecord(side->fork, st)) != hipSuccess) return e;
-    if ((e = hipStreamWaitEvent(side->st, side->fork, 0)) != hipSuccess) return e;
+    // per-model chains: the backward follows the forward on each stream
+    const bool fork = !(side->join_mode == 2 && !kFwd);
+    const bool record = !(side->join_mode == 2 && kFwd);
+    const bool wait = side->join_mode == 0 || (side->join_mode == 1 && kFwd);
+    if (fork) {
+      if ((e = hipEventRecord(side->fork, st)) != hipSuccess) return e;
+      if ((e = hipStreamWaitEvent(side->st, side->fork, 0)) != hipSuccess) return e;
+    }
     go(a_tag, st);
     (go(b_tags, side->st), ...);
-    if ((e = hipEventRecord(side->join, side->st)) != hipSuccess) return e;
-    return hipStreamWaitEvent(st, side->join, 0);
+    if (record && (e = hipEventRecord(side->join, side->st)) != hipSuccess) return e;
+    return wait ? hipStreamWaitEvent(st, side->join, 0) : hipSuccess;
   };
   switch (models) {
     case kHmm5 | kLocal | kPF:
@@ -736,7 +742,7 @@ hipError_t launch_forward(int models, const ModelScalars& ms, const Tables* tab,
                           PairMeta pm, ChainMeta cm, PairRec* rec, Scratch sc, int64_t nchains,
                           int lds_seq, hipStream_t st, const SideStream* side) {
   if (nchains <= 0) return hipSuccess;
-  const hipError_t e = launch_sweep<ForwardK>(models, ms, tab, seqs, pm, cm, rec, sc, nchains, lds_seq, st, side);
+  const hipError_t e = launch_sweep<ForwardK, true>(models, ms, tab, seqs, pm, cm, rec, sc, nchains, lds_seq, st, side);
   if (e != hipSuccess) return e;
   return hipGetLastError();
 }
@@ -745,7 +751,7 @@ hipError_t launch_backward(int models, const ModelScalars& ms, const Tables* tab
                            PairMeta pm, ChainMeta cm, PairRec* rec, Scratch sc, int64_t nchains,
                            int lds_seq, int64_t npairs, hipStream_t st, const SideStream* side) {
   if (nchains <= 0) return hipSuccess;
-  const hipError_t e = launch_sweep<BackwardK>(models, ms, tab, seqs, pm, cm, rec, sc, nchains, lds_seq, st, side);
+  const hipError_t e = launch_sweep<BackwardK, false>(models, ms, tab, seqs, pm, cm, rec, sc, nchains, lds_seq, st, side);
   if (e != hipSuccess) return e;
   // fold the 5-state backward total (needs Tables for the initial cells)
   if (models & kHmm5) return launch_fold_totals(ms, tab, seqs, pm, rec, npairs, st);
