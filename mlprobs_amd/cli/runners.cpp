@@ -62,10 +62,11 @@ struct Ctx {
     }
     check(nullptr, open_device(&c), "device", status);
     stage("device init");
-    // one family per process: a moderate batch scratch.  A fresh process's
-    // allocation waits for the driver to clear memory the previous process
-    // released (C3 512 x 400 back to back: posteriors 1.09 s at 32 GB,
-    // 7.4-10.5 s at 64 GB)
+    // one family per process: a moderate batch scratch.  Right after a
+    // process that held a lot of device memory exits, a fresh process can
+    // take ~40 GB at once; the allocation that goes past that stalls ~5.7 s
+    // (once, whatever its size or chunking: tools/probe/alloc_seq.sh,
+    // tools/ab_r03.sh chunks; profiles/r03d_*)
     const size_t scratch = s && s->scratch_bytes ? s->scratch_bytes : default_scratch;
     if (!getenv("MLP_SCRATCH_GB")) check(c, mlp_set_scratch(c, scratch), "device", status);
     if (s) s->dev = c;
@@ -141,7 +142,10 @@ int run_cpnp(std::vector<Row> seqs, bool just_features, bool progressive, cpnp::
     // 0: always the GPU) finish there before a device would be ready.
     std::vector<int> lens;
     for (const Row& r : seqs) lens.push_back(r.length());
-    cx.open(session, pair_cells(lens), 32ull << 30, 1);
+    // one family per process: a 16 GB batch scratch, like quickprobs (C3
+    // -p 0 back to back after a large process: 3.1-3.3 s every run at 16 GB;
+    // at 24 / 32 GB 3 of 4 and 2 of 4 runs stalled 4-6 s; profiles/r03d_*)
+    cx.open(session, pair_cells(lens), 16ull << 30, 1);
     mlp_ctx* ctx = cx.c;
     std::string res;
     std::vector<int64_t> off(1, 0);
@@ -242,12 +246,12 @@ int run_cpnp(std::vector<Row> seqs, bool just_features, bool progressive, cpnp::
         return mlp_profile_result(ctx);
       });
       // Profile posterior and MEA both on the device (mlp_profile_mea): only
-      // the path (and the few cells a refinement scores) come back.  Opt-in:
-      // the device MEA is a chain of dependent steps (8 waves over 64-row
-      // strips) and measured slower than the host's at C3 (QuickProbs
-      // refinement: 1.52 ms a call against ~1 ms), so by default
-      // (MLP_MEA_GPU_MIN unset) every MEA runs on the host.
-      static const int64_t mea_min = getenv("MLP_MEA_GPU_MIN") ? atoll(getenv("MLP_MEA_GPU_MIN")) : INT64_MAX;
+      // the path (and the few cells a refinement scores) come back.  By
+      // default every MEA of a device context runs there (C2 -p 1 refinement
+      // 0.66 s against 0.93 s with the host MEA, outputs identical;
+      // tools/ab_r03.sh cpnpmea); MLP_MEA_GPU_MIN sets a cell floor below
+      // which the host computes it.
+      static const int64_t mea_min = getenv("MLP_MEA_GPU_MIN") ? atoll(getenv("MLP_MEA_GPU_MIN")) : 0;
       cpnp::set_mea_backend([&](const cpnp::Profile& a, const cpnp::Profile& b, const int* w,
                                 const std::vector<int64_t>* cells, std::vector<float>* vals, std::string& path,
                                 float* score) -> bool {
@@ -380,9 +384,12 @@ int run_qp(std::vector<qph::Seq> seqs, const qph::Options& opt, int threads, Ses
         return mlp_profile_result(ctx);
       };
       // posterior and MEA both on the device, only the path comes back
-      // (opt-in, MLP_MEA_DEVICE=1: measured slower than the host MEA at C3,
-      // 1.52 ms a call against ~1 ms)
-      if (getenv("MLP_MEA_DEVICE") && atoi(getenv("MLP_MEA_DEVICE")) > 0 && !mlp_ctx_is_host(ctx)) {
+      // (k_profile_mea, strips pipelined across CUs): at C3 construction +
+      // refinement 1.72 s against 2.18-2.22 s with the host MEA, outputs
+      // identical (tools/ab_r03.sh mea); MLP_MEA_DEVICE=0 keeps the MEA on
+      // the host
+      const char* mea_dev = getenv("MLP_MEA_DEVICE");
+      if ((!mea_dev || atoi(mea_dev) > 0) && !mlp_ctx_is_host(ctx)) {
         be.device_mea = [&](const std::vector<float>& w, const qph::Profile& A, const qph::Profile& B,
                             std::string& path, float* score) -> bool {
           const int L1 = A[0].length(), L2 = B[0].length();

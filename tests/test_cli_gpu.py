@@ -101,11 +101,12 @@ QP_BIN = os.path.join(ROOT, 'mlprobs_amd', 'cli', 'quickprobs')
 @pytest.mark.parametrize('name,args', [('bb11028', []), ('bb11028', ['-c', '0']), ('bb11028', ['-c', '1', '-r', '5']),
                                        ('div12', []), ('div12', ['-c', '0']), ('sim8', []),
                                        ('sim8', ['-c', '3', '-r', '50']), ('qp_div60', []), ('qp_big210', []),
-                                       ('div12', ['mea']), ('qp_div60', ['mea']), ('qp_big210', ['mea'])])
+                                       ('div12', ['hostmea']), ('qp_div60', ['hostmea']),
+                                       ('qp_big210', ['hostmea'])])
 def test_quickprobs_cli(name, args):
-    env = ENV
-    if args == ['mea']:  # every MEA on the device (mlp_profile_mea)
-        args, env = [], dict(ENV, MLP_MEA_DEVICE='1')
+    env = ENV   # every MEA on the device (mlp_profile_mea, the default)
+    if args == ['hostmea']:  # every MEA on the host
+        args, env = [], dict(ENV, MLP_MEA_DEVICE='0')
     r = subprocess.run([QP_BIN, *args, os.path.join(GOLDEN, 'cli', f'{name}.fa')], capture_output=True, text=True,
                        timeout=300, env=env)
     assert r.returncode == 0 and r.stderr == '', r.stderr

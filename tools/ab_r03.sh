@@ -22,7 +22,7 @@ join)
       python3 -c "
 import json; d=json.load(open('$O/join$j.json'))
 k=d['kernels_ms_per_step']
-print('MLP_JOIN=$j', 'step %.1f ms' % d['ms_per_step'], ' '.join('%s %.1f' % (a, b) for a, b in k.items()), 'parity', d.get('parity', {}).get('bit_exact_pairs', ''))" | tee -a $O/summary.txt
+print('MLP_JOIN=$j', 'step %.1f ms' % d['ms_per_step'], ' '.join('%s %.1f' % (a, b) for a, b in k.items()))" | tee -a $O/summary.txt
     done
   done ;;
 mea)
@@ -42,6 +42,47 @@ jointest)
       > $O/jointest$j.log 2>&1 || { tail -20 $O/jointest$j.log; exit 1; }
     echo "MLP_JOIN=$j parity tests: $(tail -1 $O/jointest$j.log)" | tee -a $O/summary.txt
   done ;;
+cap)
+  # c_p_np_aln C3 -p 0 back to back at several scratch caps, after a process
+  # that held ~150 GB (the bench's posterior stage)
+  for cap in ${CAPS:-16 24 32}; do
+    timeout -k 10 200 python3 bench.py --no-cpu --no-e2e --no-qp --relax 0 --no-shards --steps 1 --warmup 0 > /dev/null 2>&1 || exit 1
+    for rep in 1 2 3 4; do
+      t0=$(date +%s.%N)
+      MLP_SCRATCH_GB=$cap MLP_CLI_TIMES=1 timeout -k 10 120 ./mlprobs_amd/cli/c_p_np_aln -p 0 $F3 > $O/cap.out 2> $O/cap.err || { tail -5 $O/cap.err; exit 1; }
+      t1=$(date +%s.%N)
+      echo "C3 -p 0 scratch $cap GB run $rep wall $(awk "BEGIN{print $t1 - $t0}") $(grep -E '^\[stage\] posteriors' $O/cap.err)" | tee -a $O/summary.txt
+    done
+    cmp -s $O/cap.out tests/golden/config/c3_512x400_s11.p_0.out && echo "C3 -p 0 output = reference" | tee -a $O/summary.txt
+  done ;;
+cpnpmea)
+  F2=tests/golden/config/c2_128x256_s11.fa
+  for f in $F2 $F3; do
+    for m in x 0 x 0; do
+      t0=$(date +%s.%N)
+      if [ $m = x ]; then unset MLP_MEA_GPU_MIN; else export MLP_MEA_GPU_MIN=$m; fi
+      MLP_SRAND_TIME=1700000000 MLP_CLI_TIMES=1 timeout -k 10 120 ./mlprobs_amd/cli/c_p_np_aln -p 1 $f > $O/np$m.out 2> $O/np$m.err || { tail -5 $O/np$m.err; exit 1; }
+      t1=$(date +%s.%N)
+      echo "$(basename $f) -p 1 MLP_MEA_GPU_MIN=$m wall $(awk "BEGIN{print $t1 - $t0}") $(grep -E '^\[stage\] (refinement|posteriors)|^\[host\]' $O/np$m.err | tr '\n' ' ')" | tee -a $O/summary.txt
+    done
+    unset MLP_MEA_GPU_MIN
+    cmp -s $O/npx.out $O/np0.out && echo "$(basename $f) -p 1 host / device MEA outputs identical" | tee -a $O/summary.txt
+  done ;;
+chunks)
+  # is the wait per allocation size or per process footprint?  each case after
+  # a process that held ~150 GB
+  P=tools/probe/alloc_chunks
+  V=tools/probe/vmm_probe
+  for spec in "$P 4 64" "$P 4 64" "$P 64 64" "$P 64 64" "$V 4 64" "$V 4 64" "$P 8 96" "$P 8 96" "$V 8 96" "$V 8 96"; do
+    timeout -k 10 200 python3 bench.py --no-cpu --no-e2e --no-qp --relax 0 --no-shards --steps 1 --warmup 0 > /dev/null 2>&1 || exit 1
+    t0=$(date +%s.%N)
+    timeout -k 10 60 $spec > $O/chunk.txt 2>&1 || { cat $O/chunk.txt; exit 1; }
+    t1=$(date +%s.%N)
+    echo "== $spec wall $(awk "BEGIN{print $t1 - $t0}") | $(grep -E 'malloc [0-9.]*[1-9][0-9.]* s|create\+map [0-9.]*[1-9]|memset all|reserve' $O/chunk.txt | tr '\n' ';')" | tee -a $O/summary.txt
+  done ;;
+relaxlog)
+  MLP_SCRATCH_GB=16 MLP_RELAX_LOG=1 MLP_CLI_TIMES=1 timeout -k 10 120 ./mlprobs_amd/cli/c_p_np_aln -p 0 $F3 > $O/rl.out 2> $O/rl.err || { tail -5 $O/rl.err; exit 1; }
+  cat $O/rl.err | tee -a $O/summary.txt ;;
 alloc)
   tools/probe/alloc_seq.sh > /dev/null && cat gpurun_out/alloc_seq/summary.txt >> $O/summary.txt ;;
 esac
