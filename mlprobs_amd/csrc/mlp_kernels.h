@@ -111,7 +111,8 @@ struct Scratch {
   float* f5;               // step-diagonal: 5-state fwd M, then f+b (in place)
   float* fl;               // local fwd M, then f+b
   double* zm;              // PF forward Zm (packed with frame)
-  float* pg;               // PF posterior
+  float* pg;               // PF posterior, element idx at pg[idx * pg_stride]
+  int32_t pg_stride;       // 2: in the low half of the slot's consumed PF forward Zm (zm)
   float* bl;               // step-diagonal: local bwd M (the merge adds fl + bl)
   // local-model chain totals (k_local_totals): per pair (rows 1..L1, chunks
   // of 64 columns, row-major from rm_off) the largest chain element of each

@@ -1113,7 +1113,17 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
 
   // step-diagonal bytes per slot of the models this pid runs: f5 (5-state),
   // fl + bl (local), zm + pg (partition function)
-  const int slot_bytes = ((models & kHmm5) ? 4 : 0) + ((models & kLocal) ? 8 : 0) + ((models & kPF) ? 12 : 0);
+  // Under a small scratch budget the PF posterior goes into the low half of
+  // the PF forward Zm slot of its own cell (read kPrefetch steps before the
+  // backward writes it): 4 B per cell less scratch, 20% bigger batches, at
+  // the price of a strided read in the merge.  C3 at the CLIs' 16 GB:
+  // posteriors 0.94 s against 1.01 s; at the bench's ~140 GB the batches are
+  // large anyway and the merge's extra bytes cost 17 ms a step (690 vs
+  // 679 ms; profiles/r03d_ab_tottr_pg.txt).  MLP_PG_SEPARATE=0 / 1 forces it.
+  static const char* pg_env = getenv("MLP_PG_SEPARATE");
+  const bool pg_in_zm = pg_env ? atoi(pg_env) == 0 : c->scratch_budget <= (48ull << 30);
+  const int slot_bytes =
+      ((models & kHmm5) ? 4 : 0) + ((models & kLocal) ? 8 : 0) + ((models & kPF) ? (pg_in_zm ? 8 : 12) : 0);
   auto pair_bytes = [&](int64_t q) {
     const int L1 = c->lens[c->pa[q]], L2 = c->lens[c->pb[q]];
     const int64_t rmc = (models & kLocal) ? (int64_t)L1 * local_chunks(L2) : 0;
@@ -1234,7 +1244,7 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
     Carver cv;
     const bool h5 = models & kHmm5, lo = models & kLocal, pf = models & kPF;
     const size_t o_f5 = cv.take(h5 ? P.cells * 4 : 0), o_fl = cv.take(lo ? P.cells * 4 : 0),
-                 o_bl = cv.take(lo ? P.cells * 4 : 0), o_pg = cv.take(pf ? P.cells * 4 : 0),
+                 o_bl = cv.take(lo ? P.cells * 4 : 0), o_pg = cv.take(pf && !pg_in_zm ? P.cells * 4 : 0),
                  o_zm = cv.take(pf ? P.cells * 8 : 0), o_cmf = cv.take(lo ? P.rm_total * 4 : 0),
                  o_cmb = cv.take(lo ? P.rm_total * 4 : 0),
                  o_tn = cv.take(lo ? 256 : 0), o_cl = cv.take(lo ? (size_t)tot_waves * 64 * tot_row * 4 : 0),
@@ -1253,7 +1263,8 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
     Scratch sc{};
     sc.f5 = (float*)(base + o_f5);
     sc.fl = (float*)(base + o_fl);
-    sc.pg = (float*)(base + o_pg);
+    sc.pg = pg_in_zm ? (float*)(base + o_zm) : (float*)(base + o_pg);
+    sc.pg_stride = pg_in_zm ? 2 : 1;
     sc.zm = (double*)(base + o_zm);
     sc.bl = (float*)(base + o_bl);
     sc.cmf = (float*)(base + o_cmf);

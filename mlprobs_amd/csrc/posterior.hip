@@ -492,7 +492,7 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
               if constexpr ((M & kQP) != 0) post = (post <= 1.0f && post >= 0.001f) ? post : 0.0f;
             }
           }
-          sc.pg[idx] = post;
+          sc.pg[idx * sc.pg_stride] = post;   // after this cell's zm was read (prefetch)
           if (lane == 0) {
             sc.bndz[(bo + j) * 3 + 0] = Zm;
             sc.bndz[(bo + j) * 3 + 1] = Ze;
@@ -559,7 +559,7 @@ __global__ __launch_bounds__(256, MLP_MERGE_WAVES) void k_merge(ModelScalars ms,
     const int64_t at = base + (int64_t)k * 64;
     if constexpr ((M & kHmm5) != 0) q5[k] = sc.f5[at];
     if constexpr ((M & kLocal) != 0) { ql[k] = sc.fl[at]; qb[k] = sc.bl[at]; }
-    if constexpr ((M & kPF) != 0) qg[k] = sc.pg[at];
+    if constexpr ((M & kPF) != 0) qg[k] = sc.pg[at * sc.pg_stride];
   }
   const int nseg = (W + 63) >> 6;
   for (int k = 0; k <= S; ++k) {
@@ -658,7 +658,7 @@ __global__ __launch_bounds__(256, MLP_MERGE_WAVES) void k_merge(ModelScalars ms,
         const int64_t at = base + (int64_t)min(t + QD, last) * 64;
         if constexpr ((M & kHmm5) != 0) q5[u] = sc.f5[at];
         if constexpr ((M & kLocal) != 0) { ql[u] = sc.fl[at]; qb[u] = sc.bl[at]; }
-        if constexpr ((M & kPF) != 0) qg[u] = sc.pg[at];
+        if constexpr ((M & kPF) != 0) qg[u] = sc.pg[at * sc.pg_stride];
         cursor_next(c, C, noins);
       }
     }

@@ -678,3 +678,20 @@ def test_pf_long_double_overflow():
         big.posteriors(3, 0.132548)
     assert e.value.code == 3
     big.close()
+
+
+def test_pf_posterior_in_zm_slot_bit_identical():
+    """Under a small scratch budget the PF posterior is written into the low
+    half of its cell's consumed PF forward Zm slot (mlp_posteriors, <= 48 GB);
+    the sparse store, distances and MEA scores must be the same bytes as with
+    its own array (the default budget), over several batches."""
+    seqs = _ragged_family(24, 80, 260, 46)
+    outs = []
+    for budget in (None, 64 << 20):
+        fam = Family(seqs)
+        if budget:
+            assert fam._L.mlp_set_scratch(fam._ctx, budget) == 0
+        fam.posteriors(0, 0.132548)
+        outs.append([np.ascontiguousarray(a).tobytes() for a in (*fam.export(), *fam.results())])
+        fam.close()
+    assert outs[0] == outs[1]

@@ -80,6 +80,51 @@ chunks)
     t1=$(date +%s.%N)
     echo "== $spec wall $(awk "BEGIN{print $t1 - $t0}") | $(grep -E 'malloc [0-9.]*[1-9][0-9.]* s|create\+map [0-9.]*[1-9]|memset all|reserve' $O/chunk.txt | tr '\n' ';')" | tee -a $O/summary.txt
   done ;;
+tottr)
+  MLP_TOT_TR=1 timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_configs.py -m gpu -x -q --timeout 300 \
+    --timeout-method thread > $O/tottr_test.log 2>&1 || { tail -20 $O/tottr_test.log; exit 1; }
+  echo "MLP_TOT_TR=1 parity + config tests: $(tail -1 $O/tottr_test.log)" | tee -a $O/summary.txt
+  for rep in 1 2; do
+    for j in 0 1; do
+      MLP_TOT_TR=$j timeout -k 10 300 python3 bench.py --no-e2e --no-qp --relax 0 --no-shards --steps 3 --warmup 1 \
+        --cpu-pairs 1024 > $O/tr$j.json 2> $O/tr$j.err || { tail -5 $O/tr$j.err; exit 1; }
+      python3 -c "
+import json; d=json.load(open('$O/tr$j.json'))
+k=d['kernels_ms_per_step']; p=d.get('parity') or {}
+print('MLP_TOT_TR=$j', 'step %.1f ms' % d['ms_per_step'], ' '.join('%s %.1f' % (a, b) for a, b in k.items()), 'parity max_rel_err', p.get('max_rel_err'))" | tee -a $O/summary.txt
+    done
+  done ;;
+qpprof)
+  # kernel statistics of one quickprobs C3 run (construction + refinement:
+  # 711 profile posteriors + MEAs on the device)
+  export TMPDIR=/tmp
+  MLP_CLI_TIMES=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/qpprof -o qp -- \
+    ./mlprobs_amd/cli/quickprobs $F3 > $O/qpprof.out 2> $O/qpprof.err || { tail -5 $O/qpprof.err; exit 1; }
+  grep -E '^\[(stage|host)\]' $O/qpprof.err | tee -a $O/summary.txt
+  head -12 $O/qpprof/qp_kernel_stats.csv | cut -d, -f1-4 | tee -a $O/summary.txt ;;
+pg)
+  timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_configs.py -m gpu -x -q --timeout 300 \
+    --timeout-method thread > $O/pg_test.log 2>&1 || { tail -20 $O/pg_test.log; exit 1; }
+  echo "PF posterior in the Zm slot: parity + config tests: $(tail -1 $O/pg_test.log)" | tee -a $O/summary.txt
+  for rep in 1 2; do
+    for j in 1 0; do
+      MLP_PG_SEPARATE=$j timeout -k 10 300 python3 bench.py --no-e2e --no-qp --relax 0 --no-shards --steps 3 --warmup 1 \
+        --cpu-pairs 1024 > $O/pg$j.json 2> $O/pg$j.err || { tail -5 $O/pg$j.err; exit 1; }
+      python3 -c "
+import json; d=json.load(open('$O/pg$j.json'))
+k=d['kernels_ms_per_step']; p=d.get('parity') or {}
+print('MLP_PG_SEPARATE=$j', 'step %.1f ms' % d['ms_per_step'], ' '.join('%s %.1f' % (a, b) for a, b in k.items()), 'parity max_rel_err', p.get('max_rel_err'))" | tee -a $O/summary.txt
+    done
+  done
+  for j in 1 0; do
+    for rep in 1 2; do
+      t0=$(date +%s.%N)
+      MLP_PG_SEPARATE=$j MLP_CLI_TIMES=1 timeout -k 10 120 ./mlprobs_amd/cli/c_p_np_aln -p 0 $F3 > $O/pgc.out 2> $O/pgc.err || { tail -5 $O/pgc.err; exit 1; }
+      t1=$(date +%s.%N)
+      echo "C3 -p 0 MLP_PG_SEPARATE=$j wall $(awk "BEGIN{print $t1 - $t0}") $(grep -E '^\[stage\] posteriors' $O/pgc.err)" | tee -a $O/summary.txt
+      cmp -s $O/pgc.out tests/golden/config/c3_512x400_s11.p_0.out && echo "  output = reference" | tee -a $O/summary.txt
+    done
+  done ;;
 relaxlog)
   MLP_SCRATCH_GB=16 MLP_RELAX_LOG=1 MLP_CLI_TIMES=1 timeout -k 10 120 ./mlprobs_amd/cli/c_p_np_aln -p 0 $F3 > $O/rl.out 2> $O/rl.err || { tail -5 $O/rl.err; exit 1; }
   cat $O/rl.err | tee -a $O/summary.txt ;;
