@@ -118,6 +118,13 @@ void stage(const char* name) {
 }
 
 // ---------------------------------------------------------------- c_p_np_aln
+// Profile MEAs of at least this many cells run on the device (both
+// drop-ins); MLP_MEA_GPU_MIN overrides.
+static int64_t mea_gpu_min() {
+  static const int64_t v = getenv("MLP_MEA_GPU_MIN") ? atoll(getenv("MLP_MEA_GPU_MIN")) : 0;
+  return v;
+}
+
 using cpnp::Row;
 
 int run_cpnp(std::vector<Row> seqs, bool just_features, bool progressive, cpnp::Options opt, Session* session,
@@ -251,7 +258,7 @@ int run_cpnp(std::vector<Row> seqs, bool just_features, bool progressive, cpnp::
       // 0.66 s against 0.93 s with the host MEA, outputs identical;
       // tools/ab_r03.sh cpnpmea); MLP_MEA_GPU_MIN sets a cell floor below
       // which the host computes it.
-      static const int64_t mea_min = getenv("MLP_MEA_GPU_MIN") ? atoll(getenv("MLP_MEA_GPU_MIN")) : 0;
+      const int64_t mea_min = mea_gpu_min();
       cpnp::set_mea_backend([&](const cpnp::Profile& a, const cpnp::Profile& b, const int* w,
                                 const std::vector<int64_t>* cells, std::vector<float>* vals, std::string& path,
                                 float* score) -> bool {
@@ -393,6 +400,7 @@ int run_qp(std::vector<qph::Seq> seqs, const qph::Options& opt, int threads, Ses
         be.device_mea = [&](const std::vector<float>& w, const qph::Profile& A, const qph::Profile& B,
                             std::string& path, float* score) -> bool {
           const int L1 = A[0].length(), L2 = B[0].length();
+          if ((int64_t)L1 * L2 < mea_gpu_min()) return false;
           std::vector<int32_t> l1, l2;
           for (const qph::Seq& q : A) l1.push_back(q.label);
           for (const qph::Seq& q : B) l2.push_back(q.label);

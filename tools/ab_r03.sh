@@ -125,6 +125,24 @@ print('MLP_PG_SEPARATE=$j', 'step %.1f ms' % d['ms_per_step'], ' '.join('%s %.1f
       cmp -s $O/pgc.out tests/golden/config/c3_512x400_s11.p_0.out && echo "  output = reference" | tee -a $O/summary.txt
     done
   done ;;
+meamin)
+  # profile MEA cell floor for the device (MLP_MEA_GPU_MIN), both drop-ins
+  F2=tests/golden/config/c2_128x256_s11.fa
+  for thr in ${THRS:-0 100000 250000 500000 1000000000000}; do
+    for spec in "c_p_np_aln -p 0 $F2" "c_p_np_aln -p 1 $F2" "c_p_np_aln -p 0 $F3" "quickprobs $F2" "quickprobs $F3"; do
+      set -- $spec
+      tag=$(echo "$spec" | tr ' /' '__' | tail -c 40)
+      MLP_MEA_GPU_MIN=$thr MLP_SRAND_TIME=1700000000 MLP_CLI_TIMES=1 timeout -k 10 120 ./mlprobs_amd/cli/$spec > $O/mm_$thr$tag.out 2> $O/mm.err || { tail -5 $O/mm.err; exit 1; }
+      echo "thr $thr $1 $2 $3 $(basename ${@: -1}): $(grep -E '^\[stage\] (progressive|refinement|construction)' $O/mm.err | tr '\n' ' ')" | tee -a $O/summary.txt
+    done
+  done
+  for spec in "c_p_np_aln -p 0 $F2" "c_p_np_aln -p 1 $F2" "c_p_np_aln -p 0 $F3" "quickprobs $F2" "quickprobs $F3"; do
+    tag=$(echo "$spec" | tr ' /' '__' | tail -c 40)
+    md5sum $O/mm_*$tag.out | awk '{print $1}' | sort -u | wc -l | xargs echo "distinct outputs over thresholds for $spec:" | tee -a $O/summary.txt
+  done ;;
+pmc)
+  tools/pmc_run.sh gpurun_out/pmc_r03 "--steps 1 --warmup 0 --no-cpu --no-e2e --no-qp --no-shards --relax 1" || exit 1
+  echo "pmc passes done" | tee -a $O/summary.txt ;;
 relaxlog)
   MLP_SCRATCH_GB=16 MLP_RELAX_LOG=1 MLP_CLI_TIMES=1 timeout -k 10 120 ./mlprobs_amd/cli/c_p_np_aln -p 0 $F3 > $O/rl.out 2> $O/rl.err || { tail -5 $O/rl.err; exit 1; }
   cat $O/rl.err | tee -a $O/summary.txt ;;
