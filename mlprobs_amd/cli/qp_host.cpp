@@ -467,15 +467,29 @@ struct ColumnRefiner {
 
 }  // namespace
 
-std::vector<int32_t> profile_maps(const Profile& p) {
-  std::vector<int32_t> out;
-  out.reserve(p.size() * (size_t)(p.empty() ? 0 : p[0].length() + 1));
-  for (const Seq& s : p) {  // Sequence::getMapping, appended
-    out.push_back(0);
-    const char* d = s.data.data();
-    for (int i = 1, L = s.length(); i <= L; i++)
-      if (d[i] != '-') out.push_back(i);
-  }
+std::vector<int32_t> profile_maps(const Profile& p, int threads) {
+  // Sequence::getMapping of every row, appended: row k's map has one entry
+  // per residue plus the leading 0, so every row's offset is known up front
+  // and the rows are filled independently (a refinement pass maps all n
+  // rows, ~2e5 entries at 512 x 400: on the host threads when that large)
+  std::vector<int64_t> off(p.size() + 1, 0);
+  const int64_t cells = (int64_t)p.size() * (p.empty() ? 0 : p[0].length());
+  const int nt = cells > 200000 ? std::max(1, threads) : 1;
+  mlpr::parallel_for((int64_t)p.size(), nt, [&](int64_t k) {
+    const char* d = p[k].data.data();
+    int64_t res = 0;
+    for (int i = 1, L = p[k].length(); i <= L; i++) res += d[i] != '-';
+    off[k + 1] = res + 1;
+  });
+  for (size_t k = 0; k < p.size(); k++) off[k + 1] += off[k];
+  std::vector<int32_t> out((size_t)off[p.size()]);
+  mlpr::parallel_for((int64_t)p.size(), nt, [&](int64_t k) {
+    int32_t* o = out.data() + off[k];
+    *o++ = 0;
+    const char* d = p[k].data.data();
+    for (int i = 1, L = p[k].length(); i <= L; i++)
+      if (d[i] != '-') *o++ = i;
+  });
   return out;
 }
 

@@ -102,6 +102,6 @@ Profile construct_and_refine(const std::vector<Seq>& seqs, const PosteriorBacken
                              const Options& opt, int threads);
 
 // Sequence::getMapping arrays of a profile, concatenated (len + 1 per row).
-std::vector<int32_t> profile_maps(const Profile& p);
+std::vector<int32_t> profile_maps(const Profile& p, int threads = 1);
 
 }  // namespace qph

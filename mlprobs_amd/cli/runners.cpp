@@ -119,9 +119,15 @@ void stage(const char* name) {
 
 // ---------------------------------------------------------------- c_p_np_aln
 // Profile MEAs of at least this many cells run on the device (both
-// drop-ins); MLP_MEA_GPU_MIN overrides.
+// drop-ins), smaller ones on the host's SIMD lanes, where a device round trip
+// costs more than the recurrence.  Floors 0 / 1e5 / 2.5e5 / 5e5 / never:
+// C2 -p 0 progressive 0.37 / 0.39 / 0.13 / 0.13 / 0.13 s, C2 -p 1 refinement
+// 0.62 / 0.58 / 0.55 / 0.58 / 0.80 s, QuickProbs C3 construction +
+// refinement 1.62 / 1.62 / 1.63 / 1.70 / 2.04 s, every output identical
+// (tools/ab_r03.sh meamin, profiles/r03f_ab_meamin.txt).  MLP_MEA_GPU_MIN
+// overrides.
 static int64_t mea_gpu_min() {
-  static const int64_t v = getenv("MLP_MEA_GPU_MIN") ? atoll(getenv("MLP_MEA_GPU_MIN")) : 0;
+  static const int64_t v = getenv("MLP_MEA_GPU_MIN") ? atoll(getenv("MLP_MEA_GPU_MIN")) : 250000;
   return v;
 }
 
@@ -382,7 +388,7 @@ int run_qp(std::vector<qph::Seq> seqs, const qph::Options& opt, int threads, Ses
         std::vector<int32_t> l1, l2;
         for (const qph::Seq& q : A) l1.push_back(q.label);
         for (const qph::Seq& q : B) l2.push_back(q.label);
-        const std::vector<int32_t> m1 = qph::profile_maps(A), m2 = qph::profile_maps(B);
+        const std::vector<int32_t> m1 = qph::profile_maps(A, threads), m2 = qph::profile_maps(B, threads);
         // out = NULL: the matrix stays in the library's pinned buffer
         const int rc = mlp_profile_posterior(ctx, w.data(), (int)A.size(), l1.data(), L1, m1.data(), (int)B.size(),
                                              l2.data(), L2, m2.data(), nullptr);
@@ -395,16 +401,19 @@ int run_qp(std::vector<qph::Seq> seqs, const qph::Options& opt, int threads, Ses
       // refinement 1.72 s against 2.18-2.22 s with the host MEA, outputs
       // identical (tools/ab_r03.sh mea); MLP_MEA_DEVICE=0 keeps the MEA on
       // the host
+      double t_maps = 0;
       const char* mea_dev = getenv("MLP_MEA_DEVICE");
       if ((!mea_dev || atoi(mea_dev) > 0) && !mlp_ctx_is_host(ctx)) {
         be.device_mea = [&](const std::vector<float>& w, const qph::Profile& A, const qph::Profile& B,
                             std::string& path, float* score) -> bool {
           const int L1 = A[0].length(), L2 = B[0].length();
           if ((int64_t)L1 * L2 < mea_gpu_min()) return false;
+          const auto tm0 = std::chrono::steady_clock::now();
           std::vector<int32_t> l1, l2;
           for (const qph::Seq& q : A) l1.push_back(q.label);
           for (const qph::Seq& q : B) l2.push_back(q.label);
-          const std::vector<int32_t> m1 = qph::profile_maps(A), m2 = qph::profile_maps(B);
+          const std::vector<int32_t> m1 = qph::profile_maps(A, threads), m2 = qph::profile_maps(B, threads);
+          t_maps += std::chrono::duration<double>(std::chrono::steady_clock::now() - tm0).count();
           check(ctx, mlp_profile_defer(ctx, 1), "profile posterior", 255);
           const int rc = mlp_profile_posterior(ctx, w.data(), (int)A.size(), l1.data(), L1, m1.data(), (int)B.size(),
                                                l2.data(), L2, m2.data(), nullptr);
@@ -445,6 +454,7 @@ int run_qp(std::vector<qph::Seq> seqs, const qph::Options& opt, int threads, Ses
       };
       aln = qph::construct_and_refine(seqs, be, tree, opt, threads);
       stage("construction + refinement");
+      if (getenv("MLP_CLI_TIMES")) fprintf(stderr, "[host] device MEA calls: labels and residue maps %.3f s\n", t_maps);
     }
   } catch (const RunError& e) {
     err = e.what();

@@ -1390,15 +1390,21 @@ int mlp_profile_posterior(mlp_ctx* c, const float* seq_weights, int n1, const in
     if (labels1[i] < 0 || labels1[i] >= c->n) return MLP_ERR_ARG;
   for (int j = 0; j < n2; j++)
     if (labels2[j] < 0 || labels2[j] >= c->n) return MLP_ERR_ARG;
+  const auto t0 = std::chrono::steady_clock::now();
   std::vector<float> w((int64_t)n1 * n2);
+  std::vector<double> w2(n2);
+  for (int j = 0; j < n2; j++) w2[j] = seq_weights[labels2[j]];
   double total = 0;
   for (int i = 0; i < n1; i++) {
     const double w1 = seq_weights[labels1[i]];
-    for (int j = 0; j < n2; j++) total += w1 * (double)seq_weights[labels2[j]];
+    for (int j = 0; j < n2; j++) total += w1 * w2[j];
   }
-  for (int i = 0; i < n1; i++)
-    for (int j = 0; j < n2; j++)
-      w[(int64_t)i * n2 + j] = (float)(((double)seq_weights[labels1[i]] * seq_weights[labels2[j]]) / total);
+  for (int i = 0; i < n1; i++) {
+    const double w1 = seq_weights[labels1[i]];
+    float* wi = w.data() + (int64_t)i * n2;
+    for (int j = 0; j < n2; j++) wi[j] = (float)((w1 * w2[j]) / total);
+  }
+  c->prof_t[0] += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   return profile_posterior(c, w, n1, labels1, L1, map1, n2, labels2, L2, map2, out);
 }
 

@@ -185,10 +185,15 @@ __global__ __launch_bounds__(64) void k_profile_post(ProfileArgs A) {
 // step's up, left = the lane's own previous value: every cell adds and
 // compares exactly as the serial loop does, so scores and choices are the
 // reference's bit for bit.  The strips run on different CUs at once: strip
-// s's last lane writes its row to HBM and, after every 16-step block,
-// publishes how many columns of it are final (agent-scope release); strip
-// s + 1 waits for the columns its next block reads (acquire) -- a pipeline
-// with ~100 steps of lag per strip instead of one CU doing every strip.
+// s's last lane writes its row and, after every 16-step block, publishes
+// how many columns of it are final; strip s + 1 waits for the columns its
+// next block reads -- a pipeline with ~100 steps of lag per strip instead of
+// one CU doing every strip.  The hand-off is the guide's sc1 form
+// (MI355X_MICROARCH.md, "Valid forms"): the row is stored and loaded only
+// with sc1 (relaxed agent-scope) accesses, the storing wave waits for its
+// stores (vmcnt(0)) before the sc1 flag store, the reader polls the flag with
+// sc1 loads -- no L2 write-back per block (an agent release) and no L1
+// invalidate per poll (an acquire).
 // Choices: 2 bits per cell (0 D, 1 L, 2 U), one uint32 per lane and block;
 // the host traces back.  A strip that waits implausibly long sets the error
 // word and returns (every wave reaches an exit; the host falls back).
@@ -228,7 +233,7 @@ __global__ __launch_bounds__(64) void k_profile_mea(MeaArgs A, MeaLayout M) {
   int* prog = reinterpret_cast<int*>(A.work + M.o_prog);
   int* err = reinterpret_cast<int*>(A.work + M.o_err);
   uint32_t* tbw = reinterpret_cast<uint32_t*>(A.work + M.o_tb) + (int64_t)s * M.nblk * 64;
-  if (lane == 0) below[0] = 0.f;
+  if (lane == 0) __hip_atomic_store(below, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   float v = 0.f, upp = 0.f;  // own value and up of the previous step
   float pv[kMeaBlk], pn[kMeaBlk];
 #pragma unroll
@@ -242,7 +247,7 @@ __global__ __launch_bounds__(64) void k_profile_mea(MeaArgs A, MeaLayout M) {
       int spins = 0;
       for (;;) {
         const int have = __builtin_amdgcn_readfirstlane(
-            __hip_atomic_load(prog + s - 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT));
+            __hip_atomic_load(prog + s - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
         if (have >= need) break;
         if (++spins > (1 << 22)) {  // ~seconds: give up (the host falls back)
           if (lane == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -250,7 +255,8 @@ __global__ __launch_bounds__(64) void k_profile_mea(MeaArgs A, MeaLayout M) {
         }
         __builtin_amdgcn_s_sleep(1);
       }
-      ab = above[min(t0 + lane, L2)];  // lanes 0..15: above[t0 + u]
+      // lanes 0..15: above[t0 + u]; an sc1 load (L2), like every load of the handed-off row
+      ab = __hip_atomic_load(above + min(t0 + lane, L2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     // the next block's posterior
 #pragma unroll
@@ -273,7 +279,7 @@ __global__ __launch_bounds__(64) void k_profile_mea(MeaArgs A, MeaLayout M) {
       nv = j >= 1 ? nv : 0.f;  // column 0 (and the lanes not started yet)
       bits |= c << (2 * u);
       if (lane == nr - 1 && j >= 1 && j <= L2) {
-        below[j] = nv;
+        __hip_atomic_store(below + j, nv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sc1 store
         if (s == M.nstrips - 1 && j == L2) *reinterpret_cast<float*>(A.work + M.o_score) = nv;
       }
       upp = up;
@@ -282,9 +288,11 @@ __global__ __launch_bounds__(64) void k_profile_mea(MeaArgs A, MeaLayout M) {
     tbw[(int64_t)b * 64 + lane] = bits;
 #pragma unroll
     for (int u = 0; u < kMeaBlk; ++u) pv[u] = pn[u];
-    // the last row is final through column t0 + 15 - (nr - 1)
+    // the last row is final through column t0 + 15 - (nr - 1): every store
+    // of this wave has completed (in L2) before the sc1 flag store
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (lane == 0)
-      __hip_atomic_store(prog + s, min(L2, t0 + kMeaBlk - 1 - (nr - 1)), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(prog + s, min(L2, t0 + kMeaBlk - 1 - (nr - 1)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 

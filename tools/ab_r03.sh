@@ -143,6 +143,32 @@ meamin)
 pmc)
   tools/pmc_run.sh gpurun_out/pmc_r03 "--steps 1 --warmup 0 --no-cpu --no-e2e --no-qp --no-shards --relax 1" || exit 1
   echo "pmc passes done" | tee -a $O/summary.txt ;;
+qpcli)
+  timeout -k 10 600 python3 -u -m pytest tests/test_cli_gpu.py -m gpu -x -q -k quickprobs --timeout 300 --timeout-method thread \
+    > $O/qpcli.log 2>&1 || { tail -20 $O/qpcli.log; exit 1; }
+  echo "quickprobs CLI tests: $(tail -1 $O/qpcli.log)" | tee -a $O/summary.txt ;;
+meatest)
+  timeout -k 10 600 python3 -u -m pytest tests/test_cli_gpu.py tests/test_gpu_parity.py -m gpu -x -q -k "quickprobs or profile or cli" \
+    --timeout 300 --timeout-method thread > $O/meatest.log 2>&1 || { tail -20 $O/meatest.log; exit 1; }
+  echo "CLI + profile tests: $(tail -1 $O/meatest.log)" | tee -a $O/summary.txt ;;
+qptimes)
+  for rep in 1 2; do
+    MLP_PROFILE_TIMES=1 MLP_CLI_TIMES=1 timeout -k 10 120 ./mlprobs_amd/cli/quickprobs $F3 > $O/qpt.out 2> $O/qpt.err || { tail -5 $O/qpt.err; exit 1; }
+    grep -E '^\[(stage\] construction|host|profile)' $O/qpt.err | tee -a $O/summary.txt
+    [ "$(md5sum < $O/qpt.out | cut -d' ' -f1)" = "1a8db641783cdbef0ee0b16bf46fc611" ] && echo "  output md5 = the earlier runs' (1a8db641783cdbef0ee0b16bf46fc611)" | tee -a $O/summary.txt
+  done ;;
+post)
+  timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_configs.py -m gpu -x -q --timeout 300 \
+    --timeout-method thread > $O/post_test.log 2>&1 || { tail -20 $O/post_test.log; exit 1; }
+  echo "parity + config tests: $(tail -1 $O/post_test.log)" | tee -a $O/summary.txt
+  for rep in 1 2; do
+    timeout -k 10 300 python3 bench.py --no-e2e --no-qp --relax 0 --no-shards --steps 3 --warmup 1 \
+      --cpu-pairs 1024 > $O/post.json 2> $O/post.err || { tail -5 $O/post.err; exit 1; }
+    python3 -c "
+import json; d=json.load(open('$O/post.json'))
+k=d['kernels_ms_per_step']; p=d.get('parity') or {}
+print('posterior stage', 'step %.1f ms' % d['ms_per_step'], ' '.join('%s %.1f' % (a, b) for a, b in k.items()), 'parity max_rel_err', p.get('max_rel_err'))" | tee -a $O/summary.txt
+  done ;;
 relaxlog)
   MLP_SCRATCH_GB=16 MLP_RELAX_LOG=1 MLP_CLI_TIMES=1 timeout -k 10 120 ./mlprobs_amd/cli/c_p_np_aln -p 0 $F3 > $O/rl.out 2> $O/rl.err || { tail -5 $O/rl.err; exit 1; }
   cat $O/rl.err | tee -a $O/summary.txt ;;
