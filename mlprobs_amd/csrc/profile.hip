@@ -267,15 +267,11 @@ __global__ __launch_bounds__(64) void k_profile_mea(MeaArgs A, MeaLayout M) {
       const int j = t0 + u - lane;
       const float up = mlp_shr1(v, mea_readlane(ab, u));
       const float x1 = ((j >= 1 && j <= L2) ? pv[u] : 0.f) + upp, x2 = v, x3 = up;
-      float nv;
-      uint32_t c;
-      if (x1 >= x2) {
-        if (x1 >= x3) { nv = x1; c = 0; } else { nv = x3; c = 2; }
-      } else if (x2 >= x3) {
-        nv = x2; c = 1;
-      } else {
-        nv = x3; c = 2;
-      }
+      // ChooseBestOfThree's value is the largest of the three whichever it
+      // picks (the values are non-negative sums: no NaN, no -0), so the step's
+      // dependency chain is one max3; its pick (D, else L, else U) is off it
+      float nv = fmaxf(fmaxf(x1, x2), x3);
+      const uint32_t c = (x1 >= x2 && x1 >= x3) ? 0u : (x2 >= x3 ? 1u : 2u);
       nv = j >= 1 ? nv : 0.f;  // column 0 (and the lanes not started yet)
       bits |= c << (2 * u);
       if (lane == nr - 1 && j >= 1 && j <= L2) {
