@@ -315,6 +315,7 @@ int run_cpnp(std::vector<Row> seqs, bool just_features, bool progressive, cpnp::
               (long long)nc, (long long)nd, tm);
     }
     cpnp::write_mfa(out, aln);
+    stage("alignment");
   } catch (const RunError& e) {
     err = e.what();
     return e.status;
@@ -322,7 +323,7 @@ int run_cpnp(std::vector<Row> seqs, bool just_features, bool progressive, cpnp::
     err = e.what();
     return 255;
   }
-  stage("alignment");
+  stage("context teardown");
   return 0;
 }
 
