@@ -101,16 +101,20 @@ bool load_fasta(const std::string& path, std::vector<Row>& out, std::string& err
 }
 
 void write_mfa(std::string& out, const Profile& p, int columns) {
+  // whole lines at a time (a -p 1 alignment of 512 rows is ~10 MB: per
+  // character appends took 0.2 s)
+  size_t total = out.size();
+  for (const Row& r : p) total += r.header.size() + 2 + (size_t)r.length() + r.length() / columns + 1;
+  out.reserve(total);
   for (const Row& r : p) {
     out += '>';
     out += r.header;
     out += '\n';
-    int ct = 1;
-    for (; ct <= r.length(); ct++) {
-      out += r.data[ct];
-      if (ct % columns == 0) out += '\n';
+    const int L = r.length();
+    for (int c0 = 1; c0 <= L; c0 += columns) {
+      out.append(r.data, (size_t)c0, (size_t)std::min(columns, L - c0 + 1));
+      out += '\n';
     }
-    if ((ct - 1) % columns != 0) out += '\n';
   }
 }
 

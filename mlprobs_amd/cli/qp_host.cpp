@@ -104,17 +104,19 @@ bool load_fasta_text(const std::string& buf, std::vector<Seq>& seqs, std::string
 }
 
 void write_fasta(std::string& out, const Profile& p) {
+  // 60-column lines, appended a line at a time
+  size_t total = out.size();
+  for (const Seq& s : p) total += s.header.size() + 2 + (size_t)s.length() + s.length() / 60 + 1;
+  out.reserve(total);
   for (const Seq& s : p) {
     out += '>';
     out += s.header;
     out += '\n';
     const int L = s.length();
-    int ct;
-    for (ct = 1; ct <= L; ct++) {
-      out += s.data[ct];
-      if (ct % 60 == 0) out += '\n';
+    for (int c0 = 1; c0 <= L; c0 += 60) {
+      out.append(s.data, (size_t)c0, (size_t)std::min(60, L - c0 + 1));
+      out += '\n';
     }
-    if ((ct - 1) % 60 != 0) out += '\n';
   }
 }
 

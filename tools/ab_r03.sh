@@ -169,6 +169,14 @@ import json; d=json.load(open('$O/post.json'))
 k=d['kernels_ms_per_step']; p=d.get('parity') or {}
 print('posterior stage', 'step %.1f ms' % d['ms_per_step'], ' '.join('%s %.1f' % (a, b) for a, b in k.items()), 'parity max_rel_err', p.get('max_rel_err'))" | tee -a $O/summary.txt
   done ;;
+teardown)
+  F2=tests/golden/config/c2_128x256_s11.fa
+  for f in $F2 $F3; do
+    for m in 0 1; do
+      MLP_CLI_TIMES=1 MLP_PROFILE_TIMES=1 timeout -k 10 120 ./mlprobs_amd/cli/c_p_np_aln -p $m $f > $O/td.out 2> $O/td.err || { tail -5 $O/td.err; exit 1; }
+      echo "$(basename $f) -p $m: $(grep -E '^\[(stage\] (refinement|progressive|alignment|context|output)|profile posterior\]|host\])' $O/td.err | tr '\n' ' ')" | tee -a $O/summary.txt
+    done
+  done ;;
 relaxlog)
   MLP_SCRATCH_GB=16 MLP_RELAX_LOG=1 MLP_CLI_TIMES=1 timeout -k 10 120 ./mlprobs_amd/cli/c_p_np_aln -p 0 $F3 > $O/rl.out 2> $O/rl.err || { tail -5 $O/rl.err; exit 1; }
   cat $O/rl.err | tee -a $O/summary.txt ;;
