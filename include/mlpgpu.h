@@ -206,7 +206,11 @@ const float *mlp_profile_result(const mlp_ctx *ctx);
  *     QuickProbs' computeAlignment is the same recurrence), bit-identical
  *     score and path, computed on the device; path = 'B'/'X'/'Y' in forward
  *     order, capacity L1 + L2 bytes;
- *   mlp_profile_gather: vals[k] = matrix[cells[k]] (row-major (L2 + 1)). */
+ *   mlp_profile_gather: vals[k] = matrix[cells[k]] (row-major (L2 + 1)).
+ * mlp_profile_mea returns MLP_ERR_STATE (nothing written) when a strip of
+ * the device pipeline gave up waiting for the one above (bounded spins);
+ * the matrix is still on the device and the caller computes the MEA on the
+ * host instead. */
 int mlp_profile_defer(mlp_ctx *ctx, int on);
 int mlp_profile_mea(mlp_ctx *ctx, char *path, int32_t *path_len, float *score);
 int mlp_profile_gather(mlp_ctx *ctx, int64_t n, const int64_t *cells, float *vals);

@@ -286,7 +286,12 @@ int run_cpnp(std::vector<Row> seqs, bool just_features, bool progressive, cpnp::
                 "profile posterior", 1);
         path.resize((size_t)L1 + L2);
         int32_t np = 0;
-        check(ctx, mlp_profile_mea(ctx, &path[0], &np, score), "MEA", 1);
+        const int mrc = mlp_profile_mea(ctx, &path[0], &np, score);
+        if (mrc == MLP_ERR_STATE) {   // the device pipeline gave up: the host MEA
+          check(ctx, mlp_profile_defer(ctx, 0), "profile posterior", 1);
+          return false;
+        }
+        check(ctx, mrc, "MEA", 1);
         path.resize(np);
         check(ctx, mlp_profile_defer(ctx, 0), "profile posterior", 1);
         return true;
@@ -425,7 +430,12 @@ int run_qp(std::vector<qph::Seq> seqs, const qph::Options& opt, int threads, Ses
           check(ctx, rc, "profile posterior", 255);
           path.resize((size_t)L1 + L2);
           int32_t np = 0;
-          check(ctx, mlp_profile_mea(ctx, &path[0], &np, score), "MEA", 255);
+          const int mrc = mlp_profile_mea(ctx, &path[0], &np, score);
+          if (mrc == MLP_ERR_STATE) {  // the device pipeline gave up: the host MEA
+            check(ctx, mlp_profile_defer(ctx, 0), "profile posterior", 255);
+            return false;
+          }
+          check(ctx, mrc, "MEA", 255);
           path.resize(np);
           check(ctx, mlp_profile_defer(ctx, 0), "profile posterior", 255);
           return true;

@@ -400,6 +400,7 @@ struct MeaArgs {
   const float* post;         // (L1 + 1) x (L2 + 1)
   int L1, L2;
   uint8_t* work;             // mea_layout(L1, L2).bytes
+  int spin_limit;            // polls a strip waits before giving up (1 << 22; MLP_MEA_SPINS: test hook)
 };
 hipError_t launch_profile_mea(const MeaArgs& a, hipStream_t st);
 hipError_t launch_profile_gather(const float* post, const int64_t* cells, int64_t n, float* out, hipStream_t st);

@@ -1603,6 +1603,10 @@ int mlp_profile_mea(mlp_ctx* c, char* path, int32_t* path_len, float* score) {
   a.L1 = L1;
   a.L2 = L2;
   a.work = (uint8_t*)c->r_mea.p;
+  // MLP_MEA_SPINS: test hook (0 makes a waiting strip give up at once: the
+  // caller's host fallback)
+  static const int spins = getenv("MLP_MEA_SPINS") ? atoi(getenv("MLP_MEA_SPINS")) : (1 << 22);
+  a.spin_limit = spins;
   HIPCHK(c, launch_profile_mea(a, c->stream));
   HIPCHK(c, hipMemcpyAsync(c->h_mea, c->r_mea.p, back, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipMemcpyAsync(c->h_mea + back, (uint8_t*)c->r_mea.p + m.o_score, 4, hipMemcpyDeviceToHost, c->stream));
@@ -1610,9 +1614,9 @@ int mlp_profile_mea(mlp_ctx* c, char* path, int32_t* path_len, float* score) {
   HIPCHK(c, hipStreamSynchronize(c->stream));
   int err = 0;
   memcpy(&err, c->h_mea + back + 4, 4);
-  if (err) {
+  if (err) {  // recoverable: the caller falls back to the host MEA
     c->err = "device MEA: a strip timed out waiting for the one above";
-    return MLP_ERR_HIP;
+    return MLP_ERR_STATE;
   }
   if (score) memcpy(score, c->h_mea + back, 4);
   // traceback (ProbabilisticModel.h:846-858): row 0 moves left, column 0 up;

@@ -249,7 +249,7 @@ __global__ __launch_bounds__(64) void k_profile_mea(MeaArgs A, MeaLayout M) {
         const int have = __builtin_amdgcn_readfirstlane(
             __hip_atomic_load(prog + s - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
         if (have >= need) break;
-        if (++spins > (1 << 22)) {  // ~seconds: give up (the host falls back)
+        if (++spins > A.spin_limit) {  // ~seconds: give up (the host falls back)
           if (lane == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           return;
         }

@@ -39,7 +39,7 @@ def test_cli_progressive(name, flags, suffix):
 
 @pytest.mark.parametrize('name', ['bb11028', 'div12', 'sim8'])
 @pytest.mark.parametrize('flags,suffix', [((), 'p_0'), (('-p', '1'), 'p_1'), (('-p', '1', '-ir', '0'), 'p_1_ir_0')])
-@pytest.mark.parametrize('mea', ['host', 'device'])
+@pytest.mark.parametrize('mea', ['host', 'device', 'device-gives-up'])
 def test_cli_profile_posterior_on_gpu(name, flags, suffix, mea):
     """Every progressive merge and refinement pass through the GPU's
     BuildPosterior (MLP_PROFILE_GPU_MIN=1: no host fallback for small
@@ -47,8 +47,10 @@ def test_cli_profile_posterior_on_gpu(name, flags, suffix, mea):
     (MLP_MEA_GPU_MIN=0: mlp_profile_mea for every merge): still the
     reference's bytes."""
     env = dict(ENV, MLP_PROFILE_GPU_MIN='1', MLP_SRAND_TIME='1700000000')
-    if mea == 'device':
+    if mea.startswith('device'):
         env['MLP_MEA_GPU_MIN'] = '0'
+        if mea == 'device-gives-up':   # every device MEA may give up: the host fallback
+            env['MLP_MEA_SPINS'] = '0'
     else:
         env['MLP_MEA_GPU_MIN'] = str(1 << 40)
     r = subprocess.run([BIN, *(flags or ('-p', '0')), os.path.join(GOLDEN, 'cli', f'{name}.fa')], capture_output=True,
@@ -175,4 +177,18 @@ def test_cli_config_families(name):
     r = _run('-p', '0', os.path.join(GOLDEN, 'config', f'{name}.fa'))
     assert r.returncode == 0 and r.stderr == '', r.stderr
     with open(out) as fh:
+        assert r.stdout == fh.read()
+
+
+@pytest.mark.parametrize('name', ['qp_div60', 'qp_big210'])
+def test_quickprobs_device_mea_gives_up(name):
+    """A device MEA strip that gives up waiting for the one above
+    (MLP_MEA_SPINS=0: at the first poll that finds it not ready) returns
+    MLP_ERR_STATE and the drop-in computes that MEA on the host: still the
+    reference's bytes, nothing on stderr."""
+    env = dict(ENV, MLP_MEA_SPINS='0', MLP_MEA_GPU_MIN='0')
+    r = subprocess.run([QP_BIN, os.path.join(GOLDEN, 'cli', f'{name}.fa')], capture_output=True, text=True,
+                       timeout=300, env=env)
+    assert r.returncode == 0 and r.stderr == '', r.stderr
+    with open(os.path.join(GOLDEN, 'cli', f'{name}.out' if name.startswith('qp_') else f'qp_{name}.out')) as fh:
         assert r.stdout == fh.read()
