@@ -2,10 +2,11 @@
 of libmlpgpu (mlp_shard_plan / mlp_gather_layout, the host logic behind
 mlp_shard_range and mlp_allgather) with real process-group exchange.
 
-Each rank computes the posteriors of its own shard (here with the oracle, the
-checker, standing in for the GPU kernels), the ranks exchange (p0, p1,
-entries) and their CSR blocks over gloo, place them where the library's
-layout says, and every rank must end up with the single-process store
+Each rank computes the posteriors of its own shard with the library itself
+(its host context, mlp_ctx_create_host: the product's pair body on host
+threads, no GPU here), the ranks exchange (p0, p1, entries) and their CSR
+blocks over gloo, place them where the library's layout says, and every rank
+must end up with the single-process store of the oracle, the checker
 (bit-identical results for any rank count).
 """
 import os
@@ -58,6 +59,21 @@ def _store(fam, pid, p0, p1):
     return cat(rps, np.int32), cat(cols, np.uint16), cat(vals, np.float32), np.array(dists, np.float32)
 
 
+def _store_lib(fam, pid, p0, p1):
+    """The same pieces from libmlpgpu's host context over pairs [p0, p1)."""
+    from mlprobs_amd.engine import Family
+    f = Family(fam, host=True)
+    try:
+        f.posteriors(pid, DELTA, p0, p1)
+        rp_full, eo, cols, vals = f.export()
+        d, _, _ = f.results(p0, p1)
+        rp = rp_full[f.rp_off[p0]:f.rp_off[p1]].astype(np.int32)
+        e0, e1 = int(eo[p0]), int(eo[p1])
+        return rp, cols[e0:e1].copy(), vals[e0:e1].copy(), d.astype(np.float32)
+    finally:
+        f.close()
+
+
 def _worker(rank, world, port, pid, q):
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
     dist.init_process_group('gloo', rank=rank, world_size=world)
@@ -67,7 +83,7 @@ def _worker(rank, world, port, pid, q):
         lens = np.array([len(s) for s in fam], np.int32)
         P = len(fam) * (len(fam) - 1) // 2
         p0, p1 = engine.shard_plan(lens, world, rank)
-        rp, cols, vals, dists = _store(fam, pid, p0, p1)
+        rp, cols, vals, dists = _store_lib(fam, pid, p0, p1)
         shards = [None] * world
         dist.all_gather_object(shards, (p0, p1, int(len(cols))))
         ebase = engine.gather_layout(P, shards)
