@@ -39,15 +39,19 @@ constexpr int kPrefetch = 4;
 // Waves per SIMD the sweeps are compiled for (launch bounds: 6 waves <=> at
 // most 80 VGPRs, 5 <=> 96): the chains of a batch keep ~8 waves per SIMD
 // queued, and the extra resident waves hide the DP's dependency stalls.  The
-// PF backward holds more fp64 state and stays at 5 (6 would spill); the
-// all-in-one M = 7 build keeps the compiler's choice.
+// PF backward holds more fp64 state and runs at MLP_PF_BWD_WAVES (5: 94
+// VGPRs; at 6 it now fits 80 VGPRs without spilling); the all-in-one M = 7
+// build keeps the compiler's choice.
 #ifndef MLP_SWEEP_WAVES
 #define MLP_SWEEP_WAVES 6
+#endif
+#ifndef MLP_PF_BWD_WAVES
+#define MLP_PF_BWD_WAVES 5
 #endif
 template <int M>
 struct SweepWaves {
   static constexpr int fwd = M == 7 ? 1 : MLP_SWEEP_WAVES;
-  static constexpr int bwd = M == 7 ? 1 : ((M & 4) != 0 && MLP_SWEEP_WAVES > 5 ? 5 : MLP_SWEEP_WAVES);
+  static constexpr int bwd = M == 7 ? 1 : ((M & 4) != 0 && MLP_SWEEP_WAVES > MLP_PF_BWD_WAVES ? MLP_PF_BWD_WAVES : MLP_SWEEP_WAVES);
 };
 
 // Bring three scaled-fp64 frames to their common maximum (exact: powers of two).
