@@ -323,7 +323,10 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));  // plain vector: st
 #else
 #define MLP_PF_LOAD(dst, src) (dst) = (src)
 #endif
-constexpr int kRelaxZChunk = 32;  // z schedule entries per LDS fill (64 B each); 32 leaves the staging area 7.7 KB more than 128 (C3 round 1 1.258 -> 1.205 s)
+#ifndef MLP_RELAX_ZCHUNK
+#define MLP_RELAX_ZCHUNK 32
+#endif
+constexpr int kRelaxZChunk = MLP_RELAX_ZCHUNK;  // z schedule entries per LDS fill (64 B each); 32 leaves the staging area 7.7 KB more than 128 (C3 round 1 1.258 -> 1.205 s)
 constexpr int kZEntBytes = 64;
 // LDS: [z schedule][QuickProbs z weights][per-output A bases, weights, weight sums][tile]
 static __host__ __device__ inline size_t relax_tile_off() {
