@@ -60,6 +60,9 @@ def parse():
     ap.add_argument('--no-qp', action='store_true', help='skip the QuickProbs posterior/consistency timings')
     ap.add_argument('--e2e-runs', type=int, default=3, help='fresh-process runs per end-to-end leg')
     ap.add_argument('--no-shards', action='store_true', help='skip the 8-virtual-shard all-gather timing')
+    ap.add_argument('--c5-stride', type=int, default=1,
+                    help='C5 leg over every k-th TEST/ox + sabre family (default 1: all 818)')
+    ap.add_argument('--no-c5', action='store_true', help='skip the C5 pipeline leg')
     return ap.parse_args()
 
 
@@ -373,15 +376,35 @@ def _stages(stderr):
     return st
 
 
+def _e2e_record(runs):
+    """Every run's wall time and stage split (MLP_CLI_TIMES), the median and
+    the maximum; a run more than 15% above the median is named with the
+    stage that grew most against the median run's split."""
+    order = sorted(range(len(runs)), key=lambda k: runs[k][0])
+    med_dt, r = runs[order[len(order) // 2]]
+    med_st = _stages(r.stderr)
+    rec = {'median_s': med_dt, 'max_s': max(x[0] for x in runs), 'runs_s': [x[0] for x in runs],
+           'exit': r.returncode, 'stages_s': med_st,
+           'runs': [{'s': dt, 'exit': x.returncode, 'stages_s': _stages(x.stderr)} for dt, x in runs]}
+    slow = []
+    for k, (dt, x) in enumerate(runs):
+        if dt > 1.15 * med_dt:
+            st = _stages(x.stderr)
+            grew = max(st, key=lambda n: st[n] - med_st.get(n, 0.0)) if st else None
+            slow.append({'run': k, 's': dt, 'stage': grew,
+                         'stage_excess_s': (st[grew] - med_st.get(grew, 0.0)) if grew else None})
+    rec['outliers'] = slow
+    return rec, r
+
+
 def e2e_families(args):
     """End-to-end seconds per family of the c_p_np_aln drop-in (-p 0: family
     test, posteriors, guide tree, 2 consistency rounds, progressive alignment,
     refinement; -p 1: family test, posteriors, 2 consistency rounds, alignment
     graph, refinement), one fresh process per run (as MLProbs starts them),
     wall clock around the process; three runs each, every run listed with
-    the median and the maximum (a process can wait for the driver to clear
-    memory an earlier process released); the stage split is the median run's
-    (MLP_CLI_TIMES).  The -p 0 outputs are compared in the run with the
+    its stage split (MLP_CLI_TIMES), the median and the maximum, and any run
+    more than 15% above the median named with the stage that grew.  The -p 0 outputs are compared in the run with the
     reference CLI's own output on the same family (tests/golden/config), with
     MLProbs' SP score (un_sp) and TC against it."""
     from mlprobs_amd import synth
@@ -401,11 +424,8 @@ def e2e_families(args):
                     r = subprocess.run([cli, '-p', mode, fa], capture_output=True, text=True, timeout=600,
                                        env=dict(os.environ, MLP_CLI_TIMES='1'))
                     runs.append((time.perf_counter() - t0, r))
-            order = sorted(range(len(runs)), key=lambda k: runs[k][0])
-            med_dt, r = runs[order[len(order) // 2]]
+            rec, r = _e2e_record(runs)
             log(f'e2e {tag} -p {mode}: ' + ', '.join(f'{x[0]:.2f}' for x in runs) + f' s (exit {r.returncode})')
-            rec = {'median_s': med_dt, 'max_s': max(x[0] for x in runs), 'runs_s': [x[0] for x in runs],
-                   'exit': r.returncode, 'stages_s': _stages(r.stderr)}
             g = os.path.join(ROOT, 'tests', 'golden', 'config', f'{gold}.p_0.out')
             if mode == '0' and os.path.exists(g) and args.s == 0.7:
                 with open(g) as fh:
@@ -433,10 +453,7 @@ def e2e_families(args):
                     r = subprocess.run([qp, fa], capture_output=True, text=True, timeout=600,
                                        env=dict(os.environ, MLP_CLI_TIMES='1'))
                     runs.append((time.perf_counter() - t0, r))
-                order = sorted(range(len(runs)), key=lambda k: runs[k][0])
-                dt, r = runs[order[len(order) // 2]]
-                res[tag] = {'median_s': dt, 'max_s': max(x[0] for x in runs), 'runs_s': [x[0] for x in runs],
-                            'exit': r.returncode, 'stages_s': _stages(r.stderr)}
+                res[tag], r = _e2e_record(runs)
                 log(f'e2e {tag}: ' + ', '.join(f'{x[0]:.2f}' for x in runs) + f' s (exit {r.returncode})')
                 if n <= 128 and os.path.exists(ref) and not args.no_cpu:
                     t0 = time.perf_counter()
@@ -506,19 +523,23 @@ def c5_pipeline(args):
     -- features, classifier 1, c_p_np_aln -p 0|1, column scores, classifiers
     3/2, region split, quickprobs on every region kept if not worse, combine,
     fallbacks -- as `mlprobs_amd/cli/mlprobs`, one process per family (as
-    MLProbs.py runs), aligners in-process (host context for small families,
-    one device context otherwise), on every 15th TEST/ox + TEST/sabre family
-    of tests/golden/sweep.json.xz (50).  Baseline: the same orchestration
+    MLProbs.py runs), aligners in-process (host context up to 4e6 pair-cells,
+    one device context above: the default dispatch), over EVERY TEST/ox +
+    TEST/sabre family (818, inputs from tests/golden/sweep.json.xz), one after
+    another, as the reference's harness times them (script.py:42-60: every
+    family of a benchmark, mean seconds).  Baseline: the same orchestration
     driving the reference CLIs built from source as external commands,
     exactly as MLProbs.py spawns them (c_p_np_aln with its own thread count
-    and passive OpenMP waits, quickprobs -t --cpu-threads); the reference's
-    Python orchestration itself (not on the box) is not in that time, so the
-    baseline is a lower bound of the reference pipeline's.  Readouts: MLProbs'
-    SP score (un_sp) of each final MSA and TC against the published MLProbs
-    output of the family (output4evaluation/, tests/golden/c5_published.json.xz),
-    and whether the two pipelines' outputs are identical (the reference's
-    multi-threaded quickprobs and time-seeded -p 1 make this informative
-    only; byte parity at every stage is pinned by tests/test_pipeline.py)."""
+    and passive OpenMP waits, quickprobs -t --cpu-threads) on the same
+    families; the reference's Python orchestration itself (not on the box) is
+    not in that time, so the baseline is a lower bound of the reference
+    pipeline's.  Times are split by the path the family took (trace
+    `device_runs`).  Readouts: MLProbs' SP score (un_sp) of each final MSA and
+    TC against the published MLProbs output of the family (output4evaluation/,
+    tests/golden/c5_published.json.xz), and how many outputs equal the
+    reference CLIs' (the reference's multi-threaded quickprobs and
+    time-seeded -p 1 make this informative only; byte parity at every stage
+    is pinned by tests/test_pipeline.py and tests/test_heavy_gpu.py)."""
     import lzma
     bin_ = os.path.join(ROOT, 'mlprobs_amd', 'cli', 'mlprobs')
     ref_cp = os.path.join(ROOT, 'oracle', '_ref', 'c_p_np_aln')
@@ -532,22 +553,27 @@ def c5_pipeline(args):
     if os.path.exists(pub_path):
         with lzma.open(pub_path, 'rt') as fh:
             pub = json.load(fh)
-    names = [k for k in sorted(fams) if k.split('/')[0] in ('ox', 'sabre') and 'p_0' in fams[k]][::15]
-    ours, theirs, same, host, calls, paths = [], [], 0, 0, 0, {}
-    sp_o, sp_r, sp_p, tc_o, tc_r, fails = [], [], [], [], [], 0
+    names = [k for k in sorted(fams) if k.split('/')[0] in ('ox', 'sabre')]
+    if args.c5_stride > 1:
+        names = names[::args.c5_stride]
+    with_ref = os.path.exists(ref_cp) and os.path.exists(ref_qp) and not args.no_cpu
+    recs, calls, paths, fails, same = [], 0, {}, 0, 0
+    sp_o, sp_r, sp_p, tc_o, tc_r = [], [], [], [], []
     env_ref = dict(os.environ, OMP_NUM_THREADS=str(args.cpu_threads), OMP_WAIT_POLICY='passive')
+    t_start = time.perf_counter()
     with tempfile.TemporaryDirectory() as td:
         for k, name in enumerate(names):
-            if k % 10 == 0:
-                log(f'c5 family {k}/{len(names)}')
+            if k % 50 == 0:
+                log(f'c5 family {k}/{len(names)} ({time.perf_counter() - t_start:.0f} s)')
             e = fams[name]
             fa = os.path.join(td, 'f.fa')
             with open(fa, 'wb') as fh:
                 fh.write(e['fa'].encode('latin-1'))
             out, trace = os.path.join(td, 'o.msa'), os.path.join(td, 't.json')
             t0 = time.perf_counter()
-            r = subprocess.run([bin_, '-q', '--trace', trace, fa, out], capture_output=True, timeout=600)
-            ours.append(time.perf_counter() - t0)
+            r = subprocess.run([bin_, '-q', '--trace', trace, fa, out], capture_output=True, timeout=900)
+            rec = {'name': name, 'cells': e['cells'], 's': time.perf_counter() - t0, 'device': False, 'ref_s': None}
+            recs.append(rec)
             if r.returncode != 0:
                 fails += 1
                 continue
@@ -555,19 +581,19 @@ def c5_pipeline(args):
                 mine = fh.read()
             with open(trace) as fh:
                 tr = json.load(fh)
+            rec['device'] = tr.get('device_runs', 0) > 0
             calls += tr['quickprobs_calls']
             paths[tr['path']] = paths.get(tr['path'], 0) + 1
-            host += e['cells'] <= 4e6
             sp_o.append(sp_score(mine))
             if name in pub:
                 sp_p.append(sp_score(pub[name]))
                 tc_o.append(tc_score(mine, pub[name]))
-            if os.path.exists(ref_cp) and os.path.exists(ref_qp) and not args.no_cpu:
+            if with_ref:
                 out2 = os.path.join(td, 'r.msa')
                 t0 = time.perf_counter()
                 subprocess.run([bin_, '-q', '--cpnp', ref_cp, '--quickprobs', f'{ref_qp} -t {args.cpu_threads}',
-                                '--tmp', td, fa, out2], capture_output=True, timeout=600, env=env_ref)
-                theirs.append(time.perf_counter() - t0)
+                                '--tmp', td, fa, out2], capture_output=True, timeout=1800, env=env_ref)
+                rec['ref_s'] = time.perf_counter() - t0
                 with open(out2, encoding='latin-1') as fh:
                     refo = fh.read()
                 same += refo == mine
@@ -579,23 +605,43 @@ def c5_pipeline(args):
         v = [x for x in v if x is not None]
         return float(np.mean(v)) if v else None
 
+    def summary(sel):
+        ours = [x['s'] for x in sel]
+        out = {'families': len(sel), 'pair_cells': int(sum(x['cells'] for x in sel))}
+        if ours:
+            out.update(s_per_family={'median': float(np.median(ours)), 'mean': float(np.mean(ours)),
+                                     'max': float(np.max(ours)), 'total': float(np.sum(ours))})
+        refs = [x['ref_s'] for x in sel if x['ref_s'] is not None]
+        if refs and len(refs) == len(sel):
+            out['reference_clis_s_per_family'] = {'median': float(np.median(refs)), 'mean': float(np.mean(refs)),
+                                                  'total': float(np.sum(refs))}
+            out['speedup_mean'] = float(np.mean(refs)) / float(np.mean(ours))
+            out['speedup_median'] = float(np.median(refs)) / float(np.median(ours))
+        return out
+
+    dev = [x for x in recs if x['device']]
     res = {'families': len(names), 'failed': fails,
-           'sample': 'every 15th TEST/ox + TEST/sabre family of tests/golden/sweep.json.xz',
-           'pipeline': 'mlprobs (MLProbs.py + utils/*.py restated in C++, aligners in-process)',
-           'host_path_families': host, 'quickprobs_region_calls': calls, 'paths': paths,
-           's_per_family': {'median': float(np.median(ours)), 'mean': float(np.mean(ours)), 'max': float(np.max(ours))},
+           'sample': 'every TEST/ox + TEST/sabre family' if args.c5_stride <= 1 else
+                     f'every {args.c5_stride}th TEST/ox + TEST/sabre family',
+           'pipeline': 'mlprobs (MLProbs.py + utils/*.py restated in C++, aligners in-process, default dispatch)',
+           'host_path_families': len(recs) - len(dev), 'device_path_families': len(dev),
+           'quickprobs_region_calls': calls, 'paths': paths,
+           'all': summary(recs), 'device_path': summary(dev), 'host_path': summary([x for x in recs if not x['device']]),
+           'slowest': sorted(({'name': x['name'], 's': x['s'], 'ref_s': x['ref_s'], 'cells': x['cells']}
+                              for x in recs), key=lambda x: -x['s'])[:8],
            'sp_un_sp_mean': mean(sp_o), 'published_sp_un_sp_mean': mean(sp_p),
-           'tc_vs_published_mean': mean(tc_o)}
-    if theirs:
-        res['reference_clis_s_per_family'] = {
-            'median': float(np.median(theirs)), 'mean': float(np.mean(theirs)),
-            'how': 'the same orchestration driving oracle/_ref/c_p_np_aln (its own thread count, passive OpenMP '
-                   f'waits) and oracle/_ref/quickprobs -t {args.cpu_threads} as external commands'}
-        res['speedup_median'] = float(np.median(theirs)) / float(np.median(ours))
-        res['speedup_mean'] = float(np.mean(theirs)) / float(np.mean(ours))
+           'tc_vs_published_mean': mean(tc_o), 'wall_s': time.perf_counter() - t_start}
+    res['s_per_family'] = res['all'].get('s_per_family')
+    if with_ref:
+        res['reference_clis'] = ('the same orchestration driving oracle/_ref/c_p_np_aln (its own thread count, '
+                                 f'passive OpenMP waits) and oracle/_ref/quickprobs -t {args.cpu_threads} as external '
+                                 'commands')
+        res['speedup_mean'] = res['all'].get('speedup_mean')
+        res['speedup_median'] = res['all'].get('speedup_median')
         res['identical_to_reference_clis'] = same
         res['reference_clis_sp_un_sp_mean'] = mean(sp_r)
         res['reference_clis_tc_vs_published_mean'] = mean(tc_r)
+    log(f"c5: {len(recs)} families in {res['wall_s']:.0f} s, {len(dev)} on the device")
     return res
 
 
@@ -655,7 +701,7 @@ def main():
     log('start')
     stream = hbm_stream() if world == 1 else None
     e2e = e2e_families(args) if (not args.no_e2e and world == 1) else None
-    c5 = c5_pipeline(args) if (not args.no_e2e and world == 1 and rank == 0) else None
+    c5 = c5_pipeline(args) if (not args.no_e2e and not args.no_c5 and world == 1 and rank == 0) else None
     if args.relax < 0:
         args.relax = 4 if world == 1 else 0
     fam_in = synth.family(args.n, args.len, args.s, seed=args.seed)

@@ -56,7 +56,8 @@ static std::string json_num(double v) {
   return b;
 }
 
-static void write_trace(const std::string& path, const mlpp::Trace& tr, const std::string& tools) {
+static void write_trace(const std::string& path, const mlpp::Trace& tr, const std::string& tools,
+                        const mlpr::Session& session) {
   std::string j = "{";
   j += "\"tools\": " + json_str(tools);
   j += ", \"features_line\": " + json_str(tr.features_line);
@@ -78,6 +79,8 @@ static void write_trace(const std::string& path, const mlpp::Trace& tr, const st
   j += "], \"kept_original\": [";
   for (size_t i = 0; i < tr.kept_original.size(); i++) j += (i ? ", " : "") + std::to_string(tr.kept_original[i]);
   j += "], \"path\": " + json_str(tr.path) + ", \"quickprobs_calls\": " + std::to_string(tr.quickprobs_calls);
+  j += ", \"device_runs\": " + std::to_string(session.device_runs) +
+       ", \"host_runs\": " + std::to_string(session.host_runs);
   j += ", \"times\": {";
   bool first = true;
   for (const auto& kv : tr.times) {
@@ -223,7 +226,7 @@ int main(int argc, char** argv) {
   std::string result;
   mlpp::Trace tr;
   const bool ok = mlpp::run_pipeline(in, *tools, M, result, tr, err, verbose);
-  if (!trace.empty()) write_trace(trace, tr, tools->name());
+  if (!trace.empty()) write_trace(trace, tr, tools->name(), session);
   if (!ok) {
     fprintf(stderr, "mlprobs: %s\n", err.c_str());
     return 1;

@@ -51,11 +51,13 @@ struct Ctx {
   void open(Session* s, double cells, size_t default_scratch, int status) {
     const double host_max = s ? s->host_max() : Session().host_max();
     if (cells <= host_max) {
+      if (s) s->host_runs++;
       check(nullptr, mlp_ctx_create_host(&c), "host context", status);
       owned = true;
       stage("host context");
       return;
     }
+    if (s) s->device_runs++;
     if (s && s->dev) {
       c = s->dev;
       return;

@@ -23,6 +23,7 @@ struct Session {
   mlp_ctx* dev = nullptr;
   size_t scratch_bytes = 0;   // 0: the caller's default (32 GB c_p_np_aln, 16 GB quickprobs)
   double host_max_cells = -1; // < 0: MLP_HOST_MAX_CELLS or 4e6
+  int device_runs = 0, host_runs = 0;  // aligner runs per context kind (the pipeline's trace)
   ~Session();
   double host_max() const;
 };

@@ -25,6 +25,14 @@ more MSAs (the reference's published outputs, output4evaluation/) and on
 synthetic score vectors for every class_lens.
 
     python tests/golden/gen_pipeline.py [/root/reference]
+    python tests/golden/gen_pipeline.py --heavy [workers]
+
+--heavy writes tests/golden/pipeline_heavy/: the same per-family records for
+12 TEST/ox + TEST/sabre families above 4e6 pair-cells (the families the
+drop-ins send to the GPU under their default dispatch; together 46% of C5's
+pair-cells), plus the reference CLIs' own outputs on each (c_p_np_aln -p 0
+and -p 1 single-threaded under the fixed clock, quickprobs -t 1), one worker
+process per family.
 """
 import hashlib
 import importlib
@@ -41,8 +49,9 @@ ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, os.path.join(ROOT, 'tests'))
 import forest_ref  # noqa: E402
 
-REF = sys.argv[1] if len(sys.argv) > 1 else '/root/reference'
-OUT = os.path.join(HERE, 'pipeline')
+HEAVY = '--heavy' in sys.argv
+REF = '/root/reference' if HEAVY or len(sys.argv) < 2 else sys.argv[1]
+OUT = os.path.join(HERE, 'pipeline_heavy' if HEAVY else 'pipeline')
 FIXED_TIME = '1700000000'
 MAX_CELLS = 4e6
 
@@ -61,13 +70,13 @@ def cells(path):
     return sum((lens[a] + 1) * (lens[b] + 1) for a in range(len(lens)) for b in range(a + 1, len(lens)))
 
 
-def setup_workdir(work):
+def setup_workdir(work, cpu=0):
     os.makedirs(os.path.join(work, 'baseMSA', 'C_P_NP_Aln'))
     os.makedirs(os.path.join(work, 'realign', 'QuickProbs', 'bin'))
     cp = os.path.join(work, 'baseMSA', 'C_P_NP_Aln', 'c_p_np_aln')
     with open(cp, 'w') as fh:
-        fh.write('#!/bin/sh\nREF_FIXED_TIME=%s exec taskset -c 0 %s "$@"\n'
-                 % (FIXED_TIME, os.path.join(ROOT, 'oracle', '_ref', 'c_p_np_aln_ft')))
+        fh.write('#!/bin/sh\nREF_FIXED_TIME=%s exec taskset -c %d %s "$@"\n'
+                 % (FIXED_TIME, cpu, os.path.join(ROOT, 'oracle', '_ref', 'c_p_np_aln_ft')))
     qp = os.path.join(work, 'realign', 'QuickProbs', 'bin', 'quickprobs')
     with open(qp, 'w') as fh:
         fh.write('#!/bin/sh\nexec %s -t 1 "$@"\n' % os.path.join(ROOT, 'oracle', '_ref', 'quickprobs'))
@@ -163,6 +172,60 @@ def pick_families():
     return out
 
 
+# the heavy set: the three largest named by the round-3 review plus the
+# next-largest families of both benchmarks (4.6e6 .. 9.6e7 pair-cells)
+HEAVY_FAMILIES = [('ox', '____12'), ('ox', '12t119'), ('sabre', 'sup_215'), ('ox', '12t117'), ('ox', '12t116'),
+                  ('sabre', 'sup_214'), ('ox', '____22'), ('sabre', 'sup_126'), ('sabre', 'twi_114'),
+                  ('ox', '___136'), ('sabre', 'sup_092'), ('sabre', 'sup_065')]
+
+
+def heavy_one(job):
+    """One heavy family in its own scratch working directory: the pipeline
+    record plus the reference CLIs' direct outputs."""
+    bench, name = job
+    path = os.path.join(REF, 'TEST', bench, 'in', name)
+    U = load_reference_utils()
+    forests = {n: forest_ref.load_forest(n) for n in ('branch', 'regions', 'seq_lens')}
+    work = tempfile.mkdtemp(prefix='mlp_heavy_')
+    try:
+        # one core per worker (c_p_np_aln single-threaded, as in main())
+        setup_workdir(work, HEAVY_FAMILIES.index(job) % os.cpu_count())
+        os.chdir(work)
+        rec = run_family(U, path, forests)
+        clis = {}
+        for tag, cmd in (('p_0', ['./baseMSA/C_P_NP_Aln/c_p_np_aln', '-p', '0', path]),
+                         ('p_1', ['./baseMSA/C_P_NP_Aln/c_p_np_aln', '-p', '1', path]),
+                         ('qp', ['./realign/QuickProbs/bin/quickprobs', path])):
+            r = subprocess.run(cmd, capture_output=True)
+            clis[tag] = [r.returncode, r.stdout.decode('latin-1')]
+        rec['reference_cli'] = clis
+    finally:
+        os.chdir('/')
+        shutil.rmtree(work, ignore_errors=True)
+    tag = f'{bench}_{name}'
+    shutil.copyfile(path, os.path.join(OUT, f'{tag}.fa'))
+    with open(os.path.join(OUT, f'{tag}.json'), 'w') as fh:
+        json.dump(rec, fh)
+    return {'family': f'{bench}/{name}', 'tag': tag, 'cells': cells(path), 'class1': rec['class1'],
+            'class_region': rec['class_region'], 'class_lens': rec['class_lens'], 'regions': len(rec['regions']),
+            'killed_stage': rec['killed_stage']}
+
+
+def main_heavy():
+    from multiprocessing import Pool
+    workers = int(sys.argv[-1]) if sys.argv[-1].isdigit() else 6
+    os.makedirs(OUT, exist_ok=True)
+    with Pool(workers) as pool:
+        manifest = list(pool.imap(heavy_one, HEAVY_FAMILIES))
+    for m in manifest:
+        print(m, flush=True)
+    with open(os.path.join(OUT, 'manifest.json'), 'w') as fh:
+        json.dump({'generator': 'tests/golden/gen_pipeline.py --heavy',
+                   'reference': 'kuangmeng/MLProbs utils/*.py + oracle/_ref CLIs (c_p_np_aln single thread, '
+                                'fixed time %s; quickprobs -t 1); reference_cli: the CLIs run directly' % FIXED_TIME,
+                   'families': manifest}, fh, indent=1)
+
+
 def scores_fixture(U):
     """calculateColScore / getAvgColScore on published outputs, and both region
     detectors on synthetic score vectors."""
@@ -227,4 +290,4 @@ def main():
 
 
 if __name__ == '__main__':
-    main()
+    main_heavy() if HEAVY else main()
