@@ -164,6 +164,17 @@ def cpu_baseline(fasta, args, n, lens, store, gpu_dist):
             'sample': f'first {args.cpu_pairs} pairs, {dt:.1f} s, oracle port'}, None
 
 
+def store_hash(fam):
+    """sha256 over the canonical store and the per-pair results (distances,
+    MEA scores, entry counts): the bit-identity check between the unsharded
+    and the virtually sharded runs."""
+    import hashlib
+    h = hashlib.sha256()
+    for a in list(fam.export()) + list(fam.results()):
+        h.update(np.ascontiguousarray(a).tobytes())
+    return h.hexdigest()
+
+
 def relax_work(n, lens, store):
     """The reference's multiply-adds for one consistency round over this store
     (for output (x, y) and each z, every entry of P_xz meets
@@ -221,6 +232,7 @@ def relax_leg(fam, args, n, lens, total_cells):
         rounds.append({'seconds': dt, 'nnz_in': nnz0 if it == 0 else rounds[-1]['nnz_out'], 'nnz_out': nnz,
                        'kernels_ms': {k: v['ms'] for k, v in kt.items() if v['launches']}})
         if it == 0:
+            hash1 = store_hash(fam)
             k_ms = kt['relax']['ms']
             k_launch = max(kt['relax']['launches'], 1)
             if not args.no_cpu:
@@ -234,6 +246,7 @@ def relax_leg(fam, args, n, lens, total_cells):
         if g:
             traffic = g['traffic_bytes_per_nnz_in'] * nnz0 / k_launch / 1e9
     res = {'rounds': len(rounds), 'per_round': rounds, 'seconds': sum(r['seconds'] for r in rounds),
+           'round1_hash': hash1,
            'nnz_per_round': [nnz0] + [r['nnz_out'] for r in rounds],
            'round1': {'macs_reference': macs, 'mac_per_s': macs / (k_ms * 1e-3), 'flop_per_s': 2 * macs / (k_ms * 1e-3),
                       'kernel_ms': k_ms},
@@ -464,7 +477,7 @@ def e2e_families(args):
     return res
 
 
-def shard_gather(args, seqs):
+def shard_gather(args, seqs, post_hash=None, relax_hash=None):
     """SURVEY.md section 8e on one GPU: the C3 posterior stage and one
     consistency round with 8 virtual shards (mlp_set_shards; real N > 1 GPUs
     are unmeasured here), timing the all-gathers of the sparse set (every
@@ -485,6 +498,7 @@ def shard_gather(args, seqs):
         runs.append((time.perf_counter() - t0, fam.kernel_times()['allgather']['ms']))
     t_post, gms = runs[1]
     kt = {'ms': gms}
+    sh_post = store_hash(fam)
     rp, eo, cols, vals = fam.export()
     store_bytes = int(eo[-1]) * 6 + rp.nbytes
     res = {'shards': 8, 'posterior_stage_s': t_post, 'gather_ms': kt['ms'], 'store_bytes': store_bytes,
@@ -497,7 +511,15 @@ def shard_gather(args, seqs):
     fam.synchronize()
     res['relax_round_s'] = time.perf_counter() - t0
     res['relax_gather_ms'] = fam.kernel_times()['allgather']['ms']  # counters reset before the round
+    sh_relax = store_hash(fam)
+    # the sharded run must equal the unsharded one bit for bit (store,
+    # distances, MEA scores, entry counts; posterior stage and round 1)
+    res['identical_to_unsharded'] = {'posterior_stage': None if post_hash is None else sh_post == post_hash,
+                                     'relax_round1': None if relax_hash is None else sh_relax == relax_hash}
     fam.close()
+    for k, v in res['identical_to_unsharded'].items():
+        if v is False:
+            raise SystemExit(f'8 virtual shards: {k} differs from the unsharded run')
     log(f"shards: posteriors {t_post:.2f} s (gather {kt['ms']:.1f} ms), relax round {res['relax_round_s']:.2f} s")
     return res
 
@@ -751,6 +773,7 @@ def main():
     gpu_dist, nnz = gpu_dist.copy(), nnz.copy()
     # the posterior store, kept for the same-run parity readouts (rank 0)
     post_store = [a.copy() for a in fam.export()] if (rank == 0 and world == 1 and not args.no_cpu) else None
+    post_hash = store_hash(fam) if (world == 1 and not args.no_shards) else None
     log('relaxation rounds')
     relax_info = relax_leg(fam, args, args.n, lens, total_cells) if (args.relax > 0 and world == 1) else None
     value = total_cells * args.steps / dt
@@ -784,7 +807,7 @@ def main():
         fam.close()
         fam = None
         log('virtual shards')
-        shards_info = shard_gather(args, seqs)
+        shards_info = shard_gather(args, seqs, post_hash, relax_info['round1_hash'] if relax_info else None)
     out = None
     if rank == 0:
         cpu, parity = None, None

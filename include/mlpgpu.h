@@ -67,8 +67,10 @@ int mlp_ctx_is_host(const mlp_ctx *ctx);
  * split into contiguous pair ranges, one shard (child context) per device:
  * posteriors balanced by DP cells (mlp_shard_plan), consistency rounds by
  * estimated multiply-adds (mlp_relax_shard_plan); the shards' sparse sets are
- * gathered over xGMI (peer copies) into this context's store, and the whole
- * store goes back to every shard before each relaxation round.  With 2-4
+ * all-gathered over xGMI (every shard pulls every other shard's new block on
+ * its own copy streams, peer copies), so every shard holds the whole store
+ * after each stage and round; the whole store is sent to the shards only
+ * when it came another way (an unsharded stage, mlp_csr_import).  With 2-8
  * virtual shards on one GPU the results are bit-identical to one device
  * (tests/test_gpu_shards.py); runs over several physical GPUs are untested
  * (no multi-GPU box here).  Everything else runs on the first device. */
@@ -242,9 +244,20 @@ int mlp_gather_layout(int nranks, int64_t npairs, const int64_t *info, int64_t *
  * nnz(z, y) / L_z + (n - 2) nnz(x, y) per output pair (x, y), from the
  * current per-pair entry counts.  bounds: nranks + 1. */
 int mlp_relax_shard_plan(int n, const int32_t *lens, const int64_t *pair_nnz, int nranks, int64_t *bounds);
-/* After every rank ran mlp_posteriors on its shard: all-gather the CSR
- * store and the per-pair scalars so every rank holds the whole family. */
+/* After every rank ran mlp_posteriors on its shard (or mlp_relax_range on
+ * its output range): all-gather the CSR store and the per-pair scalars so
+ * every rank holds the whole family (RCCL grouped broadcasts of each rank's
+ * block into its global place).  Without a communicator, or at one rank, a
+ * no-op; MLP_ALLGATHER_FORCE=1 runs the grouped body at one rank too (the
+ * test hook that exercises it on a one-GPU box). */
 int mlp_allgather(mlp_ctx *ctx);
+/* One C_P_NP_Aln consistency round (as mlp_relax, CPNP/MSA.cpp:1172-1360)
+ * over the output pairs [r0, r1) only, from the whole store: the range one
+ * rank computes when the caller does its own exchange (device or host
+ * context).  Afterwards the context holds that range's block, entries from 0
+ * (store range [r0, r1)), ready for mlp_allgather or the caller's exchange
+ * plus mlp_csr_import. */
+int mlp_relax_range(mlp_ctx *ctx, int64_t r0, int64_t r1);
 
 /* Wait for all device work of the context. */
 int mlp_synchronize(mlp_ctx *ctx);

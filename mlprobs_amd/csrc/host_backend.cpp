@@ -678,9 +678,12 @@ void qp_posteriors(const mlp::Tables& T, const mlp::ModelScalars& ms, const Fami
   }
 }
 
-void relax(const FamilyView& f, const std::vector<int64_t>& rp_off, Store& st, int64_t* nnz, const QpRelaxHost* qp) {
+void relax(const FamilyView& f, const std::vector<int64_t>& rp_off, Store& st, int64_t* nnz, const QpRelaxHost* qp,
+           int64_t r0, int64_t r1) {
   const int n = f.n;
   const int64_t P = (int64_t)n * (n - 1) / 2;
+  if (r1 < 0) r1 = P;
+  const int64_t nout = r1 - r0;
   auto pidx = [&](int a, int b) { return (int64_t)a * n - (int64_t)a * (a + 1) / 2 + (b - a - 1); };
   // stable transposes of every block (SparseMatrix::ComputeTranspose): rows
   // = the second sequence's residues, entries in the first sequence's order
@@ -721,7 +724,8 @@ void relax(const FamilyView& f, const std::vector<int64_t>& rp_off, Store& st, i
   std::vector<std::vector<uint16_t>> nc(P);
   std::vector<std::vector<float>> nv(P);
   std::vector<int32_t> nrp(st.rowptr.size());
-  parallel_for(P, threads_for(P), [&](int64_t p) {
+  parallel_for(nout, threads_for(nout), [&](int64_t k) {
+    const int64_t p = r0 + k;
     const int x = f.pa[p], y = f.pb[p];
     const int Lx = f.lens[x], Ly = f.lens[y], W = Ly + 1;
     const int32_t* rp = st.rowptr.data() + rp_off[p];
@@ -788,13 +792,13 @@ void relax(const FamilyView& f, const std::vector<int64_t>& rp_off, Store& st, i
   int64_t run = 0;
   for (int64_t p = 0; p < P; p++) {
     st.ent_off[p] = run;
-    nnz[p] = (int64_t)nc[p].size();
-    run += nnz[p];
+    if (p >= r0 && p < r1) nnz[p] = (int64_t)nc[p].size();
+    run += (int64_t)nc[p].size();
   }
   st.ent_off[P] = run;
   st.cols.resize(run);
   st.vals.resize(run);
-  for (int64_t p = 0; p < P; p++) {
+  for (int64_t p = r0; p < r1; p++) {
     std::copy(nc[p].begin(), nc[p].end(), st.cols.begin() + st.ent_off[p]);
     std::copy(nv[p].begin(), nv[p].end(), st.vals.begin() + st.ent_off[p]);
   }

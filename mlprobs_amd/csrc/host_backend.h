@@ -80,8 +80,10 @@ struct QpRelaxHost {
 };
 
 // One MSA::DoRelaxation round (CPNP/MSA.cpp:1172-1360) over every pair, or
-// QuickProbs' round when qp is given.
+// QuickProbs' round when qp is given.  With an output range [r0, r1) only
+// those pairs are computed: the store then holds their block, entries from 0
+// (ent_off[r0] = 0 .. ent_off[r1]), rows of other pairs cleared.
 void relax(const FamilyView& f, const std::vector<int64_t>& rp_off, Store& st, int64_t* nnz,
-           const QpRelaxHost* qp = nullptr);
+           const QpRelaxHost* qp = nullptr, int64_t r0 = 0, int64_t r1 = -1);
 
 }  // namespace mlph

@@ -2135,7 +2135,9 @@ int mlp_comm_init(mlp_ctx* c, const unsigned char id[128], int nranks, int rank)
 // gather every rank holds [0, P) in canonical layout.
 int mlp_allgather(mlp_ctx* c) {
   if (!c) return MLP_ERR_ARG;
-  if (!c->comm || c->nranks == 1) return MLP_OK;
+  // MLP_ALLGATHER_FORCE=1: the grouped body at one rank as well (test hook)
+  static const bool force = getenv("MLP_ALLGATHER_FORCE") && atoi(getenv("MLP_ALLGATHER_FORCE")) > 0;
+  if (!c->comm || (c->nranks == 1 && !force)) return MLP_OK;
   hipSetDevice(c->device);
   const int R = c->nranks;
   Timer tm(c, KGATHER, 0);
@@ -2215,6 +2217,7 @@ int mlp_allgather(mlp_ctx* c) {
 
 // ------------------------------------------------------------------ relax
 static int relax_rounds(mlp_ctx* c, int iters, const QpRelax& qp, const float* h_w, const float* h_sel);
+static int relax_one(mlp_ctx* c, const QpRelax& qp, bool last);
 
 int mlp_relax(mlp_ctx* c, int iters) {
   if (!c || iters < 0) return MLP_ERR_ARG;
@@ -2231,6 +2234,33 @@ int mlp_relax(mlp_ctx* c, int iters) {
     return MLP_OK;
   }
   return relax_rounds(c, iters, QpRelax{0, nullptr, 0.f, nullptr, 200.f}, nullptr, nullptr);
+}
+
+int mlp_relax_range(mlp_ctx* c, int64_t r0, int64_t r1) {
+  if (!c || r0 < 0 || r1 < r0 || r1 > c->P) return MLP_ERR_ARG;
+  if (c->n < 2) return MLP_ERR_STATE;
+  if (c->store_p0 != 0 || c->store_p1 != c->P) {
+    c->err = "relaxation needs every pair";
+    return MLP_ERR_STATE;
+  }
+  if (c->host) {
+    mlph::relax(host_view(c), c->rp_off, c->hs, c->nnz.data(), nullptr, r0, r1);
+    c->ent_off = c->hs.ent_off;
+    c->store_p0 = r0;
+    c->store_p1 = r1;
+    c->store_total = c->hs.ent_off[r1];
+    ++c->store_ver;
+    return MLP_OK;
+  }
+  if (c->comm && c->nranks > 1) {
+    c->err = "mlp_relax_range with a communicator: mlp_relax shards the rounds itself";
+    return MLP_ERR_STATE;
+  }
+  c->rel_r0 = r0;
+  c->rel_r1 = r1;
+  const int rc = relax_one(c, QpRelax{0, nullptr, 0.f, nullptr, 200.f}, true);
+  c->rel_r0 = c->rel_r1 = -1;
+  return rc;
 }
 
 // QuickProbs' consistency stage (ConsistencyStage::operator() / run,

@@ -68,6 +68,7 @@ def lib():
         L.mlp_csr_export.argtypes = [P, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
         L.mlp_csr_import.argtypes = [P, I32P, I64P, U16P, F32P]
         L.mlp_relax.argtypes = [P, C.c_int]
+        L.mlp_relax_range.argtypes = [P, I64, I64]
         L.mlp_relax_qp.argtypes = [P, C.c_int, F32P]
         L.mlp_relax_qp_selective.argtypes = [P, C.c_int, F32P, C.c_void_p, C.c_float]
         L.mlp_profile_posterior.argtypes = [P, F32P, C.c_int, I32P, C.c_int, I32P, C.c_int, I32P, C.c_int, I32P,
@@ -111,7 +112,7 @@ EXPORTED = ['mlp_ctx_create', 'mlp_ctx_destroy', 'mlp_last_error', 'mlp_set_scra
             'mlp_shard_range', 'mlp_shard_plan', 'mlp_gather_layout', 'mlp_allgather', 'mlp_synchronize', 'mlp_profile',
             'mlp_kernel_times', 'mlp_profile_reset', 'mlp_ctx_create_mask', 'mlp_set_shards', 'mlp_shard_count',
             'mlp_relax_shard_plan', 'mlp_ctx_create_host', 'mlp_ctx_is_host', 'mlp_relax_blockmfma_eval',
-            'mlp_profile_defer', 'mlp_profile_mea', 'mlp_profile_gather']
+            'mlp_profile_defer', 'mlp_profile_mea', 'mlp_profile_gather', 'mlp_relax_range']
 
 
 def shard_plan(lens, nranks, rank):
@@ -321,6 +322,12 @@ class Family:
     def relax(self, iters):
         self._csr = None
         self._chk(self._L.mlp_relax(self._ctx, int(iters)))
+
+    def relax_range(self, r0, r1):
+        """One C_P_NP_Aln round over output pairs [r0, r1) (one rank's share,
+        mlp_relax_range); the store then holds that block, entries from 0."""
+        self._csr = None
+        self._chk(self._L.mlp_relax_range(self._ctx, int(r0), int(r1)))
 
     # ---- multi-GPU
     @staticmethod

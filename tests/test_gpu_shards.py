@@ -94,3 +94,82 @@ def test_virtual_shards_imported_store():
         np.testing.assert_array_equal(x, y)
     one.close()
     many.close()
+
+
+_RCCL_CHILD = r'''
+import sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+from mlprobs_amd import synth
+from mlprobs_amd.engine import Family
+
+def store(f):
+    return [a.copy() for a in f.export()] + [a.copy() for a in f.results()]
+
+def same(a, b, what):
+    for k, (x, y) in enumerate(zip(a, b)):
+        assert np.array_equal(x, y), (what, k)
+
+seqs = [s for _, s in synth.family(40, 150, 0.7, seed=93)]
+ref = Family(seqs)
+ref.posteriors(0, 0.132548)
+s_post = store(ref)
+ref.relax(1)
+s_relax = store(ref)
+ref.close()
+f = Family(seqs)
+f.comm_init(Family.unique_id(), 1, 0)
+f.profile(True)
+f.posteriors(0, 0.132548)
+f.allgather()
+assert f.kernel_times()['allgather']['launches'] > 0, 'the grouped body did not run'
+same(store(f), s_post, 'posteriors after the RCCL all-gather')
+# a rank's relaxation round followed by its all-gather, as mlp_relax does
+# with several ranks
+f.relax(1)
+f.allgather()
+same(store(f), s_relax, 'relax round after the RCCL all-gather')
+f.close()
+print('rccl allgather ok')
+'''
+
+
+def test_rccl_allgather_grouped_body_one_rank():
+    """The one-process-per-GPU path's RCCL all-gather (mlp_comm_init +
+    mlp_allgather's grouped broadcasts, per-rank entry placement, scalar
+    exchange, ent_off rebuild) at one rank, forced past the one-rank early
+    return (MLP_ALLGATHER_FORCE=1): the store, distances and MEA scores after
+    the gather equal the context's own, after the posterior stage and after a
+    relaxation round.  In a child process: the hook is read once per
+    process."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, '-c', _RCCL_CHILD, root], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, MLP_ALLGATHER_FORCE='1'))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    assert 'rccl allgather ok' in r.stdout
+
+
+def test_relax_range_matches_full_round():
+    """mlp_relax_range on the device: each output range's block equals the
+    same pairs of a full round, bit for bit."""
+    seqs = [s for _, s in synth.family(36, 150, 0.7, seed=94)]
+    full = Family(seqs)
+    full.posteriors(0, 0.132548)
+    base = [a.copy() for a in full.export()]
+    full.relax(1)
+    rp_f, eo_f, c_f, v_f = full.export()
+    P = len(eo_f) - 1
+    for r0, r1 in ((0, P // 3), (P // 3, P), (P // 2, P // 2 + 1)):
+        part = Family(seqs)
+        part.import_csr(*base)
+        part.relax_range(r0, r1)
+        rp, eo, c, v = part.export()
+        a, b = int(part.rp_off[r0]), int(part.rp_off[r1])
+        np.testing.assert_array_equal(rp[a:b], rp_f[a:b])
+        np.testing.assert_array_equal(c[int(eo[r0]):int(eo[r1])], c_f[int(eo_f[r0]):int(eo_f[r1])])
+        np.testing.assert_array_equal(v[int(eo[r0]):int(eo[r1])], v_f[int(eo_f[r0]):int(eo_f[r1])])
+        part.close()
+    full.close()

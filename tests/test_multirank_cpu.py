@@ -159,29 +159,56 @@ def test_gather_layout_rejects_gaps():
 
 
 # ---- consistency rounds: output pairs split by estimated multiply-adds
+ROUNDS = 2
+
+
 def _relax_worker(rank, world, port, q):
+    """One rank of the sharded consistency rounds, all in the library: the
+    posterior stage on its host context, then per round its MAC-balanced
+    output range (mlp_relax_shard_plan) relaxed by mlp_relax_range, the
+    blocks exchanged over gloo and placed with the library's gather layout,
+    and the gathered store imported back (mlp_csr_import) for the next
+    round -- what mlp_allgather does over RCCL."""
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
     dist.init_process_group('gloo', rank=rank, world_size=world)
     try:
-        import orc
         from mlprobs_amd import engine
+        from mlprobs_amd.engine import Family
         fam = _family()
         lens = np.array([len(s) for s in fam], np.int32)
         P = len(fam) * (len(fam) - 1) // 2
-        rp, cols, vals, _ = _store(fam, 0, 0, P)  # every rank holds the whole set (after the gather)
-        eo = np.zeros(P + 1, np.int64)
-        L1, ro, _ = orc.store_view(lens, np.arange(P), rp, np.zeros(P + 1, np.int64))
-        for p in range(P):
-            eo[p + 1] = eo[p] + rp[ro[p] + L1[p] + 1]
-        bounds = engine.relax_shard_plan(lens, np.diff(eo), world)
-        sel = np.zeros(P, np.uint8)
-        sel[bounds[rank]:bounds[rank + 1]] = 1
-        o_rp, o_eo, o_c, o_v = orc.relax_subset(lens, rp, eo, cols, vals, sel)
-        mine = [(p, o_rp[ro[p]:ro[p] + L1[p] + 2].copy(), o_c[o_eo[p]:o_eo[p + 1]].copy(),
-                 o_v[o_eo[p]:o_eo[p + 1]].copy()) for p in range(bounds[rank], bounds[rank + 1])]
-        allb = [None] * world
-        dist.all_gather_object(allb, (list(bounds), mine))
-        q.put((rank, allb))
+        f = Family(fam, host=True)
+        try:
+            f.posteriors(0, DELTA)
+            rounds = []
+            for _ in range(ROUNDS):
+                _, eo, _, _ = f.export()
+                bounds = engine.relax_shard_plan(lens, np.diff(eo), world)
+                r0, r1 = int(bounds[rank]), int(bounds[rank + 1])
+                f.relax_range(r0, r1)
+                rp_full, eo, cols, vals = f.export()
+                rp = rp_full[f.rp_off[r0]:f.rp_off[r1]].astype(np.int32)
+                blk = (rp, cols[int(eo[r0]):int(eo[r1])].copy(), vals[int(eo[r0]):int(eo[r1])].copy())
+                shards = [None] * world
+                dist.all_gather_object(shards, (r0, r1, int(len(blk[1]))))
+                ebase = engine.gather_layout(P, shards)
+                blocks = [None] * world
+                dist.all_gather_object(blocks, blk)
+                g_rp = np.concatenate([b[0] for b in blocks])
+                g_cols = np.zeros(int(ebase[-1]), np.uint16)
+                g_vals = np.zeros(int(ebase[-1]), np.float32)
+                for r, b in enumerate(blocks):
+                    g_cols[ebase[r]:ebase[r + 1]] = b[1]
+                    g_vals[ebase[r]:ebase[r + 1]] = b[2]
+                # canonical entry offsets from the gathered row pointers
+                g_eo = np.zeros(P + 1, np.int64)
+                for p in range(P):
+                    g_eo[p + 1] = g_eo[p] + g_rp[f.rp_off[p + 1] - 1]
+                f.import_csr(g_rp, g_eo, g_cols, g_vals)
+                rounds.append((list(map(int, bounds)), g_rp, g_eo, g_cols, g_vals))
+            q.put((rank, rounds))
+        finally:
+            f.close()
     finally:
         dist.destroy_process_group()
 
@@ -209,16 +236,22 @@ def test_sharded_relaxation_matches_single_process():
         r = rp[ro[p]:ro[p] + L1[p] + 2]
         blocks.append((r.astype(np.int32), cols[e:e + r[-1]].astype(np.int32), vals[e:e + r[-1]]))
         e += r[-1]
-    ref = orc.relax(lens, blocks)
-    for rank, allb in got:
-        bounds = allb[0][0]
-        assert all(b[0] == bounds for b in allb) and bounds[0] == 0 and bounds[-1] == P
-        seen = set()
-        for _, mine in allb:
-            for p, r, c, v in mine:
-                assert np.array_equal(r, ref[p][0]) and np.array_equal(c, ref[p][1]) and np.array_equal(v, ref[p][2])
-                seen.add(p)
-        assert seen == set(range(P))
+    # the checker: the oracle's single-process rounds
+    want = []
+    for _ in range(ROUNDS):
+        blocks = orc.relax(lens, blocks)
+        want.append(blocks)
+    for rank, rounds in got:
+        assert len(rounds) == ROUNDS
+        for it, (bounds, g_rp, g_eo, g_cols, g_vals) in enumerate(rounds):
+            assert bounds[0] == 0 and bounds[-1] == P and sorted(bounds) == bounds
+            assert sum(bounds[r + 1] > bounds[r] for r in range(world)) >= 2  # the work is really split
+            for p in range(P):
+                r = g_rp[ro[p]:ro[p] + L1[p] + 2]
+                c = g_cols[g_eo[p]:g_eo[p + 1]].astype(np.int32)
+                v = g_vals[g_eo[p]:g_eo[p + 1]]
+                ref = want[it][p]
+                assert np.array_equal(r, ref[0]) and np.array_equal(c, ref[1]) and np.array_equal(v, ref[2]), (it, p)
 
 
 def test_relax_shard_plan_balance():
