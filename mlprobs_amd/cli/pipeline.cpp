@@ -512,13 +512,26 @@ struct InProcess : Tools {
   }
 };
 
+// One shell word: the path in single quotes, embedded quotes as '\''.  The
+// tool commands themselves (--cpnp / --quickprobs) stay shell text, as
+// MLProbs.py's os.system strings are; only the file paths are quoted.
+std::string shell_quote(const std::string& a) {
+  std::string r = "'";
+  for (char ch : a) {
+    if (ch == '\'') r += "'\\''";
+    else r += ch;
+  }
+  return r + "'";
+}
+
 struct External : Tools {
   std::string cp, qp, tmp;
   int count = 0;
   External(const std::string& c, const std::string& q, const std::string& t) : cp(c), qp(q), tmp(t) {}
   const char* name() const override { return "external"; }
   int cpnp(const std::string& seq_file, bool features, int program, std::string& text) override {
-    const std::string cmd = cp + (features ? " -G " : " -p " + std::to_string(program) + " ") + seq_file + " 2>&1";
+    const std::string cmd =
+        cp + (features ? " -G " : " -p " + std::to_string(program) + " ") + shell_quote(seq_file) + " 2>&1";
     FILE* p = popen(cmd.c_str(), "r");
     text.clear();
     if (!p) return 127;
@@ -531,7 +544,7 @@ struct External : Tools {
   }
   std::string run_qp(const std::string& in) {
     const std::string out = tmp + "/mlprobs_" + std::to_string(getpid()) + "_qp_out_" + std::to_string(count++);
-    const std::string cmd = qp + " " + in + " > " + out;
+    const std::string cmd = qp + " " + shell_quote(in) + " > " + shell_quote(out);
     if (system(cmd.c_str()) == -1) return std::string();
     std::string res;
     read_file(out, res);
@@ -583,8 +596,11 @@ bool has_upper(const std::string& s) {
   return false;
 }
 
-// doRealign (do_realign.py:49-71) + perProcess (:20-47) + addPerProcess (:73-101)
-void realign_region(Tools& tools, Dir& dir, const std::string& name, Trace& tr) {
+// doRealign (do_realign.py:49-71) + perProcess (:20-47) + addPerProcess (:73-101).
+// false (err set) where the reference raises: getAvgColScore indexes every
+// row at every column of the last row (calculate_column_scores.py:106-112),
+// so a ragged MSA raises IndexError and MLProbs.py ends without output.
+bool realign_region(Tools& tools, Dir& dir, const std::string& name, Trace& tr, std::string& err) {
   const std::string ret = base_name(name) + ".reliable";
   const std::string region = dir[name];
   // perProcess: rows with a letter, gaps removed; all-gap rows set aside
@@ -604,7 +620,13 @@ void realign_region(Tools& tools, Dir& dir, const std::string& name, Trace& tr) 
   std::string out = tools.quickprobs_text(tmp_file);
   tr.quickprobs_calls++;
   bool kept = false;
-  if (out.empty() || avg_col_score(region) > avg_col_score(out)) {   // os.path.getsize / getAvgColScore
+  bool ragged = false;
+  // os.path.getsize / getAvgColScore, left operand first like Python
+  if (out.empty() || avg_col_score(region, &ragged) > (ragged ? 0.0 : avg_col_score(out, &ragged)) || ragged) {
+    if (ragged) {
+      err = "IndexError: string index out of range (calculate_column_scores.py:110, getAvgColScore on " + name + ")";
+      return false;
+    }
     out = region;
     kept = true;
   }
@@ -617,6 +639,7 @@ void realign_region(Tools& tools, Dir& dir, const std::string& name, Trace& tr) 
   for (const auto& kv : r.rows) s += kv.first + "\n" + kv.second + "\n";
   for (const std::string& h : tmp_array) s += h + "\n" + std::string(lens, '-') + "\n";
   dir[ret] = s;
+  return true;
 }
 
 // combineFiles (do_realign.py:121-199); false where the reference raises
@@ -846,7 +869,8 @@ bool run_pipeline(const std::string& seq_file, Tools& tools, const Models& M, st
       std::vector<std::string> names;
       for (const auto& kv : dir)
         if (ext_of(kv.first) == "unreliable" && kv.first[0] != '.') names.push_back(kv.first);
-      for (const std::string& f : names) realign_region(tools, dir, f, tr);
+      for (const std::string& f : names)
+        if (!realign_region(tools, dir, f, tr, err)) return false;
     } else {   // ExceptionHandling (:201-204): quickprobs on the whole family
       dir.clear();
       dir["0-0.reliable"] = tools.quickprobs_file(seq_file);

@@ -4,6 +4,7 @@
 #include <stdlib.h>
 
 #include <condition_variable>
+#include <exception>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -21,6 +22,7 @@ struct Pool {
   const std::function<void(int, int)>* job = nullptr;
   int T = 0, remaining = 0;
   uint64_t gen = 0;
+  std::exception_ptr error;   // the first exception a worker's body threw (rethrown on the caller)
 
   void loop(int id) {
     t_inside = true;
@@ -33,8 +35,14 @@ struct Pool {
       const std::function<void(int, int)>* j = job;
       const int TT = T;
       l.unlock();
-      (*j)(id, TT);
+      std::exception_ptr e;
+      try {
+        (*j)(id, TT);
+      } catch (...) {
+        e = std::current_exception();
+      }
       l.lock();
+      if (e && !error) error = e;
       if (--remaining == 0) done.notify_one();
     }
   }
@@ -75,11 +83,30 @@ void parallel(int T, const std::function<void(int, int)>& body) {
     ++p.gen;
   }
   p.go.notify_all();
-  t_inside = true;
-  body(0, T);
-  t_inside = false;
+  // the caller's share: whatever it throws, the workers still run `body`
+  // (which lives in the caller's frame), so wait for them before unwinding;
+  // a worker's exception is rethrown here
+  struct Inside {
+    Inside() { t_inside = true; }
+    ~Inside() { t_inside = false; }
+  };
+  std::exception_ptr mine;
+  {
+    Inside in;
+    try {
+      body(0, T);
+    } catch (...) {
+      mine = std::current_exception();
+    }
+  }
   std::unique_lock<std::mutex> l(p.m);
   p.done.wait(l, [&] { return p.remaining == 0; });
+  std::exception_ptr theirs = p.error;
+  p.error = nullptr;
+  p.job = nullptr;
+  l.unlock();
+  if (mine) std::rethrow_exception(mine);
+  if (theirs) std::rethrow_exception(theirs);
 }
 
 }  // namespace mlpr

@@ -255,6 +255,10 @@ __global__ __launch_bounds__(64) void k_profile_mea(MeaArgs A, MeaLayout M) {
         }
         __builtin_amdgcn_s_sleep(1);
       }
+      // the poll matched: an agent-scope acquire orders the row loads below
+      // after it (once per 16-step block, not per poll; the writer's release
+      // is its s_waitcnt vmcnt(0) before the flag store)
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       // lanes 0..15: above[t0 + u]; an sc1 load (L2), like every load of the handed-off row
       ab = __hip_atomic_load(above + min(t0 + lane, L2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -307,6 +311,11 @@ hipError_t launch_profile_mea(const MeaArgs& a, hipStream_t st) {
   if (a.L1 <= 0 || a.L2 <= 0) return hipSuccess;
   const MeaLayout m = mea_layout(a.L1, a.L2);
   hipError_t e = hipMemsetAsync(a.work + m.o_prog, 0, m.o_err + 4 - m.o_prog, st);  // progress, score, error
+  if (e != hipSuccess) return e;
+  // the handed-off rows start as NaN every launch: a read that ever got
+  // ahead of its hand-off would poison the path's scores and show up in the
+  // byte-identical tests instead of silently reusing the previous call's row
+  e = hipMemsetAsync(a.work + m.o_row, 0xff, (size_t)m.nstrips * m.rowpitch * 4, st);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_profile_mea, dim3((unsigned)m.nstrips), dim3(64), 0, st, a, m);
   return hipGetLastError();

@@ -191,3 +191,43 @@ def test_forest_evaluators(name):
         pytest.skip('scikit-learn not importable')
     np.testing.assert_array_equal(clf.predict_proba(X), want)
     np.testing.assert_array_equal(clf.predict(X), want_cls)
+
+
+def test_external_tools_quote_paths(tmp_path):
+    """File paths reach the external commands as single shell words: an input
+    and a --tmp directory with spaces and quotes still run (the drop-in CLIs
+    as the external tools, host path; the reference QuickProbs CLI itself
+    cannot open a path with spaces), output identical to the fixture's."""
+    tag = 'ox__10t13'
+    rec = load(tag)
+    d = tmp_path / "dir with space's"
+    d.mkdir()
+    fa = d / 'in put.fa'
+    fa.write_bytes(open(os.path.join(FIX, f'{tag}.fa'), 'rb').read())
+    out = d / 'o.msa'
+    cli = os.path.join(ROOT, 'mlprobs_amd', 'cli')
+    r = subprocess.run([BIN, '-q', '--cpnp', os.path.join(cli, 'c_p_np_aln'), '--quickprobs',
+                        os.path.join(cli, 'quickprobs'), '--tmp', str(d), str(fa), str(out)],
+                       capture_output=True, timeout=600, env=dict(ENV, MLP_HOST_MAX_CELLS='1e12'))
+    assert r.returncode == 0, r.stderr.decode()
+    assert out.read_text(encoding='latin-1') == rec['final']
+
+
+def test_ragged_realignment_raises_like_reference(tmp_path):
+    """getAvgColScore indexes every row at every column of the last row
+    (calculate_column_scores.py:106-112): a realigned region whose rows are
+    ragged raises IndexError in the reference, and MLProbs.py ends without an
+    output file.  A stand-in realigner that prints a ragged MSA must make
+    mlprobs fail the same way (exit 1, no output)."""
+    tag = 'ox__10t13'
+    fake = tmp_path / 'ragged_qp.sh'
+    fake.write_text('#!/bin/sh\nprintf ">a\\nAC-D\\n>b\\nACD\\n>c\\nA-CDE\\n"\n')
+    fake.chmod(0o755)
+    out = tmp_path / 'o.msa'
+    cp = os.path.join(ROOT, 'mlprobs_amd', 'cli', 'c_p_np_aln')
+    r = subprocess.run([BIN, '-q', '--cpnp', cp, '--quickprobs', str(fake), '--tmp', str(tmp_path),
+                        os.path.join(FIX, f'{tag}.fa'), str(out)], capture_output=True, timeout=600,
+                       env=dict(ENV, MLP_HOST_MAX_CELLS='1e12'))
+    assert r.returncode == 1, r.stderr.decode()
+    assert b'IndexError' in r.stderr
+    assert not out.exists()
