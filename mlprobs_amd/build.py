@@ -39,11 +39,15 @@ def variant_path(name):
     return os.path.join(LIBDIR, f'libmlpgpu_{name}.so')
 
 
-def build(force=False, verbose=False, variant=None, defines=()):
+def build(force=False, verbose=False, variant=None, defines=(), src_root=None):
     """Build the library; `variant` builds an experiment copy
     lib/libmlpgpu_<variant>.so with extra -D defines (loaded when
-    MLP_LIB_VARIANT=<variant>; never the default)."""
+    MLP_LIB_VARIANT=<variant>; never the default), optionally from another
+    source tree `src_root` (its csrc/ and include/, e.g. a git revision
+    exported by tools/build_variants.py --rev, for same-call A/Bs)."""
     out = variant_path(variant) if variant else LIB
+    csrc = os.path.join(src_root, 'mlprobs_amd', 'csrc') if src_root else CSRC
+    inc = os.path.join(src_root, 'include') if src_root else os.path.join(ROOT, 'include')
     if not variant and not force and not _stale():
         return LIB
     os.makedirs(LIBDIR, exist_ok=True)
@@ -52,12 +56,12 @@ def build(force=False, verbose=False, variant=None, defines=()):
     # independent translation units), then one link
     objdir = os.path.join(HERE, '_build', variant or 'default')
     os.makedirs(objdir, exist_ok=True)
-    base = [HIPCC] + FLAGS + extra + ['-D' + d for d in defines] + ['-I', os.path.join(ROOT, 'include')]
+    base = [HIPCC] + FLAGS + extra + ['-D' + d for d in defines] + ['-I', inc]
     procs, objs = [], []
     for f in SOURCES:
         obj = os.path.join(objdir, f + '.o')
         objs.append(obj)
-        cmd = base + ['-c', os.path.join(CSRC, f), '-o', obj]
+        cmd = base + ['-c', os.path.join(csrc, f), '-o', obj]
         if verbose:
             print(' '.join(cmd))
         procs.append(subprocess.Popen(cmd))

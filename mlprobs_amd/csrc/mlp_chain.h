@@ -20,7 +20,7 @@ template <bool H> struct LdsHmmPart {
   float match[26 * 26];
 };
 template <> struct LdsHmmPart<false> {};
-template <bool P> struct LdsPfPart { double sub[26 * 26]; };
+template <bool P> struct LdsPfPart { double sub[26 * 26], rsub[26 * 26]; };
 template <> struct LdsPfPart<false> {};
 template <bool H, bool P>
 struct LdsTablesT : LdsHmmPart<H>, LdsPfPart<P> {
@@ -33,7 +33,10 @@ template <bool H, bool P>
 __device__ __forceinline__ void stage_tables(LdsTablesT<H, P>& L, const Tables* __restrict__ tab) {
   for (int k = threadIdx.x; k < 26 * 26; k += blockDim.x) {
     if constexpr (H) L.match[k] = tab->match[k];
-    if constexpr (P) L.sub[k] = tab->sub[k];
+    if constexpr (P) {
+      L.sub[k] = tab->sub[k];
+      L.rsub[k] = tab->rsub[k];
+    }
   }
   if (threadIdx.x < 26) L.ins[threadIdx.x] = tab->ins[threadIdx.x];
   if constexpr (H) {
@@ -70,13 +73,15 @@ __device__ __forceinline__ void wave_sync_lds() {
 }
 
 // ---------------------------------------------------------------- chains
-// LDS copy of one chain member's bookkeeping (64 bytes).
+// LDS copy of one chain member's bookkeeping (80 bytes).
 struct ChainPair {
   int L1, L2, row0, roff, coff, slot;
   float T5, TL;      // merge: pair totals
   int64_t rm, ell;   // local-chain base, first ELL row
   double zmant;      // backward: PF total
   int zexp, pad;
+  double rzmant;     // backward: 1 / zmant
+  double pad2;
 };
 // each wave's LDS region: the members' bookkeeping (count + 1 entries),
 // then the residues (chain_lds_pack)
@@ -127,10 +132,11 @@ __device__ ChainView stage_chain(uint8_t* dyn, int lds_seq, int64_t ch, SeqSet s
     ChainPair c;
     c.L1 = L1; c.L2 = L2; c.row0 = pm.row0[slot]; c.roff = roff; c.coff = roff + L1 + 2; c.slot = slot;
     c.T5 = 0.f; c.TL = 0.f; c.rm = pm.rm_off[slot]; c.ell = pm.ell_row[slot];
-    c.zmant = 1.0; c.zexp = 0; c.pad = 0;
+    c.zmant = 1.0; c.zexp = 0; c.pad = 0; c.rzmant = 1.0; c.pad2 = 0.0;
     if constexpr (KIND == kStageBwd) {
       c.zmant = rec[slot].zmant;
       c.zexp = rec[slot].zexp;
+      c.rzmant = 1.0 / c.zmant;
     }
     if constexpr (KIND == kStageMerge) {
       // CPNP/ProbabilisticModel.h:405-454: T = (T_fwd + T_bwd) / 2; the
@@ -174,7 +180,7 @@ struct Cursor {
   int slot;
   int64_t rm, ell;
   float T5, TL;
-  double zmant;
+  double zmant, rzmant;
   int zexp;
 };
 
@@ -200,6 +206,7 @@ __device__ __forceinline__ void locate(Cursor& c, const ChainView& C, const floa
   c.T5 = m.T5;
   c.TL = m.TL;
   c.zmant = m.zmant;
+  c.rzmant = m.rzmant;
   c.zexp = m.zexp;
   c.c1 = C.seq[m.roff + c.i];
   c.c1n = C.seq[m.roff + c.i + 1];

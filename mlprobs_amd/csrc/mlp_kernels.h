@@ -65,6 +65,7 @@ struct Tables {
   float match[26 * 26];   // matchProb['A'+r]['A'+c]
   float ins[26];          // insProb['A'+r][*]
   double sub[26 * 26];    // PF score factor, [seq2 letter][seq1 letter]
+  double rsub[26 * 26];   // 1 / sub (correctly rounded; the PF backward's posterior quotient)
 };
 
 // Per-pair bookkeeping of one batch (device arrays indexed by slot; slots

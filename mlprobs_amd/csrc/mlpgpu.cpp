@@ -350,6 +350,7 @@ static void build_tables(Tables& T, ModelScalars& ms, float delta, bool qp = fal
     ms.pf_open = mlp_qp_pf_open;
     ms.pf_ext = mlp_qp_pf_extend;
   }
+  for (int k = 0; k < 26 * 26; k++) T.rsub[k] = 1.0 / T.sub[k];
   // CPNP/ProbabilisticModel.h:1068-1070: LOG(0.6080327034), LOG(0.1959836632) x 2
   ms.vit_init[0] = logf(0.6080327034f);
   ms.vit_init[1] = logf(0.1959836632f);
@@ -1139,7 +1140,17 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
   // compaction into the store) before batch b + 1 reuses the scratch.
   const bool two = getenv("MLP_TWO") && atoi(getenv("MLP_TWO")) > 0;  // experiment hook
   const SideStream* side = (two || getenv("MLP_NO_SIDE")) ? nullptr : &c->side;  // MLP_NO_SIDE: experiment hook
-  size_t batch_target = batch_target_for(c, p0, p1, pair_bytes, two ? c->scratch_budget / 2 : 0);
+  // k_local_totals: persistent waves, each with 64 candidate rows as wide as
+  // the family's widest chain row (<= 1 GB of lists), sized once per call so
+  // every batch carves the same bytes (no reallocation between batches) and
+  // counted inside the scratch budget
+  const int tot_row = (chain_width(c->max_len) + 15) & ~15;
+  int tot_waves = (int)std::max<int64_t>(64, std::min<int64_t>(kTotalsWaves, (int64_t)(1LL << 30) / (64LL * tot_row * 4)));
+  tot_waves = (tot_waves + kWavesPerBlock - 1) / kWavesPerBlock * kWavesPerBlock;  // whole workgroups
+  const size_t clist_bytes = (models & kLocal) ? (size_t)tot_waves * 64 * tot_row * 4 : 0;
+  auto budget_for = [&](size_t b) { return std::max<size_t>(b > clist_bytes ? b - clist_bytes : 0, 32u << 20); };
+  size_t batch_target =
+      batch_target_for(c, p0, p1, pair_bytes, budget_for(two ? c->scratch_budget / 2 : c->scratch_budget));
   int64_t all_cells = 0, done_cells = 0;
   for (int64_t k = p0; k < p1; k++) all_cells += pair_cost_cells(c, k);
   const int64_t base_total = c->store_total;
@@ -1233,21 +1244,13 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
     hipStream_t st = streams[slot];
     const int64_t np = P.np, nch = P.nch;
     // ---- carve scratch
-    // k_local_totals: persistent waves, each with 64 candidate rows of the
-    // batch's widest row (at most ~1 GB of lists)
-    int tot_row = 16;
-    for (int64_t h = 0; h < P.nch; h++) tot_row = std::max(tot_row, P.width[h]);
-    tot_row = (tot_row + 15) & ~15;
-    int tot_waves = (int)std::max<int64_t>(
-        64, std::min<int64_t>({(int64_t)kTotalsWaves, P.np, (int64_t)(1LL << 30) / (64LL * tot_row * 4)}));
-    tot_waves = (tot_waves + kWavesPerBlock - 1) / kWavesPerBlock * kWavesPerBlock;  // whole workgroups
     Carver cv;
     const bool h5 = models & kHmm5, lo = models & kLocal, pf = models & kPF;
     const size_t o_f5 = cv.take(h5 ? P.cells * 4 : 0), o_fl = cv.take(lo ? P.cells * 4 : 0),
                  o_bl = cv.take(lo ? P.cells * 4 : 0), o_pg = cv.take(pf && !pg_in_zm ? P.cells * 4 : 0),
                  o_zm = cv.take(pf ? P.cells * 8 : 0), o_cmf = cv.take(lo ? P.rm_total * 4 : 0),
                  o_cmb = cv.take(lo ? P.rm_total * 4 : 0),
-                 o_tn = cv.take(lo ? 256 : 0), o_cl = cv.take(lo ? (size_t)tot_waves * 64 * tot_row * 4 : 0),
+                 o_tn = cv.take(lo ? 256 : 0), o_cl = cv.take(clist_bytes),
                  o_b5 = cv.take(P.bnd * 20), o_bnl = cv.take(P.bnd * 12), o_bz = cv.take(P.bnd * 24),
                  o_be = cv.take(P.bnd * 4), o_bm = cv.take(P.bnd * 4), o_bc = cv.take(P.bnd * 4), o_ec = cv.take(P.ell_rows * kEll * 2),
                  o_ev = cv.take(P.ell_rows * kEll * 4), o_en = cv.take(P.ell_rows * 4),
@@ -1256,7 +1259,8 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
     if ((rc = ensure(c, *scr[slot], cv.off))) {
       if (rc != MLP_ERR_MEMORY || c->scratch_budget < (64u << 20)) return rc;
       c->scratch_budget /= 2;  // the device is shared: plan smaller batches and retry
-      batch_target = batch_target_for(c, p, p1, pair_bytes, two ? c->scratch_budget / 2 : 0);
+      batch_target =
+          batch_target_for(c, p, p1, pair_bytes, budget_for(two ? c->scratch_budget / 2 : c->scratch_budget));
       continue;
     }
     char* base = (char*)scr[slot]->p;

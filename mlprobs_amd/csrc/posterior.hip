@@ -260,18 +260,24 @@ __global__ __launch_bounds__(256, SweepWaves<M>::fwd) void k_forward(ModelScalar
             double uZm = UZm, uZe = UZe, uZf = UZf, dZm = DZm, dZe = DZe, dZf = DZf;
             double lZm = LZm, lZe = LZe, lZf = LZf;
             E = pf_align_fast(uZm, uZe, uZf, Ue, dZm, dZe, dZf, De, lZm, lZe, lZf, Le);
-            const double o0 = (j == L2) ? 1.0 : pfo, e0 = (j == L2) ? 1.0 : pfe;
-            const double o1 = (i == L1) ? 1.0 : pfo, e1 = (i == L1) ? 1.0 : pfe;
-            Ze = uZm * o0 + uZe * e0;
-            Zf = lZm * o1 + lZf * e1;
+            // the last column / row use factors 1.0 (x * 1.0 + y * 1.0 ==
+            // x + y exactly): both forms computed, one selected -- no
+            // per-lane selects of the factors themselves
+            const double ze_g = uZm * pfo + uZe * pfe, ze_1 = uZm + uZe;
+            const double zf_g = lZm * pfo + lZf * pfe, zf_1 = lZm + lZf;
+            Ze = (j == L2) ? ze_1 : ze_g;
+            Zf = (i == L1) ? zf_1 : zf_g;
             // QuickProbs' Ze/Zf are ours transposed (QP/PartitionFunction.cpp:128-130)
             Zm = ((M & kQP) != 0 ? (dZm + dZf) + dZe : (dZm + dZe) + dZf) * score;
             pf_rescale_fast(Zm, Ze, Zf, E);
           }
           sc.zm[idx] = mlp_pf_pack(Zm, E);
           if (act) {
-            // QuickProbs' plain double has no such stop; frames past 2^50000 are ours
-            if ((M & kQP) != 0 ? E > 250 : mlp_pf_ldbl_overflow(Zm, Ze, Zf, E)) atomicOr(&rec[c.slot].flags, 1);
+            // QuickProbs' plain double has no such stop; frames past 2^50000 are
+            // ours.  Frames reach 81 (2^16200) only near overflow: the
+            // three-way maximum runs only when some lane's frame got there
+            if (!wave_none(E > ((M & kQP) != 0 ? 250 : 80)))
+              if ((M & kQP) != 0 ? E > 250 : mlp_pf_ldbl_overflow(Zm, Ze, Zf, E)) atomicOr(&rec[c.slot].flags, 1);
             if (i == L1 && j == L2) {  // CPNP/MSAPartProbs.cpp:591,612; QP/PartitionFunction.cpp:132,155
               rec[c.slot].zmant = (M & kQP) != 0 ? (Zm + Zf) + Ze : (Zm + Ze) + Zf;
               rec[c.slot].zexp = E;
@@ -470,7 +476,7 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
             double nZm = NZm, nZe = NZe, nZf = NZf, rZm = RZm, rZe = RZe, rZf = RZf;
             double gZm = GZm, gZe = GZe, gZf = GZf;
             int ne = Ne, re = Re, ge = Ge;
-            double o0 = pfo, e0 = pfe, o1 = pfo, e1 = pfe;
+            const double o0 = pfo, e0 = pfe, o1 = pfo, e1 = pfe;
             // boundary row L1+1 / column L2+1 (init of CPNP/MSAPartProbs.cpp:217-226)
             if (i == L1) { nZm = 0.0; nZf = 1.0; nZe = 0.0; ne = 0; }
             if (j == L2) { rZm = 0.0; rZf = 0.0; rZe = 1.0; re = 0; }
@@ -480,17 +486,26 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
             } else if (i == L1) {
               gZm = 0.0; gZf = 1.0; gZe = 0.0; ge = 0;
             }
-            if (j == 1) { o0 = 1.0; e0 = 1.0; }
-            if (i == 1) { o1 = 1.0; e1 = 1.0; }
             E = pf_align_fast(nZm, nZe, nZf, ne, rZm, rZe, rZf, re, gZm, gZe, gZf, ge);
-            Zf = rZm * o1 + rZf * e1;
-            Ze = nZm * o0 + nZe * e0;
+            // first row / column: factors 1.0 (x * 1.0 + y * 1.0 == x + y)
+            const double zf_g = rZm * o1 + rZf * e1, zf_1 = rZm + rZf;
+            const double ze_g = nZm * o0 + nZe * e0, ze_1 = nZm + nZe;
+            Zf = (i == 1) ? zf_1 : zf_g;
+            Ze = (j == 1) ? ze_1 : ze_g;
             Zm = ((M & kQP) != 0 ? (gZm + gZe) + gZf : (gZm + gZf) + gZe) * score;  // QP/PartitionFunction.cpp:260
             pf_rescale_fast(Zm, Ze, Zf, E);
             if (act) {
               int ef;
               const double zf = mlp_pf_unpack(zmv, &ef);
-              const double qv = (zf * Zm) / (score * c.zmant);
+              // C_P_NP_Aln (long double in the reference, parity within 1e-4):
+              // the quotient as products with the factor's and the total's
+              // reciprocals (a few fp64 ulps from the division); QuickProbs
+              // (plain double, bit-exact) divides like the reference
+              double qv;
+              if constexpr ((M & kQP) != 0)
+                qv = (zf * Zm) / (score * c.zmant);
+              else
+                qv = (zf * Zm) * (T_.rsub[c2 * 26 + c1] * c.rzmant);
               post = (float)ldexp(qv, MLP_PF_STEP * (ef + E - c.zexp));
               // QuickProbs stores only probabilities in [0.001, 1] (QP/PartitionFunction.cpp:266-272)
               if constexpr ((M & kQP) != 0) post = (post <= 1.0f && post >= 0.001f) ? post : 0.0f;

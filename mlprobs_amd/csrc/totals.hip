@@ -212,7 +212,12 @@ __global__ __launch_bounds__(256) void k_local_totals(ModelScalars ms, const Tab
     const uint8_t* s1 = sq.res + sq.off[pm.pa[p]];
     const uint8_t* s2 = sq.res + sq.off[pm.pb[p]];
     const int64_t rm = pm.rm_off[p];
+#ifdef MLP_EXP_TOT_NOFOLD  // timing experiment: the listing pass alone (local posteriors then read as 0)
+    float tf = local_fwd_fold<false>(sc.cmf + rm, sc.fl, L1, L2, row0, W, cell_off, lk, region, sc.clist_row, lane);
+    tf = tf == 12345.f ? 0.f : 1e30f;
+#else
     float tf = local_fwd_fold(sc.cmf + rm, sc.fl, L1, L2, row0, W, cell_off, lk, region, sc.clist_row, lane);
+#endif
     float tb = fold_chunks<true>(LZ, 0, (int64_t)L1 * local_chunks(L2), sc.cmb + rm, sc.bl, L2, row0, W, cell_off, s1,
                                  s2, match, ins, 2 * ms.rt1, lk, lane);
 #ifdef MLP_EXP_TOT_STRM2  // the forward streaming pass twice (no second fold)
