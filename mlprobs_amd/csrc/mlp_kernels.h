@@ -125,6 +125,14 @@ struct Scratch {
   float* clist;
   int32_t clist_row;
   int32_t* tot_next;
+  // lane-per-pair forward chain fold (k_local_bounds / k_local_list /
+  // k_local_fold): per ELL row, the chain's lower bound at the row's start
+  // (the exact fold of the chunk maxima of the rows before); the per-row
+  // candidate counts go to ell_cnt until the merge overwrites it; pairs
+  // whose bound failed the fold's check are listed in rep ([0] = count) for
+  // k_local_totals to redo
+  float* crb;
+  int32_t* rep;
   float* bnd5;             // chain boundary row: 5 floats per column
   float* bndl;             // 3 floats per column
   double* bndz;            // 3 doubles per column
@@ -185,6 +193,12 @@ hipError_t launch_backward(int models, const ModelScalars& ms, const Tables* tab
                            int lds_seq, int64_t npairs, hipStream_t st, const SideStream* side);
 hipError_t launch_local_totals(const ModelScalars& ms, const Tables* tab, SeqSet seqs, PairMeta pm, ChainMeta cm,
                                PairRec* rec, Scratch sc, int64_t npairs, int nwaves, hipStream_t st);
+// The same totals with the forward chain folded one pair per lane (models
+// with the partition function: the candidates go to the dead PF forward Zm
+// slots): bounds, listing + backward chain, fold, repair of failed bounds.
+hipError_t launch_local_totals_lanefold(const ModelScalars& ms, const Tables* tab, SeqSet seqs, PairMeta pm,
+                                        ChainMeta cm, PairRec* rec, Scratch sc, int64_t npairs, int nwaves,
+                                        hipStream_t st);
 // resident waves of k_local_totals (persistent: each takes pairs off a counter)
 constexpr int kTotalsWaves = 8192;
 // chunk maxima per pair row (columns 1..L2 in chunks of 64)

@@ -1130,7 +1130,7 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
     const int64_t rmc = (models & kLocal) ? (int64_t)L1 * local_chunks(L2) : 0;
     return (size_t)(pair_slots_bound(c, q) * slot_bytes + rmc * 8) +
            (size_t)pair_width_bound(c, q) * (5 * 4 + 3 * 4 + 3 * 8 + 4 + 4 + 4) +
-           (size_t)L1 * (kEll * 6 + 4) + kPerSlotMeta;
+           (size_t)L1 * (kEll * 6 + 4 + 4) + 4 + kPerSlotMeta;  // + the lane fold's row bounds, repair slot
   };
   // Batches run one after another on the context stream (two batches
   // alternating over two streams with half the scratch each measured slower
@@ -1148,6 +1148,16 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
   int tot_waves = (int)std::max<int64_t>(64, std::min<int64_t>(kTotalsWaves, (int64_t)(1LL << 30) / (64LL * tot_row * 4)));
   tot_waves = (tot_waves + kWavesPerBlock - 1) / kWavesPerBlock * kWavesPerBlock;  // whole workgroups
   const size_t clist_bytes = (models & kLocal) ? (size_t)tot_waves * 64 * tot_row * 4 : 0;
+  // the forward local chain folded one pair per lane (k_local_fold) when the
+  // PF forward Zm slots are dead by then (the partition function ran, and
+  // both backward sweeps joined before the totals); MLP_TOT_LANEFOLD=0 / 1
+  // forces the one-wave-per-pair fold / this
+#ifndef MLP_TOT_LANEFOLD_DEFAULT
+#define MLP_TOT_LANEFOLD_DEFAULT 0
+#endif
+  static const char* lf_env = getenv("MLP_TOT_LANEFOLD");
+  const bool lanefold = (models & kLocal) && (models & kPF) && (!side || side->join_mode == 0) &&
+                        (lf_env ? atoi(lf_env) != 0 : MLP_TOT_LANEFOLD_DEFAULT != 0);
   auto budget_for = [&](size_t b) { return std::max<size_t>(b > clist_bytes ? b - clist_bytes : 0, 32u << 20); };
   size_t batch_target =
       batch_target_for(c, p0, p1, pair_bytes, budget_for(two ? c->scratch_budget / 2 : c->scratch_budget));
@@ -1251,6 +1261,7 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
                  o_zm = cv.take(pf ? P.cells * 8 : 0), o_cmf = cv.take(lo ? P.rm_total * 4 : 0),
                  o_cmb = cv.take(lo ? P.rm_total * 4 : 0),
                  o_tn = cv.take(lo ? 256 : 0), o_cl = cv.take(clist_bytes),
+                 o_crb = cv.take(lanefold ? P.ell_rows * 4 : 0), o_rep = cv.take(lanefold ? (np + 1) * 4 : 0),
                  o_b5 = cv.take(P.bnd * 20), o_bnl = cv.take(P.bnd * 12), o_bz = cv.take(P.bnd * 24),
                  o_be = cv.take(P.bnd * 4), o_bm = cv.take(P.bnd * 4), o_bc = cv.take(P.bnd * 4), o_ec = cv.take(P.ell_rows * kEll * 2),
                  o_ev = cv.take(P.ell_rows * kEll * 4), o_en = cv.take(P.ell_rows * 4),
@@ -1276,6 +1287,8 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
     sc.clist = (float*)(base + o_cl);
     sc.clist_row = tot_row;
     sc.tot_next = (int32_t*)(base + o_tn);
+    sc.crb = (float*)(base + o_crb);
+    sc.rep = (int32_t*)(base + o_rep);
     sc.bnd5 = (float*)(base + o_b5);
     sc.bndl = (float*)(base + o_bnl);
     sc.bndz = (double*)(base + o_bz);
@@ -1305,7 +1318,10 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
     }
     if (models & kLocal) {
       Timer t(c, KTOT, bcells, st);
-      HIPCHK(c, launch_local_totals(ms, c->d_tables, seqs, pm, cm, d_rec, sc, np, tot_waves, st));
+      if (lanefold)
+        HIPCHK(c, launch_local_totals_lanefold(ms, c->d_tables, seqs, pm, cm, d_rec, sc, np, tot_waves, st));
+      else
+        HIPCHK(c, launch_local_totals(ms, c->d_tables, seqs, pm, cm, d_rec, sc, np, tot_waves, st));
       EXP_SYNC("totals");
     }
     if (side && side->join_mode != 0) HIPCHK(c, hipStreamWaitEvent(st, side->join, 0));  // deferred join

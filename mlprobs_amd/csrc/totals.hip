@@ -4,6 +4,8 @@
 // wave; no wavefront).
 #include <stdio.h>
 
+#include <algorithm>
+
 #include "mlp_kernels.h"
 #include "mlp_numerics.h"
 
@@ -147,7 +149,11 @@ __device__ __forceinline__ float local_fwd_fold(const float* __restrict__ cmf, c
         const int j = t0 + u - lane;
         if (row_in && j >= 1 && j <= L2) {
           if (!(run - x[u] >= 7.5f)) {
+#ifdef MLP_EXP_TOT_NOSTORE  // timing experiment: count the candidates, store nothing
+            cnt++;
+#else
             mine[cnt++] = x[u];
+#endif
           }
           run = fmaxf(run, x[u]);
         }
@@ -185,10 +191,11 @@ __device__ __forceinline__ float local_fwd_fold(const float* __restrict__ cmf, c
 }
 
 // Persistent: gridDim.x * 4 waves, each taking pairs off Scratch::tot_next
-// until none is left (every wave reaches the exit).
+// until none is left (every wave reaches the exit).  With `only` (the
+// lane-fold path's repair list: [0] = count, then slots) just those pairs.
 __global__ __launch_bounds__(256) void k_local_totals(ModelScalars ms, const Tables* __restrict__ tab, SeqSet sq,
                                                       PairMeta pm, ChainMeta cm, PairRec* __restrict__ rec,
-                                                      Scratch sc, int64_t npairs) {
+                                                      Scratch sc, int64_t npairs, const int32_t* __restrict__ only) {
   __shared__ float4 lk[kLookupRows];
   __shared__ float match[26 * 26], ins[26];
   if (threadIdx.x == 0) mlp_lookup_table(lk);
@@ -204,7 +211,9 @@ __global__ __launch_bounds__(256) void k_local_totals(ModelScalars ms, const Tab
     const int got = atomicAdd(sc.tot_next, lane == 0 ? 1 : 0);
     return __builtin_amdgcn_readfirstlane(got);
   };
-  for (int64_t p = take(); p < npairs; p = take()) {
+  const int64_t ntask = only ? (int64_t)only[0] : npairs;
+  for (int64_t task = take(); task < ntask; task = take()) {
+    const int64_t p = only ? (int64_t)only[1 + task] : task;
     const int L1 = sq.len[pm.pa[p]], L2 = sq.len[pm.pb[p]];
     const int h = pm.chain[p];
     const int W = cm.width[h], row0 = pm.row0[p];
@@ -229,6 +238,159 @@ __global__ __launch_bounds__(256) void k_local_totals(ModelScalars ms, const Tab
       rec[p].tfl = tf;
       rec[p].tbl = tb;
     }
+  }
+}
+
+// =====================================================================
+// Lane-per-pair forward chain (models with the partition function).  The
+// chain itself is serial, so one wave folding one pair issues ~20 wave
+// instructions per folded element with one useful lane; here 64 pairs share
+// a wave, one per lane, after a listing pass has put each pair's candidates
+// in chain order into its region of the dead PF forward Zm slots.
+//
+// The listing uses a tighter exact skip bound than the running maximum: the
+// chain value at the start of row i is at least the exact LOG_ADD fold of the
+// chunk maxima of the rows before (a subsequence of the chain, in order:
+// folding fewer terms cannot give more, up to LOG_ADD's non-monotonic step
+// at the 7.5 cutoff, ~5.5e-4).  That is checked where it is used: the fold
+// compares each row's bound with the chain value at the row's start, and a
+// pair whose bound exceeded it is redone by k_local_totals (repair list).
+// At C3 the bound lists ~19% of the elements against ~35% for the running
+// maximum (the elements that change the value: ~11%).
+// =====================================================================
+
+// Lane per pair: crb[ell + i - 1] = fold of the chunk maxima of rows 1..i-1.
+__global__ __launch_bounds__(256) void k_local_bounds(SeqSet sq, PairMeta pm, Scratch sc, int64_t npairs) {
+  __shared__ float4 lk[kLookupRows];
+  if (threadIdx.x == 0) mlp_lookup_table(lk);
+  __syncthreads();
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= npairs) return;
+  const int L1 = sq.len[pm.pa[p]], L2 = sq.len[pm.pb[p]];
+  const int nch = local_chunks(L2);
+  const float* __restrict__ cmx = sc.cmf + pm.rm_off[p];
+  float* __restrict__ rb = sc.crb + pm.ell_row[p];
+  float acc = LZ;
+  constexpr int kRow = 8;  // a row's chunk maxima loaded together (L2 <= 512), then folded
+  for (int i = 0; i < L1; ++i) {
+    rb[i] = acc;
+    for (int c0 = 0; c0 < nch; c0 += kRow) {
+      float v[kRow];
+#pragma unroll
+      for (int u = 0; u < kRow; ++u) v[u] = c0 + u < nch ? cmx[(int64_t)i * nch + c0 + u] : LZ;
+#pragma unroll
+      for (int u = 0; u < kRow; ++u) acc = mlp_log_add_t(acc, v[u], lk);  // LOG_ADD(acc, LZ) == acc
+    }
+  }
+}
+
+// Candidate k of pair row i (1-based) in the pair's region of the PF forward
+// Zm slots: slots cell_off + row0 W .. (the pair's own (L1 + 1) W slots),
+// high halves (the low halves may hold the PF posterior, Scratch::pg_stride).
+__device__ __forceinline__ float* lanefold_area(const Scratch& sc, int64_t cell_off, int row0, int W) {
+  return reinterpret_cast<float*>(sc.zm) + 2 * (cell_off + (int64_t)row0 * W) + 1;
+}
+
+// Wave per pair (persistent, as k_local_totals): the backward chain as there,
+// and the forward chain's candidates listed row by row (element x of row i is
+// listed unless max(crb[i], max of the row so far) - x >= 7.5).
+__global__ __launch_bounds__(256) void k_local_list(ModelScalars ms, const Tables* __restrict__ tab, SeqSet sq,
+                                                    PairMeta pm, ChainMeta cm, PairRec* __restrict__ rec,
+                                                    Scratch sc, int64_t npairs) {
+  __shared__ float4 lk[kLookupRows];
+  __shared__ float match[26 * 26], ins[26];
+  if (threadIdx.x == 0) mlp_lookup_table(lk);
+  for (int k = threadIdx.x; k < 26 * 26; k += blockDim.x) match[k] = tab->match[k];
+  if (threadIdx.x < 26) ins[threadIdx.x] = tab->ins[threadIdx.x];
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  auto take = [&]() -> int64_t {
+    const int got = atomicAdd(sc.tot_next, lane == 0 ? 1 : 0);
+    return __builtin_amdgcn_readfirstlane(got);
+  };
+  for (int64_t p = take(); p < npairs; p = take()) {
+    const int L1 = sq.len[pm.pa[p]], L2 = sq.len[pm.pb[p]];
+    const int h = pm.chain[p];
+    const int W = cm.width[h], row0 = pm.row0[p];
+    const int64_t cell_off = cm.cell_off[h];
+    const int64_t ell = pm.ell_row[p];
+    float* __restrict__ area = lanefold_area(sc, cell_off, row0, W);
+    const int S0 = (row0 + 1) >> 6, S1 = (row0 + L1) >> 6;
+    const int tend = L2 + 63;
+    for (int S = S0; S <= S1; ++S) {
+      const int i = 64 * S + lane - row0;
+      const bool row_in = i >= 1 && i <= L1;
+      float run = row_in ? sc.crb[ell + i - 1] : LZ;
+      float* __restrict__ mine = area + 2 * (int64_t)(row_in ? i - 1 : 0) * L2;
+      int cnt = 0;
+      const float* slab = sc.fl + cell_off + ((int64_t)W * S + 1) * 64 + lane;
+      for (int t0 = 1; t0 <= tend; t0 += 8) {
+        float x[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) x[u] = (t0 + u <= tend) ? slab[(int64_t)(t0 + u) * 64] : LZ;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int j = t0 + u - lane;
+          if (row_in && j >= 1 && j <= L2) {
+            if (!(run - x[u] >= 7.5f)) mine[2 * cnt++] = x[u];
+            run = fmaxf(run, x[u]);
+          }
+        }
+      }
+      if (row_in) sc.ell_cnt[ell + i - 1] = cnt;
+    }
+    const int64_t rm = pm.rm_off[p];
+    const uint8_t* s1 = sq.res + sq.off[pm.pa[p]];
+    const uint8_t* s2 = sq.res + sq.off[pm.pb[p]];
+    const float tb = fold_chunks<true>(LZ, 0, (int64_t)L1 * local_chunks(L2), sc.cmb + rm, sc.bl, L2, row0, W, cell_off,
+                                       s1, s2, match, ins, 2 * ms.rt1, lk, lane);
+    if (lane == 0) rec[p].tbl = tb;
+  }
+}
+
+// Lane per pair: the forward chain over the listed candidates, rows in
+// lockstep across the wave (row i of every lane's pair in the same outer
+// iteration); the next group of four candidates is loaded while the current
+// one folds.  LOG_ADD(acc, x) == acc whenever acc - x >= 7.5, and LOG_ADD(acc,
+// LOG_ZERO) == acc: every listed element and the padding fold unconditionally.
+__global__ __launch_bounds__(256) void k_local_fold(SeqSet sq, PairMeta pm, ChainMeta cm, PairRec* __restrict__ rec,
+                                                    Scratch sc, int64_t npairs) {
+  __shared__ float4 lk[kLookupRows];
+  if (threadIdx.x == 0) mlp_lookup_table(lk);
+  __syncthreads();
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= npairs) return;
+  const int L1 = sq.len[pm.pa[p]], L2 = sq.len[pm.pb[p]];
+  const int h = pm.chain[p];
+  const float* __restrict__ area = lanefold_area(sc, cm.cell_off[h], pm.row0[p], cm.width[h]);
+  const int64_t ell = pm.ell_row[p];
+  float acc = LZ;
+  bool bad = false;
+  int n = sc.ell_cnt[ell];
+  float rb = sc.crb[ell];
+  for (int i = 1; i <= L1; ++i) {
+    const float* __restrict__ src = area + 2 * (int64_t)(i - 1) * L2;
+    // the next row's count and bound, loaded ahead
+    const int n_next = i < L1 ? sc.ell_cnt[ell + i] : 0;
+    const float rb_next = i < L1 ? sc.crb[ell + i] : LZ;
+    bad |= rb > acc;  // the listing's bound must not exceed the chain at the row's start
+    float x0 = 0 < n ? src[0] : LZ, x1 = 1 < n ? src[2] : LZ, x2 = 2 < n ? src[4] : LZ, x3 = 3 < n ? src[6] : LZ;
+    for (int k = 0; k < n; k += 4) {
+      const float y0 = k + 4 < n ? src[2 * (k + 4)] : LZ, y1 = k + 5 < n ? src[2 * (k + 5)] : LZ;
+      const float y2 = k + 6 < n ? src[2 * (k + 6)] : LZ, y3 = k + 7 < n ? src[2 * (k + 7)] : LZ;
+      acc = mlp_log_add_t(acc, x0, lk);
+      acc = mlp_log_add_t(acc, x1, lk);
+      acc = mlp_log_add_t(acc, x2, lk);
+      acc = mlp_log_add_t(acc, x3, lk);
+      x0 = y0; x1 = y1; x2 = y2; x3 = y3;
+    }
+    n = n_next;
+    rb = rb_next;
+  }
+  rec[p].tfl = acc;
+  if (bad) {
+    const int k = atomicAdd(&sc.rep[0], 1);
+    sc.rep[1 + k] = (int32_t)p;
   }
 }
 
@@ -313,7 +475,28 @@ hipError_t launch_local_totals(const ModelScalars& ms, const Tables* tab, SeqSet
   if (e != hipSuccess) return e;
   if (nwaves % kWavesPerBlock) return hipErrorInvalidValue;  // every wave owns a list region
   hipLaunchKernelGGL(k_local_totals, wave_grid(nwaves), dim3(64 * kWavesPerBlock), 0, st, ms, tab, seqs, pm, cm, rec,
-                     sc, npairs);
+                     sc, npairs, (const int32_t*)nullptr);
+  return hipGetLastError();
+}
+
+hipError_t launch_local_totals_lanefold(const ModelScalars& ms, const Tables* tab, SeqSet seqs, PairMeta pm,
+                                        ChainMeta cm, PairRec* rec, Scratch sc, int64_t npairs, int nwaves,
+                                        hipStream_t st) {
+  if (npairs <= 0) return hipSuccess;
+  if (nwaves % kWavesPerBlock) return hipErrorInvalidValue;
+  hipError_t e;
+  if ((e = hipMemsetAsync(sc.rep, 0, sizeof(int32_t), st)) != hipSuccess) return e;
+  const dim3 lanes((unsigned)((npairs + 255) / 256));
+  hipLaunchKernelGGL(k_local_bounds, lanes, dim3(256), 0, st, seqs, pm, sc, npairs);
+  if ((e = hipMemsetAsync(sc.tot_next, 0, sizeof(int32_t), st)) != hipSuccess) return e;
+  hipLaunchKernelGGL(k_local_list, wave_grid(nwaves), dim3(64 * kWavesPerBlock), 0, st, ms, tab, seqs, pm, cm, rec, sc,
+                     npairs);
+  hipLaunchKernelGGL(k_local_fold, lanes, dim3(256), 0, st, seqs, pm, cm, rec, sc, npairs);
+  // pairs whose bound failed (normally none: the waves find an empty list
+  // and exit) are redone with the running-maximum bound
+  if ((e = hipMemsetAsync(sc.tot_next, 0, sizeof(int32_t), st)) != hipSuccess) return e;
+  hipLaunchKernelGGL(k_local_totals, wave_grid(std::min(nwaves, 1024)), dim3(64 * kWavesPerBlock), 0, st, ms, tab, seqs,
+                     pm, cm, rec, sc, npairs, (const int32_t*)sc.rep);
   return hipGetLastError();
 }
 

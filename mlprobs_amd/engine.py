@@ -195,6 +195,12 @@ class Family:
         self.rp_off = rp
         self._csr = None
 
+    def set_scratch(self, nbytes):
+        """Device bytes the posterior stage may hold as batch scratch
+        (mlp_set_scratch; small budgets mean several batches and the PF
+        posterior in the Zm slots)."""
+        self._chk(self._L.mlp_set_scratch(self._ctx, int(nbytes)))
+
     def _chk(self, rc, ctx=True):
         if rc != 0:
             msg = self._L.mlp_last_error(self._ctx).decode() if ctx else 'context creation failed'

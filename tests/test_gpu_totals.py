@@ -1,0 +1,57 @@
+"""The local-model chain totals two ways (CPNP/ProbabilisticModel.h:435-450:
+one serial, non-associative LOG_ADD chain per pair): one wave per pair with
+the running-maximum skip bound (MLP_TOT_LANEFOLD=0) and one pair per lane
+after a listing pass with the folded chunk-maximum bound (=1, the default
+where the partition function runs).  Both are exact, so the sparse store,
+distances and MEA scores must be bit-identical, at pid 0 and 1 (the models
+with the partition function) on similar and divergent families, and with
+the PF posterior in the Zm slots (small scratch budget) as well.  Each
+setting runs in a child process: the switch is read once per process."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+_CHILD = r'''
+import hashlib, sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+from mlprobs_amd import synth
+from mlprobs_amd.engine import Family
+out = []
+for n, L, s, seed, pid in ((48, 300, 0.7, 31, 0), (40, 260, 0.35, 32, 0), (36, 220, 0.9, 33, 1), (6, 900, 0.6, 34, 0)):
+    seqs = [q for _, q in synth.family(n, L, s, seed=seed)]
+    f = Family(seqs)
+    if len(sys.argv) > 2:
+        f.set_scratch(int(sys.argv[2]))
+    f.posteriors(pid, 0.132548)
+    h = hashlib.sha256()
+    for a in list(f.export()) + list(f.results()):
+        h.update(np.ascontiguousarray(a).tobytes())
+    out.append(h.hexdigest())
+    f.close()
+print(' '.join(out))
+'''
+
+
+def _run(lanefold, scratch=None):
+    env = dict(os.environ, MLP_TOT_LANEFOLD=str(lanefold))
+    args = [sys.executable, '-c', _CHILD, ROOT] + ([str(scratch)] if scratch else [])
+    r = subprocess.run(args, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return r.stdout.split()
+
+
+def test_lanefold_totals_bit_identical():
+    assert _run(1) == _run(0)
+
+
+def test_lanefold_totals_bit_identical_small_scratch():
+    # 1 GB: several batches, the PF posterior in the low halves of the Zm
+    # slots whose high halves hold the candidates
+    assert _run(1, 1 << 30) == _run(0, 1 << 30)
