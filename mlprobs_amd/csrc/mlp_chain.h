@@ -253,13 +253,18 @@ __device__ __forceinline__ void cursor_prev(Cursor& c, const ChainView& C, const
 // stores issued since (vmcnt is in order on gfx9).  Column indices are
 // clamped to the chain's W columns; columns a lane must not use are never
 // consumed by an active cell.
+#ifndef MLP_BND_ROTATE
+#define MLP_BND_ROTATE 1
+#endif
 template <int M>
 struct BoundaryChunks {
   float c5[5], n5[5], cl[3], nl[3];
   double cz[3], nz[3];
   int ce, ne;
-  __device__ __forceinline__ void load_next(const Scratch& sc, int64_t bo, int W, int col0, int lane) {
-    const int64_t bi = bo + min(max(col0 + lane, 0), W - 1);
+  // back: lanes the chunk is loaded shifted up by, so that lane 63 holds the
+  // segment's first column (the backward sweep's partial segments)
+  __device__ __forceinline__ void load_next(const Scratch& sc, int64_t bo, int W, int col0, int lane, int back = 0) {
+    const int64_t bi = bo + min(max(col0 + lane - back, 0), W - 1);
     if constexpr ((M & kHmm5) != 0) {
 #pragma unroll
       for (int k = 0; k < 5; ++k) n5[k] = sc.bnd5[bi * 5 + k];
@@ -283,30 +288,56 @@ struct BoundaryChunks {
   }
   // Neighbour shift of one step: X = src shifted by one lane toward higher
   // lanes (SHR, forward) or lower lanes (backward); the vacated lane (0 / 63)
-  // takes column q of the current chunk when TAKE, else 0 (unused there).
+  // takes the current chunk's column for this step when TAKE, else 0 (unused
+  // there).  The chunk rotates one lane per step (toward lane 0 forward,
+  // toward lane 63 backward), so that column is always in the vacated lane
+  // and enters through the DPP shift's `old` operand: no readlane per value.
+  // TAKE steps of a segment run consecutively from its first column.
+  // (MLP_BND_ROTATE=0: the column read with readlane instead, round 3.)
   template <bool SHR, bool TAKE>
   __device__ __forceinline__ void shift(int q, const float* S5, float* X5, const float* SL, float* XL,
                                         double sZm, double sZe, double sZf, int se,
-                                        double& Zm, double& Ze, double& Zf, int& e) const {
+                                        double& Zm, double& Ze, double& Zf, int& e) {
+#if MLP_BND_ROTATE
+    (void)q;
+#define MLP_BC(c) (c)
+#define MLP_BCD(c) (c)
+#define MLP_BCI(c) (c)
+#else
+#define MLP_BC(c) readlane_f(c, q)
+#define MLP_BCD(c) readlane_d(c, q)
+#define MLP_BCI(c) __builtin_amdgcn_readlane(c, q)
+#endif
     if constexpr ((M & kHmm5) != 0) {
 #pragma unroll
-      for (int k = 0; k < 5; ++k)
-        X5[k] = TAKE ? (SHR ? mlp_shr1(S5[k], readlane_f(c5[k], q)) : mlp_shl1(S5[k], readlane_f(c5[k], q)))
+      for (int k = 0; k < 5; ++k) {
+        X5[k] = TAKE ? (SHR ? mlp_shr1(S5[k], MLP_BC(c5[k])) : mlp_shl1(S5[k], MLP_BC(c5[k])))
                      : (SHR ? mlp_shr1z(S5[k]) : mlp_shl1z(S5[k]));
+        if (TAKE && MLP_BND_ROTATE) c5[k] = SHR ? mlp_shl1z(c5[k]) : mlp_shr1z(c5[k]);
+      }
     }
     if constexpr ((M & kLocal) != 0) {
 #pragma unroll
-      for (int k = 0; k < 3; ++k)
-        XL[k] = TAKE ? (SHR ? mlp_shr1(SL[k], readlane_f(cl[k], q)) : mlp_shl1(SL[k], readlane_f(cl[k], q)))
+      for (int k = 0; k < 3; ++k) {
+        XL[k] = TAKE ? (SHR ? mlp_shr1(SL[k], MLP_BC(cl[k])) : mlp_shl1(SL[k], MLP_BC(cl[k])))
                      : (SHR ? mlp_shr1z(SL[k]) : mlp_shl1z(SL[k]));
+        if (TAKE && MLP_BND_ROTATE) cl[k] = SHR ? mlp_shl1z(cl[k]) : mlp_shr1z(cl[k]);
+      }
     }
     if constexpr ((M & kPF) != 0) {
       if constexpr (TAKE) {
-        Zm = SHR ? mlp_shr1d(sZm, readlane_d(cz[0], q)) : mlp_shl1d(sZm, readlane_d(cz[0], q));
-        Ze = SHR ? mlp_shr1d(sZe, readlane_d(cz[1], q)) : mlp_shl1d(sZe, readlane_d(cz[1], q));
-        Zf = SHR ? mlp_shr1d(sZf, readlane_d(cz[2], q)) : mlp_shl1d(sZf, readlane_d(cz[2], q));
-        const int ee = __builtin_amdgcn_readlane(ce, q);
-        e = SHR ? mlp_shr1i(se, ee) : mlp_shl1i(se, ee);
+        Zm = SHR ? mlp_shr1d(sZm, MLP_BCD(cz[0])) : mlp_shl1d(sZm, MLP_BCD(cz[0]));
+        Ze = SHR ? mlp_shr1d(sZe, MLP_BCD(cz[1])) : mlp_shl1d(sZe, MLP_BCD(cz[1]));
+        Zf = SHR ? mlp_shr1d(sZf, MLP_BCD(cz[2])) : mlp_shl1d(sZf, MLP_BCD(cz[2]));
+        e = SHR ? mlp_shr1i(se, MLP_BCI(ce)) : mlp_shl1i(se, MLP_BCI(ce));
+        if (MLP_BND_ROTATE) {
+#pragma unroll
+          for (int k = 0; k < 3; ++k) cz[k] = SHR ? mlp_shl1zd(cz[k]) : mlp_shr1zd(cz[k]);
+          ce = SHR ? mlp_shl1zi(ce) : mlp_shr1zi(ce);
+        }
+#undef MLP_BC
+#undef MLP_BCD
+#undef MLP_BCI
       } else {
         Zm = SHR ? mlp_shr1zd(sZm) : mlp_shl1zd(sZm);
         Ze = SHR ? mlp_shr1zd(sZe) : mlp_shl1zd(sZe);

@@ -1158,6 +1158,14 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
   static const char* lf_env = getenv("MLP_TOT_LANEFOLD");
   const bool lanefold = (models & kLocal) && (models & kPF) && (!side || side->join_mode == 0) &&
                         (lf_env ? atoi(lf_env) != 0 : MLP_TOT_LANEFOLD_DEFAULT != 0);
+  // the one-wave fold's listing bound: the folded chunk maxima of the rows
+  // before (k_local_bounds) instead of their maximum (MLP_TOT_FOLDBOUND=0 / 1)
+#ifndef MLP_TOT_FOLDBOUND_DEFAULT
+#define MLP_TOT_FOLDBOUND_DEFAULT 1
+#endif
+  static const char* fb_env = getenv("MLP_TOT_FOLDBOUND");
+  const bool foldbound = (models & kLocal) && !lanefold &&
+                         (fb_env ? atoi(fb_env) != 0 : MLP_TOT_FOLDBOUND_DEFAULT != 0);
   auto budget_for = [&](size_t b) { return std::max<size_t>(b > clist_bytes ? b - clist_bytes : 0, 32u << 20); };
   size_t batch_target =
       batch_target_for(c, p0, p1, pair_bytes, budget_for(two ? c->scratch_budget / 2 : c->scratch_budget));
@@ -1261,7 +1269,8 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
                  o_zm = cv.take(pf ? P.cells * 8 : 0), o_cmf = cv.take(lo ? P.rm_total * 4 : 0),
                  o_cmb = cv.take(lo ? P.rm_total * 4 : 0),
                  o_tn = cv.take(lo ? 256 : 0), o_cl = cv.take(clist_bytes),
-                 o_crb = cv.take(lanefold ? P.ell_rows * 4 : 0), o_rep = cv.take(lanefold ? (np + 1) * 4 : 0),
+                 o_crb = cv.take(lanefold || foldbound ? P.ell_rows * 4 : 0),
+                 o_rep = cv.take(lanefold ? (np + 1) * 4 : 0),
                  o_b5 = cv.take(P.bnd * 20), o_bnl = cv.take(P.bnd * 12), o_bz = cv.take(P.bnd * 24),
                  o_be = cv.take(P.bnd * 4), o_bm = cv.take(P.bnd * 4), o_bc = cv.take(P.bnd * 4), o_ec = cv.take(P.ell_rows * kEll * 2),
                  o_ev = cv.take(P.ell_rows * kEll * 4), o_en = cv.take(P.ell_rows * 4),
@@ -1287,7 +1296,7 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
     sc.clist = (float*)(base + o_cl);
     sc.clist_row = tot_row;
     sc.tot_next = (int32_t*)(base + o_tn);
-    sc.crb = (float*)(base + o_crb);
+    sc.crb = lanefold || foldbound ? (float*)(base + o_crb) : nullptr;
     sc.rep = (int32_t*)(base + o_rep);
     sc.bnd5 = (float*)(base + o_b5);
     sc.bndl = (float*)(base + o_bnl);

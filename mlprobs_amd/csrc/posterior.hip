@@ -359,7 +359,11 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
         boundary_fence();
         bc.advance();
         // chunk before (k, m): (k, m-1) or (k-1, last); holds stacked row 64k+64
-        bc.load_next(sc, bo, W, m > 0 ? 64 * (m - 1) : 64 * (nseg - 1), lane);
+        {
+          const int col0 = m > 0 ? 64 * (m - 1) : 64 * (nseg - 1);
+          // that segment's first step is its column min(63, W - 1 - col0): lane 63 holds it
+          bc.load_next(sc, bo, W, col0, lane, MLP_BND_ROTATE ? 63 - min(63, W - 1 - col0) : 0);
+        }
       } else {
         t_lo = -1;
         t_hi = 62;
@@ -605,11 +609,22 @@ __global__ __launch_bounds__(256, MLP_MERGE_WAVES) void k_merge(ModelScalars ms,
         // backward sweep used to do in place
         const float f5v = q5[u], flv = ql[u] + qb[u], pgv = qg[u];
         Dv = Uv;
+        // boundary column t - t_lo in lane 0 of the rotating chunk (BoundaryChunks::shift)
+#if MLP_BND_ROTATE
+        Uv = take_bnd ? mlp_shr1(Lv, bch) : mlp_shr1z(Lv);
+        if (take_bnd) bch = mlp_shl1z(bch);
+        if constexpr (NP) {
+          Dc = Uc;
+          Uc = take_bnd ? mlp_shr1i(Lc, cch) : mlp_shr1zi(Lc);
+          if (take_bnd) cch = mlp_shl1zi(cch);
+        }
+#else
         Uv = take_bnd ? mlp_shr1(Lv, readlane_f(bch, t - t_lo)) : mlp_shr1z(Lv);
         if constexpr (NP) {
           Dc = Uc;
           Uc = take_bnd ? mlp_shr1i(Lc, __builtin_amdgcn_readlane(cch, t - t_lo)) : mlp_shr1zi(Lc);
         }
+#endif
         const bool act = c.q >= 0 && i >= 1 && j >= 1 && j <= L2;
         float P = 0.f;
         if (act) {

@@ -684,6 +684,31 @@ __global__ __launch_bounds__(kRelaxThreads, KP == 5 && kRelaxThreads == 1024 ? 8
     const uint64_t tc0 = clock64();
 #endif
 #ifndef MLP_RELAX_NOCOMPUTE  // (timing experiment: staging only)
+    // per word pair: the load, then the common columns of each word (a single
+    // loop over loads and hits, MLP_RELAX_FLAT in round 4, ran 1.69 s against
+    // 1.21 s: the wave issues both bodies every iteration)
+#define MLP_WALK(pa, pc, we, a0, c0)                                                                  \
+    for (int w = max(a0, c0); w < we; w += 2) {                                                       \
+      const uint2 xa0 = pa[w], xa1 = pa[w + 1], xc0 = pc[w], xc1 = pc[w + 1];                         \
+      uint32_t m0 = xa0.x & xc0.x;                                                                    \
+      uint32_t m1 = w + 1 < we ? xa1.x & xc1.x : 0u;                                                  \
+      while (m0) { /* common columns k, ascending */                                                  \
+        const uint32_t bit = 1u << __builtin_ctz(m0);                                                 \
+        m0 ^= bit;                                                                                    \
+        const float va = QP ? wk * Avals[xa0.y + __popc(xa0.x & (bit - 1u))]                          \
+                            : Avals[xa0.y + __popc(xa0.x & (bit - 1u))];                              \
+        const float vc = Cvals[xc0.y + __popc(xc0.x & (bit - 1u))];                                   \
+        ac += va * vc;                                                                                \
+      }                                                                                               \
+      while (m1) {                                                                                    \
+        const uint32_t bit = 1u << __builtin_ctz(m1);                                                 \
+        m1 ^= bit;                                                                                    \
+        const float va = QP ? wk * Avals[xa1.y + __popc(xa1.x & (bit - 1u))]                          \
+                            : Avals[xa1.y + __popc(xa1.x & (bit - 1u))];                              \
+        const float vc = Cvals[xc1.y + __popc(xc1.x & (bit - 1u))];                                   \
+        ac += va * vc;                                                                                \
+      }                                                                                               \
+    }
     // the cell loop, twice: with every image in LDS, and (GA) for a z where
     // some output image is read in place from HBM (generic loads)
 #define MLP_CELLS(GA) \
@@ -725,28 +750,7 @@ _Pragma("unroll")                                                               
           const float* Avals = (const float*)(ab + z4.x);                                                        \
           const float wk = QP ? zw[cl >> 26] : 1.0f;  /* weight * XZ * ZY (ConsistencyStage.cpp:284) */          \
           float ac = acc[s];                                                                                     \
-          /* two words per step (the second masked off past the overlap) */                                      \
-          for (int w = max(a0, c0); w < we; w += 2) {                                                            \
-            const uint2 xa0 = pa[w], xa1 = pa[w + 1], xc0 = pc[w], xc1 = pc[w + 1];                              \
-            uint32_t m0 = xa0.x & xc0.x;                                                                         \
-            uint32_t m1 = w + 1 < we ? xa1.x & xc1.x : 0u;                                                       \
-            while (m0) {  /* common columns k, ascending */                                                      \
-              const uint32_t bit = 1u << __builtin_ctz(m0);                                                      \
-              m0 ^= bit;                                                                                         \
-              const float va = QP ? wk * Avals[xa0.y + __popc(xa0.x & (bit - 1u))]                               \
-                                  : Avals[xa0.y + __popc(xa0.x & (bit - 1u))];                                   \
-              const float vc = Cvals[xc0.y + __popc(xc0.x & (bit - 1u))];                                        \
-              ac += va * vc;                                                                                     \
-            }                                                                                                    \
-            while (m1) {                                                                                         \
-              const uint32_t bit = 1u << __builtin_ctz(m1);                                                      \
-              m1 ^= bit;                                                                                         \
-              const float va = QP ? wk * Avals[xa1.y + __popc(xa1.x & (bit - 1u))]                               \
-                                  : Avals[xa1.y + __popc(xa1.x & (bit - 1u))];                                   \
-              const float vc = Cvals[xc1.y + __popc(xc1.x & (bit - 1u))];                                        \
-              ac += va * vc;                                                                                     \
-            }                                                                                                    \
-          }                                                                                                      \
+          MLP_WALK(pa, pc, we, a0, c0)                                                                           \
           acc[s] = ac;                                                                                           \
         }                                                                                                        \
         cl = cl1;                                                                                                \
@@ -758,6 +762,7 @@ _Pragma("unroll")                                                               
     }
     if (gmz) MLP_CELLS(true) else MLP_CELLS(false)
 #undef MLP_CELLS
+#undef MLP_WALK
 #endif
 #ifdef MLP_RELAX_TIMING
     {

@@ -110,10 +110,39 @@ __device__ __forceinline__ float fold_chunks(float acc, int64_t kb, int64_t ke, 
 // rows in order: per 64 listed elements, a ballot of those that pass the
 // test against acc, the lowest folded, the ballot renewed (the rest of the
 // list stays in order; an element that stopped passing is skipped, exactly).
+//
+// The row lists are written a whole 64-byte line at a time: each lane keeps
+// the latest listed elements of its row in LDS (`lbuf`, this wave's
+// kLbufSlots x 64 floats, lane-interleaved: conflict-free, a ring per lane)
+// and, checked once per 8 steps (so the divergent flush runs at most once per
+// 8 steps, not every step some lane fills up), stores its oldest 16 with
+// four 16-byte stores once 16 have gathered (the strip's remainder at its
+// end).
+// Single 4-byte stores to 64 rows' lists left partly written lines that the
+// caches evicted long before they filled (the lists of all resident waves
+// exceed L2 and MALL): at C3 the listing took 104 ms a step with the stores,
+// 19 ms without them (profiles/r04e_ab_totals_nostore.txt).
+#ifndef MLP_TOT_LDSBUF
+#define MLP_TOT_LDSBUF 1
+#endif
+constexpr int kLbufSlots = 24;  // 16 to flush + up to 8 listed since the last check
+// the 16 elements from ring slot s0 (a multiple of 16 in list order) to dst
+__device__ __forceinline__ void lbuf_flush16(float* __restrict__ dst, const float* lbuf, int s0, int lane) {
+  float4* d = reinterpret_cast<float4*>(dst);
+  // s0 is 0, 8 or 16: the 16 slots are two contiguous runs of 8 at most
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    int slot = s0 + 4 * q;
+    slot = slot >= kLbufSlots ? slot - kLbufSlots : slot;  // 4 | kLbufSlots: a group never wraps
+    const float* b = lbuf + slot * 64 + lane;
+    d[q] = make_float4(b[0], b[64], b[128], b[192]);
+  }
+}
 template <bool FOLD = true>
 __device__ __forceinline__ float local_fwd_fold(const float* __restrict__ cmf, const float* __restrict__ fl, int L1,
                                                 int L2, int row0, int W, int64_t cell_off, const float4* lk,
-                                                float* __restrict__ region, int row_cap, int lane) {
+                                                float* __restrict__ region, int row_cap, int lane,
+                                                float* __restrict__ lbuf, const float* __restrict__ rbp, bool* bad) {
   const int nch = local_chunks(L2);
   float acc = LZ, carry = LZ;  // carry: the largest element of the pair's rows before strip S
   const int S0 = (row0 + 1) >> 6, S1 = (row0 + L1) >> 6;
@@ -134,9 +163,13 @@ __device__ __forceinline__ float local_fwd_fold(const float* __restrict__ cmf, c
     }
     float before = __shfl_up(incl, 1);
     if (lane == 0) before = LZ;
-    float run = fmaxf(carry, before);
+    // rbp (k_local_bounds): the fold of the chunk maxima of the rows before,
+    // a tighter bound than their maximum, checked where the fold reaches the row
+    const float rb = (rbp && row_in) ? rbp[i - 1] : LZ;
+    float run = fmaxf(fmaxf(carry, before), rb);
     carry = fmaxf(carry, readlane_f(incl, 63));
     int cnt = 0;
+    int done = 0;  // list elements already stored (a multiple of 16)
     const float* slab = fl + cell_off + ((int64_t)W * S + 1) * 64 + lane;  // + t * 64: step W S + t
     for (int t0 = 1; t0 <= tend; t0 += 8) {
       float x[8];
@@ -151,6 +184,9 @@ __device__ __forceinline__ float local_fwd_fold(const float* __restrict__ cmf, c
           if (!(run - x[u] >= 7.5f)) {
 #ifdef MLP_EXP_TOT_NOSTORE  // timing experiment: count the candidates, store nothing
             cnt++;
+#elif MLP_TOT_LDSBUF
+            lbuf[(cnt % kLbufSlots) * 64 + lane] = x[u];
+            ++cnt;
 #else
             mine[cnt++] = x[u];
 #endif
@@ -158,7 +194,16 @@ __device__ __forceinline__ float local_fwd_fold(const float* __restrict__ cmf, c
           run = fmaxf(run, x[u]);
         }
       }
+#if MLP_TOT_LDSBUF && !defined(MLP_EXP_TOT_NOSTORE)
+      if (cnt - done >= 16) {  // at most 8 listed since the last check: <= 24 in the ring
+        lbuf_flush16(mine + done, lbuf, done % kLbufSlots, lane);
+        done += 16;
+      }
+#endif
     }
+#if MLP_TOT_LDSBUF && !defined(MLP_EXP_TOT_NOSTORE)
+    for (int k = done; k < cnt; ++k) mine[k] = lbuf[(k % kLbufSlots) * 64 + lane];  // the strip's remainder
+#endif
     TOT_STAT(1, cnt);
     if constexpr (!FOLD) {  // timing experiment: streaming only
       acc = fmaxf(acc, (float)__builtin_amdgcn_readlane(cnt, 5));
@@ -169,6 +214,10 @@ __device__ __forceinline__ float local_fwd_fold(const float* __restrict__ cmf, c
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     // the strip's rows in order
     for (int r = 0; r < 64; ++r) {
+      if (rbp && readlane_f(rb, r) > acc) {  // the row's bound exceeds the chain: the caller redoes the pair
+        *bad = true;
+        return acc;
+      }
       const int n = __builtin_amdgcn_readlane(cnt, r);
       const float* lst = region + (int64_t)r * row_cap;
       for (int k0 = 0; k0 < n; k0 += 64) {
@@ -198,12 +247,14 @@ __global__ __launch_bounds__(256) void k_local_totals(ModelScalars ms, const Tab
                                                       Scratch sc, int64_t npairs, const int32_t* __restrict__ only) {
   __shared__ float4 lk[kLookupRows];
   __shared__ float match[26 * 26], ins[26];
+  __shared__ float lbuf_all[MLP_TOT_LDSBUF ? kWavesPerBlock * kLbufSlots * 64 : 1];  // per wave: a ring per lane
   if (threadIdx.x == 0) mlp_lookup_table(lk);
   for (int k = threadIdx.x; k < 26 * 26; k += blockDim.x) match[k] = tab->match[k];
   if (threadIdx.x < 26) ins[threadIdx.x] = tab->ins[threadIdx.x];
   __syncthreads();
   const int lane = threadIdx.x & 63;
   float* region = sc.clist + wave_index() * 64 * (int64_t)sc.clist_row;
+  float* lbuf = lbuf_all + (MLP_TOT_LDSBUF ? (threadIdx.x >> 6) * kLbufSlots * 64 : 0);
 
   // one counter increment per wave, every lane taking part (no divergent
   // branch around the atomic): lane 0 receives the pair number
@@ -221,16 +272,29 @@ __global__ __launch_bounds__(256) void k_local_totals(ModelScalars ms, const Tab
     const uint8_t* s1 = sq.res + sq.off[pm.pa[p]];
     const uint8_t* s2 = sq.res + sq.off[pm.pb[p]];
     const int64_t rm = pm.rm_off[p];
+    bool bad = false;
 #ifdef MLP_EXP_TOT_NOFOLD  // timing experiment: the listing pass alone (local posteriors then read as 0)
-    float tf = local_fwd_fold<false>(sc.cmf + rm, sc.fl, L1, L2, row0, W, cell_off, lk, region, sc.clist_row, lane);
+    float tf = local_fwd_fold<false>(sc.cmf + rm, sc.fl, L1, L2, row0, W, cell_off, lk, region, sc.clist_row, lane, lbuf,
+                                     nullptr, &bad);
     tf = tf == 12345.f ? 0.f : 1e30f;
 #else
-    float tf = local_fwd_fold(sc.cmf + rm, sc.fl, L1, L2, row0, W, cell_off, lk, region, sc.clist_row, lane);
+    // with the folded bound (sc.crb) when k_local_bounds ran; a pair whose
+    // bound failed is redone with the running maximum (exact either way)
+    const float* rbp = sc.crb ? sc.crb + pm.ell_row[p] : nullptr;
+    float tf = local_fwd_fold(sc.cmf + rm, sc.fl, L1, L2, row0, W, cell_off, lk, region, sc.clist_row, lane, lbuf, rbp,
+                              &bad);
+    if (bad) {
+      bad = false;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      tf = local_fwd_fold(sc.cmf + rm, sc.fl, L1, L2, row0, W, cell_off, lk, region, sc.clist_row, lane, lbuf, nullptr,
+                          &bad);
+    }
 #endif
     float tb = fold_chunks<true>(LZ, 0, (int64_t)L1 * local_chunks(L2), sc.cmb + rm, sc.bl, L2, row0, W, cell_off, s1,
                                  s2, match, ins, 2 * ms.rt1, lk, lane);
 #ifdef MLP_EXP_TOT_STRM2  // the forward streaming pass twice (no second fold)
-    if (local_fwd_fold<false>(sc.cmf + rm, sc.fl, L1, L2, row0, W, cell_off, lk, region, sc.clist_row, lane) ==
+    if (local_fwd_fold<false>(sc.cmf + rm, sc.fl, L1, L2, row0, W, cell_off, lk, region, sc.clist_row, lane, lbuf,
+                              nullptr, &bad) ==
         12345.f)
       tf = 0.f;
 #endif
@@ -471,6 +535,8 @@ void tot_stats_print() {
 hipError_t launch_local_totals(const ModelScalars& ms, const Tables* tab, SeqSet seqs, PairMeta pm, ChainMeta cm,
                                PairRec* rec, Scratch sc, int64_t npairs, int nwaves, hipStream_t st) {
   if (npairs <= 0) return hipSuccess;
+  if (sc.crb)  // the folded row bounds (lane per pair)
+    hipLaunchKernelGGL(k_local_bounds, dim3((unsigned)((npairs + 255) / 256)), dim3(256), 0, st, seqs, pm, sc, npairs);
   hipError_t e = hipMemsetAsync(sc.tot_next, 0, sizeof(int32_t), st);
   if (e != hipSuccess) return e;
   if (nwaves % kWavesPerBlock) return hipErrorInvalidValue;  // every wave owns a list region

@@ -1,12 +1,13 @@
-"""The local-model chain totals two ways (CPNP/ProbabilisticModel.h:435-450:
+"""The local-model chain totals three ways (CPNP/ProbabilisticModel.h:435-450:
 one serial, non-associative LOG_ADD chain per pair): one wave per pair with
-the running-maximum skip bound (MLP_TOT_LANEFOLD=0) and one pair per lane
-after a listing pass with the folded chunk-maximum bound (=1, the default
-where the partition function runs).  Both are exact, so the sparse store,
-distances and MEA scores must be bit-identical, at pid 0 and 1 (the models
-with the partition function) on similar and divergent families, and with
-the PF posterior in the Zm slots (small scratch budget) as well.  Each
-setting runs in a child process: the switch is read once per process."""
+the running-maximum skip bound (MLP_TOT_FOLDBOUND=0), the same with the
+folded chunk-maximum bound (=1, the default), and one pair per lane after a
+listing pass into the dead PF forward Zm slots (MLP_TOT_LANEFOLD=1).  All are
+exact, so the sparse store, distances and MEA scores must be bit-identical,
+at pid 0 and 1 (the models with the partition function) on similar and
+divergent families, and with several batches and the PF posterior in the Zm
+slots (small scratch budget) as well.  Each setting runs in a child process:
+the switches are read once per process."""
 import os
 import subprocess
 import sys
@@ -39,19 +40,23 @@ print(' '.join(out))
 '''
 
 
-def _run(lanefold, scratch=None):
-    env = dict(os.environ, MLP_TOT_LANEFOLD=str(lanefold))
+def _run(lanefold, scratch=None, foldbound=1):
+    env = dict(os.environ, MLP_TOT_LANEFOLD=str(lanefold), MLP_TOT_FOLDBOUND=str(foldbound))
     args = [sys.executable, '-c', _CHILD, ROOT] + ([str(scratch)] if scratch else [])
     r = subprocess.run(args, capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     return r.stdout.split()
 
 
-def test_lanefold_totals_bit_identical():
-    assert _run(1) == _run(0)
+def test_totals_bit_identical():
+    ref = _run(0, foldbound=0)
+    assert _run(0) == ref
+    assert _run(1) == ref
 
 
-def test_lanefold_totals_bit_identical_small_scratch():
+def test_totals_bit_identical_small_scratch():
     # 1 GB: several batches, the PF posterior in the low halves of the Zm
-    # slots whose high halves hold the candidates
-    assert _run(1, 1 << 30) == _run(0, 1 << 30)
+    # slots whose high halves hold the lane fold's candidates
+    ref = _run(0, 1 << 30, foldbound=0)
+    assert _run(0, 1 << 30) == ref
+    assert _run(1, 1 << 30) == ref
