@@ -17,6 +17,9 @@ namespace mlp {
 // tables are 3 KB, the PF factors 5.4 KB).
 template <bool H> struct LdsHmmPart {
   float4 lk[kLookupRows];
+#if MLP_PK
+  float4 lk2[2 * kLookupRows * kLookupRows];  // interval pairs (mlp_log_add_t2)
+#endif
   float match[26 * 26];
 };
 template <> struct LdsHmmPart<false> {};
@@ -41,6 +44,9 @@ __device__ __forceinline__ void stage_tables(LdsTablesT<H, P>& L, const Tables* 
   if (threadIdx.x < 26) L.ins[threadIdx.x] = tab->ins[threadIdx.x];
   if constexpr (H) {
     if (threadIdx.x == 0) mlp_lookup_table(L.lk);
+#if MLP_PK
+    for (int e = threadIdx.x; e < kLookupRows * kLookupRows; e += blockDim.x) mlp_lookup_table2_entry(L.lk2, e);
+#endif
   }
   __syncthreads();
 }
@@ -48,6 +54,13 @@ template <bool H, bool P>
 __device__ __forceinline__ const float4* lookup_of(const LdsTablesT<H, P>& L) {
   if constexpr (H) return L.lk;
   else return nullptr;
+}
+template <bool H, bool P>
+__device__ __forceinline__ const float4* lookup2_of(const LdsTablesT<H, P>& L) {
+#if MLP_PK
+  if constexpr (H) return L.lk2;
+#endif
+  return nullptr;
 }
 
 __device__ __forceinline__ int64_t wave_index() {

@@ -41,17 +41,27 @@ constexpr int kPrefetch = 4;
 // queued, and the extra resident waves hide the DP's dependency stalls.  The
 // PF backward holds more fp64 state and runs at MLP_PF_BWD_WAVES (5: 94
 // VGPRs; at 6 it now fits 80 VGPRs without spilling); the all-in-one M = 7
-// build keeps the compiler's choice.
+// build keeps the compiler's choice.  The forward sweeps run at 5 waves
+// (MLP_FWD_WAVES) since round 4: at 94 VGPRs the compiler keeps what it
+// rematerialised at 80, and the forward group took 202-203 ms a C3 step
+// against 215-217 at 6 waves (the backward group 219 against 224 beside it;
+// profiles/r04k_ab_fwd_waves.txt).
 #ifndef MLP_SWEEP_WAVES
 #define MLP_SWEEP_WAVES 6
 #endif
 #ifndef MLP_PF_BWD_WAVES
 #define MLP_PF_BWD_WAVES 5
 #endif
+#ifndef MLP_FWD_WAVES
+#define MLP_FWD_WAVES 5
+#endif
+#ifndef MLP_BWD_WAVES
+#define MLP_BWD_WAVES MLP_SWEEP_WAVES
+#endif
 template <int M>
 struct SweepWaves {
-  static constexpr int fwd = M == 7 ? 1 : MLP_SWEEP_WAVES;
-  static constexpr int bwd = M == 7 ? 1 : ((M & 4) != 0 && MLP_SWEEP_WAVES > MLP_PF_BWD_WAVES ? MLP_PF_BWD_WAVES : MLP_SWEEP_WAVES);
+  static constexpr int fwd = M == 7 ? 1 : MLP_FWD_WAVES;
+  static constexpr int bwd = M == 7 ? 1 : ((M & 4) != 0 && MLP_BWD_WAVES > MLP_PF_BWD_WAVES ? MLP_PF_BWD_WAVES : MLP_BWD_WAVES);
 };
 
 // Bring three scaled-fp64 frames to their common maximum (exact: powers of two).
@@ -108,6 +118,7 @@ __global__ __launch_bounds__(256, SweepWaves<M>::fwd) void k_forward(ModelScalar
   const int64_t ch = wave_index();
   if (ch >= nchains) return;
   const float4* __restrict__ lk = lookup_of(T_);
+  const float4* __restrict__ lk2 = lookup2_of(T_);  // interval pairs (MLP_PK)
   const int lane = threadIdx.x & 63;
   const ChainView C = stage_chain<kStageFwd>(dyn, lds_seq, ch, sq, pm, cm, rec);
   const int W = C.W, S = C.S;
@@ -171,11 +182,44 @@ __global__ __launch_bounds__(256, SweepWaves<M>::fwd) void k_forward(ModelScalar
         else
           bc.template shift<true, false>(0, L5, U5, LL, UL, LZm, LZe, LZf, Le, UZm, UZe, UZf, Ue);
         const int64_t idx = base + (int64_t)t * 64;
+        // the local model's M / X / Y values when they ride in the other half
+        // of the 5-state model's packed LOG_ADDs (MLP_PK)
+        float lvm = 0.f, lvx = 0.f, lvy = 0.f;
         // ------------------------------------------------ 5-state forward
         if constexpr ((M & kHmm5) != 0) {
           const float mt = T_.match[c1 * 26 + c2];
           const float ins2 = T_.ins[c2];
           // CPNP/ProbabilisticModel.h:213-256
+#if MLP_PK
+          // independent LOG_ADDs in pairs: the 5-state M chain beside the
+          // local M chain (each in its own order), X1 / X2, Y1 / Y2, local X / Y
+          float vm;
+          if constexpr ((M & kLocal) != 0) {
+            const float bs = mt - ins1 - ins2;
+            mlp_f2 v = {D5[0] + ms.t[0][0], bs - two_rt1};
+            v = mlp_log_add_t2(v, mlp_f2{D5[1] + ms.t[1][0], bs + DL[0] + ms.lt[0][0] - two_rt1}, lk2);
+            v = mlp_log_add_t2(v, mlp_f2{D5[2] + ms.t[2][0], bs + DL[1] + ms.lt[1][0] - two_rt1}, lk2);
+            v = mlp_log_add_t2(v, mlp_f2{D5[3] + ms.t[3][0], bs + DL[2] + ms.lt[2][0] - two_rt1}, lk2);
+            vm = mlp_log_add_t(v.x, D5[4] + ms.t[4][0], lk);
+            lvm = v.y;
+            const mlp_f2 l = mlp_log_add_t2(mlp_f2{UL[0] + ms.lt[0][1] - rt1, LL[0] + ms.lt[0][2] - rt1},
+                                            mlp_f2{UL[1] + ms.lt[1][1] - rt1, LL[2] + ms.lt[2][2] - rt1}, lk2);
+            lvx = l.x;
+            lvy = l.y;
+          } else {
+            vm = D5[0] + ms.t[0][0];
+            vm = mlp_log_add_t(vm, D5[1] + ms.t[1][0], lk);
+            vm = mlp_log_add_t(vm, D5[2] + ms.t[2][0], lk);
+            vm = mlp_log_add_t(vm, D5[3] + ms.t[3][0], lk);
+            vm = mlp_log_add_t(vm, D5[4] + ms.t[4][0], lk);
+          }
+          vm = vm + mt;
+          const mlp_f2 vx = mlp_f2(ins1) + mlp_log_add_t2(mlp_f2{U5[0] + ms.t[0][1], U5[0] + ms.t[0][3]},
+                                                          mlp_f2{U5[1] + ms.t[1][1], U5[3] + ms.t[3][3]}, lk2);
+          const mlp_f2 vy = mlp_f2(ins2) + mlp_log_add_t2(mlp_f2{L5[0] + ms.t[0][2], L5[0] + ms.t[0][4]},
+                                                          mlp_f2{L5[2] + ms.t[2][2], L5[4] + ms.t[4][4]}, lk2);
+          const float vx1 = vx.x, vx2 = vx.y, vy1 = vy.x, vy2 = vy.y;
+#else
           float vm = D5[0] + ms.t[0][0];
           vm = mlp_log_add_t(vm, D5[1] + ms.t[1][0], lk);
           vm = mlp_log_add_t(vm, D5[2] + ms.t[2][0], lk);
@@ -186,6 +230,7 @@ __global__ __launch_bounds__(256, SweepWaves<M>::fwd) void k_forward(ModelScalar
           const float vx2 = ins1 + mlp_log_add_t(U5[0] + ms.t[0][3], U5[3] + ms.t[3][3], lk);
           const float vy1 = ins2 + mlp_log_add_t(L5[0] + ms.t[0][2], L5[2] + ms.t[2][2], lk);
           const float vy2 = ins2 + mlp_log_add_t(L5[0] + ms.t[0][4], L5[4] + ms.t[4][4], lk);
+#endif
           float Cc[5];
 #pragma unroll
           for (int k5 = 0; k5 < 5; ++k5) Cc[k5] = LZ;
@@ -217,12 +262,19 @@ __global__ __launch_bounds__(256, SweepWaves<M>::fwd) void k_forward(ModelScalar
           const float mt = T_.match[c1 * 26 + c2];
           const float ins2 = T_.ins[c2];
           const float bs = mt - ins1 - ins2;
-          float vm = bs - two_rt1;
-          vm = mlp_log_add_t(vm, bs + DL[0] + ms.lt[0][0] - two_rt1, lk);
-          vm = mlp_log_add_t(vm, bs + DL[1] + ms.lt[1][0] - two_rt1, lk);
-          vm = mlp_log_add_t(vm, bs + DL[2] + ms.lt[2][0] - two_rt1, lk);
-          const float vx = mlp_log_add_t(UL[0] + ms.lt[0][1] - rt1, UL[1] + ms.lt[1][1] - rt1, lk);
-          const float vy = mlp_log_add_t(LL[0] + ms.lt[0][2] - rt1, LL[2] + ms.lt[2][2] - rt1, lk);
+          float vm, vx, vy;
+          if constexpr (MLP_PK && (M & kHmm5) != 0) {  // computed beside the 5-state values
+            vm = lvm;
+            vx = lvx;
+            vy = lvy;
+          } else {
+            vm = bs - two_rt1;
+            vm = mlp_log_add_t(vm, bs + DL[0] + ms.lt[0][0] - two_rt1, lk);
+            vm = mlp_log_add_t(vm, bs + DL[1] + ms.lt[1][0] - two_rt1, lk);
+            vm = mlp_log_add_t(vm, bs + DL[2] + ms.lt[2][0] - two_rt1, lk);
+            vx = mlp_log_add_t(UL[0] + ms.lt[0][1] - rt1, UL[1] + ms.lt[1][1] - rt1, lk);
+            vy = mlp_log_add_t(LL[0] + ms.lt[0][2] - rt1, LL[2] + ms.lt[2][2] - rt1, lk);
+          }
           float Cm = LZ, Cx = LZ, Cy = LZ;
           if (i == 1 && j == 1) Cm = bs - two_rt1;
           if (gen) {
@@ -312,6 +364,7 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
   const int64_t ch = wave_index();
   if (ch >= nchains) return;
   const float4* __restrict__ lk = lookup_of(T_);
+  const float4* __restrict__ lk2 = lookup2_of(T_);  // interval pairs (MLP_PK)
   const int lane = threadIdx.x & 63;
   const ChainView C = stage_chain<kStageBwd>(dyn, lds_seq, ch, sq, pm, cm, rec);
   const int W = C.W, S = C.S;
@@ -410,6 +463,25 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
 #pragma unroll
           for (int k5 = 0; k5 < 5; ++k5)
             B[k5] = last ? ms.init[k5] : ((in_i && in_j) ? mlp_log_add_from_zero(pxy + ms.t[k5][0]) : LZ);
+#if MLP_PK
+          // B[0]'s chain in its order, each step paired with one of B[1..4]
+          if (in_i) {
+            mlp_f2 b = mlp_log_add_t2(mlp_f2{B[0], B[1]},
+                                      mlp_f2{N5[1] + ins1n + ms.t[0][1], N5[1] + ins1n + ms.t[1][1]}, lk2);
+            B[1] = b.y;
+            b = mlp_log_add_t2(mlp_f2{b.x, B[3]}, mlp_f2{N5[3] + ins1n + ms.t[0][3], N5[3] + ins1n + ms.t[3][3]}, lk2);
+            B[0] = b.x;
+            B[3] = b.y;
+          }
+          if (in_j) {
+            mlp_f2 b = mlp_log_add_t2(mlp_f2{B[0], B[2]},
+                                      mlp_f2{R5[2] + ins2n + ms.t[0][2], R5[2] + ins2n + ms.t[2][2]}, lk2);
+            B[2] = b.y;
+            b = mlp_log_add_t2(mlp_f2{b.x, B[4]}, mlp_f2{R5[4] + ins2n + ms.t[0][4], R5[4] + ins2n + ms.t[4][4]}, lk2);
+            B[0] = b.x;
+            B[4] = b.y;
+          }
+#else
           if (in_i) {
             B[0] = mlp_log_add_t(B[0], N5[1] + ins1n + ms.t[0][1], lk);
             B[1] = mlp_log_add_t(B[1], N5[1] + ins1n + ms.t[1][1], lk);
@@ -422,6 +494,7 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
             B[0] = mlp_log_add_t(B[0], R5[4] + ins2n + ms.t[0][4], lk);
             B[4] = mlp_log_add_t(B[4], R5[4] + ins2n + ms.t[4][4], lk);
           }
+#endif
           sc.f5[idx] = f5v + B[0];   // f + b (CPNP/ProbabilisticModel.h:484)
           if (act) {
             if (i == 1 && j == 1) rec[c.slot].b5[0] = B[0];
@@ -446,6 +519,18 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
             Bx = mlp_log_add_from_zero(pxy + ms.lt[1][0] - two_rt1);
             By = mlp_log_add_from_zero(pxy + ms.lt[2][0] - two_rt1);
           }
+#if MLP_PK
+          if (in_i) {
+            const mlp_f2 b = mlp_log_add_t2(mlp_f2{Bm, Bx}, mlp_f2{NL[1] + ms.lt[0][1] - rt1, NL[1] + ms.lt[1][1] - rt1}, lk2);
+            Bm = b.x;
+            Bx = b.y;
+          }
+          if (in_j) {
+            const mlp_f2 b = mlp_log_add_t2(mlp_f2{Bm, By}, mlp_f2{RL[2] + ms.lt[0][2] - rt1, RL[2] + ms.lt[2][2] - rt1}, lk2);
+            Bm = b.x;
+            By = b.y;
+          }
+#else
           if (in_i) {
             Bm = mlp_log_add_t(Bm, NL[1] + ms.lt[0][1] - rt1, lk);
             Bx = mlp_log_add_t(Bx, NL[1] + ms.lt[1][1] - rt1, lk);
@@ -454,6 +539,7 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
             Bm = mlp_log_add_t(Bm, RL[2] + ms.lt[0][2] - rt1, lk);
             By = mlp_log_add_t(By, RL[2] + ms.lt[2][2] - rt1, lk);
           }
+#endif
           sc.bl[idx] = Bm;   // f + b is formed by the merge (the same float add)
           if (lane == 0) {
             sc.bndl[(bo + j) * 3 + 0] = Bm;
