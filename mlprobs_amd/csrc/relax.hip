@@ -360,6 +360,12 @@ __device__ __forceinline__ uint4 rfl(uint4 v) {
 #ifdef MLP_RELAX_TIMING  // measurement variant: per-z compute imbalance across the 16 waves
 __device__ unsigned long long g_rtime[8];
 #endif
+#ifdef MLP_RELAX_STATS  // measurement variant: trips of the word walk and the hit loop, lane sums vs wave maxima
+__device__ unsigned long long g_rstat[4];
+#define RSTAT_INC(v) ++(v)
+#else
+#define RSTAT_INC(v)
+#endif
 template <int KP, int SL, bool QP>
 // KP = 5 (tiles within half the LDS): two workgroups per CU, so 8 waves per
 // SIMD and at most 64 VGPRs; KP = 9: one workgroup, 4 waves per SIMD
@@ -634,6 +640,24 @@ __global__ __launch_bounds__(kRelaxThreads, KP == 5 && kRelaxThreads == 1024 ? 8
   const uint4 fC = nC, fAo = nAo, fNa = nNa, fAc = nAc;
   const float4 fW = nW;
 #endif
+#ifdef MLP_RELAX_STATS
+  // per (slot, z): lanes' word steps and hits summed, and 64 x the wave's
+  // maximum (the trips the wave issues); lane 0 keeps the wave's totals
+  uint32_t st_w = 0, st_h = 0;
+  unsigned long long sw_sum = 0, sw_max = 0, sh_sum = 0, sh_max = 0;
+#define RSTAT_SLOT()                                                                  \
+  {                                                                                   \
+    uint32_t a_ = st_w, b_ = st_h, ma_ = st_w, mb_ = st_h;                            \
+    for (int o_ = 32; o_; o_ >>= 1) {                                                 \
+      a_ += __shfl_xor(a_, o_); b_ += __shfl_xor(b_, o_);                             \
+      ma_ = max(ma_, (uint32_t)__shfl_xor(ma_, o_)); mb_ = max(mb_, (uint32_t)__shfl_xor(mb_, o_)); \
+    }                                                                                 \
+    sw_sum += a_; sh_sum += b_; sw_max += 64ull * ma_; sh_max += 64ull * mb_;         \
+    st_w = st_h = 0;                                                                  \
+  }
+#else
+#define RSTAT_SLOT()
+#endif
   while (more) {
 #ifdef MLP_RELAX_TIMING
     const uint64_t ts0 = clock64();
@@ -689,10 +713,12 @@ __global__ __launch_bounds__(kRelaxThreads, KP == 5 && kRelaxThreads == 1024 ? 8
     // 1.21 s: the wave issues both bodies every iteration)
 #define MLP_WALK(pa, pc, we, a0, c0)                                                                  \
     for (int w = max(a0, c0); w < we; w += 2) {                                                       \
+      RSTAT_INC(st_w);                                                                                \
       const uint2 xa0 = pa[w], xa1 = pa[w + 1], xc0 = pc[w], xc1 = pc[w + 1];                         \
       uint32_t m0 = xa0.x & xc0.x;                                                                    \
       uint32_t m1 = w + 1 < we ? xa1.x & xc1.x : 0u;                                                  \
       while (m0) { /* common columns k, ascending */                                                  \
+        RSTAT_INC(st_h);                                                                              \
         const uint32_t bit = 1u << __builtin_ctz(m0);                                                 \
         m0 ^= bit;                                                                                    \
         const float va = QP ? wk * Avals[xa0.y + __popc(xa0.x & (bit - 1u))]                          \
@@ -701,6 +727,7 @@ __global__ __launch_bounds__(kRelaxThreads, KP == 5 && kRelaxThreads == 1024 ? 8
         ac += va * vc;                                                                                \
       }                                                                                               \
       while (m1) {                                                                                    \
+        RSTAT_INC(st_h);                                                                              \
         const uint32_t bit = 1u << __builtin_ctz(m1);                                                 \
         m1 ^= bit;                                                                                    \
         const float va = QP ? wk * Avals[xa1.y + __popc(xa1.x & (bit - 1u))]                          \
@@ -753,6 +780,7 @@ _Pragma("unroll")                                                               
           MLP_WALK(pa, pc, we, a0, c0)                                                                           \
           acc[s] = ac;                                                                                           \
         }                                                                                                        \
+        RSTAT_SLOT();                                                                                            \
         cl = cl1;                                                                                                \
         z4 = z41;                                                                                                \
         ha = ha1;                                                                                                \
@@ -797,6 +825,15 @@ _Pragma("unroll")                                                               
   }
 #endif
 #undef MLP_ISSUE
+#undef RSTAT_SLOT
+#ifdef MLP_RELAX_STATS
+  if ((tid & 63) == 0) {
+    atomicAdd(&g_rstat[0], sw_sum);
+    atomicAdd(&g_rstat[1], sw_max);
+    atomicAdd(&g_rstat[2], sh_sum);
+    atomicAdd(&g_rstat[3], sh_max);
+  }
+#endif
   __syncthreads();  // the weight sums of the last chunk
   const float fn = (float)n;  // CPNP/MSA.cpp:1233-1235; QuickProbs: / the weight sum
 #pragma unroll
@@ -865,6 +902,18 @@ hipError_t launch_relax_tiles(const TileRelaxArgs& a, int slots, bool one_per_cu
           (double)h[5] / h[3], (double)h[6] / h[3], (double)h[7] / h[3]);
   for (auto& v : h) v = 0;
   hipMemcpyToSymbol(HIP_SYMBOL(g_rtime), h, sizeof h);
+#endif
+#ifdef MLP_RELAX_STATS
+  {
+    unsigned long long h[4];
+    hipStreamSynchronize(st);
+    hipMemcpyFromSymbol(h, HIP_SYMBOL(g_rstat), sizeof h);
+    fprintf(stderr, "relax stats: slots %d word steps lane-sum %llu wave-issued %llu (efficiency %.3f) | hits lane-sum %llu "
+            "wave-issued %llu (efficiency %.3f)\n", slots, h[0], h[1], h[1] ? (double)h[0] / h[1] : 0.0, h[2], h[3],
+            h[3] ? (double)h[2] / h[3] : 0.0);
+    for (auto& v : h) v = 0;
+    hipMemcpyToSymbol(HIP_SYMBOL(g_rstat), h, sizeof h);
+  }
 #endif
   return e;
 }
