@@ -52,6 +52,9 @@ constexpr int kPrefetch = 4;
 #ifndef MLP_PF_BWD_WAVES
 #define MLP_PF_BWD_WAVES 5
 #endif
+#ifndef MLP_BND_UNIFORM  // one boundary-shift form for every step (needs MLP_BND_ROTATE)
+#define MLP_BND_UNIFORM MLP_BND_ROTATE
+#endif
 #ifndef MLP_FWD_WAVES
 #define MLP_FWD_WAVES 5
 #endif
@@ -177,7 +180,11 @@ __global__ __launch_bounds__(256, SweepWaves<M>::fwd) void k_forward(ModelScalar
           for (int k3 = 0; k3 < 3; ++k3) DL[k3] = UL[k3];
         }
         if constexpr ((M & kPF) != 0) { DZm = UZm; DZe = UZe; DZf = UZf; De = Ue; }
-        if (take_bnd)
+        // MLP_BND_UNIFORM: every step takes lane 0's value from the chunk (in
+        // strip 0 and the skew tail lane 0's up value is unused -- row 0 of
+        // the chain, the idle tail -- so whatever the chunk holds is harmless);
+        // one form of the shift, no branch joining two register assignments
+        if (MLP_BND_UNIFORM || take_bnd)
           bc.template shift<true, true>(t - t_lo, L5, U5, LL, UL, LZm, LZe, LZf, Le, UZm, UZe, UZf, Ue);
         else
           bc.template shift<true, false>(0, L5, U5, LL, UL, LZm, LZe, LZf, Le, UZm, UZe, UZf, Ue);
@@ -447,7 +454,9 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
           for (int k3 = 0; k3 < 3; ++k3) GL[k3] = NL[k3];
         }
         if constexpr ((M & kPF) != 0) { GZm = NZm; GZe = NZe; GZf = NZf; Ge = Ne; }
-        if (take_bnd)
+        // (MLP_BND_UNIFORM: lane 63's down value is unused in the last strip
+        // -- the chain's last row, in_i false -- and in the skew head)
+        if (MLP_BND_UNIFORM || take_bnd)
           bc.template shift<false, true>(t - t_lo, R5, N5, RL, NL, RZm, RZe, RZf, Re, NZm, NZe, NZf, Ne);
         else
           bc.template shift<false, false>(0, R5, N5, RL, NL, RZm, RZe, RZf, Re, NZm, NZe, NZf, Ne);
