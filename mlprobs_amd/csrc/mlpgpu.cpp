@@ -1150,14 +1150,17 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
   const size_t clist_bytes = (models & kLocal) ? (size_t)tot_waves * 64 * tot_row * 4 : 0;
   // the forward local chain folded one pair per lane (k_local_fold) when the
   // PF forward Zm slots are dead by then (the partition function ran, and
-  // both backward sweeps joined before the totals); MLP_TOT_LANEFOLD=0 / 1
-  // forces the one-wave-per-pair fold / this
+  // both backward sweeps joined before the totals); by default when the PF
+  // posterior has its own array, so the candidate rows are contiguous in the
+  // dead slots (MLP_TOT_LANEFOLD_DEFAULT -1); MLP_TOT_LANEFOLD=0 / 1 forces
+  // the one-wave-per-pair fold / this
 #ifndef MLP_TOT_LANEFOLD_DEFAULT
-#define MLP_TOT_LANEFOLD_DEFAULT 0
+#define MLP_TOT_LANEFOLD_DEFAULT -1
 #endif
   static const char* lf_env = getenv("MLP_TOT_LANEFOLD");
-  const bool lanefold = (models & kLocal) && (models & kPF) && (!side || side->join_mode == 0) &&
-                        (lf_env ? atoi(lf_env) != 0 : MLP_TOT_LANEFOLD_DEFAULT != 0);
+  const bool lf_want = lf_env ? atoi(lf_env) != 0
+                              : (MLP_TOT_LANEFOLD_DEFAULT < 0 ? !pg_in_zm : MLP_TOT_LANEFOLD_DEFAULT != 0);
+  const bool lanefold = (models & kLocal) && (models & kPF) && (!side || side->join_mode == 0) && lf_want;
   // the one-wave fold's listing bound: the folded chunk maxima of the rows
   // before (k_local_bounds) instead of their maximum (MLP_TOT_FOLDBOUND=0 / 1)
 #ifndef MLP_TOT_FOLDBOUND_DEFAULT

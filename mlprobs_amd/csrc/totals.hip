@@ -354,6 +354,15 @@ __global__ __launch_bounds__(256) void k_local_bounds(SeqSet sq, PairMeta pm, Sc
 __device__ __forceinline__ float* lanefold_area(const Scratch& sc, int64_t cell_off, int row0, int W) {
   return reinterpret_cast<float*>(sc.zm) + 2 * (cell_off + (int64_t)row0 * W) + 1;
 }
+// With the PF posterior in its own array (pg_stride 1) the whole 8-byte slots
+// are dead: row i's candidates are contiguous at rows + (i - 1) * RS, RS = L2
+// rounded up to 4 floats, from the first 16-byte boundary of the pair's slots
+// ((L1 + 1) W >= (L1 + 1)(L2 + 1) slots of 8 bytes hold 16 + 4 L1 RS bytes).
+__device__ __forceinline__ float* lanefold_rows(const Scratch& sc, int64_t cell_off, int row0, int W) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(sc.zm + cell_off + (int64_t)row0 * W);
+  return reinterpret_cast<float*>((a + 15) & ~static_cast<uintptr_t>(15));
+}
+__device__ __forceinline__ int lanefold_rs(int L2) { return (L2 + 3) & ~3; }
 
 // Wave per pair (persistent, as k_local_totals): the backward chain as there,
 // and the forward chain's candidates listed row by row (element x of row i is
@@ -363,11 +372,14 @@ __global__ __launch_bounds__(256) void k_local_list(ModelScalars ms, const Table
                                                     Scratch sc, int64_t npairs) {
   __shared__ float4 lk[kLookupRows];
   __shared__ float match[26 * 26], ins[26];
+  __shared__ float lbuf_all[kWavesPerBlock * kLbufSlots * 64];  // contiguous rows: per wave a ring per lane
   if (threadIdx.x == 0) mlp_lookup_table(lk);
   for (int k = threadIdx.x; k < 26 * 26; k += blockDim.x) match[k] = tab->match[k];
   if (threadIdx.x < 26) ins[threadIdx.x] = tab->ins[threadIdx.x];
   __syncthreads();
   const int lane = threadIdx.x & 63;
+  float* lbuf = lbuf_all + (threadIdx.x >> 6) * kLbufSlots * 64;
+  const bool contig = sc.pg_stride == 1;
   auto take = [&]() -> int64_t {
     const int got = atomicAdd(sc.tot_next, lane == 0 ? 1 : 0);
     return __builtin_amdgcn_readfirstlane(got);
@@ -379,25 +391,55 @@ __global__ __launch_bounds__(256) void k_local_list(ModelScalars ms, const Table
     const int64_t cell_off = cm.cell_off[h];
     const int64_t ell = pm.ell_row[p];
     float* __restrict__ area = lanefold_area(sc, cell_off, row0, W);
+    float* __restrict__ rows = lanefold_rows(sc, cell_off, row0, W);
+    const int RS = lanefold_rs(L2);
     const int S0 = (row0 + 1) >> 6, S1 = (row0 + L1) >> 6;
     const int tend = L2 + 63;
     for (int S = S0; S <= S1; ++S) {
       const int i = 64 * S + lane - row0;
       const bool row_in = i >= 1 && i <= L1;
       float run = row_in ? sc.crb[ell + i - 1] : LZ;
-      float* __restrict__ mine = area + 2 * (int64_t)(row_in ? i - 1 : 0) * L2;
       int cnt = 0;
       const float* slab = sc.fl + cell_off + ((int64_t)W * S + 1) * 64 + lane;
-      for (int t0 = 1; t0 <= tend; t0 += 8) {
-        float x[8];
+      if (contig) {
+        // a row's list contiguous, written 64 bytes at a time through the
+        // lane's LDS ring (as local_fwd_fold's lists)
+        float* __restrict__ mine = rows + (int64_t)(row_in ? i - 1 : 0) * RS;
+        int done = 0;
+        for (int t0 = 1; t0 <= tend; t0 += 8) {
+          float x[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) x[u] = (t0 + u <= tend) ? slab[(int64_t)(t0 + u) * 64] : LZ;
+          for (int u = 0; u < 8; ++u) x[u] = (t0 + u <= tend) ? slab[(int64_t)(t0 + u) * 64] : LZ;
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const int j = t0 + u - lane;
-          if (row_in && j >= 1 && j <= L2) {
-            if (!(run - x[u] >= 7.5f)) mine[2 * cnt++] = x[u];
-            run = fmaxf(run, x[u]);
+          for (int u = 0; u < 8; ++u) {
+            const int j = t0 + u - lane;
+            if (row_in && j >= 1 && j <= L2) {
+              if (!(run - x[u] >= 7.5f)) {
+                lbuf[(cnt % kLbufSlots) * 64 + lane] = x[u];
+                ++cnt;
+              }
+              run = fmaxf(run, x[u]);
+            }
+          }
+          if (cnt - done >= 16) {  // at most 8 listed since the last check: <= 24 in the ring
+            lbuf_flush16(mine + done, lbuf, done % kLbufSlots, lane);
+            done += 16;
+          }
+        }
+        for (int k = done; k < cnt; ++k) mine[k] = lbuf[(k % kLbufSlots) * 64 + lane];
+      } else {
+        float* __restrict__ mine = area + 2 * (int64_t)(row_in ? i - 1 : 0) * L2;
+        for (int t0 = 1; t0 <= tend; t0 += 8) {
+          float x[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) x[u] = (t0 + u <= tend) ? slab[(int64_t)(t0 + u) * 64] : LZ;
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const int j = t0 + u - lane;
+            if (row_in && j >= 1 && j <= L2) {
+              if (!(run - x[u] >= 7.5f)) mine[2 * cnt++] = x[u];
+              run = fmaxf(run, x[u]);
+            }
           }
         }
       }
@@ -432,6 +474,43 @@ __global__ __launch_bounds__(256) void k_local_fold(SeqSet sq, PairMeta pm, Chai
   bool bad = false;
   int n = sc.ell_cnt[ell];
   float rb = sc.crb[ell];
+  if (sc.pg_stride == 1) {
+    // contiguous rows, 16-byte loads: two ahead within the row, and the next
+    // row's first two (its count read two rows ahead) loaded at the row's start
+    const float4* __restrict__ rows4 = reinterpret_cast<const float4*>(lanefold_rows(sc, cm.cell_off[h], pm.row0[p], cm.width[h]));
+    const int RS4 = lanefold_rs(L2) >> 2;
+    const float4 Z4 = make_float4(LZ, LZ, LZ, LZ);
+    int n1 = L1 > 1 ? sc.ell_cnt[ell + 1] : 0;
+    float4 a = n > 0 ? rows4[0] : Z4, b = n > 4 ? rows4[1] : Z4;
+    for (int i = 1; i <= L1; ++i) {
+      const float4* __restrict__ src = rows4 + (int64_t)(i - 1) * RS4;
+      const float4* __restrict__ nxt = src + RS4;
+      const int n2 = i + 1 < L1 ? sc.ell_cnt[ell + i + 1] : 0;
+      const float rb_next = i < L1 ? sc.crb[ell + i] : LZ;
+      const float4 na = n1 > 0 ? nxt[0] : Z4, nb = n1 > 4 ? nxt[1] : Z4;
+      bad |= rb > acc;  // the listing's bound must not exceed the chain at the row's start
+      for (int k = 0; k < n; k += 4) {
+        const float4 c = k + 8 < n ? src[(k >> 2) + 2] : Z4;
+        acc = mlp_log_add_t(acc, a.x, lk);  // k < n
+        acc = mlp_log_add_t(acc, k + 1 < n ? a.y : LZ, lk);
+        acc = mlp_log_add_t(acc, k + 2 < n ? a.z : LZ, lk);
+        acc = mlp_log_add_t(acc, k + 3 < n ? a.w : LZ, lk);
+        a = b;
+        b = c;
+      }
+      a = na;
+      b = nb;
+      n = n1;
+      n1 = n2;
+      rb = rb_next;
+    }
+    rec[p].tfl = acc;
+    if (bad) {
+      const int k = atomicAdd(&sc.rep[0], 1);
+      sc.rep[1 + k] = (int32_t)p;
+    }
+    return;
+  }
   for (int i = 1; i <= L1; ++i) {
     const float* __restrict__ src = area + 2 * (int64_t)(i - 1) * L2;
     // the next row's count and bound, loaded ahead
