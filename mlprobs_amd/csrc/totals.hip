@@ -475,31 +475,44 @@ __global__ __launch_bounds__(256) void k_local_fold(SeqSet sq, PairMeta pm, Chai
   int n = sc.ell_cnt[ell];
   float rb = sc.crb[ell];
   if (sc.pg_stride == 1) {
-    // contiguous rows, 16-byte loads: two ahead within the row, and the next
-    // row's first two (its count read two rows ahead) loaded at the row's start
+    // contiguous rows, 16-byte loads: the fold runs one lane's chain per
+    // pair, so the kernel lasts as long as the longest chain and every load
+    // the chain waits for adds to it.  Within a row, eight elements per step
+    // with the next 16 in flight; the next row's first 16 (its count read
+    // two rows ahead) loaded at the row's start.
     const float4* __restrict__ rows4 = reinterpret_cast<const float4*>(lanefold_rows(sc, cm.cell_off[h], pm.row0[p], cm.width[h]));
     const int RS4 = lanefold_rs(L2) >> 2;
     const float4 Z4 = make_float4(LZ, LZ, LZ, LZ);
     int n1 = L1 > 1 ? sc.ell_cnt[ell + 1] : 0;
-    float4 a = n > 0 ? rows4[0] : Z4, b = n > 4 ? rows4[1] : Z4;
+    float4 a0 = n > 0 ? rows4[0] : Z4, a1 = n > 4 ? rows4[1] : Z4;
+    float4 b0 = n > 8 ? rows4[2] : Z4, b1 = n > 12 ? rows4[3] : Z4;
+    auto fold4 = [&](const float4 v, int k) {
+      acc = mlp_log_add_t(acc, k < n ? v.x : LZ, lk);
+      acc = mlp_log_add_t(acc, k + 1 < n ? v.y : LZ, lk);
+      acc = mlp_log_add_t(acc, k + 2 < n ? v.z : LZ, lk);
+      acc = mlp_log_add_t(acc, k + 3 < n ? v.w : LZ, lk);
+    };
     for (int i = 1; i <= L1; ++i) {
       const float4* __restrict__ src = rows4 + (int64_t)(i - 1) * RS4;
       const float4* __restrict__ nxt = src + RS4;
       const int n2 = i + 1 < L1 ? sc.ell_cnt[ell + i + 1] : 0;
       const float rb_next = i < L1 ? sc.crb[ell + i] : LZ;
-      const float4 na = n1 > 0 ? nxt[0] : Z4, nb = n1 > 4 ? nxt[1] : Z4;
+      const float4 na0 = n1 > 0 ? nxt[0] : Z4, na1 = n1 > 4 ? nxt[1] : Z4;
+      const float4 nb0 = n1 > 8 ? nxt[2] : Z4, nb1 = n1 > 12 ? nxt[3] : Z4;
       bad |= rb > acc;  // the listing's bound must not exceed the chain at the row's start
-      for (int k = 0; k < n; k += 4) {
-        const float4 c = k + 8 < n ? src[(k >> 2) + 2] : Z4;
-        acc = mlp_log_add_t(acc, a.x, lk);  // k < n
-        acc = mlp_log_add_t(acc, k + 1 < n ? a.y : LZ, lk);
-        acc = mlp_log_add_t(acc, k + 2 < n ? a.z : LZ, lk);
-        acc = mlp_log_add_t(acc, k + 3 < n ? a.w : LZ, lk);
-        a = b;
-        b = c;
+      for (int k = 0; k < n; k += 8) {
+        const float4 c0 = k + 16 < n ? src[(k >> 2) + 4] : Z4, c1 = k + 20 < n ? src[(k >> 2) + 5] : Z4;
+        fold4(a0, k);
+        if (k + 4 < n) fold4(a1, k + 4);
+        a0 = b0;
+        a1 = b1;
+        b0 = c0;
+        b1 = c1;
       }
-      a = na;
-      b = nb;
+      a0 = na0;
+      a1 = na1;
+      b0 = nb0;
+      b1 = nb1;
       n = n1;
       n1 = n2;
       rb = rb_next;
@@ -546,9 +559,16 @@ __global__ __launch_bounds__(256) void k_compact(SeqSet sq, PairMeta pm, Scratch
                                                  const int64_t* __restrict__ rowptr_base,
                                                  uint16_t* __restrict__ out_cols,
                                                  float* __restrict__ out_vals, int64_t npairs) {
+  // per wave: the row (lane) of each entry of the current 64-row chunk, and
+  // the rows' first entries, so the chunk's entries are copied 64 consecutive
+  // ones at a time (coalesced stores) instead of one row per lane
+  __shared__ uint8_t rowid_all[kWavesPerBlock][64 * kEll];
+  __shared__ int32_t rstart_all[kWavesPerBlock][64];
   const int64_t p = wave_index();
   if (p >= npairs) return;
   const int lane = threadIdx.x & 63;
+  uint8_t* rowid = rowid_all[threadIdx.x >> 6];
+  int32_t* rstart = rstart_all[threadIdx.x >> 6];
   const int L1 = sq.len[pm.pa[p]];
   const int64_t er0 = pm.ell_row[p];
   const int64_t eb = ent_base[p];
@@ -564,15 +584,25 @@ __global__ __launch_bounds__(256) void k_compact(SeqSet sq, PairMeta pm, Scratch
       const int y = __shfl_up(x, off);
       if (lane >= off) x += y;
     }
-    const int start = run + x - c;
-    if (i <= L1) {
-      rp[i + 1] = start + c;
-      for (int k = 0; k < c; ++k) {
-        out_cols[eb + start + k] = sc.ell_col[(er0 + i - 1) * kEll + k];
-        out_vals[eb + start + k] = sc.ell_val[(er0 + i - 1) * kEll + k];
-      }
+    const int first = x - c;  // within the chunk
+    if (i <= L1) rp[i + 1] = run + x;
+    rstart[lane] = first;
+    for (int k = 0; k < c; ++k) rowid[first + k] = (uint8_t)lane;
+    const int tot = __shfl(x, 63);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int64_t src0 = (er0 + r0 - 1) * kEll;
+    for (int e = lane; e < tot; e += 64) {
+      const int r = rowid[e];
+      const int64_t s = src0 + (int64_t)r * kEll + (e - rstart[r]);
+      out_cols[eb + run + e] = sc.ell_col[s];
+      out_vals[eb + run + e] = sc.ell_val[s];
     }
-    run += __shfl(x, 63);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    run += tot;
   }
 }
 
