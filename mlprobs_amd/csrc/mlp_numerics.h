@@ -181,6 +181,19 @@ __device__ __forceinline__ float mlp_post_from_sum(float s, float T) {
   return mlp_exp_nonpos(v < MLP_LOG_ONE ? v : MLP_LOG_ONE);
 }
 
+// x / 3 correctly rounded for 0 <= x <= 3 (the RMS merge's sum of three
+// squared posteriors) in three instructions instead of the IEEE division
+// sequence (v_div_scale x2, v_rcp, 5 FMAs, v_div_fmas, v_div_fixup): the
+// product with RN(1/3), its exact residual by FMA, one corrected FMA.
+// Checked against RN(x / 3) on every float in [0, 3], denormals included
+// (tests/test_numerics_div3.py; tools/check_div3.py runs the whole range).
+__device__ __forceinline__ float mlp_div3(float x) {
+  const float r = 0x1.555556p-2f;  // RN(1/3)
+  const float q = x * r;
+  const float e = __builtin_fmaf(-q, 3.0f, x);
+  return __builtin_fmaf(e, r, q);
+}
+
 // ---- wave-level neighbour exchange (DPP wave shifts, gfx9 family) --------
 // lane l receives lane l-1's value; lane 0 keeps `old`.
 __device__ __forceinline__ float mlp_shr1(float v, float old) {

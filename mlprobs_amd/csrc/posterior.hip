@@ -738,9 +738,9 @@ __global__ __launch_bounds__(256, MLP_MERGE_WAVES) void k_merge(ModelScalars ms,
             const float v2 = pgv;
             const float v3 = mlp_post_from_sum_t(flv, c.TL, ex);
             if constexpr (NP)
-              P = sqrtf((v2 * v2 + v3 * v3 + v1 * v1) / 3);  // CPNP/MSA.cpp:1699-1708
+              P = sqrtf(mlp_div3(v2 * v2 + v3 * v3 + v1 * v1));  // CPNP/MSA.cpp:1699-1708
             else
-              P = sqrtf((v1 * v1 + v2 * v2 + v3 * v3) / 3);  // CPNP/MSA.cpp:992-1001
+              P = sqrtf(mlp_div3(v1 * v1 + v2 * v2 + v3 * v3));  // CPNP/MSA.cpp:992-1001
           }
         }
         // MEA (CPNP/ProbabilisticModel.h:831-834): value of ChooseBestOfThree
