@@ -58,6 +58,9 @@ constexpr int kPrefetch = 4;
 #ifndef MLP_FWD_WAVES
 #define MLP_FWD_WAVES 5
 #endif
+#ifndef MLP_FWD_INTERIOR  // forward: the edge selects only in wave-steps that touch an edge
+#define MLP_FWD_INTERIOR 1
+#endif
 #ifndef MLP_BWD_WAVES
 #define MLP_BWD_WAVES MLP_SWEEP_WAVES
 #endif
@@ -165,6 +168,14 @@ __global__ __launch_bounds__(256, SweepWaves<M>::fwd) void k_forward(ModelScalar
         const int i = c.i, j = c.j, L1 = c.L1, L2 = c.L2;
         const bool act = c.q >= 0 && j <= L2;
         const bool gen = i > 1 || j > 1;
+        // wave-uniform: no lane on an initial cell, row 0 or column 0 (the
+        // common case away from the pairs' edges), so the recurrences' values
+        // are taken as they are, without the per-lane selects of the edges
+#if MLP_FWD_INTERIOR
+        const bool interior = wave_none(!(i >= 1 && j >= 1 && gen));
+#else
+        const bool interior = false;
+#endif
         const int c1 = c.c1;
         const int c2 = C.seq[c.ca];          // residue j (0 at j = 0 and past L2)
         const float ins1 = c.ins1;
@@ -239,16 +250,20 @@ __global__ __launch_bounds__(256, SweepWaves<M>::fwd) void k_forward(ModelScalar
           const float vy2 = ins2 + mlp_log_add_t(L5[0] + ms.t[0][4], L5[4] + ms.t[4][4], lk);
 #endif
           float Cc[5];
+          if (interior) {  // every lane's cell takes all five recurrences
+            Cc[0] = vm; Cc[1] = vx1; Cc[2] = vy1; Cc[3] = vx2; Cc[4] = vy2;
+          } else {
 #pragma unroll
-          for (int k5 = 0; k5 < 5; ++k5) Cc[k5] = LZ;
-          // CPNP/ProbabilisticModel.h:173-183 initial cells
-          if (i == 1 && j == 1) Cc[0] = ms.init[0] + mt;
-          if (i == 1 && j == 0) { Cc[1] = ms.init[1] + ins1; Cc[3] = ms.init[3] + ins1; }
-          if (i == 0 && j == 1) { Cc[2] = ms.init[2] + ins2; Cc[4] = ms.init[4] + ins2; }
-          if (gen) {
-            if (i > 0 && j > 0) Cc[0] = vm;
-            if (i > 0) { Cc[1] = vx1; Cc[3] = vx2; }
-            if (j > 0) { Cc[2] = vy1; Cc[4] = vy2; }
+            for (int k5 = 0; k5 < 5; ++k5) Cc[k5] = LZ;
+            // CPNP/ProbabilisticModel.h:173-183 initial cells
+            if (i == 1 && j == 1) Cc[0] = ms.init[0] + mt;
+            if (i == 1 && j == 0) { Cc[1] = ms.init[1] + ins1; Cc[3] = ms.init[3] + ins1; }
+            if (i == 0 && j == 1) { Cc[2] = ms.init[2] + ins2; Cc[4] = ms.init[4] + ins2; }
+            if (gen) {
+              if (i > 0 && j > 0) Cc[0] = vm;
+              if (i > 0) { Cc[1] = vx1; Cc[3] = vx2; }
+              if (j > 0) { Cc[2] = vy1; Cc[4] = vy2; }
+            }
           }
           sc.f5[idx] = Cc[0];   // every lane: values of idle cells are never used
           if (act && i == L1 && j == L2) {  // CPNP/ProbabilisticModel.h:415-419 (forward half)
@@ -283,11 +298,15 @@ __global__ __launch_bounds__(256, SweepWaves<M>::fwd) void k_forward(ModelScalar
             vy = mlp_log_add_t(LL[0] + ms.lt[0][2] - rt1, LL[2] + ms.lt[2][2] - rt1, lk);
           }
           float Cm = LZ, Cx = LZ, Cy = LZ;
-          if (i == 1 && j == 1) Cm = bs - two_rt1;
-          if (gen) {
-            if (i > 0 && j > 0) Cm = vm;
-            if (i > 0) Cx = vx;
-            if (j > 0) Cy = vy;
+          if (interior) {
+            Cm = vm; Cx = vx; Cy = vy;
+          } else {
+            if (i == 1 && j == 1) Cm = bs - two_rt1;
+            if (gen) {
+              if (i > 0 && j > 0) Cm = vm;
+              if (i > 0) Cx = vx;
+              if (j > 0) Cy = vy;
+            }
           }
           sc.fl[idx] = Cm;
           if (lane == 63) {
