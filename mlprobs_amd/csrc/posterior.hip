@@ -61,6 +61,9 @@ constexpr int kPrefetch = 4;
 #ifndef MLP_FWD_INTERIOR  // forward: the edge selects only in wave-steps that touch an edge
 #define MLP_FWD_INTERIOR 1
 #endif
+#ifndef MLP_BWD_INTERIOR  // backward: the same
+#define MLP_BWD_INTERIOR 1
+#endif
 #ifndef MLP_BWD_WAVES
 #define MLP_BWD_WAVES MLP_SWEEP_WAVES
 #endif
@@ -455,6 +458,13 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
         const int i = c.i, j = c.j, L1 = c.L1, L2 = c.L2;
         const bool act = c.q >= 0 && j <= L2;
         const bool in_i = i < L1, in_j = j < L2;
+        // wave-uniform: every lane inside its pair (not the last row, column
+        // or cell), so the recurrences run without the edge selects
+#if MLP_BWD_INTERIOR
+        const bool interior = wave_none(!(in_i && in_j && !(i == L1 && j == L2)));
+#else
+        const bool interior = false;
+#endif
         const float f5v = q5[u];
         const double zmv = qz[u];
         const int c1 = c.c1, c1n = c.c1n;
@@ -488,6 +498,20 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
           // CPNP/ProbabilisticModel.h:310-313, 340-378
           const float pxy = G5[0] + mn;
           const bool last = (i == L1 && j == L2);
+#if !MLP_PK
+          if (interior) {  // every lane: in_i, in_j, not the last cell -- no per-lane selects
+#pragma unroll
+            for (int k5 = 0; k5 < 5; ++k5) B[k5] = mlp_log_add_from_zero(pxy + ms.t[k5][0]);
+            B[0] = mlp_log_add_t(B[0], N5[1] + ins1n + ms.t[0][1], lk);
+            B[1] = mlp_log_add_t(B[1], N5[1] + ins1n + ms.t[1][1], lk);
+            B[0] = mlp_log_add_t(B[0], N5[3] + ins1n + ms.t[0][3], lk);
+            B[3] = mlp_log_add_t(B[3], N5[3] + ins1n + ms.t[3][3], lk);
+            B[0] = mlp_log_add_t(B[0], R5[2] + ins2n + ms.t[0][2], lk);
+            B[2] = mlp_log_add_t(B[2], R5[2] + ins2n + ms.t[2][2], lk);
+            B[0] = mlp_log_add_t(B[0], R5[4] + ins2n + ms.t[0][4], lk);
+            B[4] = mlp_log_add_t(B[4], R5[4] + ins2n + ms.t[4][4], lk);
+          } else {
+#endif
 #pragma unroll
           for (int k5 = 0; k5 < 5; ++k5)
             B[k5] = last ? ms.init[k5] : ((in_i && in_j) ? mlp_log_add_from_zero(pxy + ms.t[k5][0]) : LZ);
@@ -522,6 +546,7 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
             B[0] = mlp_log_add_t(B[0], R5[4] + ins2n + ms.t[0][4], lk);
             B[4] = mlp_log_add_t(B[4], R5[4] + ins2n + ms.t[4][4], lk);
           }
+          }  // !interior
 #endif
           sc.f5[idx] = f5v + B[0];   // f + b (CPNP/ProbabilisticModel.h:484)
           if (act) {
@@ -541,6 +566,18 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
           const float ins2n = T_.ins[c2n];
           const float mn = T_.match[c1n * 26 + c2n];
           float Bm = MLP_LOG_ONE, Bx = LZ, By = LZ;
+#if !MLP_PK
+          if (interior) {
+            const float pxy = GL[0] + mn - ins1n - ins2n;
+            Bm = mlp_log_add_t(Bm, pxy + ms.lt[0][0] - two_rt1, lk);
+            Bx = mlp_log_add_from_zero(pxy + ms.lt[1][0] - two_rt1);
+            By = mlp_log_add_from_zero(pxy + ms.lt[2][0] - two_rt1);
+            Bm = mlp_log_add_t(Bm, NL[1] + ms.lt[0][1] - rt1, lk);
+            Bx = mlp_log_add_t(Bx, NL[1] + ms.lt[1][1] - rt1, lk);
+            Bm = mlp_log_add_t(Bm, RL[2] + ms.lt[0][2] - rt1, lk);
+            By = mlp_log_add_t(By, RL[2] + ms.lt[2][2] - rt1, lk);
+          } else {
+#endif
           if (in_i && in_j) {
             const float pxy = GL[0] + mn - ins1n - ins2n;
             Bm = mlp_log_add_t(Bm, pxy + ms.lt[0][0] - two_rt1, lk);
@@ -567,6 +604,7 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
             Bm = mlp_log_add_t(Bm, RL[2] + ms.lt[0][2] - rt1, lk);
             By = mlp_log_add_t(By, RL[2] + ms.lt[2][2] - rt1, lk);
           }
+          }  // !interior
 #endif
           sc.bl[idx] = Bm;   // f + b is formed by the merge (the same float add)
           if (lane == 0) {
