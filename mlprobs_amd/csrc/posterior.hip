@@ -628,11 +628,22 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
           int E = 0;
           float post = 0.0f;
           const double score = T_.sub[c2 * 26 + c1];
+          // wave-uniform: every lane strictly inside rows 2..L1-1, columns 2..L2-1
+#if MLP_BWD_INTERIOR
+          const bool pf_inner = wave_none(!(i >= 2 && i < L1 && j >= 2 && j < L2));
+#else
+          const bool pf_inner = false;
+#endif
           if (i >= 1 && j >= 1) {
             double nZm = NZm, nZe = NZe, nZf = NZf, rZm = RZm, rZe = RZe, rZf = RZf;
             double gZm = GZm, gZe = GZe, gZf = GZf;
             int ne = Ne, re = Re, ge = Ge;
             const double o0 = pfo, e0 = pfe, o1 = pfo, e1 = pfe;
+            if (pf_inner) {  // no lane on row 1, L1 or column 1, L2: no boundary values, general factors
+              E = pf_align_fast(nZm, nZe, nZf, ne, rZm, rZe, rZf, re, gZm, gZe, gZf, ge);
+              Zf = rZm * o1 + rZf * e1;
+              Ze = nZm * o0 + nZe * e0;
+            } else {
             // boundary row L1+1 / column L2+1 (init of CPNP/MSAPartProbs.cpp:217-226)
             if (i == L1) { nZm = 0.0; nZf = 1.0; nZe = 0.0; ne = 0; }
             if (j == L2) { rZm = 0.0; rZf = 0.0; rZe = 1.0; re = 0; }
@@ -648,6 +659,7 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
             const double ze_g = nZm * o0 + nZe * e0, ze_1 = nZm + nZe;
             Zf = (i == 1) ? zf_1 : zf_g;
             Ze = (j == 1) ? ze_1 : ze_g;
+            }
             Zm = ((M & kQP) != 0 ? (gZm + gZe) + gZf : (gZm + gZf) + gZe) * score;  // QP/PartitionFunction.cpp:260
             pf_rescale_fast(Zm, Ze, Zf, E);
             if (act) {
