@@ -737,7 +737,10 @@ __global__ __launch_bounds__(256, MLP_MERGE_WAVES) void k_merge(ModelScalars ms,
   // MEA boundary row (stacked row 64k - 1), double-buffered as in BoundaryChunks
   float bch = 0.f, bnx = 0.f;
   int cch = 0, cnx = 0;
-  constexpr int QD = 8;
+#ifndef MLP_MERGE_QD
+#define MLP_MERGE_QD 8
+#endif
+  constexpr int QD = MLP_MERGE_QD;
   // fixed-register load queue: slot u serves steps t0 + u (segments hold
   // whole groups of QD steps); values of idle cells are never used
   float q5[QD] = {}, ql[QD] = {}, qb[QD] = {}, qg[QD] = {};
