@@ -737,10 +737,7 @@ __global__ __launch_bounds__(256, MLP_MERGE_WAVES) void k_merge(ModelScalars ms,
   // MEA boundary row (stacked row 64k - 1), double-buffered as in BoundaryChunks
   float bch = 0.f, bnx = 0.f;
   int cch = 0, cnx = 0;
-#ifndef MLP_MERGE_QD
-#define MLP_MERGE_QD 8
-#endif
-  constexpr int QD = MLP_MERGE_QD;
+  constexpr int QD = 8;  // divides every segment (chain widths are multiples of 8): 12 or 16 break the queue
   // fixed-register load queue: slot u serves steps t0 + u (segments hold
   // whole groups of QD steps); values of idle cells are never used
   float q5[QD] = {}, ql[QD] = {}, qb[QD] = {}, qg[QD] = {};
