@@ -826,7 +826,7 @@ def main():
     qp_info = quickprobs_stage(fam, fam_in, total_cells, args) if (world == 1 and not args.no_qp) else None
     shards_info = None
     if world == 1 and not args.no_shards:
-        # the main context's batch scratch (45% of the device) goes first: the
+        # the main context's batch scratch (most of the device) goes first: the
         # 8 shard contexts need their own
         fam.close()
         fam = None

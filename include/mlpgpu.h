@@ -83,8 +83,10 @@ int mlp_set_shards(mlp_ctx *ctx, int nshards);
 int mlp_shard_count(mlp_ctx *ctx);
 void mlp_ctx_destroy(mlp_ctx *ctx);
 const char *mlp_last_error(const mlp_ctx *ctx);
-/* Device bytes the posterior stage may hold as batch scratch (default: 45%
- * of the device; larger batches shorten the per-batch kernel tails).  A
+/* Device bytes the posterior stage may hold as batch scratch (default: the
+ * device's free HBM less a reserve of max(16 GiB, 7%) for the store and the
+ * relaxation, ~224 GiB on MI355X; larger batches shorten the per-batch
+ * kernel tails).  A
  * one-shot process (the c_p_np_aln drop-in) asks for less: a fresh process's
  * large allocation waits while the driver clears memory another process just
  * released.  No reference counterpart (the reference allocates per pair). */

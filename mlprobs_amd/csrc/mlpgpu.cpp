@@ -403,13 +403,20 @@ int mlp_ctx_create(int device, mlp_ctx** out) {
   }
   size_t freeb = 0, total = 0;
   hipMemGetInfo(&freeb, &total);
-  // half of the free HBM for per-batch scratch (the rest: CSR store, relaxation
-  // buffers): larger batches keep every SIMD busy through the serial
-  // local-total chains and shorten the per-batch tails
-  // (free memory may read low for a while after another process released a
-  // large allocation -- the driver clears it lazily -- so plan with at least
-  // 45% of the device; an allocation that really fails halves the budget)
-  c->scratch_budget = std::max<size_t>(freeb, total / 10 * 9) / 2;
+  // per-batch scratch: the free HBM less a reserve for the CSR store and the
+  // relaxation's own buffers (its temporaries are carved from this scratch
+  // when it is idle): larger batches keep every SIMD busy through the serial
+  // local-total chains and shorten the per-batch tails -- on MI355X ~224 GiB,
+  // the C3 posterior stage in three batches instead of five (step 576 -> 545-557
+  // ms, totals 61 -> 48.5 ms; round 4 measured half the free HBM until then).
+  // Free memory may read low for a while after another process released a
+  // large allocation (the driver clears it lazily), so plan with at least 90%
+  // of the device; an allocation that really fails halves the budget.
+  {
+    const size_t usable = std::max<size_t>(freeb, total / 10 * 9);
+    const size_t reserve = std::max<size_t>(16ull << 30, usable / 100 * 7);
+    c->scratch_budget = usable > 2 * reserve ? usable - reserve : usable / 2;
+  }
   if (const char* s = getenv("MLP_SCRATCH_GB")) c->scratch_budget = (size_t)(atof(s) * (1ull << 30));
   *out = c;
   return MLP_OK;
