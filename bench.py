@@ -490,6 +490,11 @@ def shard_gather(args, seqs, post_hash=None, relax_hash=None):
     xGMI on a multi-GPU box."""
     from mlprobs_amd.engine import Family
     fam = Family(seqs, shards=8)
+    # the 8 shards split the parent's scratch budget; with the library's
+    # default (most of the device) plus 9 copies of the store the device runs
+    # full and the gather stalls (411 ms against 17 ms, round 4): the round-3
+    # budget, 120 GiB, leaves the copies room
+    fam.set_scratch(120 << 30)
     # twice: the first stage allocates the shards' scratch and store copies
     # (a fresh allocation can stall ~5.7 s while the driver releases what the
     # bench's own stage freed, DESIGN.md section 3), the second is warm
