@@ -72,7 +72,8 @@ def main(d):
 
 
 GROUPS = {'forward': ('k_forward',), 'backward': ('k_backward', 'k_fold_totals'),
-          'local_totals': ('k_local_totals',), 'merge_mea_sparsify': ('k_merge',), 'compact': ('k_compact',)}
+          'local_totals': ('k_local_totals', 'k_local_bounds', 'k_local_list', 'k_local_fold'),
+          'merge_mea_sparsify': ('k_merge',), 'compact': ('k_compact',)}
 
 
 def groups(o, d):
