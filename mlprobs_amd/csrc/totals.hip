@@ -359,8 +359,11 @@ __device__ __forceinline__ float* lanefold_area(const Scratch& sc, int64_t cell_
 // rounded up to 4 floats, from the first 16-byte boundary of the pair's slots
 // ((L1 + 1) W >= (L1 + 1)(L2 + 1) slots of 8 bytes hold 16 + 4 L1 RS bytes).
 __device__ __forceinline__ float* lanefold_rows(const Scratch& sc, int64_t cell_off, int row0, int W) {
-  const uintptr_t a = reinterpret_cast<uintptr_t>(sc.zm + cell_off + (int64_t)row0 * W);
-  return reinterpret_cast<float*>((a + 15) & ~static_cast<uintptr_t>(15));
+  // (pointer arithmetic from the slot, not an integer round trip: the
+  // compiler keeps the global address space -- global, not flat, loads)
+  float* const b = reinterpret_cast<float*>(sc.zm + cell_off + (int64_t)row0 * W);
+  const int mis = (int)((reinterpret_cast<uintptr_t>(b) >> 2) & 3);
+  return b + ((4 - mis) & 3);
 }
 __device__ __forceinline__ int lanefold_rs(int L2) { return (L2 + 3) & ~3; }
 
@@ -479,13 +482,15 @@ __global__ __launch_bounds__(256) void k_local_fold(SeqSet sq, PairMeta pm, Chai
     // pair, so the kernel lasts as long as the longest chain and every load
     // the chain waits for adds to it.  Within a row, eight elements per step
     // with the next 16 in flight; the next row's first 16 (its count read
-    // two rows ahead) loaded at the row's start.
+    // two rows ahead) loaded at the row's start.  The loads are unconditional
+    // (elements past a row's count are masked where they are folded; the
+    // reads stay inside the pair's slots or, past its last row, inside the
+    // batch scratch): predicated loads made every wait a vmcnt(0).
     const float4* __restrict__ rows4 = reinterpret_cast<const float4*>(lanefold_rows(sc, cm.cell_off[h], pm.row0[p], cm.width[h]));
     const int RS4 = lanefold_rs(L2) >> 2;
     const float4 Z4 = make_float4(LZ, LZ, LZ, LZ);
-    int n1 = L1 > 1 ? sc.ell_cnt[ell + 1] : 0;
-    float4 a0 = n > 0 ? rows4[0] : Z4, a1 = n > 4 ? rows4[1] : Z4;
-    float4 b0 = n > 8 ? rows4[2] : Z4, b1 = n > 12 ? rows4[3] : Z4;
+    int n1 = sc.ell_cnt[ell + min(1, L1 - 1)];
+    float4 a0 = rows4[0], a1 = rows4[1], b0 = rows4[2], b1 = rows4[3];
     auto fold4 = [&](const float4 v, int k) {
       acc = mlp_log_add_t(acc, k < n ? v.x : LZ, lk);
       acc = mlp_log_add_t(acc, k + 1 < n ? v.y : LZ, lk);
@@ -495,13 +500,12 @@ __global__ __launch_bounds__(256) void k_local_fold(SeqSet sq, PairMeta pm, Chai
     for (int i = 1; i <= L1; ++i) {
       const float4* __restrict__ src = rows4 + (int64_t)(i - 1) * RS4;
       const float4* __restrict__ nxt = src + RS4;
-      const int n2 = i + 1 < L1 ? sc.ell_cnt[ell + i + 1] : 0;
-      const float rb_next = i < L1 ? sc.crb[ell + i] : LZ;
-      const float4 na0 = n1 > 0 ? nxt[0] : Z4, na1 = n1 > 4 ? nxt[1] : Z4;
-      const float4 nb0 = n1 > 8 ? nxt[2] : Z4, nb1 = n1 > 12 ? nxt[3] : Z4;
+      const int n2 = sc.ell_cnt[ell + min(i + 1, L1 - 1)];  // (past the last row: unused)
+      const float rb_next = sc.crb[ell + min(i, L1 - 1)];
+      const float4 na0 = nxt[0], na1 = nxt[1], nb0 = nxt[2], nb1 = nxt[3];
       bad |= rb > acc;  // the listing's bound must not exceed the chain at the row's start
       for (int k = 0; k < n; k += 8) {
-        const float4 c0 = k + 16 < n ? src[(k >> 2) + 4] : Z4, c1 = k + 20 < n ? src[(k >> 2) + 5] : Z4;
+        const float4 c0 = src[(k >> 2) + 4], c1 = src[(k >> 2) + 5];
         fold4(a0, k);
         if (k + 4 < n) fold4(a1, k + 4);
         a0 = b0;
