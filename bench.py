@@ -27,7 +27,12 @@ sys.path.insert(0, ROOT)
 METRIC = 'pair-HMM DP cell updates/s (all-pairs) + end-to-end MSA sec/family'
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 # VALU issue peak: 256 CUs x 4 SIMD-32 x 2.4 GHz, one wave64 VALU instruction
-# per 2 cycles per SIMD (MI355X_MICROARCH.md, "Wave scheduling")
+# per 2 cycles per SIMD (MI355X_MICROARCH.md, "Wave scheduling").  Measured
+# (tools/probe/valu_rate, profiles/r05c_valu_rate_operands.json): v_add / mul /
+# fma_f32, v_add_u32, v_and, v_bitop3 with VGPR, literal or inline operands at
+# 2.3-2.5 cycles (1.0-1.1e12 wave-instr/s at 8 waves per SIMD); any VALU
+# instruction with an SGPR operand, v_max / min_f32, v_cvt_i32_f32, v_bcnt,
+# v_lshl_add, v_mov_dpp, f64 and packed f32 at 4.3-4.5 cycles (half this peak)
 VALU_PEAK_WAVE_INSTS = 256 * 4 * 2.4e9 / 2
 # Algorithmic HBM bytes per pair-cell for each kernel of the pid-0 pipeline
 # ("Kernels and their rooflines"), round-3 layout: the forward
@@ -43,7 +48,7 @@ def parse():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=3)
     ap.add_argument('--warmup', type=int, default=1)
-    ap.add_argument('--n', type=int, default=512)
+    ap.add_argument('--n', '--nseq', dest='n', type=int, default=512)  # (--nseq: under torchrun, --n is ambiguous)
     ap.add_argument('--len', type=int, default=400)
     ap.add_argument('--s', type=float, default=0.7)
     ap.add_argument('--seed', type=int, default=11)
@@ -67,6 +72,9 @@ def parse():
                     help='reference-CLI leg of C5: every family (minutes), a sample (every 8th family plus the '
                          'heavy golden families; default) or none')
     ap.add_argument('--only-c5', action='store_true', help='run the C5 leg only and print its JSON')
+    ap.add_argument('--host', action='store_true',
+                    help='N ranks on host contexts over gloo: the CPU dry run of the multi-rank path '
+                         '(tests/test_multirank_cpu.py); no GPU')
     return ap.parse_args()
 
 
@@ -168,15 +176,146 @@ def cpu_baseline(fasta, args, n, lens, store, gpu_dist):
             'sample': f'first {args.cpu_pairs} pairs, {dt:.1f} s, oracle port'}, None
 
 
-def store_hash(fam):
+def store_hash(fam, results=True):
     """sha256 over the canonical store and the per-pair results (distances,
     MEA scores, entry counts): the bit-identity check between the unsharded
-    and the virtually sharded runs."""
+    and the virtually sharded runs (results=False: the store alone, which is
+    what the host dry run's gloo exchange carries)."""
     import hashlib
     h = hashlib.sha256()
-    for a in list(fam.export()) + list(fam.results()):
+    for a in list(fam.export()) + (list(fam.results()) if results else []):
         h.update(np.ascontiguousarray(a).tobytes())
     return h.hexdigest()
+
+
+class RankExchange:
+    """The exchange steps of the N-rank run.  On GPUs the library's own: the
+    RCCL all-gather of the posterior store (mlp_allgather) and mlp_relax,
+    which relaxes this rank's MAC-balanced output range and all-gathers after
+    the round, both timed by the library's kernel timers ('allgather').  With
+    --host (the CPU dry run) the same placement over gloo: each rank's CSR
+    block goes where mlp_gather_layout puts it and the gathered store is
+    imported back (mlp_csr_import), timed on the host clock -- what
+    tests/test_multirank_cpu.py checks against the single-process store."""
+
+    def __init__(self, fam, world, rank, dist, host):
+        self.fam, self.world, self.rank, self.dist, self.host = fam, world, rank, dist, host
+        self.host_gather_s = 0.0
+        self.received_bytes = 0
+
+    def _place(self, r0, r1):
+        from mlprobs_amd import engine
+        f = self.fam
+        rp_full, eo, cols, vals = f.export()
+        rp = rp_full[f.rp_off[r0]:f.rp_off[r1]].astype(np.int32)
+        blk = (rp, cols[int(eo[r0]):int(eo[r1])].copy(), vals[int(eo[r0]):int(eo[r1])].copy())
+        shards = [None] * self.world
+        self.dist.all_gather_object(shards, (r0, r1, int(len(blk[1]))))
+        ebase = engine.gather_layout(f.npairs, shards)
+        blocks = [None] * self.world
+        self.dist.all_gather_object(blocks, blk)
+        g_rp = np.concatenate([b[0] for b in blocks])
+        g_cols = np.zeros(int(ebase[-1]), np.uint16)
+        g_vals = np.zeros(int(ebase[-1]), np.float32)
+        for r, b in enumerate(blocks):
+            g_cols[ebase[r]:ebase[r + 1]] = b[1]
+            g_vals[ebase[r]:ebase[r + 1]] = b[2]
+        g_eo = np.zeros(f.npairs + 1, np.int64)
+        g_eo[1:] = np.cumsum(g_rp[np.asarray(f.rp_off[1:], np.int64) - 1])
+        f.import_csr(g_rp, g_eo, g_cols, g_vals)
+
+    def gather(self, p0, p1):
+        """After this rank's posterior range: every rank's block everywhere."""
+        if not self.host:
+            self.fam.allgather()
+            return
+        t0 = time.perf_counter()
+        self._place(p0, p1)
+        self.host_gather_s += time.perf_counter() - t0
+
+    def relax_round(self, lens):
+        """One consistency round over this rank's output range, then the gather."""
+        if not self.host:
+            self.fam.relax(1)
+            return
+        from mlprobs_amd import engine
+        _, eo, _, _ = self.fam.export()
+        bounds = engine.relax_shard_plan(np.asarray(lens, np.int32), np.diff(eo), self.world)
+        r0, r1 = int(bounds[self.rank]), int(bounds[self.rank + 1])
+        self.fam.relax_range(r0, r1)
+        t0 = time.perf_counter()
+        self._place(r0, r1)
+        self.host_gather_s += time.perf_counter() - t0
+
+    def gather_ms(self, kt):
+        return self.host_gather_s * 1e3 if self.host else kt['allgather']['ms']
+
+    def reset(self):
+        self.host_gather_s = 0.0
+
+
+def store_bytes(fam, p0=0, p1=None):
+    """Bytes of the canonical store of pairs [p0, p1): entries (uint16 column
+    + fp32 value), row pointers (int32) and per-pair results (distance, MEA
+    score, entry count: 16 B) -- what the all-gather moves."""
+    p1 = fam.npairs if p1 is None else p1
+    nnz = fam.results()[2]
+    return (int(nnz[p0:p1].sum()) * 6 + int(fam.rp_off[p1] - fam.rp_off[p0]) * 4 + (p1 - p0) * 16)
+
+
+def group_roofline(kt, steps):
+    """The dominant kernel group of this rank's posterior stage and its HBM
+    roofline (algorithmic bytes per launch / average launch time)."""
+    cand = [k for k in ALGO_BYTES if kt[k]['launches']]
+    if not cand:
+        return None
+    dom = max(cand, key=lambda k: kt[k]['ms'])
+    launches = max(kt[dom]['launches'], 1)
+    avg_ms = kt[dom]['ms'] / launches
+    achieved = ALGO_BYTES[dom] * kt[dom]['cells'] / launches / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+    return {'bound': 'hbm', 'kernel': dom, 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+            'frac': achieved / HBM_PEAK_GBS, 'avg_launch_ms': avg_ms, 'algo_bytes_per_cell': ALGO_BYTES[dom]}
+
+
+def multirank_legs(fam, ex, args, world, rank, dist, lens, p0, p1, dt, kt, sync):
+    """Per-rank records of the N-rank run (rank 0 gets the list): pairs,
+    pair-cells, posterior and all-gather time per step, the bytes the gather
+    brought in and its rate, the rank's dominant kernel roofline; then
+    args.relax consistency rounds, each timed as the max over ranks with its
+    per-rank relaxation-kernel and gather times."""
+    gms = ex.gather_ms(kt) / args.steps
+    recv = store_bytes(fam) - store_bytes(fam, p0, p1)
+    cells = int(sum((lens[a] + 1) * (lens[b] + 1) for a, b in
+                    __import__('mlprobs_amd.engine', fromlist=['x']).pairs_of(len(lens))[p0:p1]))
+    me = {'rank': rank, 'pairs': p1 - p0, 'pair_cells': cells,
+          'step_ms': dt / args.steps * 1e3, 'gather_ms': gms,
+          'posterior_ms': dt / args.steps * 1e3 - gms, 'gather_bytes_in': recv,
+          'gather_GBps': recv / (gms * 1e-3) / 1e9 if gms > 0 else None,
+          'kernels_ms_per_step': {k: v['ms'] / args.steps for k, v in kt.items() if v['launches']},
+          'roofline': group_roofline(kt, args.steps),
+          'store_hash': store_hash(fam, results=False)}  # every rank must hold the same gathered store
+    ranks = [None] * world
+    dist.all_gather_object(ranks, me)
+    relax = None
+    if args.relax > 0:
+        per = []
+        for _ in range(args.relax):
+            fam.profile(True)
+            ex.reset()
+            sync()
+            t0 = time.perf_counter()
+            ex.relax_round(lens)
+            sync()
+            rdt = time.perf_counter() - t0
+            kr = fam.kernel_times()
+            mine = {'rank': rank, 'seconds': rdt, 'relax_kernel_ms': kr['relax']['ms'], 'gather_ms': ex.gather_ms(kr),
+                    'store_hash': store_hash(fam, results=False)}
+            allr = [None] * world
+            dist.all_gather_object(allr, mine)
+            per.append({'seconds': max(r['seconds'] for r in allr), 'gather_ms': max(r['gather_ms'] for r in allr),
+                        'nnz_out': int(fam.results()[2].sum()), 'ranks': allr})
+        relax = {'rounds': len(per), 'per_round': per, 'seconds': sum(r['seconds'] for r in per)}
+    return ranks, relax
 
 
 def relax_work(n, lens, store):
@@ -739,8 +878,11 @@ def main():
     if world > 1:
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        if args.host:
+            dist.init_process_group('gloo')
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group('nccl', device_id=torch.device('cuda', local))
     from mlprobs_amd import synth
     from mlprobs_amd.engine import Family
 
@@ -750,21 +892,22 @@ def main():
     if args.only_c5:
         print(json.dumps({'c5_pipeline': c5_pipeline(args)}))
         return
-    stream = hbm_stream() if world == 1 else None
+    stream = hbm_stream() if (world == 1 and not args.host) else None
     e2e = e2e_families(args) if (not args.no_e2e and world == 1) else None
     c5 = c5_pipeline(args) if (not args.no_e2e and not args.no_c5 and world == 1 and rank == 0) else None
     if args.relax < 0:
-        args.relax = 4 if world == 1 else 0
+        args.relax = 4 if world == 1 else 1
     fam_in = synth.family(args.n, args.len, args.s, seed=args.seed)
     seqs = [s for _, s in fam_in]
     lens = np.array([len(s) for s in seqs], np.int64)
-    fam = Family(seqs, device=local if world > 1 else 0)
-    if world > 1:
+    fam = Family(seqs, host=True) if args.host else Family(seqs, device=local if world > 1 else 0)
+    if world > 1 and not args.host:
         uid = Family.unique_id() if rank == 0 else None
         obj = [uid]
         dist.broadcast_object_list(obj, src=0)
         fam.comm_init(obj[0], world, rank)
     p0, p1 = fam.shard(world, rank)
+    ex = RankExchange(fam, world, rank, dist, args.host) if world > 1 else None
     total_cells = 0
     for a in range(args.n):
         total_cells += int(((lens[a] + 1) * (lens[a + 1:] + 1)).sum())
@@ -772,13 +915,14 @@ def main():
     def step():
         fam.posteriors(args.pid, args.delta, p0, p1)
         if world > 1:
-            fam.allgather()
+            ex.gather(p0, p1)
 
     def barrier():
         fam.synchronize()
         if world > 1:
-            import torch
-            torch.cuda.synchronize()
+            if not args.host:
+                import torch
+                torch.cuda.synchronize()
             dist.barrier()
 
     log('posterior stage')
@@ -786,18 +930,25 @@ def main():
         fam.profile(False)
         step()
     fam.profile(True)
+    if ex:
+        ex.reset()
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     barrier()
     dt = time.perf_counter() - t0
+    dt_rank = dt
     if world > 1:
         import torch
-        t = torch.tensor([dt], dtype=torch.float64, device='cuda')
+        t = torch.tensor([dt], dtype=torch.float64, device='cpu' if args.host else 'cuda')
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     kt = fam.kernel_times()
+    ranks_info, relax_multi = None, None
+    if world > 1:
+        log('per-rank records and consistency rounds')
+        ranks_info, relax_multi = multirank_legs(fam, ex, args, world, rank, dist, lens, p0, p1, dt_rank, kt, barrier)
     gpu_dist, _, nnz = fam.results()  # posterior-stage sparse set (before any relaxation)
     gpu_dist, nnz = gpu_dist.copy(), nnz.copy()
     # the posterior store, kept for the same-run parity readouts (rank 0)
@@ -811,13 +962,13 @@ def main():
     launches = max(kt[dom]['launches'], 1)
     avg_ms = kt[dom]['ms'] / launches
     bytes_per_launch = ALGO_BYTES[dom] * kt[dom]['cells'] / launches
-    achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
+    achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     # measured HBM bytes and VALU instructions per pair-cell of this kernel
     # group from the committed PMC passes (tools/pmc_run.sh), scaled to the
     # cells of one launch here
     traffic, valu = None, None
     pmc = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
-    if os.path.exists(pmc):
+    if os.path.exists(pmc) and avg_ms > 0:
         with open(pmc) as fh:
             g = json.load(fh).get(dom)
         if g:
@@ -828,9 +979,9 @@ def main():
                     'frac': issued / VALU_PEAK_WAVE_INSTS,
                     'insts_per_cell': g['valu_insts_per_cell']}
     log('quickprobs stage')
-    qp_info = quickprobs_stage(fam, fam_in, total_cells, args) if (world == 1 and not args.no_qp) else None
+    qp_info = quickprobs_stage(fam, fam_in, total_cells, args) if (world == 1 and not args.no_qp and not args.host) else None
     shards_info = None
-    if world == 1 and not args.no_shards:
+    if world == 1 and not args.no_shards and not args.host:
         # the main context's batch scratch (most of the device) goes first: the
         # 8 shard contexts need their own
         fam.close()
@@ -899,6 +1050,20 @@ def main():
             out['quickprobs'] = qp_info
         if shards_info is not None:
             out['virtual_shards'] = shards_info
+        if ranks_info is not None:
+            out['ranks'] = ranks_info
+            out['gather_ms'] = max(r['gather_ms'] for r in ranks_info)
+            moved = sum(r['gather_bytes_in'] for r in ranks_info)
+            out['gather_GBps'] = moved / (out['gather_ms'] * 1e-3) / 1e9 if out['gather_ms'] > 0 else None
+            out['gather_note'] = ('per step: max over ranks of the all-gather time; gather_GBps = bytes all ranks '
+                                  'received / that time' + (' (host dry run over gloo)' if args.host else
+                                                            ' (RCCL over xGMI)'))
+            out['ranks_identical'] = len({r['store_hash'] for r in ranks_info}) == 1 and all(
+                len({r['store_hash'] for r in rr['ranks']}) == 1 for rr in (relax_multi or {}).get('per_round', []))
+            if relax_multi is not None:
+                out['relax'] = relax_multi
+            if args.host:
+                out['data'] = 'synthetic (host contexts over gloo: CPU dry run, not a GPU measurement)'
         print(json.dumps(out))
     if fam is not None:
         fam.close()

@@ -17,9 +17,6 @@ namespace mlp {
 // tables are 3 KB, the PF factors 5.4 KB).
 template <bool H> struct LdsHmmPart {
   float4 lk[kLookupRows];
-#if MLP_PK
-  float4 lk2[2 * kLookupRows * kLookupRows];  // interval pairs (mlp_log_add_t2)
-#endif
   float match[26 * 26];
 };
 template <> struct LdsHmmPart<false> {};
@@ -44,9 +41,6 @@ __device__ __forceinline__ void stage_tables(LdsTablesT<H, P>& L, const Tables* 
   if (threadIdx.x < 26) L.ins[threadIdx.x] = tab->ins[threadIdx.x];
   if constexpr (H) {
     if (threadIdx.x == 0) mlp_lookup_table(L.lk);
-#if MLP_PK
-    for (int e = threadIdx.x; e < kLookupRows * kLookupRows; e += blockDim.x) mlp_lookup_table2_entry(L.lk2, e);
-#endif
   }
   __syncthreads();
 }
@@ -54,13 +48,6 @@ template <bool H, bool P>
 __device__ __forceinline__ const float4* lookup_of(const LdsTablesT<H, P>& L) {
   if constexpr (H) return L.lk;
   else return nullptr;
-}
-template <bool H, bool P>
-__device__ __forceinline__ const float4* lookup2_of(const LdsTablesT<H, P>& L) {
-#if MLP_PK
-  if constexpr (H) return L.lk2;
-#endif
-  return nullptr;
 }
 
 __device__ __forceinline__ int64_t wave_index() {
@@ -266,9 +253,6 @@ __device__ __forceinline__ void cursor_prev(Cursor& c, const ChainView& C, const
 // stores issued since (vmcnt is in order on gfx9).  Column indices are
 // clamped to the chain's W columns; columns a lane must not use are never
 // consumed by an active cell.
-#ifndef MLP_BND_ROTATE
-#define MLP_BND_ROTATE 1
-#endif
 template <int M>
 struct BoundaryChunks {
   float c5[5], n5[5], cl[3], nl[3];
@@ -306,51 +290,37 @@ struct BoundaryChunks {
   // toward lane 63 backward), so that column is always in the vacated lane
   // and enters through the DPP shift's `old` operand: no readlane per value.
   // TAKE steps of a segment run consecutively from its first column.
-  // (MLP_BND_ROTATE=0: the column read with readlane instead, round 3.)
+  // (Round 3 read the column with readlane instead.)
   template <bool SHR, bool TAKE>
   __device__ __forceinline__ void shift(int q, const float* S5, float* X5, const float* SL, float* XL,
                                         double sZm, double sZe, double sZf, int se,
                                         double& Zm, double& Ze, double& Zf, int& e) {
-#if MLP_BND_ROTATE
     (void)q;
-#define MLP_BC(c) (c)
-#define MLP_BCD(c) (c)
-#define MLP_BCI(c) (c)
-#else
-#define MLP_BC(c) readlane_f(c, q)
-#define MLP_BCD(c) readlane_d(c, q)
-#define MLP_BCI(c) __builtin_amdgcn_readlane(c, q)
-#endif
     if constexpr ((M & kHmm5) != 0) {
 #pragma unroll
       for (int k = 0; k < 5; ++k) {
-        X5[k] = TAKE ? (SHR ? mlp_shr1(S5[k], MLP_BC(c5[k])) : mlp_shl1(S5[k], MLP_BC(c5[k])))
+        X5[k] = TAKE ? (SHR ? mlp_shr1(S5[k], c5[k]) : mlp_shl1(S5[k], c5[k]))
                      : (SHR ? mlp_shr1z(S5[k]) : mlp_shl1z(S5[k]));
-        if (TAKE && MLP_BND_ROTATE) c5[k] = SHR ? mlp_shl1z(c5[k]) : mlp_shr1z(c5[k]);
+        if (TAKE) c5[k] = SHR ? mlp_shl1z(c5[k]) : mlp_shr1z(c5[k]);
       }
     }
     if constexpr ((M & kLocal) != 0) {
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
-        XL[k] = TAKE ? (SHR ? mlp_shr1(SL[k], MLP_BC(cl[k])) : mlp_shl1(SL[k], MLP_BC(cl[k])))
+        XL[k] = TAKE ? (SHR ? mlp_shr1(SL[k], cl[k]) : mlp_shl1(SL[k], cl[k]))
                      : (SHR ? mlp_shr1z(SL[k]) : mlp_shl1z(SL[k]));
-        if (TAKE && MLP_BND_ROTATE) cl[k] = SHR ? mlp_shl1z(cl[k]) : mlp_shr1z(cl[k]);
+        if (TAKE) cl[k] = SHR ? mlp_shl1z(cl[k]) : mlp_shr1z(cl[k]);
       }
     }
     if constexpr ((M & kPF) != 0) {
       if constexpr (TAKE) {
-        Zm = SHR ? mlp_shr1d(sZm, MLP_BCD(cz[0])) : mlp_shl1d(sZm, MLP_BCD(cz[0]));
-        Ze = SHR ? mlp_shr1d(sZe, MLP_BCD(cz[1])) : mlp_shl1d(sZe, MLP_BCD(cz[1]));
-        Zf = SHR ? mlp_shr1d(sZf, MLP_BCD(cz[2])) : mlp_shl1d(sZf, MLP_BCD(cz[2]));
-        e = SHR ? mlp_shr1i(se, MLP_BCI(ce)) : mlp_shl1i(se, MLP_BCI(ce));
-        if (MLP_BND_ROTATE) {
+        Zm = SHR ? mlp_shr1d(sZm, cz[0]) : mlp_shl1d(sZm, cz[0]);
+        Ze = SHR ? mlp_shr1d(sZe, cz[1]) : mlp_shl1d(sZe, cz[1]);
+        Zf = SHR ? mlp_shr1d(sZf, cz[2]) : mlp_shl1d(sZf, cz[2]);
+        e = SHR ? mlp_shr1i(se, ce) : mlp_shl1i(se, ce);
 #pragma unroll
-          for (int k = 0; k < 3; ++k) cz[k] = SHR ? mlp_shl1zd(cz[k]) : mlp_shr1zd(cz[k]);
-          ce = SHR ? mlp_shl1zi(ce) : mlp_shr1zi(ce);
-        }
-#undef MLP_BC
-#undef MLP_BCD
-#undef MLP_BCI
+        for (int k = 0; k < 3; ++k) cz[k] = SHR ? mlp_shl1zd(cz[k]) : mlp_shr1zd(cz[k]);
+        ce = SHR ? mlp_shl1zi(ce) : mlp_shr1zi(ce);
       } else {
         Zm = SHR ? mlp_shr1zd(sZm) : mlp_shl1zd(sZm);
         Ze = SHR ? mlp_shr1zd(sZe) : mlp_shl1zd(sZe);

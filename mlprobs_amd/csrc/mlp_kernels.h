@@ -133,6 +133,7 @@ struct Scratch {
   // k_local_totals to redo
   float* crb;
   int32_t* rep;
+  int32_t force_repair;    // test hook (MLP_TOT_FORCE_REPAIR): every pair goes to the repair list
   float* bnd5;             // chain boundary row: 5 floats per column
   float* bndl;             // 3 floats per column
   double* bndz;            // 3 doubles per column
@@ -193,19 +194,21 @@ hipError_t launch_backward(int models, const ModelScalars& ms, const Tables* tab
                            int lds_seq, int64_t npairs, hipStream_t st, const SideStream* side);
 hipError_t launch_local_totals(const ModelScalars& ms, const Tables* tab, SeqSet seqs, PairMeta pm, ChainMeta cm,
                                PairRec* rec, Scratch sc, int64_t npairs, int nwaves, hipStream_t st);
-// The same totals with the forward chain folded one pair per lane (models
-// with the partition function: the candidates go to the dead PF forward Zm
-// slots): bounds, listing + backward chain, fold, repair of failed bounds.
-hipError_t launch_local_totals_lanefold(const ModelScalars& ms, const Tables* tab, SeqSet seqs, PairMeta pm,
-                                        ChainMeta cm, PairRec* rec, Scratch sc, int64_t npairs, int nwaves,
-                                        hipStream_t st);
+// The same totals with the forward chain folded one pair per lane: its half
+// between the forward and the backward sweeps (bounds, listing into the
+// still-dead local backward array, fold), the rest after the backward sweep
+// (backward chains, repair of failed bounds).
+hipError_t launch_local_fwd_lanefold(SeqSet seqs, PairMeta pm, ChainMeta cm, PairRec* rec, Scratch sc, int64_t npairs,
+                                     int nwaves, hipStream_t st);
+hipError_t launch_local_bwd_lanefold(const ModelScalars& ms, const Tables* tab, SeqSet seqs, PairMeta pm, ChainMeta cm,
+                                     PairRec* rec, Scratch sc, int64_t npairs, int nwaves, hipStream_t st);
+// bytes after the local backward array the lane fold's unconditional
+// read-ahead may touch past a batch's last pair (24 floats, rounded up)
+constexpr size_t kLaneFoldPad = 256;
 // resident waves of k_local_totals (persistent: each takes pairs off a counter)
 constexpr int kTotalsWaves = 8192;
 // chunk maxima per pair row (columns 1..L2 in chunks of 64)
 __host__ __device__ constexpr int local_chunks(int L2) { return (L2 + 63) >> 6; }
-#ifdef MLP_EXP_TOT_STATS
-void tot_stats_print();
-#endif
 hipError_t launch_fold_totals(const ModelScalars& ms, const Tables* tab, SeqSet seqs, PairMeta pm,
                               PairRec* rec, int64_t npairs, hipStream_t st);
 hipError_t launch_merge(int models, int pid, const ModelScalars& ms, SeqSet seqs, PairMeta pm,

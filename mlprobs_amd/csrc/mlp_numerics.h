@@ -60,48 +60,10 @@ constexpr int kLookupRows = 16;
 __device__ __forceinline__ float mlp_log_add_t(float x, float y, const float4* __restrict__ lk) {
   const float hi = fmaxf(x, y), lo = fminf(x, y);
   const float d = hi - lo;
-#ifdef MLP_EXP_CONSTLK  // timing experiment only (wrong results): no table read
-  const float4 c = make_float4(-0.009350833524763f, 0.130659527668286f, 0.498799810682272f, 0.693203116424741f);
-  (void)lk;
-#else
   const int q = (int)fminf(d * 0x1.fffffep0f, 15.0f);
   const float4 c = lk[q];
-#endif
   const float r = (((c.x * d + c.y) * d + c.z) * d + c.w) + lo;
   return (d >= 7.5f) ? hi : r;
-}
-
-// Two independent LOG_ADDs at once (MLP_PK): the subtraction, the interval
-// scaling and the cubic as packed f32 (v_pk_mul_f32 / v_pk_add_f32, each half
-// rounded like the scalar op: bit-identical to two mlp_log_add_t).  gfx950
-// issues a packed f32 op at about the cost of a scalar one
-// (tools/probe/pk_rate: 0.55x the time for the same lane-operations at 6 waves
-// per SIMD).  max / min / the index / the select stay scalar (no packed f32
-// max/min).  The coefficients come from a table of interval PAIRS, lk2[2 (16 q0
-// + q1)] = {a0, a1, b0, b1}, {c0, c1, w0, w1} (8 KB of LDS), so two ds_read_b128
-// land them already packed.
-#ifndef MLP_PK
-#define MLP_PK 0
-#endif
-typedef float mlp_f2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ void mlp_lookup_table2_entry(float4* lk2, int e) {  // e = 16 q0 + q1
-  float4 t[kLookupRows];
-  mlp_lookup_table(t);
-  const float4 r0 = t[e >> 4], r1 = t[e & 15];
-  lk2[2 * e] = make_float4(r0.x, r1.x, r0.y, r1.y);
-  lk2[2 * e + 1] = make_float4(r0.z, r1.z, r0.w, r1.w);
-}
-__device__ __forceinline__ mlp_f2 mlp_log_add_t2(mlp_f2 x, mlp_f2 y, const float4* __restrict__ lk2) {
-  const mlp_f2 hi = {fmaxf(x.x, y.x), fmaxf(x.y, y.y)};
-  const mlp_f2 lo = {fminf(x.x, y.x), fminf(x.y, y.y)};
-  const mlp_f2 d = hi - lo;
-  const mlp_f2 ds = d * mlp_f2(0x1.fffffep0f);
-  const int q0 = (int)fminf(ds.x, 15.0f), q1 = (int)fminf(ds.y, 15.0f);
-  const float4* e = lk2 + 2 * (q0 * 16 + q1);
-  const float4 ab = e[0], cw = e[1];
-  const mlp_f2 a = {ab.x, ab.y}, b = {ab.z, ab.w}, c = {cw.x, cw.y}, w = {cw.z, cw.w};
-  const mlp_f2 r = (((a * d + b) * d + c) * d + w) + lo;
-  return mlp_f2{d.x >= 7.5f ? hi.x : r.x, d.y >= 7.5f ? hi.y : r.y};
 }
 
 // LOG_ADD(LOG_ZERO, y) == max(LOG_ZERO, y) exactly: above LOG_ZERO the sentinel

@@ -131,7 +131,10 @@ struct mlp_ctx {
   int64_t klaunch[MLP_NKERNELS] = {0};
   int64_t kcells[MLP_NKERNELS] = {0};
   // deferred kernel timers: event pairs resolved by flush_timers()
-  struct TimerRec { int id; int64_t cells; hipEvent_t e0, e1; };
+  // e0 / e1 on the timed stream; e0b / e1b (optional) on the side stream, the
+  // group's span then runs from the earlier start to the later end, measured
+  // from eref (recorded on the context stream before both)
+  struct TimerRec { int id; int64_t cells; hipEvent_t e0, e1, e0b, e1b, eref; };
   std::vector<TimerRec> tpend;
   std::vector<hipEvent_t> evpool;
   size_t evused = 0;
@@ -229,13 +232,17 @@ static hipEvent_t pool_event(mlp_ctx* c) {
   return c->evpool[c->evused++];
 }
 // Kernel-group timer: HIP events around the launches on `st`, resolved later
-// (flush_timers), so timing never serialises the host with the device.
+// (flush_timers), so timing never serialises the host with the device.  With
+// a side stream (span()), the group's kernels on both streams: from the
+// earlier start to the later end.
 struct Timer {
   mlp_ctx* c;
   int id;
   int64_t cells;
   hipStream_t st;
   hipEvent_t e0 = nullptr;
+  hipStream_t sb = nullptr;
+  hipEvent_t e0b = nullptr, eref = nullptr;
   Timer(mlp_ctx* c_, int id_, int64_t cells_, hipStream_t st_ = nullptr)
       : c(c_), id(id_), cells(cells_), st(st_ ? st_ : c_->stream) {
     if (c->profile) {
@@ -243,18 +250,45 @@ struct Timer {
       hipEventRecord(e0, st);
     }
   }
+  // the group also has kernels on stream b; start_b: they start after this
+  // point in b's order (else they start after e0); ref: an event on the timed
+  // stream before anything of the group on either stream
+  void span(hipStream_t b, bool start_b, hipEvent_t ref) {
+    if (!c->profile || !b) return;
+    sb = b;
+    eref = ref ? ref : e0;
+    if (start_b) {
+      e0b = pool_event(c);
+      hipEventRecord(e0b, b);
+    }
+  }
   ~Timer() {
     if (!c->profile || !e0) return;
-    hipEvent_t e1 = pool_event(c);
+    hipEvent_t e1 = pool_event(c), e1b = nullptr;
     hipEventRecord(e1, st);
-    c->tpend.push_back({id, cells, e0, e1});
+    if (sb) {
+      e1b = pool_event(c);
+      hipEventRecord(e1b, sb);
+    }
+    c->tpend.push_back({id, cells, e0, e1, e0b, e1b, eref});
   }
 };
 static void flush_timers(mlp_ctx* c) {
   for (const mlp_ctx::TimerRec& r : c->tpend) {
     hipEventSynchronize(r.e1);
     float ms = 0;
-    hipEventElapsedTime(&ms, r.e0, r.e1);
+    if (r.e1b) {
+      hipEventSynchronize(r.e1b);
+      auto at = [&](hipEvent_t e) {
+        float t = 0;
+        hipEventElapsedTime(&t, r.eref, e);
+        return t;
+      };
+      const float t0 = r.e0b ? std::min(at(r.e0), at(r.e0b)) : at(r.e0);
+      ms = std::max(at(r.e1), at(r.e1b)) - t0;
+    } else {
+      hipEventElapsedTime(&ms, r.e0, r.e1);
+    }
     c->kms[r.id] += ms;
     c->klaunch[r.id] += 1;
     c->kcells[r.id] += r.cells;
@@ -1147,6 +1181,8 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
   // compaction into the store) before batch b + 1 reuses the scratch.
   const bool two = getenv("MLP_TWO") && atoi(getenv("MLP_TWO")) > 0;  // experiment hook
   const SideStream* side = (two || getenv("MLP_NO_SIDE")) ? nullptr : &c->side;  // MLP_NO_SIDE: experiment hook
+  // model sets whose sweeps run as two kernels: the partition function's on the side stream
+  const bool side_used = side && (models & kPF) && models != kPF;
   // k_local_totals: persistent waves, each with 64 candidate rows as wide as
   // the family's widest chain row (<= 1 GB of lists), sized once per call so
   // every batch carves the same bytes (no reallocation between batches) and
@@ -1155,27 +1191,31 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
   int tot_waves = (int)std::max<int64_t>(64, std::min<int64_t>(kTotalsWaves, (int64_t)(1LL << 30) / (64LL * tot_row * 4)));
   tot_waves = (tot_waves + kWavesPerBlock - 1) / kWavesPerBlock * kWavesPerBlock;  // whole workgroups
   const size_t clist_bytes = (models & kLocal) ? (size_t)tot_waves * 64 * tot_row * 4 : 0;
-  // the forward local chain folded one pair per lane (k_local_fold) when the
-  // PF forward Zm slots are dead by then (the partition function ran, and
-  // both backward sweeps joined before the totals); by default when the PF
-  // posterior has its own array, so the candidate rows are contiguous in the
-  // dead slots (MLP_TOT_LANEFOLD_DEFAULT -1); MLP_TOT_LANEFOLD=0 / 1 forces
-  // the one-wave-per-pair fold / this
-#ifndef MLP_TOT_LANEFOLD_DEFAULT
-#define MLP_TOT_LANEFOLD_DEFAULT -1
-#endif
+  // the forward local chain folded one pair per lane (k_local_list +
+  // k_local_fold) between the forward and the backward sweeps, its
+  // candidates listed into the local backward array (dead until the backward
+  // sweep writes it), on the HMM stream while the partition function's
+  // sweeps run on the side stream; the backward chains after the backward
+  // sweep.  The fold lasts as long as its longest chain (~5 ms a batch), on
+  // the HMM stream's critical path: under the CLIs' small budgets (PF
+  // posterior in the Zm slots, ~38 batches at C3) the one-wave-per-pair
+  // k_local_totals after both sweeps runs shorter (C3 drop-in posteriors
+  // 0.92 against 1.03 s, profiles/r05b_cli_lanefold.txt).  MLP_TOT_LANEFOLD=0
+  // / 1 forces either
   static const char* lf_env = getenv("MLP_TOT_LANEFOLD");
-  const bool lf_want = lf_env ? atoi(lf_env) != 0
-                              : (MLP_TOT_LANEFOLD_DEFAULT < 0 ? !pg_in_zm : MLP_TOT_LANEFOLD_DEFAULT != 0);
-  const bool lanefold = (models & kLocal) && (models & kPF) && (!side || side->join_mode == 0) && lf_want;
+  const bool lanefold = (models & kLocal) && (lf_env ? atoi(lf_env) != 0 : !pg_in_zm);
+  // the side stream joins before the merge (the partition function's sweeps
+  // run on without a join between them: the lane fold does not wait for them)
+  SideStream side_lf;
+  if (side && lanefold && side_used) {
+    side_lf = *side;
+    side_lf.join_mode = 2;
+    side = &side_lf;
+  }
   // the one-wave fold's listing bound: the folded chunk maxima of the rows
   // before (k_local_bounds) instead of their maximum (MLP_TOT_FOLDBOUND=0 / 1)
-#ifndef MLP_TOT_FOLDBOUND_DEFAULT
-#define MLP_TOT_FOLDBOUND_DEFAULT 1
-#endif
   static const char* fb_env = getenv("MLP_TOT_FOLDBOUND");
-  const bool foldbound = (models & kLocal) && !lanefold &&
-                         (fb_env ? atoi(fb_env) != 0 : MLP_TOT_FOLDBOUND_DEFAULT != 0);
+  const bool foldbound = (models & kLocal) && !lanefold && (fb_env ? atoi(fb_env) != 0 : true);
   auto budget_for = [&](size_t b) { return std::max<size_t>(b > clist_bytes ? b - clist_bytes : 0, 32u << 20); };
   size_t batch_target =
       batch_target_for(c, p0, p1, pair_bytes, budget_for(two ? c->scratch_budget / 2 : c->scratch_budget));
@@ -1209,9 +1249,6 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
     hipStream_t st = streams[B.slot];
     HIPCHK(c, hipStreamSynchronize(st));
     const int64_t np = B.np;
-#if defined(MLP_EXP_NOCHAIN) || defined(MLP_EXP_CONSTLK)
-    for (int64_t s = 0; s < np; s++) B.rec[s].flags = 0;  // timing experiments: results are not meaningful
-#endif
     for (int64_t s = 0; s < np; s++) {
       if (B.rec[s].flags & 1) {
         c->err = "partition function overflow (pair " + std::to_string(B.order[s]) + ")";
@@ -1254,9 +1291,6 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
     }
     c->store_total = run; ++c->store_ver;
     c->store_p1 = B.q;
-#ifdef MLP_EXP_TOT_STATS
-    mlp::tot_stats_print();
-#endif
     return MLP_OK;
   };
   int64_t p = p0;
@@ -1275,7 +1309,7 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
     Carver cv;
     const bool h5 = models & kHmm5, lo = models & kLocal, pf = models & kPF;
     const size_t o_f5 = cv.take(h5 ? P.cells * 4 : 0), o_fl = cv.take(lo ? P.cells * 4 : 0),
-                 o_bl = cv.take(lo ? P.cells * 4 : 0), o_pg = cv.take(pf && !pg_in_zm ? P.cells * 4 : 0),
+                 o_bl = cv.take(lo ? P.cells * 4 + (lanefold ? kLaneFoldPad : 0) : 0), o_pg = cv.take(pf && !pg_in_zm ? P.cells * 4 : 0),
                  o_zm = cv.take(pf ? P.cells * 8 : 0), o_cmf = cv.take(lo ? P.rm_total * 4 : 0),
                  o_cmb = cv.take(lo ? P.rm_total * 4 : 0),
                  o_tn = cv.take(lo ? 256 : 0), o_cl = cv.take(clist_bytes),
@@ -1308,6 +1342,8 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
     sc.tot_next = (int32_t*)(base + o_tn);
     sc.crb = lanefold || foldbound ? (float*)(base + o_crb) : nullptr;
     sc.rep = (int32_t*)(base + o_rep);
+    static const bool force_repair = getenv("MLP_TOT_FORCE_REPAIR") != nullptr;  // test hook
+    sc.force_repair = force_repair ? 1 : 0;
     sc.bnd5 = (float*)(base + o_b5);
     sc.bndl = (float*)(base + o_bnl);
     sc.bndz = (double*)(base + o_bz);
@@ -1325,20 +1361,29 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
     HIPCHK(c, hipMemsetAsync(d_rec, 0, np * sizeof(PairRec), st));
     int64_t bcells = 0;
     for (int64_t k = p; k < q; k++) bcells += pair_cost_cells(c, k);
+    hipEvent_t fwd_ref = nullptr;
     {
       Timer t(c, KFWD, bcells, st);
+      if (side_used) t.span(side->st, false, nullptr);
+      fwd_ref = t.e0;
       HIPCHK(c, launch_forward(models, ms, c->d_tables, seqs, pm, cm, d_rec, sc, nch, lds_seq, st, side));
       EXP_SYNC("forward");
     }
+    if (lanefold) {  // the forward chains, beside the partition function's sweeps
+      Timer t(c, KTOT, bcells, st);
+      HIPCHK(c, launch_local_fwd_lanefold(seqs, pm, cm, d_rec, sc, np, tot_waves, st));
+      EXP_SYNC("forward totals");
+    }
     {
       Timer t(c, KBWD, bcells, st);
+      if (side_used) t.span(side->st, true, fwd_ref);
       HIPCHK(c, launch_backward(models, ms, c->d_tables, seqs, pm, cm, d_rec, sc, nch, lds_seq, np, st, side));
       EXP_SYNC("backward");
     }
     if (models & kLocal) {
       Timer t(c, KTOT, bcells, st);
       if (lanefold)
-        HIPCHK(c, launch_local_totals_lanefold(ms, c->d_tables, seqs, pm, cm, d_rec, sc, np, tot_waves, st));
+        HIPCHK(c, launch_local_bwd_lanefold(ms, c->d_tables, seqs, pm, cm, d_rec, sc, np, tot_waves, st));
       else
         HIPCHK(c, launch_local_totals(ms, c->d_tables, seqs, pm, cm, d_rec, sc, np, tot_waves, st));
       EXP_SYNC("totals");

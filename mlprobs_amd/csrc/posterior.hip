@@ -52,17 +52,8 @@ constexpr int kPrefetch = 4;
 #ifndef MLP_PF_BWD_WAVES
 #define MLP_PF_BWD_WAVES 5
 #endif
-#ifndef MLP_BND_UNIFORM  // one boundary-shift form for every step (needs MLP_BND_ROTATE)
-#define MLP_BND_UNIFORM MLP_BND_ROTATE
-#endif
 #ifndef MLP_FWD_WAVES
 #define MLP_FWD_WAVES 5
-#endif
-#ifndef MLP_FWD_INTERIOR  // forward: the edge selects only in wave-steps that touch an edge
-#define MLP_FWD_INTERIOR 1
-#endif
-#ifndef MLP_BWD_INTERIOR  // backward: the same
-#define MLP_BWD_INTERIOR 1
 #endif
 #ifndef MLP_BWD_WAVES
 #define MLP_BWD_WAVES MLP_SWEEP_WAVES
@@ -127,7 +118,6 @@ __global__ __launch_bounds__(256, SweepWaves<M>::fwd) void k_forward(ModelScalar
   const int64_t ch = wave_index();
   if (ch >= nchains) return;
   const float4* __restrict__ lk = lookup_of(T_);
-  const float4* __restrict__ lk2 = lookup2_of(T_);  // interval pairs (MLP_PK)
   const int lane = threadIdx.x & 63;
   const ChainView C = stage_chain<kStageFwd>(dyn, lds_seq, ch, sq, pm, cm, rec);
   const int W = C.W, S = C.S;
@@ -161,7 +151,6 @@ __global__ __launch_bounds__(256, SweepWaves<M>::fwd) void k_forward(ModelScalar
         bc.advance();
         bc.load_next(sc, bo, W, m + 1 < nseg ? 64 * (m + 1) : 0, lane);
       }
-      const bool take_bnd = k >= 1 && k < S;
       // unrolled by 4 (segments hold multiples of 8 steps) so the rotating
       // left/up/diagonal roles stay in fixed registers
       for (int t0 = t_lo; t0 < t_hi; t0 += 4)
@@ -174,11 +163,7 @@ __global__ __launch_bounds__(256, SweepWaves<M>::fwd) void k_forward(ModelScalar
         // wave-uniform: no lane on an initial cell, row 0 or column 0 (the
         // common case away from the pairs' edges), so the recurrences' values
         // are taken as they are, without the per-lane selects of the edges
-#if MLP_FWD_INTERIOR
         const bool interior = wave_none(!(i >= 1 && j >= 1 && gen));
-#else
-        const bool interior = false;
-#endif
         const int c1 = c.c1;
         const int c2 = C.seq[c.ca];          // residue j (0 at j = 0 and past L2)
         const float ins1 = c.ins1;
@@ -194,53 +179,17 @@ __global__ __launch_bounds__(256, SweepWaves<M>::fwd) void k_forward(ModelScalar
           for (int k3 = 0; k3 < 3; ++k3) DL[k3] = UL[k3];
         }
         if constexpr ((M & kPF) != 0) { DZm = UZm; DZe = UZe; DZf = UZf; De = Ue; }
-        // MLP_BND_UNIFORM: every step takes lane 0's value from the chunk (in
-        // strip 0 and the skew tail lane 0's up value is unused -- row 0 of
-        // the chain, the idle tail -- so whatever the chunk holds is harmless);
-        // one form of the shift, no branch joining two register assignments
-        if (MLP_BND_UNIFORM || take_bnd)
-          bc.template shift<true, true>(t - t_lo, L5, U5, LL, UL, LZm, LZe, LZf, Le, UZm, UZe, UZf, Ue);
-        else
-          bc.template shift<true, false>(0, L5, U5, LL, UL, LZm, LZe, LZf, Le, UZm, UZe, UZf, Ue);
+        // every step takes lane 0's value from the chunk (in strip 0 and the
+        // skew tail lane 0's up value is unused -- row 0 of the chain, the
+        // idle tail -- so whatever the chunk holds is harmless): one form of
+        // the shift, no branch joining two register assignments
+        bc.template shift<true, true>(t - t_lo, L5, U5, LL, UL, LZm, LZe, LZf, Le, UZm, UZe, UZf, Ue);
         const int64_t idx = base + (int64_t)t * 64;
-        // the local model's M / X / Y values when they ride in the other half
-        // of the 5-state model's packed LOG_ADDs (MLP_PK)
-        float lvm = 0.f, lvx = 0.f, lvy = 0.f;
         // ------------------------------------------------ 5-state forward
         if constexpr ((M & kHmm5) != 0) {
           const float mt = T_.match[c1 * 26 + c2];
           const float ins2 = T_.ins[c2];
           // CPNP/ProbabilisticModel.h:213-256
-#if MLP_PK
-          // independent LOG_ADDs in pairs: the 5-state M chain beside the
-          // local M chain (each in its own order), X1 / X2, Y1 / Y2, local X / Y
-          float vm;
-          if constexpr ((M & kLocal) != 0) {
-            const float bs = mt - ins1 - ins2;
-            mlp_f2 v = {D5[0] + ms.t[0][0], bs - two_rt1};
-            v = mlp_log_add_t2(v, mlp_f2{D5[1] + ms.t[1][0], bs + DL[0] + ms.lt[0][0] - two_rt1}, lk2);
-            v = mlp_log_add_t2(v, mlp_f2{D5[2] + ms.t[2][0], bs + DL[1] + ms.lt[1][0] - two_rt1}, lk2);
-            v = mlp_log_add_t2(v, mlp_f2{D5[3] + ms.t[3][0], bs + DL[2] + ms.lt[2][0] - two_rt1}, lk2);
-            vm = mlp_log_add_t(v.x, D5[4] + ms.t[4][0], lk);
-            lvm = v.y;
-            const mlp_f2 l = mlp_log_add_t2(mlp_f2{UL[0] + ms.lt[0][1] - rt1, LL[0] + ms.lt[0][2] - rt1},
-                                            mlp_f2{UL[1] + ms.lt[1][1] - rt1, LL[2] + ms.lt[2][2] - rt1}, lk2);
-            lvx = l.x;
-            lvy = l.y;
-          } else {
-            vm = D5[0] + ms.t[0][0];
-            vm = mlp_log_add_t(vm, D5[1] + ms.t[1][0], lk);
-            vm = mlp_log_add_t(vm, D5[2] + ms.t[2][0], lk);
-            vm = mlp_log_add_t(vm, D5[3] + ms.t[3][0], lk);
-            vm = mlp_log_add_t(vm, D5[4] + ms.t[4][0], lk);
-          }
-          vm = vm + mt;
-          const mlp_f2 vx = mlp_f2(ins1) + mlp_log_add_t2(mlp_f2{U5[0] + ms.t[0][1], U5[0] + ms.t[0][3]},
-                                                          mlp_f2{U5[1] + ms.t[1][1], U5[3] + ms.t[3][3]}, lk2);
-          const mlp_f2 vy = mlp_f2(ins2) + mlp_log_add_t2(mlp_f2{L5[0] + ms.t[0][2], L5[0] + ms.t[0][4]},
-                                                          mlp_f2{L5[2] + ms.t[2][2], L5[4] + ms.t[4][4]}, lk2);
-          const float vx1 = vx.x, vx2 = vx.y, vy1 = vy.x, vy2 = vy.y;
-#else
           float vm = D5[0] + ms.t[0][0];
           vm = mlp_log_add_t(vm, D5[1] + ms.t[1][0], lk);
           vm = mlp_log_add_t(vm, D5[2] + ms.t[2][0], lk);
@@ -251,7 +200,6 @@ __global__ __launch_bounds__(256, SweepWaves<M>::fwd) void k_forward(ModelScalar
           const float vx2 = ins1 + mlp_log_add_t(U5[0] + ms.t[0][3], U5[3] + ms.t[3][3], lk);
           const float vy1 = ins2 + mlp_log_add_t(L5[0] + ms.t[0][2], L5[2] + ms.t[2][2], lk);
           const float vy2 = ins2 + mlp_log_add_t(L5[0] + ms.t[0][4], L5[4] + ms.t[4][4], lk);
-#endif
           float Cc[5];
           if (interior) {  // every lane's cell takes all five recurrences
             Cc[0] = vm; Cc[1] = vx1; Cc[2] = vy1; Cc[3] = vx2; Cc[4] = vy2;
@@ -287,19 +235,12 @@ __global__ __launch_bounds__(256, SweepWaves<M>::fwd) void k_forward(ModelScalar
           const float mt = T_.match[c1 * 26 + c2];
           const float ins2 = T_.ins[c2];
           const float bs = mt - ins1 - ins2;
-          float vm, vx, vy;
-          if constexpr (MLP_PK && (M & kHmm5) != 0) {  // computed beside the 5-state values
-            vm = lvm;
-            vx = lvx;
-            vy = lvy;
-          } else {
-            vm = bs - two_rt1;
-            vm = mlp_log_add_t(vm, bs + DL[0] + ms.lt[0][0] - two_rt1, lk);
-            vm = mlp_log_add_t(vm, bs + DL[1] + ms.lt[1][0] - two_rt1, lk);
-            vm = mlp_log_add_t(vm, bs + DL[2] + ms.lt[2][0] - two_rt1, lk);
-            vx = mlp_log_add_t(UL[0] + ms.lt[0][1] - rt1, UL[1] + ms.lt[1][1] - rt1, lk);
-            vy = mlp_log_add_t(LL[0] + ms.lt[0][2] - rt1, LL[2] + ms.lt[2][2] - rt1, lk);
-          }
+          float vm = bs - two_rt1;
+          vm = mlp_log_add_t(vm, bs + DL[0] + ms.lt[0][0] - two_rt1, lk);
+          vm = mlp_log_add_t(vm, bs + DL[1] + ms.lt[1][0] - two_rt1, lk);
+          vm = mlp_log_add_t(vm, bs + DL[2] + ms.lt[2][0] - two_rt1, lk);
+          const float vx = mlp_log_add_t(UL[0] + ms.lt[0][1] - rt1, UL[1] + ms.lt[1][1] - rt1, lk);
+          const float vy = mlp_log_add_t(LL[0] + ms.lt[0][2] - rt1, LL[2] + ms.lt[2][2] - rt1, lk);
           float Cm = LZ, Cx = LZ, Cy = LZ;
           if (interior) {
             Cm = vm; Cx = vx; Cy = vy;
@@ -393,7 +334,6 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
   const int64_t ch = wave_index();
   if (ch >= nchains) return;
   const float4* __restrict__ lk = lookup_of(T_);
-  const float4* __restrict__ lk2 = lookup2_of(T_);  // interval pairs (MLP_PK)
   const int lane = threadIdx.x & 63;
   const ChainView C = stage_chain<kStageBwd>(dyn, lds_seq, ch, sq, pm, cm, rec);
   const int W = C.W, S = C.S;
@@ -444,13 +384,12 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
         {
           const int col0 = m > 0 ? 64 * (m - 1) : 64 * (nseg - 1);
           // that segment's first step is its column min(63, W - 1 - col0): lane 63 holds it
-          bc.load_next(sc, bo, W, col0, lane, MLP_BND_ROTATE ? 63 - min(63, W - 1 - col0) : 0);
+          bc.load_next(sc, bo, W, col0, lane, 63 - min(63, W - 1 - col0));
         }
       } else {
         t_lo = -1;
         t_hi = 62;
       }
-      const bool take_bnd = k >= 0 && k < S - 1;
       for (int t0 = t_hi; t0 >= t_lo; t0 -= kPrefetch)
 #pragma unroll
       for (int u = 0; u < kPrefetch; ++u) {
@@ -460,11 +399,7 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
         const bool in_i = i < L1, in_j = j < L2;
         // wave-uniform: every lane inside its pair (not the last row, column
         // or cell), so the recurrences run without the edge selects
-#if MLP_BWD_INTERIOR
         const bool interior = wave_none(!(in_i && in_j && !(i == L1 && j == L2)));
-#else
-        const bool interior = false;
-#endif
         const float f5v = q5[u];
         const double zmv = qz[u];
         const int c1 = c.c1, c1n = c.c1n;
@@ -483,12 +418,9 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
           for (int k3 = 0; k3 < 3; ++k3) GL[k3] = NL[k3];
         }
         if constexpr ((M & kPF) != 0) { GZm = NZm; GZe = NZe; GZf = NZf; Ge = Ne; }
-        // (MLP_BND_UNIFORM: lane 63's down value is unused in the last strip
-        // -- the chain's last row, in_i false -- and in the skew head)
-        if (MLP_BND_UNIFORM || take_bnd)
-          bc.template shift<false, true>(t - t_lo, R5, N5, RL, NL, RZm, RZe, RZf, Re, NZm, NZe, NZf, Ne);
-        else
-          bc.template shift<false, false>(0, R5, N5, RL, NL, RZm, RZe, RZf, Re, NZm, NZe, NZf, Ne);
+        // (one form of the shift: lane 63's down value is unused in the last
+        // strip -- the chain's last row, in_i false -- and in the skew head)
+        bc.template shift<false, true>(t - t_lo, R5, N5, RL, NL, RZm, RZe, RZf, Re, NZm, NZe, NZf, Ne);
         const int64_t idx = base + (int64_t)t * 64;
         // ------------------------------------------------ 5-state backward
         if constexpr ((M & kHmm5) != 0) {
@@ -498,7 +430,6 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
           // CPNP/ProbabilisticModel.h:310-313, 340-378
           const float pxy = G5[0] + mn;
           const bool last = (i == L1 && j == L2);
-#if !MLP_PK
           if (interior) {  // every lane: in_i, in_j, not the last cell -- no per-lane selects
 #pragma unroll
             for (int k5 = 0; k5 < 5; ++k5) B[k5] = mlp_log_add_from_zero(pxy + ms.t[k5][0]);
@@ -511,29 +442,9 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
             B[0] = mlp_log_add_t(B[0], R5[4] + ins2n + ms.t[0][4], lk);
             B[4] = mlp_log_add_t(B[4], R5[4] + ins2n + ms.t[4][4], lk);
           } else {
-#endif
 #pragma unroll
           for (int k5 = 0; k5 < 5; ++k5)
             B[k5] = last ? ms.init[k5] : ((in_i && in_j) ? mlp_log_add_from_zero(pxy + ms.t[k5][0]) : LZ);
-#if MLP_PK
-          // B[0]'s chain in its order, each step paired with one of B[1..4]
-          if (in_i) {
-            mlp_f2 b = mlp_log_add_t2(mlp_f2{B[0], B[1]},
-                                      mlp_f2{N5[1] + ins1n + ms.t[0][1], N5[1] + ins1n + ms.t[1][1]}, lk2);
-            B[1] = b.y;
-            b = mlp_log_add_t2(mlp_f2{b.x, B[3]}, mlp_f2{N5[3] + ins1n + ms.t[0][3], N5[3] + ins1n + ms.t[3][3]}, lk2);
-            B[0] = b.x;
-            B[3] = b.y;
-          }
-          if (in_j) {
-            mlp_f2 b = mlp_log_add_t2(mlp_f2{B[0], B[2]},
-                                      mlp_f2{R5[2] + ins2n + ms.t[0][2], R5[2] + ins2n + ms.t[2][2]}, lk2);
-            B[2] = b.y;
-            b = mlp_log_add_t2(mlp_f2{b.x, B[4]}, mlp_f2{R5[4] + ins2n + ms.t[0][4], R5[4] + ins2n + ms.t[4][4]}, lk2);
-            B[0] = b.x;
-            B[4] = b.y;
-          }
-#else
           if (in_i) {
             B[0] = mlp_log_add_t(B[0], N5[1] + ins1n + ms.t[0][1], lk);
             B[1] = mlp_log_add_t(B[1], N5[1] + ins1n + ms.t[1][1], lk);
@@ -547,7 +458,6 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
             B[4] = mlp_log_add_t(B[4], R5[4] + ins2n + ms.t[4][4], lk);
           }
           }  // !interior
-#endif
           sc.f5[idx] = f5v + B[0];   // f + b (CPNP/ProbabilisticModel.h:484)
           if (act) {
             if (i == 1 && j == 1) rec[c.slot].b5[0] = B[0];
@@ -566,7 +476,6 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
           const float ins2n = T_.ins[c2n];
           const float mn = T_.match[c1n * 26 + c2n];
           float Bm = MLP_LOG_ONE, Bx = LZ, By = LZ;
-#if !MLP_PK
           if (interior) {
             const float pxy = GL[0] + mn - ins1n - ins2n;
             Bm = mlp_log_add_t(Bm, pxy + ms.lt[0][0] - two_rt1, lk);
@@ -577,25 +486,12 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
             Bm = mlp_log_add_t(Bm, RL[2] + ms.lt[0][2] - rt1, lk);
             By = mlp_log_add_t(By, RL[2] + ms.lt[2][2] - rt1, lk);
           } else {
-#endif
           if (in_i && in_j) {
             const float pxy = GL[0] + mn - ins1n - ins2n;
             Bm = mlp_log_add_t(Bm, pxy + ms.lt[0][0] - two_rt1, lk);
             Bx = mlp_log_add_from_zero(pxy + ms.lt[1][0] - two_rt1);
             By = mlp_log_add_from_zero(pxy + ms.lt[2][0] - two_rt1);
           }
-#if MLP_PK
-          if (in_i) {
-            const mlp_f2 b = mlp_log_add_t2(mlp_f2{Bm, Bx}, mlp_f2{NL[1] + ms.lt[0][1] - rt1, NL[1] + ms.lt[1][1] - rt1}, lk2);
-            Bm = b.x;
-            Bx = b.y;
-          }
-          if (in_j) {
-            const mlp_f2 b = mlp_log_add_t2(mlp_f2{Bm, By}, mlp_f2{RL[2] + ms.lt[0][2] - rt1, RL[2] + ms.lt[2][2] - rt1}, lk2);
-            Bm = b.x;
-            By = b.y;
-          }
-#else
           if (in_i) {
             Bm = mlp_log_add_t(Bm, NL[1] + ms.lt[0][1] - rt1, lk);
             Bx = mlp_log_add_t(Bx, NL[1] + ms.lt[1][1] - rt1, lk);
@@ -605,7 +501,6 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
             By = mlp_log_add_t(By, RL[2] + ms.lt[2][2] - rt1, lk);
           }
           }  // !interior
-#endif
           sc.bl[idx] = Bm;   // f + b is formed by the merge (the same float add)
           if (lane == 0) {
             sc.bndl[(bo + j) * 3 + 0] = Bm;
@@ -629,11 +524,7 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
           float post = 0.0f;
           const double score = T_.sub[c2 * 26 + c1];
           // wave-uniform: every lane strictly inside rows 2..L1-1, columns 2..L2-1
-#if MLP_BWD_INTERIOR
           const bool pf_inner = wave_none(!(i >= 2 && i < L1 && j >= 2 && j < L2));
-#else
-          const bool pf_inner = false;
-#endif
           if (i >= 1 && j >= 1) {
             double nZm = NZm, nZe = NZe, nZf = NZf, rZm = RZm, rZe = RZe, rZf = RZf;
             double gZm = GZm, gZe = GZe, gZf = GZf;
@@ -774,7 +665,6 @@ __global__ __launch_bounds__(256, MLP_MERGE_WAVES) void k_merge(ModelScalars ms,
         const float f5v = q5[u], flv = ql[u] + qb[u], pgv = qg[u];
         Dv = Uv;
         // boundary column t - t_lo in lane 0 of the rotating chunk (BoundaryChunks::shift)
-#if MLP_BND_ROTATE
         Uv = take_bnd ? mlp_shr1(Lv, bch) : mlp_shr1z(Lv);
         if (take_bnd) bch = mlp_shl1z(bch);
         if constexpr (NP) {
@@ -782,13 +672,6 @@ __global__ __launch_bounds__(256, MLP_MERGE_WAVES) void k_merge(ModelScalars ms,
           Uc = take_bnd ? mlp_shr1i(Lc, cch) : mlp_shr1zi(Lc);
           if (take_bnd) cch = mlp_shl1zi(cch);
         }
-#else
-        Uv = take_bnd ? mlp_shr1(Lv, readlane_f(bch, t - t_lo)) : mlp_shr1z(Lv);
-        if constexpr (NP) {
-          Dc = Uc;
-          Uc = take_bnd ? mlp_shr1i(Lc, __builtin_amdgcn_readlane(cch, t - t_lo)) : mlp_shr1zi(Lc);
-        }
-#endif
         const bool act = c.q >= 0 && i >= 1 && j >= 1 && j <= L2;
         float P = 0.f;
         if (act) {
@@ -864,25 +747,6 @@ __global__ __launch_bounds__(256, MLP_MERGE_WAVES) void k_merge(ModelScalars ms,
 }
 
 // ------------------------------------------------------------ launchers
-// MLP_SPLIT_HMM=1: the 5-state and local HMMs as separate sweeps (experiment)
-static bool split_hmm() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("MLP_SPLIT_HMM");
-    v = (e && e[0] == '1') ? 1 : 0;
-  }
-  return v == 1;
-}
-// MLP_FUSE=1 runs all three models in one sweep (default: two sweeps).
-static bool fuse_models() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("MLP_FUSE");
-    v = (e && e[0] == '1') ? 1 : 0;
-  }
-  return v == 1;
-}
-
 template <template <int> class K, bool kFwd>
 static hipError_t launch_sweep(int models, const ModelScalars& ms, const Tables* tab, SeqSet seqs,
                                PairMeta pm, ChainMeta cm, PairRec* rec, Scratch sc, int64_t nchains,
@@ -915,13 +779,6 @@ static hipError_t launch_sweep(int models, const ModelScalars& ms, const Tables*
   };
   switch (models) {
     case kHmm5 | kLocal | kPF:
-      if (fuse_models()) {
-        go(std::integral_constant<int, kHmm5 | kLocal | kPF>{}, st);
-        return hipSuccess;
-      }
-      if (split_hmm())
-        return pair(std::integral_constant<int, kHmm5>{}, std::integral_constant<int, kLocal>{},
-                    std::integral_constant<int, kPF>{});
       // fp32 HMMs and the fp64 partition function as two sweeps: fewer VGPRs each
       return pair(std::integral_constant<int, kHmm5 | kLocal>{}, std::integral_constant<int, kPF>{});
     case kLocal: go(std::integral_constant<int, kLocal>{}, st); break;

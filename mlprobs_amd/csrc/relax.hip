@@ -318,11 +318,7 @@ __global__ __launch_bounds__(256) void k_pack(PackArgs A) {
 // XCD-aware tile order lets tiles of one x group run on one XCD, so their A
 // blocks meet in that XCD's L2.
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));  // plain vector: stays in VGPRs
-#ifdef MLP_RELAX_NOLOAD  // timing experiment: no global loads for the staging
-#define MLP_PF_LOAD(dst, src) (dst) = u32x4{(uint32_t)c, 0u, 0u, 0u}
-#else
 #define MLP_PF_LOAD(dst, src) (dst) = (src)
-#endif
 #ifndef MLP_RELAX_ZCHUNK
 #define MLP_RELAX_ZCHUNK 32
 #endif
@@ -357,9 +353,6 @@ __device__ __forceinline__ uint4 rfl(uint4 v) {
                     __builtin_amdgcn_readfirstlane(v.z), __builtin_amdgcn_readfirstlane(v.w));
 }
 
-#ifdef MLP_RELAX_TIMING  // measurement variant: per-z compute imbalance across the 16 waves
-__device__ unsigned long long g_rtime[8];
-#endif
 #ifdef MLP_RELAX_STATS  // measurement variant: trips of the word walk and the hit loop, lane sums vs wave maxima
 __device__ unsigned long long g_rstat[4];
 #define RSTAT_INC(v) ++(v)
@@ -625,10 +618,6 @@ __global__ __launch_bounds__(kRelaxThreads, KP == 5 && kRelaxThreads == 1024 ? 8
       MLP_PF_LOAD(pf[m], g16[(uint32_t)(c + d)]);                                        \
     }                                                                                    \
   }
-#ifdef MLP_RELAX_TIMING
-  unsigned long long t_max = 0, t_mean = 0, t_step = 0, t_steps = 0, t_seg[4] = {0, 0, 0, 0};
-  uint64_t t_last = clock64();
-#endif
   // KP = 9: the next z's tile is loaded into registers while this z computes;
   // KP = 5 (two workgroups per CU): loaded at the stage, the other
   // workgroup's compute covers the wait and the registers stay free
@@ -636,10 +625,6 @@ __global__ __launch_bounds__(kRelaxThreads, KP == 5 && kRelaxThreads == 1024 ? 8
   fill();
   bool more = next();
   if (kRegPrefetch && more) MLP_ISSUE();
-#ifdef MLP_RELAX_NOSTAGE
-  const uint4 fC = nC, fAo = nAo, fNa = nNa, fAc = nAc;
-  const float4 fW = nW;
-#endif
 #ifdef MLP_RELAX_STATS
   // per (slot, z): lanes' word steps and hits summed, and 64 x the wave's
   // maximum (the trips the wave issues); lane 0 keeps the wave's totals
@@ -659,9 +644,6 @@ __global__ __launch_bounds__(kRelaxThreads, KP == 5 && kRelaxThreads == 1024 ? 8
 #define RSTAT_SLOT()
 #endif
   while (more) {
-#ifdef MLP_RELAX_TIMING
-    const uint64_t ts0 = clock64();
-#endif
     if constexpr (!kRegPrefetch) MLP_ISSUE();
     // stage the prefetched tile; outputs' A bases (+ validity) into zb
     const int tot = sg[TM] + (int)nC.z;
@@ -688,26 +670,16 @@ __global__ __launch_bounds__(kRelaxThreads, KP == 5 && kRelaxThreads == 1024 ? 8
         gptr[t] = A.img + 16 * (uint64_t)ao_[t];
       }
     }
-#ifdef MLP_RELAX_TIMING
-    const uint64_t ts1 = clock64();  // stage writes issued (after the loads landed)
-#endif
     __syncthreads();
-#ifdef MLP_RELAX_TIMING
-    const uint64_t ts2 = clock64();
-#endif
     more = next();
-#ifdef MLP_RELAX_TIMING
-    const uint64_t ts3 = clock64();
-#endif
-#ifdef MLP_RELAX_NOSTAGE  // timing experiment: every z computes on the first z's tile
-    nC = fC; nAo = fAo; nNa = fNa; nAc = fAc; nW = fW;
-#else
     if (kRegPrefetch && more) MLP_ISSUE();
-#endif
-#ifdef MLP_RELAX_TIMING
-    const uint64_t tc0 = clock64();
-#endif
-#ifndef MLP_RELAX_NOCOMPUTE  // (timing experiment: staging only)
+    // the lowest hit of m: `below` = the bits under it, m loses it; the
+    // compiler folds `below & bits` into one v_bitop3 per side (11 VALU a
+    // hit instead of 14 with 1 << ctz(m): C3 round 1 1206 -> 1155 ms)
+#define MLP_HIT_BITS(m, below)      \
+  const uint32_t t_ = (m) - 1u;     \
+  const uint32_t below = t_ & ~(m); \
+  (m) &= t_;
     // per word pair: the load, then the common columns of each word (a single
     // loop over loads and hits, MLP_RELAX_FLAT in round 4, ran 1.69 s against
     // 1.21 s: the wave issues both bodies every iteration)
@@ -719,35 +691,35 @@ __global__ __launch_bounds__(kRelaxThreads, KP == 5 && kRelaxThreads == 1024 ? 8
       uint32_t m1 = w + 1 < we ? xa1.x & xc1.x : 0u;                                                  \
       while (m0) { /* common columns k, ascending */                                                  \
         RSTAT_INC(st_h);                                                                              \
-        const uint32_t bit = 1u << __builtin_ctz(m0);                                                 \
-        m0 ^= bit;                                                                                    \
-        const float va = QP ? wk * Avals[xa0.y + __popc(xa0.x & (bit - 1u))]                          \
-                            : Avals[xa0.y + __popc(xa0.x & (bit - 1u))];                              \
-        const float vc = Cvals[xc0.y + __popc(xc0.x & (bit - 1u))];                                   \
+        MLP_HIT_BITS(m0, below);                                                                      \
+        const float va = QP ? wk * Avals[xa0.y + __popc(xa0.x & below)]                               \
+                            : Avals[xa0.y + __popc(xa0.x & below)];                                   \
+        const float vc = Cvals[xc0.y + __popc(xc0.x & below)];                                        \
         ac += va * vc;                                                                                \
       }                                                                                               \
       while (m1) {                                                                                    \
         RSTAT_INC(st_h);                                                                              \
-        const uint32_t bit = 1u << __builtin_ctz(m1);                                                 \
-        m1 ^= bit;                                                                                    \
-        const float va = QP ? wk * Avals[xa1.y + __popc(xa1.x & (bit - 1u))]                          \
-                            : Avals[xa1.y + __popc(xa1.x & (bit - 1u))];                              \
-        const float vc = Cvals[xc1.y + __popc(xc1.x & (bit - 1u))];                                   \
+        MLP_HIT_BITS(m1, below);                                                                      \
+        const float va = QP ? wk * Avals[xa1.y + __popc(xa1.x & below)]                               \
+                            : Avals[xa1.y + __popc(xa1.x & below)];                                   \
+        const float vc = Cvals[xc1.y + __popc(xc1.x & below)];                                        \
         ac += va * vc;                                                                                \
       }                                                                                               \
     }
     // the cell loop, twice: with every image in LDS, and (GA) for a z where
     // some output image is read in place from HBM (generic loads)
-#define MLP_CELLS(GA) \
+#define MLP_CELLS(GA, ONE) \
     {                                                                                                            \
       const float* Cvals = (const float*)(lds + cbase);                                                          \
       const uint32_t* Chdr = (const uint32_t*)(lds + cbase + (uint32_t)mlp_align16(4 * (int64_t)nzC));           \
       const uint2* Cwords = (const uint2*)((const uint8_t*)Chdr + (uint32_t)mlp_align16(4 * (int64_t)(Ly + 1))); \
       /* row headers of slot s + 1 are read while slot s intersects */                                           \
-      /* GA: outputs of this z may be read in HBM (generic pointers) */                                          \
+      /* GA: outputs of this z may be read in HBM (generic pointers); ONE: the */                                \
+      /* tile has one output, its bases are workgroup-uniform (SGPRs) */                                         \
       auto headers = [&](uint32_t cl, int4& z4, uint32_t& ha, uint32_t& hc, const uint8_t*& ab) {                \
-        z4 = zb[cl >> 26];                                                                                       \
-        ab = (GA) && ((gmz >> (cl >> 26)) & 1) ? gptr[cl >> 26] : (const uint8_t*)lds;                           \
+        z4 = (ONE) ? z4u : zb[cl >> 26];                                                                         \
+        ab = (GA) && ((ONE) ? (gmz & 1) != 0 : ((gmz >> (cl >> 26)) & 1) != 0) ? ((ONE) ? gp0 : gptr[cl >> 26])  \
+                                                                             : (const uint8_t*)lds;              \
         ha = z4.w ? ((const uint32_t*)(ab + z4.y))[cl & 0x1fff] : 0u;  /* nw 0: no words */                      \
         hc = Chdr[(cl >> 13) & 0x1fff];                                                                          \
       };                                                                                                         \
@@ -775,7 +747,7 @@ _Pragma("unroll")                                                               
           const uint2* pa = (const uint2*)(ab + z4.z) + ((int)(ha & 0xffff) - a0);                               \
           const uint2* pc = Cwords + ((int)(hc & 0xffff) - c0);                                                  \
           const float* Avals = (const float*)(ab + z4.x);                                                        \
-          const float wk = QP ? zw[cl >> 26] : 1.0f;  /* weight * XZ * ZY (ConsistencyStage.cpp:284) */          \
+          const float wk = QP ? ((ONE) ? w0 : zw[cl >> 26]) : 1.0f;  /* weight * XZ * ZY (ConsistencyStage.cpp:284) */ \
           float ac = acc[s];                                                                                     \
           MLP_WALK(pa, pc, we, a0, c0)                                                                           \
           acc[s] = ac;                                                                                           \
@@ -788,42 +760,26 @@ _Pragma("unroll")                                                               
         ab = ab1;                                                                                                \
       }                                                                                                          \
     }
-    if (gmz) MLP_CELLS(true) else MLP_CELLS(false)
+    // one-output tiles (most at C3: one output of up to 6144 cells): the
+    // image bases are workgroup-uniform, read once per z into SGPRs instead
+    // of an LDS read per slot (C3 round 1 1154 -> 1118 ms)
+    if (T == 1) {
+      const uint4 zu = rfl(*(const uint4*)zb);
+      const int4 z4u = make_int4((int)zu.x, (int)zu.y, (int)zu.z, (int)zu.w);
+      const uint8_t* gp0 = (const uint8_t*)(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)gptr[0] >> 32)) << 32) |
+                                            (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(uint64_t)gptr[0]));
+      const float w0 = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(zw[0])));
+      if (gmz) MLP_CELLS(true, true) else MLP_CELLS(false, true)
+    } else {
+      const int4 z4u = make_int4(0, 0, 0, 0);
+      const uint8_t* gp0 = nullptr;
+      const float w0 = 0.f;
+      if (gmz) MLP_CELLS(true, false) else MLP_CELLS(false, false)
+    }
 #undef MLP_CELLS
 #undef MLP_WALK
-#endif
-#ifdef MLP_RELAX_TIMING
-    {
-      __shared__ uint32_t wct[16];
-      const uint64_t tc1 = clock64();
-      if ((tid & 63) == 0) wct[tid >> 6] = (uint32_t)(tc1 - tc0);
-      __syncthreads();
-      if (tid == 0) {
-        uint32_t mx = 0, sm = 0;
-        for (int w = 0; w < nt / 64; ++w) { mx = max(mx, wct[w]); sm += wct[w]; }
-        t_max += mx;
-        t_mean += sm / (nt / 64);
-        t_steps += 1;
-        t_step += clock64() - t_last;
-        t_last = clock64();
-        t_seg[0] += ts1 - ts0;
-        t_seg[1] += ts2 - ts1;
-        t_seg[2] += ts3 - ts2;
-        t_seg[3] += tc0 - ts3;
-      }
-    }
-#endif
     __syncthreads();
   }
-#ifdef MLP_RELAX_TIMING
-  if (tid == 0) {
-    atomicAdd(&g_rtime[0], t_max);
-    atomicAdd(&g_rtime[1], t_mean);
-    atomicAdd(&g_rtime[2], t_step);
-    atomicAdd(&g_rtime[3], t_steps);
-    for (int q = 0; q < 4; ++q) atomicAdd(&g_rtime[4 + q], t_seg[q]);
-  }
-#endif
 #undef MLP_ISSUE
 #undef RSTAT_SLOT
 #ifdef MLP_RELAX_STATS
@@ -891,18 +847,6 @@ hipError_t launch_relax_tiles(const TileRelaxArgs& a, int slots, bool one_per_cu
     case 9: e = a.qp.on ? launch_tiles_kp<9, true>(a, slots, lds, st) : launch_tiles_kp<9, false>(a, slots, lds, st); break;
     default: return hipErrorInvalidValue;
   }
-#ifdef MLP_RELAX_TIMING
-  unsigned long long h[8];
-  hipStreamSynchronize(st);
-  hipMemcpyFromSymbol(h, HIP_SYMBOL(g_rtime), sizeof h);
-  fprintf(stderr,
-          "relax timing: z-steps %llu, cycles per step %.0f, wave compute mean %.0f max %.0f | wave0: stage-write %.0f "
-          "barrier %.0f next %.0f issue %.0f\n",
-          h[3], (double)h[2] / h[3], (double)h[1] / h[3], (double)h[0] / h[3], (double)h[4] / h[3],
-          (double)h[5] / h[3], (double)h[6] / h[3], (double)h[7] / h[3]);
-  for (auto& v : h) v = 0;
-  hipMemcpyToSymbol(HIP_SYMBOL(g_rtime), h, sizeof h);
-#endif
 #ifdef MLP_RELAX_STATS
   {
     unsigned long long h[4];

@@ -46,13 +46,7 @@ static inline dim3 wave_grid(int64_t n) {
 // Backward (0.1% of the chunks hold a candidate): chunks whose maximum
 // (Scratch::cmb) passes the test against acc are gathered and folded.
 // =====================================================================
-#ifdef MLP_EXP_TOT_STATS  // measurement variant: fold work counters, printed per batch on stderr
-__device__ unsigned long long g_totstats[8];
-#define TOT_STAT(k, v) \
-  if (lane == 0) atomicAdd(&g_totstats[k], (unsigned long long)(v))
-#else
 #define TOT_STAT(k, v)
-#endif
 
 // Fold chunks [kb, ke) of a chain (row-major chunk index (i - 1) * nch + c)
 // whose maximum passes the test against acc, elements gathered from the
@@ -122,9 +116,6 @@ __device__ __forceinline__ float fold_chunks(float acc, int64_t kb, int64_t ke, 
 // caches evicted long before they filled (the lists of all resident waves
 // exceed L2 and MALL): at C3 the listing took 104 ms a step with the stores,
 // 19 ms without them (profiles/r04e_ab_totals_nostore.txt).
-#ifndef MLP_TOT_LDSBUF
-#define MLP_TOT_LDSBUF 1
-#endif
 constexpr int kLbufSlots = 24;  // 16 to flush + up to 8 listed since the last check
 // the 16 elements from ring slot s0 (a multiple of 16 in list order) to dst
 __device__ __forceinline__ void lbuf_flush16(float* __restrict__ dst, const float* lbuf, int s0, int lane) {
@@ -182,28 +173,18 @@ __device__ __forceinline__ float local_fwd_fold(const float* __restrict__ cmf, c
         const int j = t0 + u - lane;
         if (row_in && j >= 1 && j <= L2) {
           if (!(run - x[u] >= 7.5f)) {
-#ifdef MLP_EXP_TOT_NOSTORE  // timing experiment: count the candidates, store nothing
-            cnt++;
-#elif MLP_TOT_LDSBUF
             lbuf[(cnt % kLbufSlots) * 64 + lane] = x[u];
             ++cnt;
-#else
-            mine[cnt++] = x[u];
-#endif
           }
           run = fmaxf(run, x[u]);
         }
       }
-#if MLP_TOT_LDSBUF && !defined(MLP_EXP_TOT_NOSTORE)
       if (cnt - done >= 16) {  // at most 8 listed since the last check: <= 24 in the ring
         lbuf_flush16(mine + done, lbuf, done % kLbufSlots, lane);
         done += 16;
       }
-#endif
     }
-#if MLP_TOT_LDSBUF && !defined(MLP_EXP_TOT_NOSTORE)
     for (int k = done; k < cnt; ++k) mine[k] = lbuf[(k % kLbufSlots) * 64 + lane];  // the strip's remainder
-#endif
     TOT_STAT(1, cnt);
     if constexpr (!FOLD) {  // timing experiment: streaming only
       acc = fmaxf(acc, (float)__builtin_amdgcn_readlane(cnt, 5));
@@ -247,14 +228,14 @@ __global__ __launch_bounds__(256) void k_local_totals(ModelScalars ms, const Tab
                                                       Scratch sc, int64_t npairs, const int32_t* __restrict__ only) {
   __shared__ float4 lk[kLookupRows];
   __shared__ float match[26 * 26], ins[26];
-  __shared__ float lbuf_all[MLP_TOT_LDSBUF ? kWavesPerBlock * kLbufSlots * 64 : 1];  // per wave: a ring per lane
+  __shared__ float lbuf_all[kWavesPerBlock * kLbufSlots * 64];  // per wave: a ring per lane
   if (threadIdx.x == 0) mlp_lookup_table(lk);
   for (int k = threadIdx.x; k < 26 * 26; k += blockDim.x) match[k] = tab->match[k];
   if (threadIdx.x < 26) ins[threadIdx.x] = tab->ins[threadIdx.x];
   __syncthreads();
   const int lane = threadIdx.x & 63;
   float* region = sc.clist + wave_index() * 64 * (int64_t)sc.clist_row;
-  float* lbuf = lbuf_all + (MLP_TOT_LDSBUF ? (threadIdx.x >> 6) * kLbufSlots * 64 : 0);
+  float* lbuf = lbuf_all + (threadIdx.x >> 6) * kLbufSlots * 64;
 
   // one counter increment per wave, every lane taking part (no divergent
   // branch around the atomic): lane 0 receives the pair number
@@ -273,11 +254,6 @@ __global__ __launch_bounds__(256) void k_local_totals(ModelScalars ms, const Tab
     const uint8_t* s2 = sq.res + sq.off[pm.pb[p]];
     const int64_t rm = pm.rm_off[p];
     bool bad = false;
-#ifdef MLP_EXP_TOT_NOFOLD  // timing experiment: the listing pass alone (local posteriors then read as 0)
-    float tf = local_fwd_fold<false>(sc.cmf + rm, sc.fl, L1, L2, row0, W, cell_off, lk, region, sc.clist_row, lane, lbuf,
-                                     nullptr, &bad);
-    tf = tf == 12345.f ? 0.f : 1e30f;
-#else
     // with the folded bound (sc.crb) when k_local_bounds ran; a pair whose
     // bound failed is redone with the running maximum (exact either way)
     const float* rbp = sc.crb ? sc.crb + pm.ell_row[p] : nullptr;
@@ -289,15 +265,8 @@ __global__ __launch_bounds__(256) void k_local_totals(ModelScalars ms, const Tab
       tf = local_fwd_fold(sc.cmf + rm, sc.fl, L1, L2, row0, W, cell_off, lk, region, sc.clist_row, lane, lbuf, nullptr,
                           &bad);
     }
-#endif
     float tb = fold_chunks<true>(LZ, 0, (int64_t)L1 * local_chunks(L2), sc.cmb + rm, sc.bl, L2, row0, W, cell_off, s1,
                                  s2, match, ins, 2 * ms.rt1, lk, lane);
-#ifdef MLP_EXP_TOT_STRM2  // the forward streaming pass twice (no second fold)
-    if (local_fwd_fold<false>(sc.cmf + rm, sc.fl, L1, L2, row0, W, cell_off, lk, region, sc.clist_row, lane, lbuf,
-                              nullptr, &bad) ==
-        12345.f)
-      tf = 0.f;
-#endif
     if (lane == 0) {
       rec[p].tfl = tf;
       rec[p].tbl = tb;
@@ -306,11 +275,11 @@ __global__ __launch_bounds__(256) void k_local_totals(ModelScalars ms, const Tab
 }
 
 // =====================================================================
-// Lane-per-pair forward chain (models with the partition function).  The
-// chain itself is serial, so one wave folding one pair issues ~20 wave
-// instructions per folded element with one useful lane; here 64 pairs share
-// a wave, one per lane, after a listing pass has put each pair's candidates
-// in chain order into its region of the dead PF forward Zm slots.
+// Lane-per-pair forward chain.  The chain itself is serial, so one wave
+// folding one pair issues ~20 wave instructions per folded element with one
+// useful lane; here 64 pairs share a wave, one per lane, after a listing pass
+// has put each pair's candidates in chain order into its region of the local
+// backward array, dead between the two sweeps.
 //
 // The listing uses a tighter exact skip bound than the running maximum: the
 // chain value at the start of row i is at least the exact LOG_ADD fold of the
@@ -348,41 +317,32 @@ __global__ __launch_bounds__(256) void k_local_bounds(SeqSet sq, PairMeta pm, Sc
   }
 }
 
-// Candidate k of pair row i (1-based) in the pair's region of the PF forward
-// Zm slots: slots cell_off + row0 W .. (the pair's own (L1 + 1) W slots),
-// high halves (the low halves may hold the PF posterior, Scratch::pg_stride).
-__device__ __forceinline__ float* lanefold_area(const Scratch& sc, int64_t cell_off, int row0, int W) {
-  return reinterpret_cast<float*>(sc.zm) + 2 * (cell_off + (int64_t)row0 * W) + 1;
-}
-// With the PF posterior in its own array (pg_stride 1) the whole 8-byte slots
-// are dead: row i's candidates are contiguous at rows + (i - 1) * RS, RS = L2
-// rounded up to 4 floats, from the first 16-byte boundary of the pair's slots
-// ((L1 + 1) W >= (L1 + 1)(L2 + 1) slots of 8 bytes hold 16 + 4 L1 RS bytes).
+// Candidate k of pair row i (1-based): the lists go to the local backward
+// array (Scratch::bl), dead until the backward sweep: the forward chain is
+// folded between the forward and the backward sweeps, on the HMM stream,
+// while the partition function's sweeps run on the side stream.  The pair's
+// region is bl's slots cell_off + row0 W .. + (L1 + 1) W (the chain's rows
+// partition its slots among the members); row i's candidates are contiguous
+// at rows + (i - 1) * RS, RS = L2 rounded up to 4 floats, from the first
+// 16-byte boundary: (L1 + 1) W >= L1 RS + 3 + W floats, W >= RS, W >= 8.
 __device__ __forceinline__ float* lanefold_rows(const Scratch& sc, int64_t cell_off, int row0, int W) {
   // (pointer arithmetic from the slot, not an integer round trip: the
   // compiler keeps the global address space -- global, not flat, loads)
-  float* const b = reinterpret_cast<float*>(sc.zm + cell_off + (int64_t)row0 * W);
+  float* const b = sc.bl + cell_off + (int64_t)row0 * W;
   const int mis = (int)((reinterpret_cast<uintptr_t>(b) >> 2) & 3);
   return b + ((4 - mis) & 3);
 }
 __device__ __forceinline__ int lanefold_rs(int L2) { return (L2 + 3) & ~3; }
 
-// Wave per pair (persistent, as k_local_totals): the backward chain as there,
-// and the forward chain's candidates listed row by row (element x of row i is
-// listed unless max(crb[i], max of the row so far) - x >= 7.5).
-__global__ __launch_bounds__(256) void k_local_list(ModelScalars ms, const Tables* __restrict__ tab, SeqSet sq,
-                                                    PairMeta pm, ChainMeta cm, PairRec* __restrict__ rec,
-                                                    Scratch sc, int64_t npairs) {
-  __shared__ float4 lk[kLookupRows];
-  __shared__ float match[26 * 26], ins[26];
+// Wave per pair (persistent, as k_local_totals): the forward chain's
+// candidates listed row by row (element x of row i is listed unless
+// max(crb[i], max of the row so far) - x >= 7.5), each row contiguous,
+// written 64 bytes at a time through the lane's LDS ring.
+__global__ __launch_bounds__(256) void k_local_list(SeqSet sq, PairMeta pm, ChainMeta cm, Scratch sc,
+                                                    int64_t npairs) {
   __shared__ float lbuf_all[kWavesPerBlock * kLbufSlots * 64];  // contiguous rows: per wave a ring per lane
-  if (threadIdx.x == 0) mlp_lookup_table(lk);
-  for (int k = threadIdx.x; k < 26 * 26; k += blockDim.x) match[k] = tab->match[k];
-  if (threadIdx.x < 26) ins[threadIdx.x] = tab->ins[threadIdx.x];
-  __syncthreads();
   const int lane = threadIdx.x & 63;
   float* lbuf = lbuf_all + (threadIdx.x >> 6) * kLbufSlots * 64;
-  const bool contig = sc.pg_stride == 1;
   auto take = [&]() -> int64_t {
     const int got = atomicAdd(sc.tot_next, lane == 0 ? 1 : 0);
     return __builtin_amdgcn_readfirstlane(got);
@@ -393,7 +353,6 @@ __global__ __launch_bounds__(256) void k_local_list(ModelScalars ms, const Table
     const int W = cm.width[h], row0 = pm.row0[p];
     const int64_t cell_off = cm.cell_off[h];
     const int64_t ell = pm.ell_row[p];
-    float* __restrict__ area = lanefold_area(sc, cell_off, row0, W);
     float* __restrict__ rows = lanefold_rows(sc, cell_off, row0, W);
     const int RS = lanefold_rs(L2);
     const int S0 = (row0 + 1) >> 6, S1 = (row0 + L1) >> 6;
@@ -404,64 +363,46 @@ __global__ __launch_bounds__(256) void k_local_list(ModelScalars ms, const Table
       float run = row_in ? sc.crb[ell + i - 1] : LZ;
       int cnt = 0;
       const float* slab = sc.fl + cell_off + ((int64_t)W * S + 1) * 64 + lane;
-      if (contig) {
-        // a row's list contiguous, written 64 bytes at a time through the
-        // lane's LDS ring (as local_fwd_fold's lists)
-        float* __restrict__ mine = rows + (int64_t)(row_in ? i - 1 : 0) * RS;
-        int done = 0;
-        for (int t0 = 1; t0 <= tend; t0 += 8) {
-          float x[8];
+      float* __restrict__ mine = rows + (int64_t)(row_in ? i - 1 : 0) * RS;
+      int done = 0;
+      for (int t0 = 1; t0 <= tend; t0 += 8) {
+        float x[8];
 #pragma unroll
-          for (int u = 0; u < 8; ++u) x[u] = (t0 + u <= tend) ? slab[(int64_t)(t0 + u) * 64] : LZ;
+        for (int u = 0; u < 8; ++u) x[u] = (t0 + u <= tend) ? slab[(int64_t)(t0 + u) * 64] : LZ;
 #pragma unroll
-          for (int u = 0; u < 8; ++u) {
-            const int j = t0 + u - lane;
-            if (row_in && j >= 1 && j <= L2) {
-              if (!(run - x[u] >= 7.5f)) {
-                lbuf[(cnt % kLbufSlots) * 64 + lane] = x[u];
-                ++cnt;
-              }
-              run = fmaxf(run, x[u]);
+        for (int u = 0; u < 8; ++u) {
+          const int j = t0 + u - lane;
+          if (row_in && j >= 1 && j <= L2) {
+            if (!(run - x[u] >= 7.5f)) {
+              lbuf[(cnt % kLbufSlots) * 64 + lane] = x[u];
+              ++cnt;
             }
-          }
-          if (cnt - done >= 16) {  // at most 8 listed since the last check: <= 24 in the ring
-            lbuf_flush16(mine + done, lbuf, done % kLbufSlots, lane);
-            done += 16;
+            run = fmaxf(run, x[u]);
           }
         }
-        for (int k = done; k < cnt; ++k) mine[k] = lbuf[(k % kLbufSlots) * 64 + lane];
-      } else {
-        float* __restrict__ mine = area + 2 * (int64_t)(row_in ? i - 1 : 0) * L2;
-        for (int t0 = 1; t0 <= tend; t0 += 8) {
-          float x[8];
-#pragma unroll
-          for (int u = 0; u < 8; ++u) x[u] = (t0 + u <= tend) ? slab[(int64_t)(t0 + u) * 64] : LZ;
-#pragma unroll
-          for (int u = 0; u < 8; ++u) {
-            const int j = t0 + u - lane;
-            if (row_in && j >= 1 && j <= L2) {
-              if (!(run - x[u] >= 7.5f)) mine[2 * cnt++] = x[u];
-              run = fmaxf(run, x[u]);
-            }
-          }
+        if (cnt - done >= 16) {  // at most 8 listed since the last check: <= 24 in the ring
+          lbuf_flush16(mine + done, lbuf, done % kLbufSlots, lane);
+          done += 16;
         }
       }
+      for (int k = done; k < cnt; ++k) mine[k] = lbuf[(k % kLbufSlots) * 64 + lane];
       if (row_in) sc.ell_cnt[ell + i - 1] = cnt;
     }
-    const int64_t rm = pm.rm_off[p];
-    const uint8_t* s1 = sq.res + sq.off[pm.pa[p]];
-    const uint8_t* s2 = sq.res + sq.off[pm.pb[p]];
-    const float tb = fold_chunks<true>(LZ, 0, (int64_t)L1 * local_chunks(L2), sc.cmb + rm, sc.bl, L2, row0, W, cell_off,
-                                       s1, s2, match, ins, 2 * ms.rt1, lk, lane);
-    if (lane == 0) rec[p].tbl = tb;
   }
 }
 
 // Lane per pair: the forward chain over the listed candidates, rows in
 // lockstep across the wave (row i of every lane's pair in the same outer
-// iteration); the next group of four candidates is loaded while the current
-// one folds.  LOG_ADD(acc, x) == acc whenever acc - x >= 7.5, and LOG_ADD(acc,
-// LOG_ZERO) == acc: every listed element and the padding fold unconditionally.
+// iteration).  LOG_ADD(acc, x) == acc whenever acc - x >= 7.5, and
+// LOG_ADD(acc, LOG_ZERO) == acc: every listed element and the padding fold
+// unconditionally.  16-byte loads: the fold runs one lane's chain per pair,
+// so the kernel lasts as long as the longest chain and every load the chain
+// waits for adds to it.  Within a row, eight elements per step with the next
+// 16 in flight; the next row's first 16 (its count read two rows ahead)
+// loaded at the row's start.  The loads are unconditional (elements past a
+// row's count are masked where they are folded; the reads stay inside the
+// pair's region or, past its last row, inside the batch scratch's padding
+// after bl, kLaneFoldPad): predicated loads made every wait a vmcnt(0).
 __global__ __launch_bounds__(256) void k_local_fold(SeqSet sq, PairMeta pm, ChainMeta cm, PairRec* __restrict__ rec,
                                                     Scratch sc, int64_t npairs) {
   __shared__ float4 lk[kLookupRows];
@@ -471,87 +412,73 @@ __global__ __launch_bounds__(256) void k_local_fold(SeqSet sq, PairMeta pm, Chai
   if (p >= npairs) return;
   const int L1 = sq.len[pm.pa[p]], L2 = sq.len[pm.pb[p]];
   const int h = pm.chain[p];
-  const float* __restrict__ area = lanefold_area(sc, cm.cell_off[h], pm.row0[p], cm.width[h]);
   const int64_t ell = pm.ell_row[p];
   float acc = LZ;
   bool bad = false;
   int n = sc.ell_cnt[ell];
   float rb = sc.crb[ell];
-  if (sc.pg_stride == 1) {
-    // contiguous rows, 16-byte loads: the fold runs one lane's chain per
-    // pair, so the kernel lasts as long as the longest chain and every load
-    // the chain waits for adds to it.  Within a row, eight elements per step
-    // with the next 16 in flight; the next row's first 16 (its count read
-    // two rows ahead) loaded at the row's start.  The loads are unconditional
-    // (elements past a row's count are masked where they are folded; the
-    // reads stay inside the pair's slots or, past its last row, inside the
-    // batch scratch): predicated loads made every wait a vmcnt(0).
-    const float4* __restrict__ rows4 = reinterpret_cast<const float4*>(lanefold_rows(sc, cm.cell_off[h], pm.row0[p], cm.width[h]));
-    const int RS4 = lanefold_rs(L2) >> 2;
-    const float4 Z4 = make_float4(LZ, LZ, LZ, LZ);
-    int n1 = sc.ell_cnt[ell + min(1, L1 - 1)];
-    float4 a0 = rows4[0], a1 = rows4[1], b0 = rows4[2], b1 = rows4[3];
-    auto fold4 = [&](const float4 v, int k) {
-      acc = mlp_log_add_t(acc, k < n ? v.x : LZ, lk);
-      acc = mlp_log_add_t(acc, k + 1 < n ? v.y : LZ, lk);
-      acc = mlp_log_add_t(acc, k + 2 < n ? v.z : LZ, lk);
-      acc = mlp_log_add_t(acc, k + 3 < n ? v.w : LZ, lk);
-    };
-    for (int i = 1; i <= L1; ++i) {
-      const float4* __restrict__ src = rows4 + (int64_t)(i - 1) * RS4;
-      const float4* __restrict__ nxt = src + RS4;
-      const int n2 = sc.ell_cnt[ell + min(i + 1, L1 - 1)];  // (past the last row: unused)
-      const float rb_next = sc.crb[ell + min(i, L1 - 1)];
-      const float4 na0 = nxt[0], na1 = nxt[1], nb0 = nxt[2], nb1 = nxt[3];
-      bad |= rb > acc;  // the listing's bound must not exceed the chain at the row's start
-      for (int k = 0; k < n; k += 8) {
-        const float4 c0 = src[(k >> 2) + 4], c1 = src[(k >> 2) + 5];
-        fold4(a0, k);
-        if (k + 4 < n) fold4(a1, k + 4);
-        a0 = b0;
-        a1 = b1;
-        b0 = c0;
-        b1 = c1;
-      }
-      a0 = na0;
-      a1 = na1;
-      b0 = nb0;
-      b1 = nb1;
-      n = n1;
-      n1 = n2;
-      rb = rb_next;
-    }
-    rec[p].tfl = acc;
-    if (bad) {
-      const int k = atomicAdd(&sc.rep[0], 1);
-      sc.rep[1 + k] = (int32_t)p;
-    }
-    return;
-  }
+  const float4* __restrict__ rows4 = reinterpret_cast<const float4*>(lanefold_rows(sc, cm.cell_off[h], pm.row0[p], cm.width[h]));
+  const int RS4 = lanefold_rs(L2) >> 2;
+  int n1 = sc.ell_cnt[ell + min(1, L1 - 1)];
+  float4 a0 = rows4[0], a1 = rows4[1], b0 = rows4[2], b1 = rows4[3];
+  auto fold4 = [&](const float4 v, int k) {
+    acc = mlp_log_add_t(acc, k < n ? v.x : LZ, lk);
+    acc = mlp_log_add_t(acc, k + 1 < n ? v.y : LZ, lk);
+    acc = mlp_log_add_t(acc, k + 2 < n ? v.z : LZ, lk);
+    acc = mlp_log_add_t(acc, k + 3 < n ? v.w : LZ, lk);
+  };
   for (int i = 1; i <= L1; ++i) {
-    const float* __restrict__ src = area + 2 * (int64_t)(i - 1) * L2;
-    // the next row's count and bound, loaded ahead
-    const int n_next = i < L1 ? sc.ell_cnt[ell + i] : 0;
-    const float rb_next = i < L1 ? sc.crb[ell + i] : LZ;
+    const float4* __restrict__ src = rows4 + (int64_t)(i - 1) * RS4;
+    const float4* __restrict__ nxt = src + RS4;
+    const int n2 = sc.ell_cnt[ell + min(i + 1, L1 - 1)];  // (past the last row: unused)
+    const float rb_next = sc.crb[ell + min(i, L1 - 1)];
+    const float4 na0 = nxt[0], na1 = nxt[1], nb0 = nxt[2], nb1 = nxt[3];
     bad |= rb > acc;  // the listing's bound must not exceed the chain at the row's start
-    float x0 = 0 < n ? src[0] : LZ, x1 = 1 < n ? src[2] : LZ, x2 = 2 < n ? src[4] : LZ, x3 = 3 < n ? src[6] : LZ;
-    for (int k = 0; k < n; k += 4) {
-      const float y0 = k + 4 < n ? src[2 * (k + 4)] : LZ, y1 = k + 5 < n ? src[2 * (k + 5)] : LZ;
-      const float y2 = k + 6 < n ? src[2 * (k + 6)] : LZ, y3 = k + 7 < n ? src[2 * (k + 7)] : LZ;
-      acc = mlp_log_add_t(acc, x0, lk);
-      acc = mlp_log_add_t(acc, x1, lk);
-      acc = mlp_log_add_t(acc, x2, lk);
-      acc = mlp_log_add_t(acc, x3, lk);
-      x0 = y0; x1 = y1; x2 = y2; x3 = y3;
+    for (int k = 0; k < n; k += 8) {
+      const float4 c0 = src[(k >> 2) + 4], c1 = src[(k >> 2) + 5];
+      fold4(a0, k);
+      if (k + 4 < n) fold4(a1, k + 4);
+      a0 = b0;
+      a1 = b1;
+      b0 = c0;
+      b1 = c1;
     }
-    n = n_next;
+    a0 = na0;
+    a1 = na1;
+    b0 = nb0;
+    b1 = nb1;
+    n = n1;
+    n1 = n2;
     rb = rb_next;
   }
   rec[p].tfl = acc;
-  if (bad) {
+  if (bad || sc.force_repair) {
     const int k = atomicAdd(&sc.rep[0], 1);
     sc.rep[1 + k] = (int32_t)p;
   }
+}
+
+// Wave per pair, after the backward sweep: the backward chain over the chunks
+// whose maximum passes the test (k_local_totals' second half).
+__global__ __launch_bounds__(256) void k_local_btot(ModelScalars ms, const Tables* __restrict__ tab, SeqSet sq,
+                                                    PairMeta pm, ChainMeta cm, PairRec* __restrict__ rec, Scratch sc,
+                                                    int64_t npairs) {
+  __shared__ float4 lk[kLookupRows];
+  __shared__ float match[26 * 26], ins[26];
+  if (threadIdx.x == 0) mlp_lookup_table(lk);
+  for (int k = threadIdx.x; k < 26 * 26; k += blockDim.x) match[k] = tab->match[k];
+  if (threadIdx.x < 26) ins[threadIdx.x] = tab->ins[threadIdx.x];
+  __syncthreads();
+  const int64_t p = wave_index();
+  if (p >= npairs) return;
+  const int lane = threadIdx.x & 63;
+  const int L1 = sq.len[pm.pa[p]], L2 = sq.len[pm.pb[p]];
+  const int h = pm.chain[p];
+  const uint8_t* s1 = sq.res + sq.off[pm.pa[p]];
+  const uint8_t* s2 = sq.res + sq.off[pm.pb[p]];
+  const float tb = fold_chunks<true>(LZ, 0, (int64_t)L1 * local_chunks(L2), sc.cmb + pm.rm_off[p], sc.bl, L2,
+                                     pm.row0[p], cm.width[h], cm.cell_off[h], s1, s2, match, ins, 2 * ms.rt1, lk, lane);
+  if (lane == 0) rec[p].tbl = tb;
 }
 
 // =====================================================================
@@ -634,16 +561,6 @@ __global__ void k_fold_totals(ModelScalars ms, SeqSet sq, PairMeta pm, PairRec* 
   r.b5[0] = tb;  // merge kernel reads the folded backward total here
 }
 
-#ifdef MLP_EXP_TOT_STATS
-void tot_stats_print() {
-  unsigned long long h[8];
-  hipMemcpyFromSymbol(h, HIP_SYMBOL(g_totstats), sizeof(h));
-  fprintf(stderr,
-          "[totals] rows %llu listed %llu overflow rows %llu fwd live chunks %llu bwd live chunks %llu folded %llu "
-          "row max below %llu above %llu\n",
-          h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7]);
-}
-#endif
 // ------------------------------------------------------------ launchers
 hipError_t launch_local_totals(const ModelScalars& ms, const Tables* tab, SeqSet seqs, PairMeta pm, ChainMeta cm,
                                PairRec* rec, Scratch sc, int64_t npairs, int nwaves, hipStream_t st) {
@@ -658,9 +575,10 @@ hipError_t launch_local_totals(const ModelScalars& ms, const Tables* tab, SeqSet
   return hipGetLastError();
 }
 
-hipError_t launch_local_totals_lanefold(const ModelScalars& ms, const Tables* tab, SeqSet seqs, PairMeta pm,
-                                        ChainMeta cm, PairRec* rec, Scratch sc, int64_t npairs, int nwaves,
-                                        hipStream_t st) {
+// The lane fold, forward half: between the forward and the backward sweeps
+// (the lists live in bl until the backward sweep writes it).
+hipError_t launch_local_fwd_lanefold(SeqSet seqs, PairMeta pm, ChainMeta cm, PairRec* rec, Scratch sc, int64_t npairs,
+                                     int nwaves, hipStream_t st) {
   if (npairs <= 0) return hipSuccess;
   if (nwaves % kWavesPerBlock) return hipErrorInvalidValue;
   hipError_t e;
@@ -668,11 +586,21 @@ hipError_t launch_local_totals_lanefold(const ModelScalars& ms, const Tables* ta
   const dim3 lanes((unsigned)((npairs + 255) / 256));
   hipLaunchKernelGGL(k_local_bounds, lanes, dim3(256), 0, st, seqs, pm, sc, npairs);
   if ((e = hipMemsetAsync(sc.tot_next, 0, sizeof(int32_t), st)) != hipSuccess) return e;
-  hipLaunchKernelGGL(k_local_list, wave_grid(nwaves), dim3(64 * kWavesPerBlock), 0, st, ms, tab, seqs, pm, cm, rec, sc,
-                     npairs);
+  hipLaunchKernelGGL(k_local_list, wave_grid(nwaves), dim3(64 * kWavesPerBlock), 0, st, seqs, pm, cm, sc, npairs);
   hipLaunchKernelGGL(k_local_fold, lanes, dim3(256), 0, st, seqs, pm, cm, rec, sc, npairs);
-  // pairs whose bound failed (normally none: the waves find an empty list
-  // and exit) are redone with the running-maximum bound
+  return hipGetLastError();
+}
+
+// ... and after the backward sweep: the backward chains, then the pairs whose
+// bound failed (normally none: the waves find an empty list and exit) redone
+// with the running-maximum bound, both chains.
+hipError_t launch_local_bwd_lanefold(const ModelScalars& ms, const Tables* tab, SeqSet seqs, PairMeta pm, ChainMeta cm,
+                                     PairRec* rec, Scratch sc, int64_t npairs, int nwaves, hipStream_t st) {
+  if (npairs <= 0) return hipSuccess;
+  if (nwaves % kWavesPerBlock) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_local_btot, wave_grid(npairs), dim3(64 * kWavesPerBlock), 0, st, ms, tab, seqs, pm, cm, rec, sc,
+                     npairs);
+  hipError_t e;
   if ((e = hipMemsetAsync(sc.tot_next, 0, sizeof(int32_t), st)) != hipSuccess) return e;
   hipLaunchKernelGGL(k_local_totals, wave_grid(std::min(nwaves, 1024)), dim3(64 * kWavesPerBlock), 0, st, ms, tab, seqs,
                      pm, cm, rec, sc, npairs, (const int32_t*)sc.rep);

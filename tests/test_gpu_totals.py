@@ -1,13 +1,15 @@
 """The local-model chain totals three ways (CPNP/ProbabilisticModel.h:435-450:
 one serial, non-associative LOG_ADD chain per pair): one wave per pair with
 the running-maximum skip bound (MLP_TOT_FOLDBOUND=0), the same with the
-folded chunk-maximum bound (=1, the default), and one pair per lane after a
-listing pass into the dead PF forward Zm slots (MLP_TOT_LANEFOLD=1).  All are
-exact, so the sparse store, distances and MEA scores must be bit-identical,
-at pid 0 and 1 (the models with the partition function) on similar and
-divergent families, and with several batches and the PF posterior in the Zm
-slots (small scratch budget) as well.  Each setting runs in a child process:
-the switches are read once per process."""
+folded chunk-maximum bound (=1), and one pair per lane after a listing pass
+into the local backward array between the two sweeps (MLP_TOT_LANEFOLD=1,
+the default above the CLIs' 48 GB scratch), also with every pair sent
+through the lane fold's repair pass
+(MLP_TOT_FORCE_REPAIR).  All are exact, so the sparse store, distances and
+MEA scores must be bit-identical, at pid 0, 1 and 2 (the local model alone:
+no side stream) on similar and divergent families, and with several batches
+and the PF posterior in the Zm slots (small scratch budget) as well.  Each
+setting runs in a child process: the switches are read once per process."""
 import os
 import subprocess
 import sys
@@ -25,7 +27,8 @@ sys.path.insert(0, sys.argv[1])
 from mlprobs_amd import synth
 from mlprobs_amd.engine import Family
 out = []
-for n, L, s, seed, pid in ((48, 300, 0.7, 31, 0), (40, 260, 0.35, 32, 0), (36, 220, 0.9, 33, 1), (6, 900, 0.6, 34, 0)):
+for n, L, s, seed, pid in ((48, 300, 0.7, 31, 0), (40, 260, 0.35, 32, 0), (36, 220, 0.9, 33, 1), (6, 900, 0.6, 34, 0),
+                           (30, 240, 0.6, 35, 2)):
     seqs = [q for _, q in synth.family(n, L, s, seed=seed)]
     f = Family(seqs)
     if len(sys.argv) > 2:
@@ -40,8 +43,11 @@ print(' '.join(out))
 '''
 
 
-def _run(lanefold, scratch=None, foldbound=1):
+def _run(lanefold, scratch=None, foldbound=1, repair=False):
     env = dict(os.environ, MLP_TOT_LANEFOLD=str(lanefold), MLP_TOT_FOLDBOUND=str(foldbound))
+    env.pop('MLP_TOT_FORCE_REPAIR', None)
+    if repair:
+        env['MLP_TOT_FORCE_REPAIR'] = '1'
     args = [sys.executable, '-c', _CHILD, ROOT] + ([str(scratch)] if scratch else [])
     r = subprocess.run(args, capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
@@ -52,11 +58,13 @@ def test_totals_bit_identical():
     ref = _run(0, foldbound=0)
     assert _run(0) == ref
     assert _run(1) == ref
+    assert _run(1, repair=True) == ref
 
 
 def test_totals_bit_identical_small_scratch():
     # 1 GB: several batches, the PF posterior in the low halves of the Zm
-    # slots whose high halves hold the lane fold's candidates
+    # slots (the lane fold's candidates in the local backward array either way)
     ref = _run(0, 1 << 30, foldbound=0)
     assert _run(0, 1 << 30) == ref
     assert _run(1, 1 << 30) == ref
+    assert _run(1, 1 << 30, repair=True) == ref

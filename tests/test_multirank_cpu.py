@@ -277,3 +277,48 @@ def test_relax_shard_plan_balance():
         assert b[0] == 0 and b[-1] == P and all(b[r] <= b[r + 1] for r in range(R))
         loads = [cost[b[r]:b[r + 1]].sum() for r in range(R)]
         assert max(loads) <= cost.sum() / R + cost.max() * 1.0001
+
+
+def test_bench_two_ranks_dry_run():
+    """bench.py's N-rank path (per-rank records, all-gather timing and bytes,
+    consistency rounds with their gathers) run as torchrun would on GPUs, on
+    host contexts over gloo (--host): the JSON line carries the multi-rank
+    fields, both ranks hold the same store after the posterior stage and each
+    round, and that store is the single-process one (the library's host
+    context, itself checked against the oracle above)."""
+    import hashlib
+    import json
+    import subprocess
+    from mlprobs_amd import synth
+    from mlprobs_amd.engine import Family
+    port = _free_port()
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '2', '--master-addr',
+           '127.0.0.1', '--master-port', str(port), os.path.join(ROOT, 'bench.py'), '--gpus', '2', '--host',
+           '--nseq', '10', '--len', '40', '--steps', '1', '--warmup', '0', '--no-cpu', '--no-e2e', '--no-qp',
+           '--no-shards', '--relax', '2']
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd='/tmp')
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d['n_gpus'] == 2 and len(d['ranks']) == 2
+    assert d['gather_ms'] > 0 and d['gather_GBps'] > 0
+    assert all(x['gather_bytes_in'] > 0 and x['pairs'] > 0 for x in d['ranks'])
+    assert sum(x['pairs'] for x in d['ranks']) == 45
+    assert d['relax']['rounds'] == 2 and len(d['relax']['per_round'][0]['ranks']) == 2
+    assert d['ranks_identical']
+
+    def hsh(f):
+        h = hashlib.sha256()
+        for a in f.export():
+            h.update(np.ascontiguousarray(a).tobytes())
+        return h.hexdigest()
+
+    seqs = [s for _, s in synth.family(10, 40, 0.7, seed=11)]
+    f = Family(seqs, host=True)
+    try:
+        f.posteriors(0, DELTA)
+        assert d['ranks'][0]['store_hash'] == hsh(f)
+        for rr in d['relax']['per_round']:
+            f.relax(1)
+            assert rr['ranks'][0]['store_hash'] == hsh(f)
+    finally:
+        f.close()
