@@ -254,7 +254,7 @@ class RankExchange:
         self.host_gather_s = 0.0
 
 
-def store_bytes(fam, p0=0, p1=None):
+def gather_bytes_of(fam, p0=0, p1=None):
     """Bytes of the canonical store of pairs [p0, p1): entries (uint16 column
     + fp32 value), row pointers (int32) and per-pair results (distance, MEA
     score, entry count: 16 B) -- what the all-gather moves."""
@@ -284,7 +284,7 @@ def multirank_legs(fam, ex, args, world, rank, dist, lens, p0, p1, dt, kt, sync)
     args.relax consistency rounds, each timed as the max over ranks with its
     per-rank relaxation-kernel and gather times."""
     gms = ex.gather_ms(kt) / args.steps
-    recv = store_bytes(fam) - store_bytes(fam, p0, p1)
+    recv = gather_bytes_of(fam) - gather_bytes_of(fam, p0, p1)
     cells = int(sum((lens[a] + 1) * (lens[b] + 1) for a, b in
                     __import__('mlprobs_amd.engine', fromlist=['x']).pairs_of(len(lens))[p0:p1]))
     me = {'rank': rank, 'pairs': p1 - p0, 'pair_cells': cells,
@@ -629,11 +629,10 @@ def shard_gather(args, seqs, post_hash=None, relax_hash=None):
     xGMI on a multi-GPU box."""
     from mlprobs_amd.engine import Family
     fam = Family(seqs, shards=8)
-    # the 8 shards split the parent's scratch budget; with the library's
-    # default (most of the device) plus 9 copies of the store the device runs
-    # full and the gather stalls (411 ms against 17 ms, round 4): the round-3
-    # budget, 120 GiB, leaves the copies room
-    fam.set_scratch(120 << 30)
+    # the library's default budget: the 8 shards split it less room for their
+    # 9 store copies and gather buffers (round 4 set 120 GiB here: with the
+    # whole default split, the device ran full and the gather took 411 ms
+    # against 17 ms)
     # twice: the first stage allocates the shards' scratch and store copies
     # (a fresh allocation can stall ~5.7 s while the driver releases what the
     # bench's own stage freed, DESIGN.md section 3), the second is warm
@@ -1026,6 +1025,7 @@ def main():
                                'achieved_GBps': value * STAGE_BYTES / 1e9,
                                'frac': value * STAGE_BYTES / 1e9 / HBM_PEAK_GBS},
             'kernels_ms_per_step': {k: v['ms'] / args.steps for k, v in kt.items() if v['launches']},
+            'batches_per_step': kt['forward']['launches'] / args.steps,
             'cpu_baseline': cpu,
             'parity': parity,
         }

@@ -443,12 +443,14 @@ int mlp_ctx_create(int device, mlp_ctx** out) {
   // local-total chains and shorten the per-batch tails -- on MI355X ~224 GiB,
   // the C3 posterior stage in three batches instead of five (step 576 -> 545-557
   // ms, totals 61 -> 48.5 ms; round 4 measured half the free HBM until then).
-  // Free memory may read low for a while after another process released a
-  // large allocation (the driver clears it lazily), so plan with at least 90%
-  // of the device; an allocation that really fails halves the budget.
+  // The budget is a cap: a batch allocates only what its pairs need, so a
+  // family smaller than the device takes no more than it uses.  Planned from
+  // the free HBM as the driver reports it (a device shared with another
+  // process gets smaller batches, never an oversubscription); an allocation
+  // that still fails halves the budget and retries.
   {
-    const size_t usable = std::max<size_t>(freeb, total / 10 * 9);
-    const size_t reserve = std::max<size_t>(16ull << 30, usable / 100 * 7);
+    const size_t usable = freeb;
+    const size_t reserve = std::max<size_t>(16ull << 30, total / 100 * 7);
     c->scratch_budget = usable > 2 * reserve ? usable - reserve : usable / 2;
   }
   if (const char* s = getenv("MLP_SCRATCH_GB")) c->scratch_budget = (size_t)(atof(s) * (1ull << 30));
@@ -907,8 +909,17 @@ static int ensure_shards(mlp_ctx* c, int S) {
       c->err = "shard context on device " + std::to_string(devs[di]) + " failed";
       return rc;
     }
-    // shards sharing a device share its scratch budget (and the parent's cap)
-    ch->scratch_budget = std::min(ch->scratch_budget, c->scratch_budget) / per[di];
+    // shards sharing a device share its scratch budget (and the parent's
+    // cap), less what each of them and the parent keep beside it: a gathered
+    // copy of the whole store and the all-gather's staging buffers (~0.16 B
+    // per pair-cell at C3 pid 0; 0.5 B planned)
+    double cells = 0;
+    for (int64_t p = 0; p < c->P; p++) cells += pair_cost_cells(c, p);
+    const size_t keep = (size_t)(0.5 * cells) + (256ull << 20);
+    size_t b = std::min(ch->scratch_budget, c->scratch_budget);
+    const size_t copies = keep * (size_t)(per[di] + 1);
+    b = b > 2 * copies ? b - copies : b / 2;
+    ch->scratch_budget = b / per[di];
     ch->profile = c->profile;
     c->shards.push_back(ch);
     if ((rc = mlp_family_load(ch, c->n, (const char*)c->h_res.data(), c->offs.data()))) {
@@ -2939,6 +2950,10 @@ static int relax_one(mlp_ctx* c, const QpRelax& qp, bool last) {
     for (int64_t k = 0; k < nout; k++) c->nnz[r0 + k] = pn[k];
     for (int64_t p = r0; p <= r1; p++) c->ent_off[p] = noff[p];
     c->ent_off[r1] = run;
+    // outside the range: empty blocks, as the host context lays them out
+    // (0 before r0, the range's total after r1)
+    for (int64_t p = 0; p < r0; p++) c->ent_off[p] = 0;
+    for (int64_t p = r1 + 1; p <= c->P; p++) c->ent_off[p] = run;
     c->store_p0 = r0;
     c->store_p1 = r1;
     c->store_total = run; ++c->store_ver;

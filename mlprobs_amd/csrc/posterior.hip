@@ -108,10 +108,22 @@ __device__ __forceinline__ void pf_rescale_fast(double& m, double& e, double& f,
 // Forward sweep: 5-state forward, local forward, PF forward Zm.
 // =====================================================================
 template <int M>
-__global__ __launch_bounds__(256, SweepWaves<M>::fwd) void k_forward(ModelScalars ms, const Tables* __restrict__ tab,
+__global__ __launch_bounds__(256, SweepWaves<M>::fwd) void k_forward(ModelScalars ms_in, const Tables* __restrict__ tab,
                                                  SeqSet sq, PairMeta pm, ChainMeta cm,
                                                  PairRec* __restrict__ rec, Scratch sc,
                                                  int64_t nchains, int lds_seq) {
+  ModelScalars ms = ms_in;
+#ifdef MLP_SWEEP_VCONST  // A/B: the transition constants as VGPR operands (SGPR operands issue at half rate)
+#pragma unroll
+  for (int a = 0; a < 5; ++a)
+#pragma unroll
+    for (int b = 0; b < 5; ++b) asm volatile("" : "+v"(ms.t[a][b]));
+#pragma unroll
+  for (int a = 0; a < 3; ++a)
+#pragma unroll
+    for (int b = 0; b < 3; ++b) asm volatile("" : "+v"(ms.lt[a][b]));
+  asm volatile("" : "+v"(ms.rt1));
+#endif
   __shared__ LdsTablesFor<M> T_;
   extern __shared__ __align__(16) uint8_t dyn[];
   stage_tables(T_, tab);
@@ -561,7 +573,11 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
               // reciprocals (a few fp64 ulps from the division); QuickProbs
               // (plain double, bit-exact) divides like the reference
               double qv;
+#ifdef MLP_PF_DIVIDE  // A/B build (tools/pf_quotient_ab.py): the division for C_P_NP_Aln too
+              if constexpr (true)
+#else
               if constexpr ((M & kQP) != 0)
+#endif
                 qv = (zf * Zm) / (score * c.zmant);
               else
                 qv = (zf * Zm) * (T_.rsub[c2 * 26 + c1] * c.rzmant);

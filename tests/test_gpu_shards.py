@@ -154,7 +154,8 @@ def test_rccl_allgather_grouped_body_one_rank():
 
 def test_relax_range_matches_full_round():
     """mlp_relax_range on the device: each output range's block equals the
-    same pairs of a full round, bit for bit."""
+    same pairs of a full round, bit for bit, and the entry offsets outside the
+    range are laid out as the host context lays them out."""
     seqs = [s for _, s in synth.family(36, 150, 0.7, seed=94)]
     full = Family(seqs)
     full.posteriors(0, 0.132548)
@@ -171,5 +172,30 @@ def test_relax_range_matches_full_round():
         np.testing.assert_array_equal(rp[a:b], rp_f[a:b])
         np.testing.assert_array_equal(c[int(eo[r0]):int(eo[r1])], c_f[int(eo_f[r0]):int(eo_f[r1])])
         np.testing.assert_array_equal(v[int(eo[r0]):int(eo[r1])], v_f[int(eo_f[r0]):int(eo_f[r1])])
+        # the whole entry-offset layout as the host context leaves it (0
+        # before r0, the range's total after r1)
+        host = Family(seqs, host=True)
+        host.import_csr(*base)
+        host.relax_range(r0, r1)
+        np.testing.assert_array_equal(eo, host.export()[1])
+        host.close()
         part.close()
     full.close()
+
+
+def test_virtual_shards_default_budget():
+    """Shards sharing a device on the library's default scratch budget (no
+    set_scratch): the budget they split leaves room for each shard's store
+    copy and gather buffers; store, distances and a relaxation round equal the
+    one-context run."""
+    seqs = [s for _, s in synth.family(40, 180, 0.7, seed=61)]
+    one = Family(seqs)
+    one.posteriors(0, 0.132548)
+    many = Family(seqs, shards=4)
+    many.posteriors(0, 0.132548)
+    _same(one, many, 'default budget posteriors')
+    one.relax(1)
+    many.relax(1)
+    _same(one, many, 'default budget relax round')
+    one.close()
+    many.close()
