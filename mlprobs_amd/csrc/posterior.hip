@@ -108,22 +108,10 @@ __device__ __forceinline__ void pf_rescale_fast(double& m, double& e, double& f,
 // Forward sweep: 5-state forward, local forward, PF forward Zm.
 // =====================================================================
 template <int M>
-__global__ __launch_bounds__(256, SweepWaves<M>::fwd) void k_forward(ModelScalars ms_in, const Tables* __restrict__ tab,
+__global__ __launch_bounds__(256, SweepWaves<M>::fwd) void k_forward(ModelScalars ms, const Tables* __restrict__ tab,
                                                  SeqSet sq, PairMeta pm, ChainMeta cm,
                                                  PairRec* __restrict__ rec, Scratch sc,
                                                  int64_t nchains, int lds_seq) {
-  ModelScalars ms = ms_in;
-#ifdef MLP_SWEEP_VCONST  // A/B: the transition constants as VGPR operands (SGPR operands issue at half rate)
-#pragma unroll
-  for (int a = 0; a < 5; ++a)
-#pragma unroll
-    for (int b = 0; b < 5; ++b) asm volatile("" : "+v"(ms.t[a][b]));
-#pragma unroll
-  for (int a = 0; a < 3; ++a)
-#pragma unroll
-    for (int b = 0; b < 3; ++b) asm volatile("" : "+v"(ms.lt[a][b]));
-  asm volatile("" : "+v"(ms.rt1));
-#endif
   __shared__ LdsTablesFor<M> T_;
   extern __shared__ __align__(16) uint8_t dyn[];
   stage_tables(T_, tab);

@@ -133,15 +133,37 @@ __global__ __launch_bounds__(64) void k_profile_post(ProfileArgs A) {
         if (lane < nl)
           for (int k = 0; k < cnt; ++k) st_l[start + k] = (uint8_t)lane;
         wave_sync();
-        // ---- products of every staged entry, in parallel
-        for (int t = lane; t < total_staged; t += 64) {
-          const int lo = st_l[t];
-          const int64_t ent = l_e[lo] + (t - l_st[lo]);
-          const int col = l_tr[lo] ? A.tcols[ent] : A.cols[ent];
-          const float v = l_tr[lo] ? A.tvals[ent] : A.vals[ent];
-          const int c = A.map2[A.map2_off[l_j[lo]] + col];
-          st_c[t] = c;
-          if (c >= c0 && c < c1) st_p[t] = l_w[lo] * v;  // posterior[id] += w * v
+        // ---- products of every staged entry, in parallel, four entries a
+        // lane at a time: their column / value loads (first touches of the
+        // blocks, HBM) issue together, then the column maps, then the stores
+        for (int t0 = lane; t0 < total_staged; t0 += 4 * 64) {
+          int col[4], moff[4];
+          float v[4], wq[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int t = t0 + 64 * u;
+            col[u] = 0;
+            v[u] = 0.f;
+            moff[u] = 0;
+            wq[u] = 0.f;
+            if (t < total_staged) {
+              const int lo = st_l[t];
+              const int64_t ent = l_e[lo] + (t - l_st[lo]);
+              col[u] = l_tr[lo] ? A.tcols[ent] : A.cols[ent];
+              v[u] = l_tr[lo] ? A.tvals[ent] : A.vals[ent];
+              moff[u] = (int)A.map2_off[l_j[lo]];
+              wq[u] = l_w[lo];
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int t = t0 + 64 * u;
+            if (t < total_staged) {
+              const int c = A.map2[moff[u] + col[u]];
+              st_c[t] = c;
+              if (c >= c0 && c < c1) st_p[t] = wq[u] * v[u];  // posterior[id] += w * v
+            }
+          }
         }
         wave_sync();
         // ---- add them pair by pair: LDS float adds without return, which a

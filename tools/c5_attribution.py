@@ -99,7 +99,13 @@ def main():
     ap.add_argument('--max-cells', type=float, default=5e7)
     ap.add_argument('--out', default=os.path.join(ROOT, 'profiles', 'r05_c5_attribution.json'))
     ap.add_argument('--only', default=None, help='comma-separated family names')
+    ap.add_argument('--recheck', default=None,
+                    help='a previous output: re-run each differing family\'s multi-threaded reference K more times '
+                         'with the clock fixed and reclassify (race = two multi-threaded runs differ)')
+    ap.add_argument('--k', type=int, default=4)
     args = ap.parse_args()
+    if args.recheck:
+        return recheck(args)
     with lzma.open(os.path.join(ROOT, 'tests', 'golden', 'sweep.json.xz'), 'rt') as fh:
         fams = json.load(fh)
     names = [k for k in sorted(fams) if k.split('/')[0] in ('ox', 'sabre')]
@@ -150,6 +156,60 @@ def main():
     with open(args.out, 'w') as fh:
         json.dump(res, fh, indent=1)
     print(json.dumps({k: v for k, v in res.items() if k not in ('rows', 'method')}))
+
+
+def recheck(args):
+    """Second pass over the differing families: the reference CLIs
+    multi-threaded K times and single-threaded once, clock fixed, against ours
+    (clock fixed).  Causes: race (the multi-threaded runs disagree among
+    themselves at some stage), threads (they agree with each other, not with
+    the single-threaded run), time-seed (all agree with ours and the family
+    takes the -p 1 path: the wall-clock difference is srand(time(0))),
+    race-unreproduced (all agree, -p 0 path: the wall-clock multi-threaded run
+    differed, the K fixed-clock ones did not), UNEXPLAINED (ours differs from
+    the single-threaded reference)."""
+    with open(args.recheck) as fh:
+        prev = json.load(fh)
+    with lzma.open(os.path.join(ROOT, 'tests', 'golden', 'sweep.json.xz'), 'rt') as fh:
+        fams = json.load(fh)
+    rows = []
+    with tempfile.TemporaryDirectory() as td:
+        for r in prev['rows']:
+            name = r['family']
+            fa = os.path.join(td, 'f.fa')
+            with open(fa, 'wb') as fh:
+                fh.write(fams[name]['fa'].encode('latin-1'))
+            ours = run(fa, td, 'ours_ft', threads=args.threads, fixed=True)
+            st = run(fa, td, 'st_ft', ref='st', threads=1, fixed=True)
+            mts = [run(fa, td, f'mt{k}_ft', ref='mt', threads=args.threads, fixed=True) for k in range(args.k)]
+            ok = ours is not None and st is not None and all(m is not None for m in mts)
+            stages_mt = sorted({first_diff(mts[0], m) for m in mts[1:]} - {None}, key=STAGES.index) if ok else []
+            if not ok or ours['output'] != st['output']:
+                cause = 'UNEXPLAINED'
+            elif stages_mt:
+                cause = 'race'
+            elif mts[0]['output'] != st['output']:
+                cause = 'threads'
+            elif (ours.get('class1') == 1):
+                cause = 'time-seed'
+            else:
+                cause = 'race-unreproduced'
+            distinct = len({m['output'] for m in mts}) if ok else None
+            row = dict(r, cause=cause, mt_runs=args.k, mt_distinct_outputs=distinct,
+                       mt_distinct_features=len({m['features_line'] for m in mts}) if ok else None,
+                       mt_stages_that_vary=stages_mt,
+                       first_stage_ours_vs_st_fixed_clock=first_diff(ours, st),
+                       first_stage_st_vs_mt_fixed_clock=sorted({first_diff(st, m) for m in mts} - {None},
+                                                               key=STAGES.index) if ok else None)
+            rows.append(row)
+            print(json.dumps(row), flush=True)
+    causes = {}
+    for r in rows:
+        causes[r['cause']] = causes.get(r['cause'], 0) + 1
+    res = dict(prev, causes=causes, rows=rows, recheck={'k': args.k, 'method': recheck.__doc__.replace('\n', ' ')})
+    with open(args.out, 'w') as fh:
+        json.dump(res, fh, indent=1)
+    print(json.dumps({k: v for k, v in res.items() if k not in ('rows', 'method', 'recheck')}))
 
 
 if __name__ == '__main__':

@@ -72,7 +72,7 @@ def main(d):
 
 
 GROUPS = {'forward': ('k_forward',), 'backward': ('k_backward', 'k_fold_totals'),
-          'local_totals': ('k_local_totals', 'k_local_bounds', 'k_local_list', 'k_local_fold'),
+          'local_totals': ('k_local_totals', 'k_local_bounds', 'k_local_list', 'k_local_fold', 'k_local_btot'),
           'merge_mea_sparsify': ('k_merge',), 'compact': ('k_compact',)}
 
 
