@@ -28,8 +28,12 @@ constexpr int kChainSeqMax = 50000;   // residue bytes of a single-pair chain (o
 constexpr int kMinWidth = 192;   // W floor: boundary chunks are loaded 64 columns ahead
 // W for a chain whose widest member has L2 columns (+1): multiple of 8 so the
 // unrolled step loops never straddle a boundary-chunk switch
+// chain widths are multiples of this: every wavefront segment (64 steps, or
+// W mod 64 at a row's end) is a whole number of the sweeps' and the merge's
+// load-queue groups (static_asserts in posterior.hip)
+constexpr int kWidthQuantum = 8;
 __host__ __device__ constexpr int chain_width(int maxL2) {
-  return ((maxL2 + 1 < kMinWidth ? kMinWidth : maxL2 + 1) + 7) & ~7;
+  return ((maxL2 + 1 < kMinWidth ? kMinWidth : maxL2 + 1) + kWidthQuantum - 1) & ~(kWidthQuantum - 1);
 }
 // LDS residue bytes of a chain of `n` members with sum of L1 = `sum_l1`:
 // a zero area of W + 2, then per member the padded row (L1 + 2) and column
@@ -406,14 +410,16 @@ size_t profile_lds(int L2);
 // Device MEA (k_profile_mea): one workgroup per 64-row strip, strips
 // pipelined across CUs through HBM.  Workspace layout (mea_layout): the
 // choices (2 bits a cell, per strip, 16-step block and lane a uint32), each
-// strip's last row, per strip its count of finished columns, the score and
-// an error word (a strip that waited too long for the one above).
+// strip's last row (NaN until written: the next strip polls the values), the
+// score and an error word (a strip that waited too long for the one above).
 constexpr int kMeaBlk = 16;  // steps per block (one uint32 of choices per lane)
 struct MeaLayout {
   int nstrips, nblk, rowpitch;
-  size_t o_tb, o_row, o_prog, o_score, o_err, bytes;
+  size_t o_tb, o_row, o_score, o_err, bytes;
 };
 MeaLayout mea_layout(int L1, int L2);
+static_assert(kMeaBlk % 4 == 0 && 2 * kMeaBlk <= 32, "a block's choices fill one uint32 per lane; windows load 4 at a time");
+constexpr size_t kMeaGuard = 512;              // readable bytes before and after a dense profile posterior (MEA windows)
 struct MeaArgs {
   const float* post;         // (L1 + 1) x (L2 + 1)
   int L1, L2;

@@ -429,8 +429,7 @@ int mlp_ctx_create(int device, mlp_ctx** out) {
     delete c;
     return MLP_ERR_HIP;
   }
-  // MLP_JOIN: experiment hook for SideStream::join_mode (mlp_kernels.h)
-  c->side.join_mode = getenv("MLP_JOIN") ? atoi(getenv("MLP_JOIN")) : 0;
+  c->side.join_mode = 0;
   if (hipMalloc((void**)&c->d_tables, sizeof(Tables)) != hipSuccess) {
     delete c;
     return MLP_ERR_MEMORY;
@@ -710,7 +709,6 @@ static void plan_chains(const mlp_ctx* c, int64_t p, int64_t q, ChainPlan& P) {
   int64_t total_rows = 0;
   for (int64_t k = p; k < q; k++) total_rows += c->lens[c->pa[k]] + 1;
   int64_t target_rows = std::max<int64_t>(512, std::min<int64_t>(1024, total_rows / (2 * 6 * 4 * (int64_t)c->cus)));
-  if (const char* e = getenv("MLP_CHAIN_ROWS")) target_rows = std::max(64, atoi(e));  // tuning hook
   struct ChainH { int64_t begin, end; int W, rows, seq; int64_t cost; };
   std::vector<ChainH> chains;
   ChainH cur{0, 0, 0, 0, 0, 0};
@@ -1191,7 +1189,7 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
   // kernels run, and finishes batch b (entry offsets from its pair records,
   // compaction into the store) before batch b + 1 reuses the scratch.
   const bool two = getenv("MLP_TWO") && atoi(getenv("MLP_TWO")) > 0;  // experiment hook
-  const SideStream* side = (two || getenv("MLP_NO_SIDE")) ? nullptr : &c->side;  // MLP_NO_SIDE: experiment hook
+  const SideStream* side = two ? nullptr : &c->side;
   // model sets whose sweeps run as two kernels: the partition function's on the side stream
   const bool side_used = side && (models & kPF) && models != kPF;
   // k_local_totals: persistent waves, each with 64 candidate rows as wide as
@@ -1614,7 +1612,8 @@ static int profile_posterior(mlp_ctx* c, const std::vector<float>& w, int n1, co
   memcpy(hin + o_mo, moff.data(), b_mo);
   const auto tp1 = std::chrono::steady_clock::now();
   c->prof_t[0] += std::chrono::duration<double>(tp1 - tp0).count();
-  if ((rc = ensure(c, c->r_profile, in_bytes + al(b_inv) + al(b_out)))) return rc;
+  // the dense output with kMeaGuard bytes on either side (the device MEA's row windows read past its rows)
+  if ((rc = ensure(c, c->r_profile, in_bytes + al(b_inv) + kMeaGuard + al(b_out) + kMeaGuard))) return rc;
   char* base = (char*)c->r_profile.p;
   HIPCHK(c, hipMemcpyAsync(base, hin, in_bytes, hipMemcpyHostToDevice, c->stream));
   int64_t* d_rpb = (int64_t*)(base + o_rpb);
@@ -1625,7 +1624,7 @@ static int profile_posterior(mlp_ctx* c, const std::vector<float>& w, int n1, co
   int32_t* d_inv = (int32_t*)(base + in_bytes);
   int32_t* d_m2 = (int32_t*)(base + o_m2);
   int64_t* d_mo = (int64_t*)(base + o_mo);
-  float* d_out = (float*)(base + in_bytes + al(b_inv));
+  float* d_out = (float*)(base + in_bytes + al(b_inv) + kMeaGuard);
   HIPCHK(c, hipMemsetAsync(d_inv, 0, b_inv, c->stream));
   HIPCHK(c, hipMemsetAsync(d_out, 0, (size_t)(L2 + 1) * 4, c->stream));  // row 0
   ProfileArgs pa;
@@ -2607,7 +2606,7 @@ static int relax_one(mlp_ctx* c, const QpRelax& qp, bool last) {
     const int64_t zs = (int64_t)tile_relax_lds(0);
     const int64_t budget = std::min<int64_t>(LDS_MAX - zs, tile_relax_max_cap()) & ~(int64_t)15;
     int64_t small_budget = std::min<int64_t>(budget, (80 * 1024 - zs) & ~(int64_t)15);
-    if (LDS_MAX < 160 * 1024 || getenv("MLP_RELAX_ONECLASS")) small_budget = 0;  // tuning hooks
+    if (LDS_MAX < 160 * 1024) small_budget = 0;
     if (const char* e = getenv("MLP_RELAX_SMALL_KB"))  // test hook: a small staging area for the small class
       small_budget = std::min(budget, std::max<int64_t>(64, (int64_t)atoi(e) * 1024 - zs)) & ~(int64_t)15;
     const int n = c->n;

@@ -35,6 +35,8 @@ namespace mlp {
 
 // Depth of the software-pipelined loads of the backward step loop.
 constexpr int kPrefetch = 4;
+static_assert(kWidthQuantum % kPrefetch == 0 && 64 % kPrefetch == 0,
+              "the backward's prefetch groups must divide every segment (64 steps or W mod 64)");
 
 // Waves per SIMD the sweeps are compiled for (launch bounds: 6 waves <=> at
 // most 80 VGPRs, 5 <=> 96): the chains of a batch keep ~8 waves per SIMD
@@ -633,6 +635,7 @@ __global__ __launch_bounds__(256, MLP_MERGE_WAVES) void k_merge(ModelScalars ms,
   float bch = 0.f, bnx = 0.f;
   int cch = 0, cnx = 0;
   constexpr int QD = 8;  // divides every segment (chain widths are multiples of 8): 12 or 16 break the queue
+  static_assert(kWidthQuantum % QD == 0 && 64 % QD == 0, "the merge's load queue must divide every segment");
   // fixed-register load queue: slot u serves steps t0 + u (segments hold
   // whole groups of QD steps); values of idle cells are never used
   float q5[QD] = {}, ql[QD] = {}, qb[QD] = {}, qg[QD] = {};

@@ -206,16 +206,16 @@ __global__ __launch_bounds__(64) void k_profile_post(ProfileArgs A) {
 // shift; lane 0 takes the strip above's last row), diagonal = the previous
 // step's up, left = the lane's own previous value: every cell adds and
 // compares exactly as the serial loop does, so scores and choices are the
-// reference's bit for bit.  The strips run on different CUs at once: strip
-// s's last lane writes its row and, after every 16-step block, publishes
-// how many columns of it are final; strip s + 1 waits for the columns its
-// next block reads -- a pipeline with ~100 steps of lag per strip instead of
-// one CU doing every strip.  The hand-off is the guide's sc1 form
-// (MI355X_MICROARCH.md, "Valid forms"): the row is stored and loaded only
-// with sc1 (relaxed agent-scope) accesses, the storing wave waits for its
-// stores (vmcnt(0)) before the sc1 flag store, the reader polls the flag with
-// sc1 loads -- no L2 write-back per block (an agent release) and no L1
-// invalidate per poll (an acquire).
+// reference's bit for bit.  The strips run on different CUs at once, a
+// pipeline: strip s's last lane stores each value of its row as it is final
+// (relaxed agent-scope stores, sc1); strip s + 1 polls the columns it needs
+// next with relaxed agent-scope loads of the values themselves, 64 at a time.
+// The rows are NaN-filled before every launch and a value is never NaN
+// (non-negative sums), so a column is final once it reads as a number: no
+// progress flag, no release wait on the writer, no acquire on the reader,
+// and one poll serves up to four 16-step blocks.  (Round 4's form -- a flag
+// per block behind a vmcnt(0) store drain and an acquire -- spent ~2 us a
+// block in those waits: 0.30 ms for a one-strip L2 = 2000 MEA.)
 // Choices: 2 bits per cell (0 D, 1 L, 2 U), one uint32 per lane and block;
 // the host traces back.  A strip that waits implausibly long sets the error
 // word and returns (every wave reaches an exit; the host falls back).
@@ -236,85 +236,150 @@ MeaLayout mea_layout(int L1, int L2) {
   };
   m.o_tb = take((size_t)m.nstrips * m.nblk * 64 * 4);
   m.o_row = take((size_t)m.nstrips * m.rowpitch * 4);
-  m.o_prog = take((size_t)m.nstrips * 4);
   m.o_score = take(4);
   m.o_err = take(4);
   m.bytes = o;
   return m;
 }
 
+// a lane's 16 posterior values of a block: row-contiguous columns c0 ..
+// c0 + 15, four 16-byte loads (dword-aligned).  The dense posterior has
+// kMeaGuard readable bytes before and after it, so a window that reaches past
+// the row (a strip's first and last blocks, rows of fewer than 63 columns)
+// still reads inside the buffer; mea_mask then zeroes the columns outside
+// 1 .. L2 (the recurrence starts at column 1, ProbabilisticModel.h:821-823).
+typedef float mea_f4 __attribute__((ext_vector_type(4), aligned(4)));
+__device__ __forceinline__ void mea_window(float (&p)[kMeaBlk], const float* prow, int c0) {
+#pragma unroll
+  for (int q = 0; q < kMeaBlk / 4; ++q) {
+    const mea_f4 x = *(const mea_f4*)(prow + c0 + 4 * q);
+    p[4 * q] = x.x;
+    p[4 * q + 1] = x.y;
+    p[4 * q + 2] = x.z;
+    p[4 * q + 3] = x.w;
+  }
+}
+__device__ __forceinline__ void mea_mask(float (&p)[kMeaBlk], int c0, int L2) {
+#pragma unroll
+  for (int u = 0; u < kMeaBlk; ++u) p[u] = (c0 + u >= 1 && c0 + u <= L2) ? p[u] : 0.f;
+}
+
+// One 16-step block of strip s (see above); false: the strip gave up waiting.
+struct MeaStrip {
+  const float* prow;
+  const float* above;
+  float* below;
+  uint32_t* tbw;
+  int* err;
+  float* score;  // the last strip's, else null
+  int L2, nr, lane, spin_limit;
+  float v, upp, ab;  // own value and up of the previous step; the row above: lane k holds column base + k
+  int base, have;    // columns base .. have of the row above are final
+};
+__device__ __forceinline__ bool mea_block(MeaStrip& S, float (&p)[kMeaBlk], int b) {
+  const int lane = S.lane, L2 = S.L2;
+  const int t0 = kMeaBlk * b + 1;
+  if (t0 + kMeaBlk - 64 < 1 || t0 + kMeaBlk - 1 > L2) mea_mask(p, t0 - lane, L2);  // (wave-uniform: edge blocks)
+  const int need = min(t0 + kMeaBlk - 1, L2);
+  if (need > S.have) {  // (wave-uniform) poll the next 64 columns of the row above
+    int spins = 0;
+    for (;;) {
+      const float x = __hip_atomic_load(S.above + min(t0 + lane, L2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned long long nan = __ballot(x != x);
+      const int ready = nan ? __builtin_ctzll(nan) : 64;  // a prefix of the lanes (the row fills in order)
+      S.have = min(t0 + ready - 1, L2);
+      if (S.have >= need) {
+        S.ab = x;
+        S.base = t0;
+        break;
+      }
+      if (++spins > S.spin_limit) {  // ~seconds: give up (the host falls back)
+        if (lane == 0) __hip_atomic_store(S.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return false;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  const int ab0 = t0 - S.base;  // lane of ab holding column t0
+  // the block's 16 steps: a dependency chain of one wave shift and one max3
+  // per step (ChooseBestOfThree's value is the largest of the three
+  // whichever it picks: the values are non-negative sums, no NaN, no -0; its
+  // pick, D else L else U, is off the chain).  A lane whose column is 0 or
+  // less (not started) gets 0 without a select: its inputs are all 0 (the
+  // posterior window reads 0 there, and the row above at column <= 0 is 0
+  // by the same argument; lane 0 is always at a column >= 1).
+  uint32_t bits = 0;
+  float rv[kMeaBlk];
+  float v = S.v, upp = S.upp;
+#pragma unroll
+  for (int u = 0; u < kMeaBlk; ++u) {
+    const float up = mlp_shr1(v, mea_readlane(S.ab, min(ab0 + u, 63)));  // (columns past L2: unused)
+    const float x1 = p[u] + upp;
+    const float nv = fmaxf(fmaxf(x1, v), up);
+    const uint32_t c = (x1 >= v && x1 >= up) ? 0u : (v >= up ? 1u : 2u);
+    bits |= c << (2 * u);
+    rv[u] = nv;
+    upp = up;
+    v = nv;
+  }
+  S.v = v;
+  S.upp = upp;
+  // the last row, columns t0 - (nr - 1) .. + 15: sc1 stores the next strip
+  // polls directly (no flag, no wait: a column is final once it is not NaN)
+  if (lane == S.nr - 1) {
+    const int j0 = t0 - (S.nr - 1);
+#pragma unroll
+    for (int u = 0; u < kMeaBlk; ++u) {
+      const int j = j0 + u;
+      if (j >= 1 && j <= L2) {
+        __hip_atomic_store(S.below + j, rv[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (S.score && j == L2) *S.score = rv[u];
+      }
+    }
+  }
+  S.tbw[(int64_t)b * 64 + lane] = bits;
+  return true;
+}
+
+// The posterior windows are loaded four blocks (64 steps) ahead into two
+// register sets in turn, so a load has a whole 64-step super-block to land
+// (one block ahead exposed its ~1 us L2 latency every 16 steps); the window
+// of a block past the strip's end re-reads the last block (no branch around
+// the loads, whose waits the compiler then counts exactly).
 __global__ __launch_bounds__(64) void k_profile_mea(MeaArgs A, MeaLayout M) {
   const int s = blockIdx.x, lane = threadIdx.x;
   const int L1 = A.L1, L2 = A.L2, W2 = L2 + 1;
   const int i = 64 * s + 1 + lane;
-  const int nr = min(64, L1 - 64 * s);
-  const float* prow = A.post + (int64_t)min(i, L1) * W2;
   float* rows = reinterpret_cast<float*>(A.work + M.o_row);
-  const float* above = rows + (int64_t)(s > 0 ? s - 1 : 0) * M.rowpitch;
-  float* below = rows + (int64_t)s * M.rowpitch;
-  int* prog = reinterpret_cast<int*>(A.work + M.o_prog);
-  int* err = reinterpret_cast<int*>(A.work + M.o_err);
-  uint32_t* tbw = reinterpret_cast<uint32_t*>(A.work + M.o_tb) + (int64_t)s * M.nblk * 64;
-  if (lane == 0) __hip_atomic_store(below, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  float v = 0.f, upp = 0.f;  // own value and up of the previous step
-  float pv[kMeaBlk], pn[kMeaBlk];
+  MeaStrip S;
+  S.prow = A.post + (int64_t)min(i, L1) * W2;
+  S.above = rows + (int64_t)(s > 0 ? s - 1 : 0) * M.rowpitch;
+  S.below = rows + (int64_t)s * M.rowpitch;
+  S.tbw = reinterpret_cast<uint32_t*>(A.work + M.o_tb) + (int64_t)s * M.nblk * 64;
+  S.err = reinterpret_cast<int*>(A.work + M.o_err);
+  S.score = s == M.nstrips - 1 ? reinterpret_cast<float*>(A.work + M.o_score) : nullptr;
+  S.L2 = L2;
+  S.nr = min(64, L1 - 64 * s);
+  S.lane = lane;
+  S.spin_limit = A.spin_limit;
+  S.v = S.upp = S.ab = 0.f;
+  S.base = 1;
+  S.have = s > 0 ? 0 : L2;
+  const int nb = M.nblk;
+  float PA[4][kMeaBlk], PB[4][kMeaBlk];
 #pragma unroll
-  for (int u = 0; u < kMeaBlk; ++u) pv[u] = prow[min(max(1 + u - lane, 0), L2)];
-  for (int b = 0; b < M.nblk; ++b) {
-    const int t0 = kMeaBlk * b + 1;
-    // the row above through column min(t0 + 15, L2)
-    float ab = 0.f;
-    if (s > 0) {
-      const int need = min(t0 + kMeaBlk - 1, L2);
-      int spins = 0;
-      for (;;) {
-        const int have = __builtin_amdgcn_readfirstlane(
-            __hip_atomic_load(prog + s - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        if (have >= need) break;
-        if (++spins > A.spin_limit) {  // ~seconds: give up (the host falls back)
-          if (lane == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          return;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-      // the poll matched: an agent-scope acquire orders the row loads below
-      // after it (once per 16-step block, not per poll; the writer's release
-      // is its s_waitcnt vmcnt(0) before the flag store)
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      // lanes 0..15: above[t0 + u]; an sc1 load (L2), like every load of the handed-off row
-      ab = __hip_atomic_load(above + min(t0 + lane, L2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    // the next block's posterior
+  for (int q = 0; q < 4; ++q) mea_window(PA[q], S.prow, kMeaBlk * min(q, nb - 1) + 1 - lane);
+  for (int b0 = 0; b0 < nb; b0 += 8) {
 #pragma unroll
-    for (int u = 0; u < kMeaBlk; ++u) pn[u] = prow[min(max(t0 + kMeaBlk + u - lane, 0), L2)];
-    uint32_t bits = 0;
+    for (int q = 0; q < 4; ++q) mea_window(PB[q], S.prow, kMeaBlk * min(b0 + 4 + q, nb - 1) + 1 - lane);
 #pragma unroll
-    for (int u = 0; u < kMeaBlk; ++u) {
-      const int j = t0 + u - lane;
-      const float up = mlp_shr1(v, mea_readlane(ab, u));
-      const float x1 = ((j >= 1 && j <= L2) ? pv[u] : 0.f) + upp, x2 = v, x3 = up;
-      // ChooseBestOfThree's value is the largest of the three whichever it
-      // picks (the values are non-negative sums: no NaN, no -0), so the step's
-      // dependency chain is one max3; its pick (D, else L, else U) is off it
-      float nv = fmaxf(fmaxf(x1, x2), x3);
-      const uint32_t c = (x1 >= x2 && x1 >= x3) ? 0u : (x2 >= x3 ? 1u : 2u);
-      nv = j >= 1 ? nv : 0.f;  // column 0 (and the lanes not started yet)
-      bits |= c << (2 * u);
-      if (lane == nr - 1 && j >= 1 && j <= L2) {
-        __hip_atomic_store(below + j, nv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sc1 store
-        if (s == M.nstrips - 1 && j == L2) *reinterpret_cast<float*>(A.work + M.o_score) = nv;
-      }
-      upp = up;
-      v = nv;
-    }
-    tbw[(int64_t)b * 64 + lane] = bits;
+    for (int q = 0; q < 4; ++q)
+      if (b0 + q < nb && !mea_block(S, PA[q], b0 + q)) return;
 #pragma unroll
-    for (int u = 0; u < kMeaBlk; ++u) pv[u] = pn[u];
-    // the last row is final through column t0 + 15 - (nr - 1): every store
-    // of this wave has completed (in L2) before the sc1 flag store
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0)
-      __hip_atomic_store(prog + s, min(L2, t0 + kMeaBlk - 1 - (nr - 1)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int q = 0; q < 4; ++q) mea_window(PA[q], S.prow, kMeaBlk * min(b0 + 8 + q, nb - 1) + 1 - lane);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (b0 + 4 + q < nb && !mea_block(S, PB[q], b0 + 4 + q)) return;
   }
 }
 
@@ -332,11 +397,10 @@ hipError_t launch_profile_gather(const float* post, const int64_t* cells, int64_
 hipError_t launch_profile_mea(const MeaArgs& a, hipStream_t st) {
   if (a.L1 <= 0 || a.L2 <= 0) return hipSuccess;
   const MeaLayout m = mea_layout(a.L1, a.L2);
-  hipError_t e = hipMemsetAsync(a.work + m.o_prog, 0, m.o_err + 4 - m.o_prog, st);  // progress, score, error
+  hipError_t e = hipMemsetAsync(a.work + m.o_score, 0, m.o_err + 4 - m.o_score, st);  // score, error
   if (e != hipSuccess) return e;
-  // the handed-off rows start as NaN every launch: a read that ever got
-  // ahead of its hand-off would poison the path's scores and show up in the
-  // byte-identical tests instead of silently reusing the previous call's row
+  // the handed-off rows start as NaN every launch: a column is final once it
+  // reads as a number (the next strip polls the values themselves)
   e = hipMemsetAsync(a.work + m.o_row, 0xff, (size_t)m.nstrips * m.rowpitch * 4, st);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_profile_mea, dim3((unsigned)m.nstrips), dim3(64), 0, st, a, m);

@@ -324,6 +324,8 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));  // plain vector: st
 #endif
 constexpr int kRelaxZChunk = MLP_RELAX_ZCHUNK;  // z schedule entries per LDS fill (64 B each); 32 leaves the staging area 7.7 KB more than 128 (C3 round 1 1.258 -> 1.205 s)
 constexpr int kZEntBytes = 64;
+static_assert(kRelaxZChunk <= kRelaxThreads, "one thread fills each z entry of a chunk");
+static_assert(kTileMax == 4, "a z entry packs the tile's outputs as uint4 / float4 lanes");
 // LDS: [z schedule][QuickProbs z weights][per-output A bases, weights, weight sums][tile]
 static __host__ __device__ inline size_t relax_tile_off() {
   return (size_t)kZEntBytes * kRelaxZChunk + 16 * kRelaxZChunk + 16 * kTileMax + 16 + 16 + 16 + 8 * kTileMax;
@@ -680,6 +682,39 @@ __global__ __launch_bounds__(kRelaxThreads, KP == 5 && kRelaxThreads == 1024 ? 8
   const uint32_t t_ = (m) - 1u;     \
   const uint32_t below = t_ & ~(m); \
   (m) &= t_;
+#ifdef MLP_RELAX_HIT2
+    // two hits a trip: both hits' value loads issue together, the second's
+    // sum is kept only when the word had a second common column (with none,
+    // its index is one past the word's entries: inside the image, discarded)
+#define MLP_HITS(m, xa, xc)                                                        \
+      while (m) {                                                                  \
+        RSTAT_INC(st_h);                                                           \
+        const uint32_t t1_ = (m) - 1u;                                             \
+        const uint32_t b1_ = t1_ & ~(m);                                           \
+        (m) &= t1_;                                                                \
+        const bool two_ = (m) != 0u;                                               \
+        const uint32_t t2_ = (m) - 1u;                                             \
+        const uint32_t b2_ = t2_ & ~(m);                                           \
+        (m) &= t2_;                                                                \
+        const float a1_ = Avals[xa.y + __popc(xa.x & b1_)];                        \
+        const float c1_ = Cvals[xc.y + __popc(xc.x & b1_)];                        \
+        const float a2_ = Avals[xa.y + __popc(xa.x & b2_)];                        \
+        const float c2_ = Cvals[xc.y + __popc(xc.x & b2_)];                        \
+        ac += (QP ? wk * a1_ : a1_) * c1_;                                         \
+        const float s2_ = ac + (QP ? wk * a2_ : a2_) * c2_;                        \
+        ac = two_ ? s2_ : ac;                                                      \
+      }
+#else
+#define MLP_HITS(m, xa, xc)                                                        \
+      while (m) { /* common columns k, ascending */                                \
+        RSTAT_INC(st_h);                                                           \
+        MLP_HIT_BITS(m, below);                                                    \
+        const float va = QP ? wk * Avals[xa.y + __popc(xa.x & below)]              \
+                            : Avals[xa.y + __popc(xa.x & below)];                  \
+        const float vc = Cvals[xc.y + __popc(xc.x & below)];                       \
+        ac += va * vc;                                                             \
+      }
+#endif
     // per word pair: the load, then the common columns of each word (a single
     // loop over loads and hits, MLP_RELAX_FLAT in round 4, ran 1.69 s against
     // 1.21 s: the wave issues both bodies every iteration)
@@ -689,22 +724,8 @@ __global__ __launch_bounds__(kRelaxThreads, KP == 5 && kRelaxThreads == 1024 ? 8
       const uint2 xa0 = pa[w], xa1 = pa[w + 1], xc0 = pc[w], xc1 = pc[w + 1];                         \
       uint32_t m0 = xa0.x & xc0.x;                                                                    \
       uint32_t m1 = w + 1 < we ? xa1.x & xc1.x : 0u;                                                  \
-      while (m0) { /* common columns k, ascending */                                                  \
-        RSTAT_INC(st_h);                                                                              \
-        MLP_HIT_BITS(m0, below);                                                                      \
-        const float va = QP ? wk * Avals[xa0.y + __popc(xa0.x & below)]                               \
-                            : Avals[xa0.y + __popc(xa0.x & below)];                                   \
-        const float vc = Cvals[xc0.y + __popc(xc0.x & below)];                                        \
-        ac += va * vc;                                                                                \
-      }                                                                                               \
-      while (m1) {                                                                                    \
-        RSTAT_INC(st_h);                                                                              \
-        MLP_HIT_BITS(m1, below);                                                                      \
-        const float va = QP ? wk * Avals[xa1.y + __popc(xa1.x & below)]                               \
-                            : Avals[xa1.y + __popc(xa1.x & below)];                                   \
-        const float vc = Cvals[xc1.y + __popc(xc1.x & below)];                                        \
-        ac += va * vc;                                                                                \
-      }                                                                                               \
+      MLP_HITS(m0, xa0, xc0)                                                                          \
+      MLP_HITS(m1, xa1, xc1)                                                                          \
     }
     // the cell loop, twice: with every image in LDS, and (GA) for a z where
     // some output image is read in place from HBM (generic loads)
@@ -778,6 +799,7 @@ _Pragma("unroll")                                                               
     }
 #undef MLP_CELLS
 #undef MLP_WALK
+#undef MLP_HITS
     __syncthreads();
   }
 #undef MLP_ISSUE

@@ -117,6 +117,7 @@ __device__ __forceinline__ float fold_chunks(float acc, int64_t kb, int64_t ke, 
 // exceed L2 and MALL): at C3 the listing took 104 ms a step with the stores,
 // 19 ms without them (profiles/r04e_ab_totals_nostore.txt).
 constexpr int kLbufSlots = 24;  // 16 to flush + up to 8 listed since the last check
+static_assert(kLbufSlots % 4 == 0 && kLbufSlots >= 16 + 8, "flush groups of 4 never wrap; 16 to flush + 8 listed");
 // the 16 elements from ring slot s0 (a multiple of 16 in list order) to dst
 __device__ __forceinline__ void lbuf_flush16(float* __restrict__ dst, const float* lbuf, int s0, int lane) {
   float4* d = reinterpret_cast<float4*>(dst);

@@ -470,7 +470,7 @@ def _pair(n, a, b):
     return a * n - a * (a + 1) // 2 + (b - a - 1)
 
 
-def _profile_case(seed, n, L, sub, A, B, env=None, mea=True):
+def _profile_case(seed, n, L, sub, A, B, env=None, mea=True, pad1=9, pad2=5):
     """mlp_profile_posterior (QuickProbs' buildPosterior on the GPU) against a
     plain restatement of ParallelProbabilisticModel.cpp:301-430 over the same
     relaxed sparse set: weights in double cast to float, terms in (i, j, row,
@@ -497,8 +497,8 @@ def _profile_case(seed, n, L, sub, A, B, env=None, mea=True):
             dense[(a, b)] = rows
             dense[(b, a)] = trows
     assert need
-    L1 = max(len(seqs[k]) for k in A) + 9
-    L2 = max(len(seqs[k]) for k in B) + 5
+    L1 = max(len(seqs[k]) for k in A) + pad1
+    L2 = max(len(seqs[k]) for k in B) + pad2
     mA = [_gapped(rng, seqs[k], L1)[1] for k in A]
     mB = [_gapped(rng, seqs[k], L2)[1] for k in B]
     old = {k: os.environ.get(k) for k in (env or {})}
@@ -595,6 +595,18 @@ def test_profile_posterior_stage_branches(stage, split):
 def test_profile_mea_multi_strip():
     """Device MEA over profiles of ~190 x ~185 columns (three 64-row strips)."""
     _profile_case(86, 12, 180, 0.5, [0, 2, 4, 7, 9], [1, 3, 11])
+
+
+def test_profile_mea_groups():
+    """~1150 profile-A columns: 18 strips in workgroups of four (LDS hand-off
+    inside a group, L2 between groups, a last group of two)."""
+    _profile_case(87, 4, 140, 0.5, [0, 1], [2, 3], pad1=1010)
+
+
+def test_profile_mea_wide_rows():
+    """~4150 profile-B columns: four rows exceed kMeaLdsMax, every strip is
+    its own workgroup with the L2 hand-off (k_profile_mea<1>)."""
+    _profile_case(88, 4, 140, 0.5, [0, 1], [2, 3], pad2=4010)
 
 
 def test_profile_posterior_many_sequences():
