@@ -405,11 +405,10 @@ struct ProfileArgs {
   int stage;                 // staged entries per run (<= the LDS stage; set by launch_profile_posterior)
 };
 size_t profile_lds(int L2);
-// MEA of the dense profile posterior (profile.hip): choices 2 bits per cell
-// (0 D, 1 L, 2 U), row stride (L2 + 4) / 4 bytes; rows 1..L1, columns 1..L2
-// Device MEA (k_profile_mea): one workgroup per 64-row strip, strips
-// pipelined across CUs through HBM.  Workspace layout (mea_layout): the
-// choices (2 bits a cell, per strip, 16-step block and lane a uint32), each
+// Device MEA of the dense profile posterior (k_profile_mea): one workgroup
+// per 64-row strip, strips pipelined across CUs through HBM.  Workspace
+// layout (mea_layout): the choices (2 bits a cell -- bit 0: D the largest,
+// bit 1: L >= U -- per strip, 16-step block and lane a uint32), each
 // strip's last row (NaN until written: the next strip polls the values), the
 // score and an error word (a strip that waited too long for the one above).
 constexpr int kMeaBlk = 16;  // steps per block (one uint32 of choices per lane)

@@ -1726,7 +1726,8 @@ int mlp_profile_mea(mlp_ctx* c, char* path, int32_t* path_len, float* score) {
     } else {
       const int sr = (r - 1) >> 6, ln = (r - 1) & 63, t = col + ln;
       const int blk = (t - 1) / kMeaBlk, u = (t - 1) % kMeaBlk;
-      b = (tbw[((size_t)sr * m.nblk + blk) * 64 + ln] >> (2 * u)) & 3;
+      const uint32_t w = tbw[((size_t)sr * m.nblk + blk) * 64 + ln] >> (2 * u);  // bit 0: D largest, bit 1: L >= U
+      b = (w & 1) ? 0 : (w & 2) ? 1 : 2;
     }
     if (b == 1) {
       col--;

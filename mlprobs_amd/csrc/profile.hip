@@ -216,8 +216,9 @@ __global__ __launch_bounds__(64) void k_profile_post(ProfileArgs A) {
 // and one poll serves up to four 16-step blocks.  (Round 4's form -- a flag
 // per block behind a vmcnt(0) store drain and an acquire -- spent ~2 us a
 // block in those waits: 0.30 ms for a one-strip L2 = 2000 MEA.)
-// Choices: 2 bits per cell (0 D, 1 L, 2 U), one uint32 per lane and block;
-// the host traces back.  A strip that waits implausibly long sets the error
+// Choices: 2 bits per cell (bit 0: D is the largest; bit 1: L >= U), one
+// uint32 per lane and block; the host decodes D, else L, else U and traces
+// back.  A strip that waits implausibly long sets the error
 // word and returns (every wave reaches an exit; the host falls back).
 __device__ __forceinline__ float mea_readlane(float v, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
@@ -316,8 +317,9 @@ __device__ __forceinline__ bool mea_block(MeaStrip& S, float (&p)[kMeaBlk], int 
     const float up = mlp_shr1(v, mea_readlane(S.ab, min(ab0 + u, 63)));  // (columns past L2: unused)
     const float x1 = p[u] + upp;
     const float nv = fmaxf(fmaxf(x1, v), up);
-    const uint32_t c = (x1 >= v && x1 >= up) ? 0u : (v >= up ? 1u : 2u);
-    bits |= c << (2 * u);
+    // the pick as two flags, x1 the largest (D) and v >= up (L over U); the
+    // host decodes D, else L, else U
+    bits |= (x1 == nv ? 1u : 0u) << (2 * u) | (v >= up ? 2u : 0u) << (2 * u);
     rv[u] = nv;
     upp = up;
     v = nv;
@@ -326,15 +328,26 @@ __device__ __forceinline__ bool mea_block(MeaStrip& S, float (&p)[kMeaBlk], int 
   S.upp = upp;
   // the last row, columns t0 - (nr - 1) .. + 15: sc1 stores the next strip
   // polls directly (no flag, no wait: a column is final once it is not NaN)
+  // (columns outside 1 .. L2 go to column 0, which no strip reads: one
+  // branch for the 16 stores instead of one per store)
+  const int j0 = t0 - (S.nr - 1);
   if (lane == S.nr - 1) {
-    const int j0 = t0 - (S.nr - 1);
+    if (j0 >= 1 && j0 + kMeaBlk - 1 <= L2) {  // (wave-uniform) inside the row: immediate offsets
 #pragma unroll
-    for (int u = 0; u < kMeaBlk; ++u) {
-      const int j = j0 + u;
-      if (j >= 1 && j <= L2) {
-        __hip_atomic_store(S.below + j, rv[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (S.score && j == L2) *S.score = rv[u];
+      for (int u = 0; u < kMeaBlk; ++u)
+        __hip_atomic_store(S.below + j0 + u, rv[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+#pragma unroll
+      for (int u = 0; u < kMeaBlk; ++u) {
+        const int j = j0 + u;
+        __hip_atomic_store(S.below + ((j >= 1 && j <= L2) ? j : 0), rv[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
+    }
+    if (S.score && j0 <= L2 && L2 < j0 + kMeaBlk) {  // the score: cell (L1, L2)
+      float sc = 0.f;
+#pragma unroll
+      for (int u = 0; u < kMeaBlk; ++u) sc = j0 + u == L2 ? rv[u] : sc;
+      *S.score = sc;
     }
   }
   S.tbw[(int64_t)b * 64 + lane] = bits;

@@ -1,5 +1,11 @@
 #!/bin/bash
-# r05 GPU call: one wave's dependent-chain latency per step for the MEA's lane-shift forms
+# r05 GPU call: MEA with two-flag choices and immediate-offset row stores: parity, timing, quickprobs A/B, CLI tests
 set -o pipefail
-mkdir -p gpurun_out
-timeout -k 10 60 tools/probe/dpp_latency | tee gpurun_out/dpp_latency.json
+export TMPDIR=/tmp
+O=gpurun_out/mea_bench5; mkdir -p $O
+
+timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_gpu_parity.py -k "profile or mea" > $O/t_base.txt 2>&1 &&
+timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/base -o m -- python3 tools/mea_bench.py 20 > $O/summary.txt 2> $O/base.err &&
+timeout -k 10 240 bash tools/r05_qp_ab.sh prev 2 > $O/qp.log 2>&1 &&
+timeout -k 10 500 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_cli_gpu.py > $O/t_cli.txt 2>&1
+rc=$?; tail -n 2 $O/t_base.txt $O/t_cli.txt; cat $O/summary.txt gpurun_out/qp_ab/summary.txt; exit $rc
