@@ -220,9 +220,6 @@ __global__ __launch_bounds__(64) void k_profile_post(ProfileArgs A) {
 // uint32 per lane and block; the host decodes D, else L, else U and traces
 // back.  A strip that waits implausibly long sets the error
 // word and returns (every wave reaches an exit; the host falls back).
-__device__ __forceinline__ float mea_readlane(float v, int l) {
-  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
-}
 
 MeaLayout mea_layout(int L1, int L2) {
   MeaLayout m;
@@ -274,8 +271,8 @@ struct MeaStrip {
   int* err;
   float* score;  // the last strip's, else null
   int L2, nr, lane, spin_limit;
-  float v, upp, ab;  // own value and up of the previous step; the row above: lane k holds column base + k
-  int base, have;    // columns base .. have of the row above are final
+  float v, upp, ch;  // own value and up of the previous step; the row above: lane k of ch holds column t0 + k
+  int have;          // columns .. have of the row above are final
 };
 __device__ __forceinline__ bool mea_block(MeaStrip& S, float (&p)[kMeaBlk], int b) {
   const int lane = S.lane, L2 = S.L2;
@@ -290,8 +287,7 @@ __device__ __forceinline__ bool mea_block(MeaStrip& S, float (&p)[kMeaBlk], int 
       const int ready = nan ? __builtin_ctzll(nan) : 64;  // a prefix of the lanes (the row fills in order)
       S.have = min(t0 + ready - 1, L2);
       if (S.have >= need) {
-        S.ab = x;
-        S.base = t0;
+        S.ch = x;
         break;
       }
       if (++spins > S.spin_limit) {  // ~seconds: give up (the host falls back)
@@ -301,7 +297,6 @@ __device__ __forceinline__ bool mea_block(MeaStrip& S, float (&p)[kMeaBlk], int 
       __builtin_amdgcn_s_sleep(1);
     }
   }
-  const int ab0 = t0 - S.base;  // lane of ab holding column t0
   // the block's 16 steps: a dependency chain of one wave shift and one max3
   // per step (ChooseBestOfThree's value is the largest of the three
   // whichever it picks: the values are non-negative sums, no NaN, no -0; its
@@ -311,10 +306,13 @@ __device__ __forceinline__ bool mea_block(MeaStrip& S, float (&p)[kMeaBlk], int 
   // by the same argument; lane 0 is always at a column >= 1).
   uint32_t bits = 0;
   float rv[kMeaBlk];
-  float v = S.v, upp = S.upp;
+  // The row above enters lane 0 through the wave shift's `old` operand from
+  // ch, which shifts one lane down a step (off the chain; no readlane).
+  float v = S.v, upp = S.upp, ch = S.ch;
 #pragma unroll
   for (int u = 0; u < kMeaBlk; ++u) {
-    const float up = mlp_shr1(v, mea_readlane(S.ab, min(ab0 + u, 63)));  // (columns past L2: unused)
+    const float up = mlp_shr1(v, ch);
+    ch = mlp_shl1z(ch);
     const float x1 = p[u] + upp;
     const float nv = fmaxf(fmaxf(x1, v), up);
     // the pick as two flags, x1 the largest (D) and v >= up (L over U); the
@@ -326,6 +324,7 @@ __device__ __forceinline__ bool mea_block(MeaStrip& S, float (&p)[kMeaBlk], int 
   }
   S.v = v;
   S.upp = upp;
+  S.ch = ch;
   // the last row, columns t0 - (nr - 1) .. + 15: sc1 stores the next strip
   // polls directly (no flag, no wait: a column is final once it is not NaN)
   // (columns outside 1 .. L2 go to column 0, which no strip reads: one
@@ -375,8 +374,7 @@ __global__ __launch_bounds__(64) void k_profile_mea(MeaArgs A, MeaLayout M) {
   S.nr = min(64, L1 - 64 * s);
   S.lane = lane;
   S.spin_limit = A.spin_limit;
-  S.v = S.upp = S.ab = 0.f;
-  S.base = 1;
+  S.v = S.upp = S.ch = 0.f;
   S.have = s > 0 ? 0 : L2;
   const int nb = M.nblk;
   float PA[4][kMeaBlk], PB[4][kMeaBlk];
