@@ -682,29 +682,6 @@ __global__ __launch_bounds__(kRelaxThreads, KP == 5 && kRelaxThreads == 1024 ? 8
   const uint32_t t_ = (m) - 1u;     \
   const uint32_t below = t_ & ~(m); \
   (m) &= t_;
-#ifdef MLP_RELAX_HIT2
-    // two hits a trip: both hits' value loads issue together, the second's
-    // sum is kept only when the word had a second common column (with none,
-    // its index is one past the word's entries: inside the image, discarded)
-#define MLP_HITS(m, xa, xc)                                                        \
-      while (m) {                                                                  \
-        RSTAT_INC(st_h);                                                           \
-        const uint32_t t1_ = (m) - 1u;                                             \
-        const uint32_t b1_ = t1_ & ~(m);                                           \
-        (m) &= t1_;                                                                \
-        const bool two_ = (m) != 0u;                                               \
-        const uint32_t t2_ = (m) - 1u;                                             \
-        const uint32_t b2_ = t2_ & ~(m);                                           \
-        (m) &= t2_;                                                                \
-        const float a1_ = Avals[xa.y + __popc(xa.x & b1_)];                        \
-        const float c1_ = Cvals[xc.y + __popc(xc.x & b1_)];                        \
-        const float a2_ = Avals[xa.y + __popc(xa.x & b2_)];                        \
-        const float c2_ = Cvals[xc.y + __popc(xc.x & b2_)];                        \
-        ac += (QP ? wk * a1_ : a1_) * c1_;                                         \
-        const float s2_ = ac + (QP ? wk * a2_ : a2_) * c2_;                        \
-        ac = two_ ? s2_ : ac;                                                      \
-      }
-#else
 #define MLP_HITS(m, xa, xc)                                                        \
       while (m) { /* common columns k, ascending */                                \
         RSTAT_INC(st_h);                                                           \
@@ -714,7 +691,6 @@ __global__ __launch_bounds__(kRelaxThreads, KP == 5 && kRelaxThreads == 1024 ? 8
         const float vc = Cvals[xc.y + __popc(xc.x & below)];                       \
         ac += va * vc;                                                             \
       }
-#endif
     // per word pair: the load, then the common columns of each word (a single
     // loop over loads and hits, MLP_RELAX_FLAT in round 4, ran 1.69 s against
     // 1.21 s: the wave issues both bodies every iteration)

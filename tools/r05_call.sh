@@ -1,8 +1,8 @@
 #!/bin/bash
-# r05 GPU call: MEA with two-flag choices and immediate-offset row stores: parity, timing, quickprobs A/B, CLI tests
+# r05 GPU call: MEA with the row above rotating into lane 0 (no readlane): parity, timing, quickprobs A/B, CLI tests
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/mea_bench5; mkdir -p $O
+O=gpurun_out/mea_bench6; mkdir -p $O
 
 timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_gpu_parity.py -k "profile or mea" > $O/t_base.txt 2>&1 &&
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/base -o m -- python3 tools/mea_bench.py 20 > $O/summary.txt 2> $O/base.err &&
