@@ -974,9 +974,13 @@ def main():
             cells_per_launch = kt[dom]['cells'] / launches
             traffic = g['traffic_bytes_per_cell'] * cells_per_launch / 1e9
             issued = g['valu_insts_per_cell'] * cells_per_launch / (avg_ms * 1e-3)
-            valu = {'achieved': issued, 'peak': VALU_PEAK_WAVE_INSTS, 'unit': 'wave-instr/s',
-                    'frac': issued / VALU_PEAK_WAVE_INSTS,
-                    'insts_per_cell': g['valu_insts_per_cell']}
+            # against the group's mix-weighted issue peak (its full / half-rate
+            # instruction mix, tools/valu_mix.py) and the
+            # all-full-rate 1.23e12 beside it
+            mix = g.get('valu_mix_peak') or VALU_PEAK_WAVE_INSTS
+            valu = {'achieved': issued, 'peak': mix, 'unit': 'wave-instr/s', 'frac': issued / mix,
+                    'peak_all_full_rate': VALU_PEAK_WAVE_INSTS, 'frac_of_full_rate': issued / VALU_PEAK_WAVE_INSTS,
+                    'insts_per_cell': g['valu_insts_per_cell'], 'source': 'profiles/pmc_traffic.json'}
     log('quickprobs stage')
     qp_info = quickprobs_stage(fam, fam_in, total_cells, args) if (world == 1 and not args.no_qp and not args.host) else None
     shards_info = None
