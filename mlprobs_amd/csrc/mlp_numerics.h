@@ -42,7 +42,8 @@ __device__ __forceinline__ float mlp_log_add(float x, float y) {
 // q <= 8 <=> d <= 4.5 for every float d >= 0 (checked exhaustively on [0, 8);
 // the product rounds below the even integer exactly at the three breakpoints),
 // so lk[q] (16 float4 rows, filled by mlp_lookup_table) holds the reference's
-// coefficients of d's interval.  Four VALU ops instead of compare/select chains.
+// coefficients of d's interval.  Three VALU ops (mul, convert, and) instead
+// of compare/select chains.
 __device__ __forceinline__ void mlp_lookup_table(float4* lk) {
   const float4 k0 = make_float4(-0.009350833524763f, 0.130659527668286f, 0.498799810682272f, 0.693203116424741f);
   const float4 k1 = make_float4(-0.014532321752540f, 0.139942324101744f, 0.495635523139337f, 0.692140569840976f);
@@ -60,8 +61,16 @@ constexpr int kLookupRows = 16;
 __device__ __forceinline__ float mlp_log_add_t(float x, float y, const float4* __restrict__ lk) {
   const float hi = fmaxf(x, y), lo = fminf(x, y);
   const float d = hi - lo;
-  const int q = (int)fminf(d * 0x1.fffffep0f, 15.0f);
-  const float4 c = lk[q];
+  // the row's byte offset 16 q directly: fl(d * 16 M) = 16 fl(d * M) (a power
+  // of two scales exactly), so floor(.) & 0xf0 = 16 floor(fl(d * M)) for
+  // d < 7.5, the row above; for d >= 7.5 any row (the result is hi).  The
+  // hardware conversion saturates, so no clamp (the min and the shift of the
+  // table index were two half-rate instructions per LOG_ADD: C3 forward
+  // 184 -> 180.5, backward 243.7 -> 237, local totals 97-100 -> 83-92 ms a
+  // step, profiles/r05o_ab_lookup_byteoff.txt)
+  int q16;
+  asm("v_cvt_i32_f32 %0, %1" : "=v"(q16) : "v"(d * 0x1.fffffep4f));
+  const float4 c = *(const float4*)((const char*)lk + (q16 & 0xf0));
   const float r = (((c.x * d + c.y) * d + c.z) * d + c.w) + lo;
   return (d >= 7.5f) ? hi : r;
 }
