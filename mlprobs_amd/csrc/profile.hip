@@ -168,12 +168,41 @@ __global__ __launch_bounds__(64) void k_profile_post(ProfileArgs A) {
         wave_sync();
         // ---- add them pair by pair: LDS float adds without return, which a
         // wave's LDS pipe applies in issue order (one pair's entries hit
-        // distinct columns; a later pair's add to the same cell lands after)
-        for (int l = 0; l < nl; ++l) {
-          const int s0 = l_st[l], s1 = l_st[l + 1];
-          for (int t = s0 + lane; t < s1; t += 64) {
-            const int c = st_c[t];
-            if (c >= c0 && c < c1) lds_add(&acc[c - c0], st_p[t]);
+        // distinct columns; a later pair's add to the same cell lands after).
+        // Eight pairs at a time: their entries' column / product reads issue
+        // together, then the eight adds in pair order (the reads touch other
+        // arrays than the adds), one LDS round trip per eight pairs instead of
+        // three per pair; a pair of more than 64 entries (a transposed row)
+        // takes the group through the entry loop
+        for (int l0 = 0; l0 < nl; l0 += 8) {
+          int n8 = 0;
+#pragma unroll
+          for (int u = 0; u < 8; ++u)
+            if (l0 + u < nl) n8 = max(n8, __builtin_amdgcn_readlane(cnt, l0 + u));
+          if (n8 <= 64) {
+            int cc[8];
+            float pp[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+              cc[u] = -1;
+              pp[u] = 0.f;
+              if (l0 + u < nl && lane < __builtin_amdgcn_readlane(cnt, l0 + u)) {
+                const int t = __builtin_amdgcn_readlane(start, l0 + u) + lane;
+                cc[u] = st_c[t];
+                pp[u] = st_p[t];
+              }
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+              if (cc[u] >= c0 && cc[u] < c1) lds_add(&acc[cc[u] - c0], pp[u]);
+          } else {
+            for (int l = l0; l < min(nl, l0 + 8); ++l) {
+              const int s0 = l_st[l], s1 = l_st[l + 1];
+              for (int t = s0 + lane; t < s1; t += 64) {
+                const int c = st_c[t];
+                if (c >= c0 && c < c1) lds_add(&acc[c - c0], st_p[t]);
+              }
+            }
           }
         }
       } else {
