@@ -609,7 +609,9 @@ template <int M, int PID, bool NP = false>
 #ifndef MLP_MERGE_WAVES
 #define MLP_MERGE_WAVES 6
 #endif
-__global__ __launch_bounds__(256, MLP_MERGE_WAVES) void k_merge(ModelScalars ms, SeqSet sq, PairMeta pm, ChainMeta cm,
+// (NP with all three models carries the #B counts beside their values: at 6
+// waves its 80 VGPRs spilled 56 bytes a lane; 5 waves give it 96)
+__global__ __launch_bounds__(256, NP && M == (kHmm5 | kLocal | kPF) ? 5 : MLP_MERGE_WAVES) void k_merge(ModelScalars ms, SeqSet sq, PairMeta pm, ChainMeta cm,
                                                PairRec* __restrict__ rec, Scratch sc, int64_t nchains,
                                                int lds_seq) {
   __shared__ double ex[7 * 6];
