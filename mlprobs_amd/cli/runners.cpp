@@ -128,10 +128,16 @@ void stage(const char* name) {
 // refinement 1.62 / 1.62 / 1.63 / 1.70 / 2.04 s, every output identical
 // (tools/ab_r03.sh meamin, profiles/r03f_ab_meamin.txt).  MLP_MEA_GPU_MIN
 // overrides.
-static int64_t mea_gpu_min() {
-  static const int64_t v = getenv("MLP_MEA_GPU_MIN") ? atoll(getenv("MLP_MEA_GPU_MIN")) : 250000;
-  return v;
+// QuickProbs' floor is lower: its device path keeps the posterior on the
+// device and returns only the path, and since round 5's device MEA (about
+// twice as fast) QuickProbs C3 construction + refinement runs 0.90-0.97 s at
+// 2.5e5, 0.84-0.87 at 1e5, 0.81-0.84 at 5e4 and 0 (C2: 0.063-0.068 / 0.062
+// / 0.057 / 0.058), outputs identical (profiles/r05v_qp_mea_floor.txt).
+static int64_t mea_gpu_min(int64_t dflt = 250000) {
+  static const char* e = getenv("MLP_MEA_GPU_MIN");
+  return e ? atoll(e) : dflt;
 }
+constexpr int64_t kQpMeaGpuMin = 50000;
 
 using cpnp::Row;
 
@@ -415,7 +421,7 @@ int run_qp(std::vector<qph::Seq> seqs, const qph::Options& opt, int threads, Ses
         be.device_mea = [&](const std::vector<float>& w, const qph::Profile& A, const qph::Profile& B,
                             std::string& path, float* score) -> bool {
           const int L1 = A[0].length(), L2 = B[0].length();
-          if ((int64_t)L1 * L2 < mea_gpu_min()) return false;
+          if ((int64_t)L1 * L2 < mea_gpu_min(kQpMeaGpuMin)) return false;
           const auto tm0 = std::chrono::steady_clock::now();
           std::vector<int32_t> l1, l2;
           for (const qph::Seq& q : A) l1.push_back(q.label);
