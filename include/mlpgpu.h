@@ -218,6 +218,12 @@ const float *mlp_profile_result(const mlp_ctx *ctx);
 int mlp_profile_defer(mlp_ctx *ctx, int on);
 int mlp_profile_mea(mlp_ctx *ctx, char *path, int32_t *path_len, float *score);
 int mlp_profile_gather(mlp_ctx *ctx, int64_t n, const int64_t *cells, float *vals);
+/* A dense (L1 + 1) x (L2 + 1) posterior from the host (row-major, row 0 and
+ * column 0 unused) made the context's device-resident matrix, as if a
+ * deferred mlp_profile_posterior* had computed it: for callers that build
+ * the profile posterior elsewhere, and for testing mlp_profile_mea on any
+ * matrix.  MLP_ERR_STATE on a host context. */
+int mlp_profile_set(mlp_ctx *ctx, int L1, int L2, const float *post);
 
 /* Evaluation only (not a drop-in path): the consistency transform of the
  * output pairs (x, y), x in xs, y in ys, x < y, as dense 16x16 block

@@ -496,9 +496,20 @@ void mlp_ctx_destroy(mlp_ctx* c) {
   for (mlp_ctx* ch : c->shards) mlp_ctx_destroy(ch);
   c->shards.clear();
   hipSetDevice(c->device);
+#ifdef MLP_DESTROY_TIMES  // diagnosis build: where a context's teardown goes
+  auto dt0 = std::chrono::steady_clock::now();
+  auto lap = [&](const char* what) {
+    const auto t = std::chrono::steady_clock::now();
+    fprintf(stderr, "[destroy] %s %.4f s\n", what, std::chrono::duration<double>(t - dt0).count());
+    dt0 = t;
+  };
+#else
+  auto lap = [](const char*) {};
+#endif
   hipStreamSynchronize(c->stream);
   hipStreamSynchronize(c->stream2);
   if (c->side.st) hipStreamSynchronize(c->side.st);
+  lap("sync");
   void* ptrs[] = {c->d_tables, c->d_res, c->d_off, c->d_len, c->d_rp_off, c->d_trp_off,
                   c->d_rowptr, c->d_ent_off, c->d_cols, c->d_vals};
   for (void* p : ptrs)
@@ -507,8 +518,10 @@ void mlp_ctx_destroy(mlp_ctx* c) {
                     &c->r_newcols, &c->r_newvals, &c->r_tasks_p, &c->r_tasks_r, &c->r_pairs,
                     &c->r_nnz, &c->r_newoff, &c->r_img, &c->r_imgoff, &c->r_tiles, &c->r_nwords, &c->r_weights,
                     &c->r_seldist, &c->r_profile, &c->r_mea, &c->ag_cols, &c->ag_vals};
+  lap("family buffers");
   for (DevBuf* b : bufs)
     if (b->p && !b->lent) hipFree(b->p);
+  lap("scratch and work buffers");
   if (c->comm) ncclCommDestroy(c->comm);
   for (hipEvent_t e : c->evpool) hipEventDestroy(e);
   if (getenv("MLP_PROFILE_TIMES") && (c->prof_t[0] > 0 || c->prof_t[1] > 0))
@@ -517,6 +530,7 @@ void mlp_ctx_destroy(mlp_ctx* c) {
   if (c->h_prof_in) hipHostFree(c->h_prof_in);
   if (c->h_prof_out) hipHostFree(c->h_prof_out);
   if (c->h_mea) hipHostFree(c->h_mea);
+  lap("pinned host buffers");
   for (hipStream_t st : c->cst) hipStreamDestroy(st);
   hipStreamDestroy(c->stream);
   hipStreamDestroy(c->stream2);
@@ -525,6 +539,7 @@ void mlp_ctx_destroy(mlp_ctx* c) {
     hipEventDestroy(c->side.fork);
     hipEventDestroy(c->side.join);
   }
+  lap("streams");
   delete c;
 }
 
@@ -1595,13 +1610,6 @@ static int profile_posterior(mlp_ctx* c, const std::vector<float>& w, int n1, co
     if (hipHostMalloc(&c->h_prof_in, in_bytes * 2, hipHostMallocDefault) != hipSuccess) return MLP_ERR_MEMORY;
     c->h_prof_in_bytes = in_bytes * 2;
   }
-  if (c->h_prof_out_bytes < b_out) {
-    if (c->h_prof_out) hipHostFree(c->h_prof_out);
-    c->h_prof_out = nullptr;
-    c->h_prof_out_bytes = 0;
-    if (hipHostMalloc((void**)&c->h_prof_out, b_out * 2, hipHostMallocDefault) != hipSuccess) return MLP_ERR_MEMORY;
-    c->h_prof_out_bytes = b_out * 2;
-  }
   char* hin = (char*)c->h_prof_in;
   memcpy(hin + o_rpb, rpb.data(), b_rpb);
   memcpy(hin + o_eb, eb.data(), b_eb);
@@ -1656,6 +1664,16 @@ static int profile_posterior(mlp_ctx* c, const std::vector<float>& w, int n1, co
   if (c->prof_defer && !out) {  // stays on the device for mlp_profile_mea / _gather
     c->prof_t[1] += std::chrono::duration<double>(std::chrono::steady_clock::now() - tp1).count();
     return MLP_OK;
+  }
+  // the pinned result buffer only for matrices that come back: a deferred
+  // one (the device MEA's, up to ~4300 x 7300 at C2 -p 1) never does, and
+  // pinning / unpinning hundreds of MB cost ~0.15 s of that run's teardown
+  if (c->h_prof_out_bytes < b_out) {
+    if (c->h_prof_out) hipHostFree(c->h_prof_out);
+    c->h_prof_out = nullptr;
+    c->h_prof_out_bytes = 0;
+    if (hipHostMalloc((void**)&c->h_prof_out, b_out * 2, hipHostMallocDefault) != hipSuccess) return MLP_ERR_MEMORY;
+    c->h_prof_out_bytes = b_out * 2;
   }
   HIPCHK(c, hipMemcpyAsync(c->h_prof_out, d_out, b_out, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -1744,6 +1762,23 @@ int mlp_profile_mea(mlp_ctx* c, char* path, int32_t* path_len, float* score) {
   std::reverse(path, path + k);
   *path_len = k;
   c->prof_t[1] += std::chrono::duration<double>(std::chrono::steady_clock::now() - tp).count();
+  return MLP_OK;
+}
+
+int mlp_profile_set(mlp_ctx* c, int L1, int L2, const float* post) {
+  if (!c || L1 < 0 || L2 < 0 || !post) return MLP_ERR_ARG;
+  if (c->host) return MLP_ERR_STATE;
+  hipSetDevice(c->device);
+  const size_t b_out = (size_t)(L1 + 1) * (L2 + 1) * 4;
+  int rc;
+  // the same guards as a computed posterior: the MEA's row windows read past its rows
+  if ((rc = ensure(c, c->r_profile, kMeaGuard + ((b_out + 255) & ~(size_t)255) + kMeaGuard))) return rc;
+  float* d_out = (float*)((char*)c->r_profile.p + kMeaGuard);
+  HIPCHK(c, hipMemcpyAsync(d_out, post, b_out, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->prof_dout = d_out;
+  c->prof_L1 = L1;
+  c->prof_L2 = L2;
   return MLP_OK;
 }
 

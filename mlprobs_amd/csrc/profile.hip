@@ -306,7 +306,9 @@ struct MeaStrip {
 __device__ __forceinline__ bool mea_block(MeaStrip& S, float (&p)[kMeaBlk], int b) {
   const int lane = S.lane, L2 = S.L2;
   const int t0 = kMeaBlk * b + 1;
-  if (t0 + kMeaBlk - 64 < 1 || t0 + kMeaBlk - 1 > L2) mea_mask(p, t0 - lane, L2);  // (wave-uniform: edge blocks)
+  // (wave-uniform: edge blocks) the block's columns run from t0 - 63 (lane 63,
+  // first step) to t0 + kMeaBlk - 1 (lane 0, last step)
+  if (t0 - 63 < 1 || t0 + kMeaBlk - 1 > L2) mea_mask(p, t0 - lane, L2);
   const int need = min(t0 + kMeaBlk - 1, L2);
   if (need > S.have) {  // (wave-uniform) poll the next 64 columns of the row above
     int spins = 0;

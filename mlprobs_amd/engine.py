@@ -100,6 +100,7 @@ def lib():
         L.mlp_profile_defer.argtypes = [P, C.c_int]
         L.mlp_profile_mea.argtypes = [P, C.c_char_p, C.POINTER(C.c_int32), C.POINTER(C.c_float)]
         L.mlp_profile_gather.argtypes = [P, C.c_int64, I64P, F32P]
+        L.mlp_profile_set.argtypes = [P, C.c_int, C.c_int, F32P]
         _LIB = L
     return _LIB
 
@@ -112,7 +113,7 @@ EXPORTED = ['mlp_ctx_create', 'mlp_ctx_destroy', 'mlp_last_error', 'mlp_set_scra
             'mlp_shard_range', 'mlp_shard_plan', 'mlp_gather_layout', 'mlp_allgather', 'mlp_synchronize', 'mlp_profile',
             'mlp_kernel_times', 'mlp_profile_reset', 'mlp_ctx_create_mask', 'mlp_set_shards', 'mlp_shard_count',
             'mlp_relax_shard_plan', 'mlp_ctx_create_host', 'mlp_ctx_is_host', 'mlp_relax_blockmfma_eval',
-            'mlp_profile_defer', 'mlp_profile_mea', 'mlp_profile_gather', 'mlp_relax_range']
+            'mlp_profile_defer', 'mlp_profile_mea', 'mlp_profile_gather', 'mlp_relax_range', 'mlp_profile_set']
 
 
 def shard_plan(lens, nranks, rank):
@@ -308,6 +309,12 @@ class Family:
         sc = C.c_float(0)
         self._chk(self._L.mlp_profile_mea(self._ctx, buf, C.byref(n), C.byref(sc)))
         return buf.raw[:n.value].decode(), np.float32(sc.value)
+
+    def profile_set(self, post):
+        """Make a host (L1 + 1) x (L2 + 1) posterior the device-resident
+        matrix for profile_mea / profile_gather (mlp_profile_set)."""
+        p = np.ascontiguousarray(post, np.float32)
+        self._chk(self._L.mlp_profile_set(self._ctx, p.shape[0] - 1, p.shape[1] - 1, p.reshape(-1)))
 
     def profile_gather(self, cells):
         c = np.ascontiguousarray(cells, np.int64)

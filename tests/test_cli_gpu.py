@@ -180,6 +180,33 @@ def test_cli_config_families(name):
         assert r.stdout == fh.read()
 
 
+def test_cli_config_c2_nonprogressive():
+    """C2 with -p 1 (alignment graph + refinement: some 130 profile MEAs of up
+    to 4263 x 7288 columns on the device) under the golden run's fixed clock:
+    the reference CLI's bytes (round 5: an unmasked edge block of the device
+    MEA diverged here)."""
+    out = os.path.join(GOLDEN, 'config', 'c2_128x256_s11.p_1.out')
+    r = subprocess.run([BIN, '-p', '1', os.path.join(GOLDEN, 'config', 'c2_128x256_s11.fa')], capture_output=True,
+                       text=True, timeout=300, env=dict(ENV, MLP_SRAND_TIME=NP_TIME))
+    assert r.returncode == 0 and r.stderr == '', r.stderr
+    with open(out) as fh:
+        assert r.stdout == fh.read()
+
+
+@pytest.mark.parametrize('name', ['c2_128x256_s11', 'c3_512x400_s11'])
+def test_quickprobs_config_families(name):
+    """The quickprobs drop-in on the bench's C2 / C3 families: the reference
+    QuickProbs CLI's output (tools/gen_config_goldens.sh)."""
+    out = os.path.join(GOLDEN, 'config', f'{name}.qp.out')
+    if not os.path.exists(out):
+        pytest.skip('reference output not generated')
+    r = subprocess.run([QP_BIN, os.path.join(GOLDEN, 'config', f'{name}.fa')], capture_output=True, text=True,
+                       timeout=300, env=ENV)
+    assert r.returncode == 0 and r.stderr == '', r.stderr
+    with open(out) as fh:
+        assert r.stdout == fh.read()
+
+
 @pytest.mark.parametrize('name', ['qp_div60', 'qp_big210'])
 def test_quickprobs_device_mea_gives_up(name):
     """A device MEA strip that gives up waiting for the one above

@@ -609,6 +609,52 @@ def test_profile_mea_wide_rows():
     _profile_case(88, 4, 140, 0.5, [0, 1], [2, 3], pad2=4010)
 
 
+def _mea_matrix(rng, L1, L2, kind):
+    post = np.zeros((L1 + 1, L2 + 1), np.float32)
+    body = post[1:, 1:]
+    if kind == 'dense':
+        body[:] = rng.uniform(0, 1, body.shape)
+    elif kind == 'sparse':   # a refinement's profile posterior: few entries, many exact ties
+        k = max(1, body.size // 600)
+        body.reshape(-1)[rng.choice(body.size, k, replace=False)] = rng.uniform(0.01, 8, k)
+    elif kind == 'tails':    # entries in each row's first and last 16 columns only
+        w = min(16, L2)
+        body[:, :w] = rng.uniform(0, 1, (L1, w)) * (rng.uniform(0, 1, (L1, w)) < 0.3)
+        body[:, L2 - w:] = rng.uniform(0, 1, (L1, w)) * (rng.uniform(0, 1, (L1, w)) < 0.3)
+    elif kind == 'band':
+        for i in range(L1):
+            j = int(i * L2 / L1)
+            body[i, max(0, j - 3):j + 4] = rng.uniform(0.01, 1, len(range(max(0, j - 3), min(L2, j + 4))))
+    return post   # 'zeros': every cell a tie
+
+
+@pytest.mark.parametrize('L1,L2,kind', [
+    (1, 1, 'dense'), (1, 300, 'sparse'), (40, 1, 'dense'), (50, 16, 'tails'), (64, 64, 'dense'),
+    (65, 17, 'tails'), (128, 128, 'band'), (128, 200, 'tails'), (130, 300, 'zeros'), (200, 63, 'sparse'),
+    (261, 8076, 'sparse'), (261, 2000, 'tails'), (700, 900, 'dense'), (1100, 700, 'tails'), (2000, 600, 'band')])
+def test_profile_mea_any_matrix(L1, L2, kind):
+    """Device MEA (mlp_profile_set + mlp_profile_mea) of arbitrary matrices
+    against the oracle's ComputeAlignment (orc_mea, ProbabilisticModel.h:
+    804-864): path and score bit for bit.  'tails' puts entries where a strip's
+    first blocks read past their rows (round 5: the fourth block's lanes at
+    columns <= 0 went unmasked and read the row before's last columns -- a
+    C2 -p 1 refinement diverged from the reference); 'sparse' / 'zeros' are
+    tie-heavy."""
+    rng = np.random.default_rng(L1 * 7919 + L2)
+    post = _mea_matrix(rng, L1, L2, kind)
+    fam = Family([x for _, x in synth.family(3, 20, 0.5, seed=1)])
+    try:
+        fam.profile_set(post)
+        path, score = fam.profile_mea(L1, L2)
+        rscore, rpath = orc.mea(L1, L2, post, with_path=True)
+        assert score == np.float32(rscore), (score, rscore)
+        assert path == rpath
+        cells = np.array([0, L2 + 2, (L1 + 1) * (L2 + 1) - 1], np.int64)
+        np.testing.assert_array_equal(fam.profile_gather(cells), post.reshape(-1)[cells])
+    finally:
+        fam.close()
+
+
 def test_profile_posterior_many_sequences():
     """More than 64 sequences in profile A: the column compaction runs in
     several 64-sequence chunks (and with a small stage, partial runs)."""

@@ -17,3 +17,10 @@ synth.write_fasta('$G/c3_512x400_s11.fa', synth.family(512, 400, 0.7, seed=11))
 "
 taskset -c 0 oracle/_ref/c_p_np_aln -p 0 $G/c2_128x256_s11.fa > $G/c2_128x256_s11.p_0.out
 oracle/_ref/c_p_np_aln -p 0 $G/c3_512x400_s11.fa > $G/c3_512x400_s11.p_0.out
+# -p 1 (npdoAlign + refinement) on C2 under the tests' fixed clock
+# (MLP_SRAND_TIME, read by the reference's time() stand-in oracle/fixtime.c),
+# one core (its refinement's BuildPosterior races the same way)
+MLP_SRAND_TIME=1700000000 taskset -c 0 oracle/_ref/c_p_np_aln_ft -p 1 $G/c2_128x256_s11.fa > $G/c2_128x256_s11.p_1.out
+# the reference QuickProbs CLI on C2 and C3 (its output does not depend on the thread count)
+oracle/_ref/quickprobs -t 8 $G/c2_128x256_s11.fa > $G/c2_128x256_s11.qp.out
+oracle/_ref/quickprobs -t 8 $G/c3_512x400_s11.fa > $G/c3_512x400_s11.qp.out
