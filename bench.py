@@ -560,9 +560,10 @@ def e2e_families(args):
     graph, refinement), one fresh process per run (as MLProbs starts them),
     wall clock around the process; three runs each, every run listed with
     its stage split (MLP_CLI_TIMES), the median and the maximum, and any run
-    more than 15% above the median named with the stage that grew.  The -p 0 outputs are compared in the run with the
-    reference CLI's own output on the same family (tests/golden/config), with
-    MLProbs' SP score (un_sp) and TC against it."""
+    more than 15% above the median named with the stage that grew.  The outputs are compared in the run with the
+    reference CLI's own output on the same family where one was generated
+    (tests/golden/config: -p 0 at C2 and C3, -p 1 at C2 under a fixed clock,
+    MLP_SRAND_TIME), with MLProbs' SP score (un_sp) and TC against it."""
     from mlprobs_amd import synth
     cli = os.path.join(ROOT, 'mlprobs_amd', 'cli', 'c_p_np_aln')
     if not os.path.exists(cli):
@@ -575,22 +576,23 @@ def e2e_families(args):
                 fa = os.path.join(td, 'fam.fa')
                 synth.write_fasta(fa, synth.family(n, L, args.s, seed=args.seed))
                 runs = []
+                # -p 1 seeds its refinement with time(0): the golden run's fixed clock
+                env = dict(os.environ, MLP_CLI_TIMES='1', **({'MLP_SRAND_TIME': '1700000000'} if mode == '1' else {}))
                 for _ in range(args.e2e_runs):
                     t0 = time.perf_counter()
-                    r = subprocess.run([cli, '-p', mode, fa], capture_output=True, text=True, timeout=600,
-                                       env=dict(os.environ, MLP_CLI_TIMES='1'))
+                    r = subprocess.run([cli, '-p', mode, fa], capture_output=True, text=True, timeout=600, env=env)
                     runs.append((time.perf_counter() - t0, r))
             rec, r = _e2e_record(runs)
             log(f'e2e {tag} -p {mode}: ' + ', '.join(f'{x[0]:.2f}' for x in runs) + f' s (exit {r.returncode})')
-            g = os.path.join(ROOT, 'tests', 'golden', 'config', f'{gold}.p_0.out')
-            if mode == '0' and os.path.exists(g) and args.s == 0.7:
+            g = os.path.join(ROOT, 'tests', 'golden', 'config', f'{gold}.p_{mode}.out')
+            if os.path.exists(g) and args.s == 0.7:
                 with open(g) as fh:
                     ref = fh.read()
                 rec['reference_output'] = {'identical': all(x[1].stdout == ref for x in runs),
                                            'sp_ours': sp_score(r.stdout), 'sp_reference': sp_score(ref),
                                            'tc_vs_reference': tc_score(r.stdout, ref),
-                                           'reference': f'tests/golden/config/{gold}.p_0.out (reference CLI, '
-                                                        'single thread)'}
+                                           'reference': f'tests/golden/config/{gold}.p_{mode}.out (reference CLI, '
+                                                        'single thread' + (', fixed clock)' if mode == '1' else ')')}
             res[tag if mode == '0' else f'{tag} -p 1'] = rec
     qp = os.path.join(ROOT, 'mlprobs_amd', 'cli', 'quickprobs')
     ref = os.path.join(ROOT, 'oracle', '_ref', 'quickprobs')

@@ -127,7 +127,10 @@ void stage(const char* name) {
 // 0.62 / 0.58 / 0.55 / 0.58 / 0.80 s, QuickProbs C3 construction +
 // refinement 1.62 / 1.62 / 1.63 / 1.70 / 2.04 s, every output identical
 // (tools/ab_r03.sh meamin, profiles/r03f_ab_meamin.txt).  MLP_MEA_GPU_MIN
-// overrides.
+// overrides.  Round 5 (device MEA rebuilt, deferred matrices no longer
+// pinned on the host), floors 2.5e5 / 5e4 / 0: C2 -p 0 progressive 0.14-0.30
+// / 0.28-0.32 / 0.28-0.33 s, C2 -p 1 refinement 0.22-0.25 / 0.24-0.25 /
+// 0.25-0.26 s, every output the reference's (profiles/r05x_cpnp_mea_floor.txt).
 // QuickProbs' floor is lower: its device path keeps the posterior on the
 // device and returns only the path, and since round 5's device MEA (about
 // twice as fast) QuickProbs C3 construction + refinement runs 0.90-0.97 s at
