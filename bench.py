@@ -613,6 +613,12 @@ def e2e_families(args):
                     runs.append((time.perf_counter() - t0, r))
                 res[tag], r = _e2e_record(runs)
                 log(f'e2e {tag}: ' + ', '.join(f'{x[0]:.2f}' for x in runs) + f' s (exit {r.returncode})')
+                g = os.path.join(ROOT, 'tests', 'golden', 'config', f'c{2 if n == 128 else 3}_{n}x{L}_s{args.seed}.qp.out')
+                if os.path.exists(g) and args.s == 0.7:   # the reference QuickProbs CLI's output (gen_config_goldens.sh)
+                    with open(g) as fh:
+                        ref_out = fh.read()
+                    res[tag]['reference_output'] = {'identical': all(x[1].stdout == ref_out for x in runs),
+                                                    'reference': os.path.relpath(g, ROOT)}
                 if n <= 128 and os.path.exists(ref) and not args.no_cpu:
                     t0 = time.perf_counter()
                     rr = subprocess.run([ref, '-t', str(args.cpu_threads), fa], capture_output=True, text=True,
