@@ -196,8 +196,13 @@ hipError_t launch_forward(int models, const ModelScalars& ms, const Tables* tab,
 hipError_t launch_backward(int models, const ModelScalars& ms, const Tables* tab, SeqSet seqs,
                            PairMeta pm, ChainMeta cm, PairRec* rec, Scratch sc, int64_t nchains,
                            int lds_seq, int64_t npairs, hipStream_t st, const SideStream* side);
+// parts: kTotFwd (the forward chains, one persistent wave per pair; reads
+// only what the forward sweep wrote, so it may run beside the backward sweep),
+// kTotBwd (the backward chains, one wave per pair), or both in one kernel
+constexpr int kTotFwd = 1, kTotBwd = 2;
 hipError_t launch_local_totals(const ModelScalars& ms, const Tables* tab, SeqSet seqs, PairMeta pm, ChainMeta cm,
-                               PairRec* rec, Scratch sc, int64_t npairs, int nwaves, hipStream_t st);
+                               PairRec* rec, Scratch sc, int64_t npairs, int nwaves, hipStream_t st,
+                               int parts = kTotFwd | kTotBwd);
 // The same totals with the forward chain folded one pair per lane: its half
 // between the forward and the backward sweeps (bounds, listing into the
 // still-dead local backward array, fold), the rest after the backward sweep

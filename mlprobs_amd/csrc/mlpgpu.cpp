@@ -667,10 +667,16 @@ static int grow_store(mlp_ctx* c, int64_t need, int64_t keep, int64_t want = 0) 
 template <class F>
 static size_t batch_target_for(mlp_ctx* c, int64_t p0, int64_t p1, F pair_bytes, size_t budget = 0) {
   if (!budget) budget = c->scratch_budget;
-  size_t all = 0;
-  for (int64_t q = p0; q < p1; q++) all += pair_bytes(q);
+  size_t all = 0, biggest = 0;
+  for (int64_t q = p0; q < p1; q++) {
+    const size_t b = pair_bytes(q);
+    all += b;
+    biggest = std::max(biggest, b);
+  }
   const size_t nb = (all + budget - 1) / std::max<size_t>(budget, 1);
-  if (nb > 1) return std::min(budget, all / nb + all / (nb * 64) + 1);
+  // a batch stops before the pair that would pass the target, so each holds
+  // more than all / nb - biggest: nb batches of near-equal bytes
+  if (nb > 1) return std::min(budget, all / nb + biggest);
   return budget;
 }
 template <class F>
@@ -1240,6 +1246,21 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
   // before (k_local_bounds) instead of their maximum (MLP_TOT_FOLDBOUND=0 / 1)
   static const char* fb_env = getenv("MLP_TOT_FOLDBOUND");
   const bool foldbound = (models & kLocal) && !lanefold && (fb_env ? atoi(fb_env) != 0 : true);
+  // the one-wave fold's forward chains on stream2 beside the backward sweeps
+  // (they read only what the forward sweep wrote), the backward chains after
+  // them on the context stream (MLP_TOT_BESIDE=0 / 1 / 2, 2 the default: the partition function's sweeps
+  // joined before the merge only, so the HMM backward starts right after
+  // the HMM forward).  C3 drop-in posteriors at 16 GB: 0.90 s after the
+  // sweeps, 0.83 beside, 0.82 with the late join, 0.77 with the totals
+  // kernels at wave priority 3 (profiles/r05z_cli_totals_beside.txt)
+  static const char* tb_env = getenv("MLP_TOT_BESIDE");
+  const int tb_mode = tb_env ? atoi(tb_env) : 2;
+  const bool tot_beside = (models & kLocal) && !lanefold && !two && tb_mode != 0;
+  if (side && tot_beside && side_used && tb_mode == 2) {
+    side_lf = *side;
+    side_lf.join_mode = 2;
+    side = &side_lf;
+  }
   auto budget_for = [&](size_t b) { return std::max<size_t>(b > clist_bytes ? b - clist_bytes : 0, 32u << 20); };
   size_t batch_target =
       batch_target_for(c, p0, p1, pair_bytes, budget_for(two ? c->scratch_budget / 2 : c->scratch_budget));
@@ -1320,35 +1341,97 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
   int64_t p = p0;
   int slot = 0;
   ChainPlan P;
+  // a batch's scratch layout (256-byte aligned sub-buffers); returns the bytes
+  struct BatchOffs {
+    size_t f5, fl, bl, pg, zm, cmf, cmb, tn, cl, crb, rep, b5, bnl, bz, be, bm, bc, ec, ev, en, entb, rpb, rec;
+    PlanDev pd;
+  };
+  auto carve = [&](const ChainPlan& P, BatchOffs& o) -> size_t {
+    Carver cv;
+    const int64_t np = P.np;
+    const bool h5 = models & kHmm5, lo = models & kLocal, pf = models & kPF;
+    o.f5 = cv.take(h5 ? P.cells * 4 : 0);
+    o.fl = cv.take(lo ? P.cells * 4 : 0);
+    o.bl = cv.take(lo ? P.cells * 4 + (lanefold ? kLaneFoldPad : 0) : 0);
+    o.pg = cv.take(pf && !pg_in_zm ? P.cells * 4 : 0);
+    o.zm = cv.take(pf ? P.cells * 8 : 0);
+    o.cmf = cv.take(lo ? P.rm_total * 4 : 0);
+    o.cmb = cv.take(lo ? P.rm_total * 4 : 0);
+    o.tn = cv.take(lo ? 256 : 0);
+    o.cl = cv.take(clist_bytes);
+    o.crb = cv.take(lanefold || foldbound ? P.ell_rows * 4 : 0);
+    o.rep = cv.take(lanefold ? (np + 1) * 4 : 0);
+    o.b5 = cv.take(P.bnd * 20);
+    o.bnl = cv.take(P.bnd * 12);
+    o.bz = cv.take(P.bnd * 24);
+    o.be = cv.take(P.bnd * 4);
+    o.bm = cv.take(P.bnd * 4);
+    o.bc = cv.take(P.bnd * 4);
+    o.ec = cv.take(P.ell_rows * kEll * 2);
+    o.ev = cv.take(P.ell_rows * kEll * 4);
+    o.en = cv.take(P.ell_rows * 4);
+    o.entb = cv.take(np * 8);
+    o.rpb = cv.take(np * 8);
+    o.rec = cv.take(np * sizeof(PairRec));
+    o.pd = carve_plan(cv, P);
+    return cv.off;
+  };
+  bool calibrated = false;
   while (p < p1) {
     int64_t q;
     int rc;
     if ((rc = next_batch(c, p, p1, batch_target, pair_bytes, &q))) return rc;
     Pending& B = pend[slot];
     plan_chains(c, p, q, P);          // host planning overlaps the previous batch's kernels
+    if (!calibrated) {
+      // pair_bytes bounds each pair as if alone in a chain of a wider member;
+      // the planned chains need less (C3: ~14%).  Once, from the first batch:
+      // re-plan the batches to the budget at the measured ratio, then take
+      // the first batch again (each batch is checked against the budget below)
+      calibrated = true;
+      BatchOffs o;
+      size_t bound = 0;
+      for (int64_t k = p; k < q; k++) bound += pair_bytes(k);
+      const size_t got = carve(P, o);
+      const double r = (double)(got > clist_bytes ? got - clist_bytes : 0) / (double)std::max<size_t>(bound, 1);
+      if (q < p1 && r > 0.1 && r < 0.97) {
+        const size_t slot_budget = two ? c->scratch_budget / 2 : c->scratch_budget;
+        batch_target = batch_target_for(c, p, p1, pair_bytes,
+                                        std::max<size_t>((size_t)((double)budget_for(slot_budget) / r * 0.99), 32u << 20));
+        if ((rc = next_batch(c, p, p1, batch_target, pair_bytes, &q))) return rc;
+        plan_chains(c, p, q, P);
+      }
+    }
+    {  // a batch over its slot's budget (the ratio varies with the pairs): fewer pairs
+      const size_t slot_budget = two ? c->scratch_budget / 2 : c->scratch_budget;
+      BatchOffs o;
+      while (q - p > 1 && carve(P, o) > slot_budget) {
+        q = p + std::max<int64_t>(1, (q - p) * 97 / 100);
+        plan_chains(c, p, q, P);
+      }
+    }
     if ((rc = finish(B))) return rc;  // this slot's previous batch
     hipStream_t st = streams[slot];
     const int64_t np = P.np, nch = P.nch;
     // ---- carve scratch
-    Carver cv;
-    const bool h5 = models & kHmm5, lo = models & kLocal, pf = models & kPF;
-    const size_t o_f5 = cv.take(h5 ? P.cells * 4 : 0), o_fl = cv.take(lo ? P.cells * 4 : 0),
-                 o_bl = cv.take(lo ? P.cells * 4 + (lanefold ? kLaneFoldPad : 0) : 0), o_pg = cv.take(pf && !pg_in_zm ? P.cells * 4 : 0),
-                 o_zm = cv.take(pf ? P.cells * 8 : 0), o_cmf = cv.take(lo ? P.rm_total * 4 : 0),
-                 o_cmb = cv.take(lo ? P.rm_total * 4 : 0),
-                 o_tn = cv.take(lo ? 256 : 0), o_cl = cv.take(clist_bytes),
-                 o_crb = cv.take(lanefold || foldbound ? P.ell_rows * 4 : 0),
-                 o_rep = cv.take(lanefold ? (np + 1) * 4 : 0),
-                 o_b5 = cv.take(P.bnd * 20), o_bnl = cv.take(P.bnd * 12), o_bz = cv.take(P.bnd * 24),
-                 o_be = cv.take(P.bnd * 4), o_bm = cv.take(P.bnd * 4), o_bc = cv.take(P.bnd * 4), o_ec = cv.take(P.ell_rows * kEll * 2),
-                 o_ev = cv.take(P.ell_rows * kEll * 4), o_en = cv.take(P.ell_rows * 4),
-                 o_entb = cv.take(np * 8), o_rpb = cv.take(np * 8), o_rec = cv.take(np * sizeof(PairRec));
-    const PlanDev pd = carve_plan(cv, P);
-    if ((rc = ensure(c, *scr[slot], cv.off))) {
+    BatchOffs o;
+    const size_t need = carve(P, o);
+    const PlanDev& pd = o.pd;
+    const size_t o_f5 = o.f5, o_fl = o.fl, o_bl = o.bl, o_pg = o.pg, o_zm = o.zm, o_cmf = o.cmf, o_cmb = o.cmb,
+                 o_tn = o.tn, o_cl = o.cl, o_crb = o.crb, o_rep = o.rep, o_b5 = o.b5, o_bnl = o.bnl, o_bz = o.bz,
+                 o_be = o.be, o_bm = o.bm, o_bc = o.bc, o_ec = o.ec, o_ev = o.ev, o_en = o.en, o_entb = o.entb,
+                 o_rpb = o.rpb, o_rec = o.rec;
+    // with more batches to come, 3% headroom (capped at the slot's budget):
+    // they are planned to the same bytes, and one that needs a little more
+    // would otherwise reallocate the scratch
+    const size_t slot_budget = two ? c->scratch_budget / 2 : c->scratch_budget;
+    const size_t want = q < p1 && scr[slot]->bytes < need ? std::max(need, std::min(slot_budget, need + need / 32)) : need;
+    if ((rc = ensure(c, *scr[slot], want))) {
       if (rc != MLP_ERR_MEMORY || c->scratch_budget < (64u << 20)) return rc;
       c->scratch_budget /= 2;  // the device is shared: plan smaller batches and retry
       batch_target =
           batch_target_for(c, p, p1, pair_bytes, budget_for(two ? c->scratch_budget / 2 : c->scratch_budget));
+      calibrated = false;
       continue;
     }
     char* base = (char*)scr[slot]->p;
@@ -1398,6 +1481,17 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
       HIPCHK(c, launch_local_fwd_lanefold(seqs, pm, cm, d_rec, sc, np, tot_waves, st));
       EXP_SYNC("forward totals");
     }
+    hipEvent_t tot_done = nullptr;
+    if (tot_beside) {  // the forward chains on stream2, beside the backward sweeps
+      hipEvent_t e = pool_event(c);
+      HIPCHK(c, hipEventRecord(e, st));
+      HIPCHK(c, hipStreamWaitEvent(c->stream2, e, 0));
+      Timer t(c, KTOT, bcells, c->stream2);
+      HIPCHK(c, launch_local_totals(ms, c->d_tables, seqs, pm, cm, d_rec, sc, np, tot_waves, c->stream2, kTotFwd));
+      tot_done = pool_event(c);
+      HIPCHK(c, hipEventRecord(tot_done, c->stream2));
+      EXP_SYNC("forward totals");
+    }
     {
       Timer t(c, KBWD, bcells, st);
       if (side_used) t.span(side->st, true, fwd_ref);
@@ -1406,10 +1500,14 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
     }
     if (models & kLocal) {
       Timer t(c, KTOT, bcells, st);
-      if (lanefold)
+      if (lanefold) {
         HIPCHK(c, launch_local_bwd_lanefold(ms, c->d_tables, seqs, pm, cm, d_rec, sc, np, tot_waves, st));
-      else
+      } else if (tot_beside) {
+        HIPCHK(c, launch_local_totals(ms, c->d_tables, seqs, pm, cm, d_rec, sc, np, tot_waves, st, kTotBwd));
+        HIPCHK(c, hipStreamWaitEvent(st, tot_done, 0));
+      } else {
         HIPCHK(c, launch_local_totals(ms, c->d_tables, seqs, pm, cm, d_rec, sc, np, tot_waves, st));
+      }
       EXP_SYNC("totals");
     }
     if (side && side->join_mode != 0) HIPCHK(c, hipStreamWaitEvent(st, side->join, 0));  // deferred join

@@ -226,10 +226,14 @@ __device__ __forceinline__ float local_fwd_fold(const float* __restrict__ cmf, c
 // lane-fold path's repair list: [0] = count, then slots) just those pairs.
 __global__ __launch_bounds__(256) void k_local_totals(ModelScalars ms, const Tables* __restrict__ tab, SeqSet sq,
                                                       PairMeta pm, ChainMeta cm, PairRec* __restrict__ rec,
-                                                      Scratch sc, int64_t npairs, const int32_t* __restrict__ only) {
+                                                      Scratch sc, int64_t npairs, const int32_t* __restrict__ only,
+                                                      int parts) {
   __shared__ float4 lk[kLookupRows];
   __shared__ float match[26 * 26], ins[26];
   __shared__ float lbuf_all[kWavesPerBlock * kLbufSlots * 64];  // per wave: a ring per lane
+  // beside the backward sweeps (MLP_TOT_BESIDE) the serial chains are the
+  // batch's critical path and issue little: the SIMDs serve them first
+  __builtin_amdgcn_s_setprio(3);
   if (threadIdx.x == 0) mlp_lookup_table(lk);
   for (int k = threadIdx.x; k < 26 * 26; k += blockDim.x) match[k] = tab->match[k];
   if (threadIdx.x < 26) ins[threadIdx.x] = tab->ins[threadIdx.x];
@@ -266,12 +270,12 @@ __global__ __launch_bounds__(256) void k_local_totals(ModelScalars ms, const Tab
       tf = local_fwd_fold(sc.cmf + rm, sc.fl, L1, L2, row0, W, cell_off, lk, region, sc.clist_row, lane, lbuf, nullptr,
                           &bad);
     }
-    float tb = fold_chunks<true>(LZ, 0, (int64_t)L1 * local_chunks(L2), sc.cmb + rm, sc.bl, L2, row0, W, cell_off, s1,
-                                 s2, match, ins, 2 * ms.rt1, lk, lane);
-    if (lane == 0) {
-      rec[p].tfl = tf;
-      rec[p].tbl = tb;
+    if (parts & kTotBwd) {
+      const float tb = fold_chunks<true>(LZ, 0, (int64_t)L1 * local_chunks(L2), sc.cmb + rm, sc.bl, L2, row0, W,
+                                         cell_off, s1, s2, match, ins, 2 * ms.rt1, lk, lane);
+      if (lane == 0) rec[p].tbl = tb;
     }
+    if (lane == 0) rec[p].tfl = tf;
   }
 }
 
@@ -296,6 +300,7 @@ __global__ __launch_bounds__(256) void k_local_totals(ModelScalars ms, const Tab
 // Lane per pair: crb[ell + i - 1] = fold of the chunk maxima of rows 1..i-1.
 __global__ __launch_bounds__(256) void k_local_bounds(SeqSet sq, PairMeta pm, Scratch sc, int64_t npairs) {
   __shared__ float4 lk[kLookupRows];
+  __builtin_amdgcn_s_setprio(3);  // (as k_local_totals)
   if (threadIdx.x == 0) mlp_lookup_table(lk);
   __syncthreads();
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -306,6 +311,31 @@ __global__ __launch_bounds__(256) void k_local_bounds(SeqSet sq, PairMeta pm, Sc
   float* __restrict__ rb = sc.crb + pm.ell_row[p];
   float acc = LZ;
   constexpr int kRow = 8;  // a row's chunk maxima loaded together (L2 <= 512), then folded
+  if (nch <= kRow) {
+    // rows kAhead ahead in a register ring: each lane's loads are its own
+    // pair's (uncoalesced), so a row loaded just before its fold waits the
+    // whole memory latency once per row
+    constexpr int kAhead = 4;
+    float v[kAhead][kRow];
+#pragma unroll
+    for (int a = 0; a < kAhead; ++a)
+#pragma unroll
+      for (int u = 0; u < kRow; ++u) v[a][u] = (a < L1 && u < nch) ? cmx[(int64_t)a * nch + u] : LZ;
+    for (int i = 0; i < L1; i += kAhead) {
+#pragma unroll
+      for (int a = 0; a < kAhead; ++a) {
+        if (i + a < L1) {
+          rb[i + a] = acc;
+#pragma unroll
+          for (int u = 0; u < kRow; ++u) acc = mlp_log_add_t(acc, v[a][u], lk);  // LOG_ADD(acc, LZ) == acc
+        }
+        const int nx = i + a + kAhead;
+#pragma unroll
+        for (int u = 0; u < kRow; ++u) v[a][u] = (nx < L1 && u < nch) ? cmx[(int64_t)nx * nch + u] : LZ;
+      }
+    }
+    return;
+  }
   for (int i = 0; i < L1; ++i) {
     rb[i] = acc;
     for (int c0 = 0; c0 < nch; c0 += kRow) {
@@ -564,15 +594,20 @@ __global__ void k_fold_totals(ModelScalars ms, SeqSet sq, PairMeta pm, PairRec* 
 
 // ------------------------------------------------------------ launchers
 hipError_t launch_local_totals(const ModelScalars& ms, const Tables* tab, SeqSet seqs, PairMeta pm, ChainMeta cm,
-                               PairRec* rec, Scratch sc, int64_t npairs, int nwaves, hipStream_t st) {
+                               PairRec* rec, Scratch sc, int64_t npairs, int nwaves, hipStream_t st, int parts) {
   if (npairs <= 0) return hipSuccess;
+  if (!(parts & kTotFwd)) {  // the backward chains alone
+    hipLaunchKernelGGL(k_local_btot, wave_grid(npairs), dim3(64 * kWavesPerBlock), 0, st, ms, tab, seqs, pm, cm, rec,
+                       sc, npairs);
+    return hipGetLastError();
+  }
   if (sc.crb)  // the folded row bounds (lane per pair)
     hipLaunchKernelGGL(k_local_bounds, dim3((unsigned)((npairs + 255) / 256)), dim3(256), 0, st, seqs, pm, sc, npairs);
   hipError_t e = hipMemsetAsync(sc.tot_next, 0, sizeof(int32_t), st);
   if (e != hipSuccess) return e;
   if (nwaves % kWavesPerBlock) return hipErrorInvalidValue;  // every wave owns a list region
   hipLaunchKernelGGL(k_local_totals, wave_grid(nwaves), dim3(64 * kWavesPerBlock), 0, st, ms, tab, seqs, pm, cm, rec,
-                     sc, npairs, (const int32_t*)nullptr);
+                     sc, npairs, (const int32_t*)nullptr, parts);
   return hipGetLastError();
 }
 
@@ -604,7 +639,7 @@ hipError_t launch_local_bwd_lanefold(const ModelScalars& ms, const Tables* tab, 
   hipError_t e;
   if ((e = hipMemsetAsync(sc.tot_next, 0, sizeof(int32_t), st)) != hipSuccess) return e;
   hipLaunchKernelGGL(k_local_totals, wave_grid(std::min(nwaves, 1024)), dim3(64 * kWavesPerBlock), 0, st, ms, tab, seqs,
-                     pm, cm, rec, sc, npairs, (const int32_t*)sc.rep);
+                     pm, cm, rec, sc, npairs, (const int32_t*)sc.rep, kTotFwd | kTotBwd);
   return hipGetLastError();
 }
 

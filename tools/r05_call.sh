@@ -1,11 +1,18 @@
 #!/bin/bash
-# r05 GPU call: c_p_np_aln device-MEA floor after the pinned-buffer fix -- C2 -p 0 / -p 1, floors 2.5e5 / 5e4 / 0,
-# stage times, outputs against the reference's
+# r05 GPU call: new defaults (forward-chain totals beside the backward sweeps at wave priority 3, batch
+# planning calibrated to the planned chains, balanced batches) -- GPU suite, then c_p_np_aln C3 -p 0 / -p 1 and
+# quickprobs C3 against HEAD's library, alternating
 set -o pipefail
-export TMPDIR=/tmp MLP_SRAND_TIME=1700000000
-O=gpurun_out/floor; mkdir -p $O
-c=c2_128x256_s11; FA=tests/golden/config/$c.fa
-for k in 1 2 3; do for mode in 0 1; do for m in 250000 50000 0; do
-  MLP_MEA_GPU_MIN=$m MLP_CLI_TIMES=1 timeout -k 10 120 mlprobs_amd/cli/c_p_np_aln -p $mode $FA > $O/o.msa 2> $O/e.txt || { tail -5 $O/e.txt; exit 1; }
-  echo "-p $mode floor $m run $k: $(grep -E '^\[stage\] (progressive \+ refinement|refinement|context teardown)' $O/e.txt | tr '\n' ' ') $(grep '^\[host\]' $O/e.txt) $(cmp -s $O/o.msa tests/golden/config/$c.p_$mode.out && echo identical-to-ref)" | tee -a $O/summary.txt
-done; done; done
+export TMPDIR=/tmp
+O=gpurun_out/newdef; mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/t.txt 2>&1 || { tail -30 $O/t.txt; exit 1; }
+tail -1 $O/t.txt
+mkdir -p /tmp/v_head && ln -sf $PWD/mlprobs_amd/lib/libmlpgpu_head.so /tmp/v_head/libmlpgpu.so
+FA=tests/golden/config/c3_512x400_s11.fa
+for k in 1 2 3; do for v in head new; do
+  LP=; [ $v = head ] && LP=/tmp/v_head
+  LD_LIBRARY_PATH=$LP MLP_CLI_TIMES=1 timeout -k 10 120 mlprobs_amd/cli/c_p_np_aln -p 0 $FA > $O/o.msa 2> $O/e.txt || { tail -5 $O/e.txt; exit 1; }
+  echo "$v -p 0 run $k: $(grep -E '^\[stage\] (posteriors|consistency) ' $O/e.txt | tr '\n' ' ') $(cmp -s $O/o.msa tests/golden/config/c3_512x400_s11.p_0.out && echo identical)" | tee -a $O/summary.txt
+  LD_LIBRARY_PATH=$LP MLP_CLI_TIMES=1 timeout -k 10 120 mlprobs_amd/cli/quickprobs $FA > $O/q.msa 2> $O/e.txt || { tail -5 $O/e.txt; exit 1; }
+  echo "$v qp run $k: $(grep -E '^\[stage\] (posteriors|consistency) ' $O/e.txt | tr '\n' ' ') $(cmp -s $O/q.msa tests/golden/config/c3_512x400_s11.qp.out && echo identical)" | tee -a $O/summary.txt
+done; done
