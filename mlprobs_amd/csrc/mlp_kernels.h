@@ -114,7 +114,7 @@ struct SeqSet {
 
 struct Scratch {
   float* f5;               // step-diagonal: 5-state fwd M, then f+b (in place)
-  float* fl;               // local fwd M, then f+b
+  float* fl;               // local fwd M (the merge adds fl + bl)
   double* zm;              // PF forward Zm (packed with frame)
   float* pg;               // PF posterior, element idx at pg[idx * pg_stride]
   int32_t pg_stride;       // 2: in the low half of the slot's consumed PF forward Zm (zm)
