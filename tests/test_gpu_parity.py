@@ -598,14 +598,14 @@ def test_profile_mea_multi_strip():
 
 
 def test_profile_mea_groups():
-    """~1150 profile-A columns: 18 strips in workgroups of four (LDS hand-off
-    inside a group, L2 between groups, a last group of two)."""
+    """~1150 profile-A columns: 18 strips, each polling the row the one
+    above hands off (NaN-filled rows, mlp_profile_mea)."""
     _profile_case(87, 4, 140, 0.5, [0, 1], [2, 3], pad1=1010)
 
 
 def test_profile_mea_wide_rows():
-    """~4150 profile-B columns: four rows exceed kMeaLdsMax, every strip is
-    its own workgroup with the L2 hand-off (k_profile_mea<1>)."""
+    """~4150 profile-B columns: rows of ~65 blocks, so a poll's 64 columns
+    serve up to four blocks many times over."""
     _profile_case(88, 4, 140, 0.5, [0, 1], [2, 3], pad2=4010)
 
 
