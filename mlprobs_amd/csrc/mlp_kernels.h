@@ -147,6 +147,8 @@ struct Scratch {
   uint16_t* ell_col;       // [ell row][kEll]
   float* ell_val;
   int32_t* ell_cnt;        // [ell row]
+  int32_t* lf_cnt;         // [ell row] the lane fold's candidate counts: ell_cnt (dead until the merge),
+                           // or a per-batch array when a deferred finish still compacts the last batch
   uint8_t* vt;             // step-diagonal Viterbi traceback bits
 };
 

@@ -94,6 +94,12 @@ struct mlp_ctx {
   float* prof_dout = nullptr;
   int prof_L1 = 0, prof_L2 = 0;
   uint8_t* h_mea = nullptr;           // pinned: MEA choices + score
+  PairRec* h_rec[2] = {nullptr, nullptr};  // pinned: a posterior batch's pair records (batch parity)
+  size_t h_rec_n[2] = {0, 0};
+  uint8_t* h_up[2] = {nullptr, nullptr};   // pinned: a batch's plan on its way up (batch parity)
+  size_t h_up_n[2] = {0, 0};
+  int64_t* h_ent[2] = {nullptr, nullptr};  // pinned: a batch's entry bases (parity; written when it is finished)
+  size_t h_ent_n[2] = {0, 0};
   size_t h_mea_bytes = 0;
   std::vector<float> dist, mea;
   std::vector<int64_t> nnz;
@@ -530,6 +536,12 @@ void mlp_ctx_destroy(mlp_ctx* c) {
   if (c->h_prof_in) hipHostFree(c->h_prof_in);
   if (c->h_prof_out) hipHostFree(c->h_prof_out);
   if (c->h_mea) hipHostFree(c->h_mea);
+  for (PairRec* r : c->h_rec)
+    if (r) hipHostFree(r);
+  for (uint8_t* u : c->h_up)
+    if (u) hipHostFree(u);
+  for (int64_t* u : c->h_ent)
+    if (u) hipHostFree(u);
   lap("pinned host buffers");
   for (hipStream_t st : c->cst) hipStreamDestroy(st);
   hipStreamDestroy(c->stream);
@@ -632,9 +644,11 @@ int mlp_family_load(mlp_ctx* c, int n, const char* residues, const int64_t* offs
 int64_t mlp_family_npairs(const mlp_ctx* c) { return c ? c->P : 0; }
 
 // grow the entry store to hold `need` entries, keeping `keep` existing ones
-static int grow_store(mlp_ctx* c, int64_t need, int64_t keep, int64_t want = 0) {
+static int grow_store(mlp_ctx* c, int64_t need, int64_t keep, int64_t want = 0, bool sync2 = true) {
   if (need <= c->ent_cap) return MLP_OK;
-  HIPCHK(c, hipStreamSynchronize(c->stream2));  // a compaction may still be writing the old store
+  // a compaction may still be writing the old store on stream2 (two-slot
+  // batches); the caller passes false when its compactions use the context stream
+  if (sync2) HIPCHK(c, hipStreamSynchronize(c->stream2));
   // `want`: the caller's estimate of the final size, so a growing store is
   // reallocated (and copied) once rather than every 1.5x
   int64_t cap = std::max<int64_t>(std::max<int64_t>(need, want), c->ent_cap + c->ent_cap / 2);
@@ -817,9 +831,16 @@ static PlanDev carve_plan(Carver& cv, const ChainPlan& P) {
   return d;
 }
 static int upload_plan(mlp_ctx* c, char* base, const PlanDev& d, const ChainPlan& P, PairMeta& pm,
-                       ChainMeta& cm, hipStream_t st = nullptr) {
+                       ChainMeta& cm, hipStream_t st = nullptr, uint8_t* stage = nullptr) {
   if (!st) st = c->stream;
+  // with `stage` (pinned, >= the plan region's bytes) the arrays are gathered
+  // there and go up in one asynchronous copy; else one pageable copy each
+  const size_t span = d.o_cbo + P.nch * 8 - d.o_pa;
   auto up = [&](size_t o, const void* h, size_t n) {
+    if (stage) {
+      memcpy(stage + (o - d.o_pa), h, n);
+      return hipSuccess;
+    }
     return hipMemcpyAsync(base + o, h, n, hipMemcpyHostToDevice, st);
   };
   HIPCHK(c, up(d.o_pa, P.pa.data(), P.np * 4));
@@ -835,6 +856,7 @@ static int upload_plan(mlp_ctx* c, char* base, const PlanDev& d, const ChainPlan
   HIPCHK(c, up(d.o_cs, P.seqb.data(), P.nch * 4));
   HIPCHK(c, up(d.o_cco, P.cell.data(), P.nch * 8));
   HIPCHK(c, up(d.o_cbo, P.bndo.data(), P.nch * 8));
+  if (stage) HIPCHK(c, hipMemcpyAsync(base + d.o_pa, stage, span, hipMemcpyHostToDevice, st));
   pm.pa = (const int32_t*)(base + d.o_pa);
   pm.pb = (const int32_t*)(base + d.o_pb);
   pm.row0 = (const int32_t*)(base + d.o_r0);
@@ -1279,20 +1301,37 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
     int slot = 0;
     int64_t p = 0, q = 0, np = 0, bcells = 0;
     std::vector<int64_t> order;
-    std::vector<PairRec> rec;
+    const PairRec* rec = nullptr;  // the records' host copy (pinned, c->h_rec[parity])
+    int par = 0;
     char* base = nullptr;
     size_t o_entb = 0, o_rpb = 0;
     PairMeta pm;
     Scratch sc;
     PairRec* d_rec = nullptr;
+    hipEvent_t done = nullptr;  // after the merge and the records' copy to the host
   };
   Pending pend[2];
+  // Deferred finish (one slot): batch b + 1's sweeps are launched before the
+  // host finishes batch b (entry offsets, store growth, its compaction), so
+  // that host work overlaps the sweeps instead of idling the device between
+  // batches; batch b + 1's merge follows b's compaction in stream order.  What
+  // b's compaction reads (plan, records, entry bases, ELL rows) lives in a
+  // front region the sweeps never write: plan and records twice (batch
+  // parity), ELL rows once (written only by the merges).  MLP_DEFER_FINISH=0
+  // finishes each batch before the next is launched.
+  static const char* df_env = getenv("MLP_DEFER_FINISH");
+  const bool defer = !two && (df_env ? atoi(df_env) != 0 : true);
+  struct Front {
+    bool set = false;
+    int64_t np = 0, nch = 0, ell = 0;  // capacities
+  } front;
+  int par = 0;
   // host part + compaction of a launched batch
   auto finish = [&](Pending& B) -> int {
     if (!B.live) return MLP_OK;
     B.live = false;
     hipStream_t st = streams[B.slot];
-    HIPCHK(c, hipStreamSynchronize(st));
+    HIPCHK(c, B.done ? hipEventSynchronize(B.done) : hipStreamSynchronize(st));
     const int64_t np = B.np;
     for (int64_t s = 0; s < np; s++) {
       if (B.rec[s].flags & 1) {
@@ -1306,7 +1345,19 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
       }
     }
     // ---- canonical entry offsets (pair order) and compaction
-    std::vector<int64_t> slot_of(np), h_entb(np), h_rpb(np);
+    // entry bases through pinned staging of the batch's parity: its last
+    // copy (two batches back) ran before the merge finish() waited for last
+    std::vector<int64_t> slot_of(np);
+    if (c->h_ent_n[B.par] < (size_t)np * 2) {
+      if (c->h_ent[B.par]) hipHostFree(c->h_ent[B.par]);
+      c->h_ent[B.par] = nullptr;
+      c->h_ent_n[B.par] = 0;
+      const size_t n = (size_t)np * 2 + (size_t)np / 4 + 128;
+      HIPCHK(c, hipHostMalloc((void**)&c->h_ent[B.par], n * 8, hipHostMallocDefault));
+      c->h_ent_n[B.par] = n;
+    }
+    int64_t* h_entb = c->h_ent[B.par];
+    int64_t* h_rpb = h_entb + np;
     for (int64_t s = 0; s < np; s++) slot_of[B.order[s] - B.p] = s;
     int64_t run = c->store_total;
     for (int64_t k = 0; k < np; k++) {
@@ -1326,9 +1377,9 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
     // the set's final size, extrapolated from the pairs done so far (+10%)
     const int64_t want = run + (int64_t)((double)(run - base_total) / (double)done_cells *
                                          (double)(all_cells - done_cells) * 1.1);
-    if ((rc = grow_store(c, run, c->store_total, want))) return rc;
-    HIPCHK(c, hipMemcpyAsync(B.base + B.o_entb, h_entb.data(), np * 8, hipMemcpyHostToDevice, st));
-    HIPCHK(c, hipMemcpyAsync(B.base + B.o_rpb, h_rpb.data(), np * 8, hipMemcpyHostToDevice, st));
+    if ((rc = grow_store(c, run, c->store_total, want, two))) return rc;
+    HIPCHK(c, hipMemcpyAsync(B.base + B.o_entb, h_entb, np * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(c, hipMemcpyAsync(B.base + B.o_rpb, h_rpb, np * 8, hipMemcpyHostToDevice, st));
     {
       Timer t(c, KCOMPACT, B.bcells, st);
       HIPCHK(c, launch_compact(seqs, B.pm, B.d_rec, B.sc, (const int64_t*)(B.base + B.o_entb), c->d_rowptr,
@@ -1343,13 +1394,27 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
   ChainPlan P;
   // a batch's scratch layout (256-byte aligned sub-buffers); returns the bytes
   struct BatchOffs {
-    size_t f5, fl, bl, pg, zm, cmf, cmb, tn, cl, crb, rep, b5, bnl, bz, be, bm, bc, ec, ev, en, entb, rpb, rec;
+    size_t f5, fl, bl, pg, zm, cmf, cmb, tn, cl, crb, rep, lfc, b5, bnl, bz, be, bm, bc, ec, ev, en, entb, rpb, rec;
     PlanDev pd;
   };
   auto carve = [&](const ChainPlan& P, BatchOffs& o) -> size_t {
     Carver cv;
     const int64_t np = P.np;
     const bool h5 = models & kHmm5, lo = models & kLocal, pf = models & kPF;
+    if (defer && front.set) {  // the front region (capacities), this batch's parity
+      ChainPlan cap;
+      cap.np = front.np;
+      cap.nch = front.nch;
+      const PlanDev pd0 = carve_plan(cv, cap), pd1 = carve_plan(cv, cap);
+      const size_t r0 = cv.take(front.np * sizeof(PairRec)), r1 = cv.take(front.np * sizeof(PairRec));
+      o.pd = par ? pd1 : pd0;
+      o.rec = par ? r1 : r0;
+      o.entb = cv.take(front.np * 8);
+      o.rpb = cv.take(front.np * 8);
+      o.ec = cv.take(front.ell * kEll * 2);
+      o.ev = cv.take(front.ell * kEll * 4);
+      o.en = cv.take(front.ell * 4);
+    }
     o.f5 = cv.take(h5 ? P.cells * 4 : 0);
     o.fl = cv.take(lo ? P.cells * 4 : 0);
     o.bl = cv.take(lo ? P.cells * 4 + (lanefold ? kLaneFoldPad : 0) : 0);
@@ -1361,19 +1426,22 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
     o.cl = cv.take(clist_bytes);
     o.crb = cv.take(lanefold || foldbound ? P.ell_rows * 4 : 0);
     o.rep = cv.take(lanefold ? (np + 1) * 4 : 0);
+    o.lfc = cv.take(lanefold && defer ? P.ell_rows * 4 : 0);  // (else the lane fold counts in ell_cnt)
     o.b5 = cv.take(P.bnd * 20);
     o.bnl = cv.take(P.bnd * 12);
     o.bz = cv.take(P.bnd * 24);
     o.be = cv.take(P.bnd * 4);
     o.bm = cv.take(P.bnd * 4);
     o.bc = cv.take(P.bnd * 4);
-    o.ec = cv.take(P.ell_rows * kEll * 2);
-    o.ev = cv.take(P.ell_rows * kEll * 4);
-    o.en = cv.take(P.ell_rows * 4);
-    o.entb = cv.take(np * 8);
-    o.rpb = cv.take(np * 8);
-    o.rec = cv.take(np * sizeof(PairRec));
-    o.pd = carve_plan(cv, P);
+    if (!(defer && front.set)) {
+      o.ec = cv.take(P.ell_rows * kEll * 2);
+      o.ev = cv.take(P.ell_rows * kEll * 4);
+      o.en = cv.take(P.ell_rows * 4);
+      o.entb = cv.take(np * 8);
+      o.rpb = cv.take(np * 8);
+      o.rec = cv.take(np * sizeof(PairRec));
+      o.pd = carve_plan(cv, P);
+    }
     return cv.off;
   };
   bool calibrated = false;
@@ -1410,7 +1478,20 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
         plan_chains(c, p, q, P);
       }
     }
-    if ((rc = finish(B))) return rc;  // this slot's previous batch
+    if (defer) {
+      // front capacities from the first batch with 5% slack; a batch that
+      // needs more finishes the pending one first (nothing then reads the old
+      // front) and widens them
+      if (!front.set || P.np > front.np || P.nch > front.nch || P.ell_rows > front.ell) {
+        if ((rc = finish(B))) return rc;
+        front.set = true;
+        front.np = std::max<int64_t>(front.np, P.np + P.np / 20 + 64);
+        front.nch = std::max<int64_t>(front.nch, P.nch + P.nch / 20 + 64);
+        front.ell = std::max<int64_t>(front.ell, P.ell_rows + P.ell_rows / 20 + 1024);
+      }
+    } else if ((rc = finish(B))) {  // this slot's previous batch
+      return rc;
+    }
     hipStream_t st = streams[slot];
     const int64_t np = P.np, nch = P.nch;
     // ---- carve scratch
@@ -1426,6 +1507,7 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
     // would otherwise reallocate the scratch
     const size_t slot_budget = two ? c->scratch_budget / 2 : c->scratch_budget;
     const size_t want = q < p1 && scr[slot]->bytes < need ? std::max(need, std::min(slot_budget, need + need / 32)) : need;
+    if (scr[slot]->bytes < want && (rc = finish(B))) return rc;  // a reallocation: nothing may still read the old one
     if ((rc = ensure(c, *scr[slot], want))) {
       if (rc != MLP_ERR_MEMORY || c->scratch_budget < (64u << 20)) return rc;
       c->scratch_budget /= 2;  // the device is shared: plan smaller batches and retry
@@ -1460,10 +1542,22 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
     sc.ell_col = (uint16_t*)(base + o_ec);
     sc.ell_val = (float*)(base + o_ev);
     sc.ell_cnt = (int32_t*)(base + o_en);
+    sc.lf_cnt = lanefold && defer ? (int32_t*)(base + o.lfc) : sc.ell_cnt;
     PairRec* d_rec = (PairRec*)(base + o_rec);
     PairMeta pm;
     ChainMeta cm;
-    if ((rc = upload_plan(c, base, pd, P, pm, cm, st))) return rc;
+    {  // the plan through this parity's pinned staging (its last batch is finished)
+      const size_t up_need = pd.o_cbo + P.nch * 8 - pd.o_pa;
+      if (c->h_up_n[par] < up_need) {
+        if (c->h_up[par]) hipHostFree(c->h_up[par]);
+        c->h_up[par] = nullptr;
+        c->h_up_n[par] = 0;
+        const size_t n = up_need + up_need / 8 + 4096;
+        HIPCHK(c, hipHostMalloc((void**)&c->h_up[par], n, hipHostMallocDefault));
+        c->h_up_n[par] = n;
+      }
+    }
+    if ((rc = upload_plan(c, base, pd, P, pm, cm, st, c->h_up[par]))) return rc;
     const int lds_seq = P.lds_seq;
     HIPCHK(c, hipMemsetAsync(d_rec, 0, np * sizeof(PairRec), st));
     int64_t bcells = 0;
@@ -1510,6 +1604,9 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
       }
       EXP_SYNC("totals");
     }
+    // the previous batch: its host part while this batch's sweeps run, its
+    // compaction before this batch's merge overwrites the ELL rows
+    if (defer && (rc = finish(B))) return rc;
     if (side && side->join_mode != 0) HIPCHK(c, hipStreamWaitEvent(st, side->join, 0));  // deferred join
     {
       Timer t(c, KMERGE, bcells, st);
@@ -1523,18 +1620,36 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
     B.np = np;
     B.bcells = bcells;
     B.order = P.order;
-    B.rec.assign(np, PairRec());
+    // the records come back into pinned memory: a pageable copy would hold
+    // the host until the merge has run, and the next batch's planning and
+    // launches with it (the buffer's last batch was finished before this one)
+    if (c->h_rec_n[par] < (size_t)np) {
+      if (c->h_rec[par]) hipHostFree(c->h_rec[par]);
+      c->h_rec[par] = nullptr;
+      c->h_rec_n[par] = 0;
+      const size_t n = (size_t)np + (size_t)np / 8 + 64;
+      HIPCHK(c, hipHostMalloc((void**)&c->h_rec[par], n * sizeof(PairRec), hipHostMallocDefault));
+      c->h_rec_n[par] = n;
+    }
+    B.rec = c->h_rec[par];
+    B.par = par;
     B.base = base;
     B.o_entb = o_entb;
     B.o_rpb = o_rpb;
     B.pm = pm;
     B.sc = sc;
     B.d_rec = d_rec;
-    HIPCHK(c, hipMemcpyAsync(B.rec.data(), d_rec, np * sizeof(PairRec), hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipMemcpyAsync(c->h_rec[par], d_rec, np * sizeof(PairRec), hipMemcpyDeviceToHost, st));
+    B.done = nullptr;
+    if (defer) {
+      B.done = pool_event(c);
+      HIPCHK(c, hipEventRecord(B.done, st));
+    }
     // the other slot's batch (launched before this one) compacts now, in pair
     // order, while this batch's sweeps run
     if ((rc = finish(pend[slot ^ 1]))) return rc;
     if (two) slot ^= 1;
+    par ^= 1;
     p = q;
   }
   int rc;

@@ -417,7 +417,7 @@ __global__ __launch_bounds__(256) void k_local_list(SeqSet sq, PairMeta pm, Chai
         }
       }
       for (int k = done; k < cnt; ++k) mine[k] = lbuf[(k % kLbufSlots) * 64 + lane];
-      if (row_in) sc.ell_cnt[ell + i - 1] = cnt;
+      if (row_in) sc.lf_cnt[ell + i - 1] = cnt;
     }
   }
 }
@@ -446,11 +446,11 @@ __global__ __launch_bounds__(256) void k_local_fold(SeqSet sq, PairMeta pm, Chai
   const int64_t ell = pm.ell_row[p];
   float acc = LZ;
   bool bad = false;
-  int n = sc.ell_cnt[ell];
+  int n = sc.lf_cnt[ell];
   float rb = sc.crb[ell];
   const float4* __restrict__ rows4 = reinterpret_cast<const float4*>(lanefold_rows(sc, cm.cell_off[h], pm.row0[p], cm.width[h]));
   const int RS4 = lanefold_rs(L2) >> 2;
-  int n1 = sc.ell_cnt[ell + min(1, L1 - 1)];
+  int n1 = sc.lf_cnt[ell + min(1, L1 - 1)];
   float4 a0 = rows4[0], a1 = rows4[1], b0 = rows4[2], b1 = rows4[3];
   auto fold4 = [&](const float4 v, int k) {
     acc = mlp_log_add_t(acc, k < n ? v.x : LZ, lk);
@@ -461,7 +461,7 @@ __global__ __launch_bounds__(256) void k_local_fold(SeqSet sq, PairMeta pm, Chai
   for (int i = 1; i <= L1; ++i) {
     const float4* __restrict__ src = rows4 + (int64_t)(i - 1) * RS4;
     const float4* __restrict__ nxt = src + RS4;
-    const int n2 = sc.ell_cnt[ell + min(i + 1, L1 - 1)];  // (past the last row: unused)
+    const int n2 = sc.lf_cnt[ell + min(i + 1, L1 - 1)];  // (past the last row: unused)
     const float rb_next = sc.crb[ell + min(i, L1 - 1)];
     const float4 na0 = nxt[0], na1 = nxt[1], nb0 = nxt[2], nb1 = nxt[3];
     bad |= rb > acc;  // the listing's bound must not exceed the chain at the row's start
