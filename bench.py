@@ -553,6 +553,18 @@ def _e2e_record(runs):
     return rec, r
 
 
+def _posterior_stage(rec, fam):
+    """The drop-in's own posterior stage (its 16 GB scratch, a fresh process)
+    beside the library headline: pair-cells per second at the median run."""
+    lens = np.array([len(x) for _, x in fam], np.int64)
+    cells = int(((lens + 1).sum() ** 2 - ((lens + 1) ** 2).sum()) // 2)
+    post = sorted(x['stages_s'].get('posteriors', 0.0) for x in rec['runs'])
+    if post and post[len(post) // 2] > 0:
+        rec['posterior_stage'] = {'pair_cells': cells, 'median_s': post[len(post) // 2],
+                                  'pair_cells_per_s': cells / post[len(post) // 2],
+                                  'runs_s': [x['stages_s'].get('posteriors') for x in rec['runs']]}
+
+
 def e2e_families(args):
     """End-to-end seconds per family of the c_p_np_aln drop-in (-p 0: family
     test, posteriors, guide tree, 2 consistency rounds, progressive alignment,
@@ -576,8 +588,6 @@ def e2e_families(args):
                 fa = os.path.join(td, 'fam.fa')
                 fam = synth.family(n, L, args.s, seed=args.seed)
                 synth.write_fasta(fa, fam)
-                lens = np.array([len(x) for _, x in fam], np.int64)
-                fam_cells = int(((lens + 1).sum() ** 2 - ((lens + 1) ** 2).sum()) // 2)
                 runs = []
                 # -p 1 seeds its refinement with time(0): the golden run's fixed clock
                 env = dict(os.environ, MLP_CLI_TIMES='1', **({'MLP_SRAND_TIME': '1700000000'} if mode == '1' else {}))
@@ -586,13 +596,7 @@ def e2e_families(args):
                     r = subprocess.run([cli, '-p', mode, fa], capture_output=True, text=True, timeout=600, env=env)
                     runs.append((time.perf_counter() - t0, r))
             rec, r = _e2e_record(runs)
-            # the drop-in's own posterior stage (its 16 GB scratch, a fresh
-            # process) beside the library headline: pair-cells per second
-            post = sorted(x['stages_s'].get('posteriors', 0.0) for x in rec['runs'])
-            if post and post[len(post) // 2] > 0:
-                rec['posterior_stage'] = {'pair_cells': fam_cells, 'median_s': post[len(post) // 2],
-                                          'pair_cells_per_s': fam_cells / post[len(post) // 2],
-                                          'runs_s': [x['stages_s'].get('posteriors') for x in rec['runs']]}
+            _posterior_stage(rec, fam)
             log(f'e2e {tag} -p {mode}: ' + ', '.join(f'{x[0]:.2f}' for x in runs) + f' s (exit {r.returncode})')
             g = os.path.join(ROOT, 'tests', 'golden', 'config', f'{gold}.p_{mode}.out')
             if os.path.exists(g) and args.s == 0.7:
@@ -614,7 +618,8 @@ def e2e_families(args):
         for tag, n, L in (('quickprobs C2 128x256', 128, 256), (f'quickprobs C3 {args.n}x{args.len}', args.n, args.len)):
             with tempfile.TemporaryDirectory() as td:
                 fa = os.path.join(td, 'fam.fa')
-                synth.write_fasta(fa, synth.family(n, L, args.s, seed=args.seed))
+                fam = synth.family(n, L, args.s, seed=args.seed)
+                synth.write_fasta(fa, fam)
                 runs = []
                 for _ in range(args.e2e_runs):
                     t0 = time.perf_counter()
@@ -622,6 +627,7 @@ def e2e_families(args):
                                        env=dict(os.environ, MLP_CLI_TIMES='1'))
                     runs.append((time.perf_counter() - t0, r))
                 res[tag], r = _e2e_record(runs)
+                _posterior_stage(res[tag], fam)
                 log(f'e2e {tag}: ' + ', '.join(f'{x[0]:.2f}' for x in runs) + f' s (exit {r.returncode})')
                 g = os.path.join(ROOT, 'tests', 'golden', 'config', f'c{2 if n == 128 else 3}_{n}x{L}_s{args.seed}.qp.out')
                 if os.path.exists(g) and args.s == 0.7:   # the reference QuickProbs CLI's output (gen_config_goldens.sh)
