@@ -12,8 +12,10 @@ and the PF posterior in the Zm slots (small scratch budget) as well.  The
 one-wave totals run after both sweeps (MLP_TOT_BESIDE=0, the reference run
 here) or with their forward chains on a second stream beside the backward
 sweeps (=1, and =2 the default: the partition function joined before the
-merge only).  Each setting runs in a child process: the switches are read
-once per process."""
+merge only).  Several batches also run with the next batch launched before
+the last one is finished (the default) and finished first
+(MLP_DEFER_FINISH=0).  Each setting runs in a child process: the switches
+are read once per process."""
 import os
 import subprocess
 import sys
@@ -47,9 +49,9 @@ print(' '.join(out))
 '''
 
 
-def _run(lanefold, scratch=None, foldbound=1, repair=False, beside=2):
+def _run(lanefold, scratch=None, foldbound=1, repair=False, beside=2, defer=1):
     env = dict(os.environ, MLP_TOT_LANEFOLD=str(lanefold), MLP_TOT_FOLDBOUND=str(foldbound),
-               MLP_TOT_BESIDE=str(beside))
+               MLP_TOT_BESIDE=str(beside), MLP_DEFER_FINISH=str(defer))
     env.pop('MLP_TOT_FORCE_REPAIR', None)
     if repair:
         env['MLP_TOT_FORCE_REPAIR'] = '1'
@@ -71,8 +73,10 @@ def test_totals_bit_identical():
 def test_totals_bit_identical_small_scratch():
     # 1 GB: several batches, the PF posterior in the low halves of the Zm
     # slots (the lane fold's candidates in the local backward array either way)
-    ref = _run(0, 1 << 30, foldbound=0, beside=0)
+    ref = _run(0, 1 << 30, foldbound=0, beside=0, defer=0)
+    assert _run(0, 1 << 30, foldbound=0, beside=0) == ref
     assert _run(0, 1 << 30, foldbound=0) == ref
+    assert _run(1, 1 << 30, defer=0) == ref
     assert _run(0, 1 << 30, beside=1) == ref
     assert _run(0, 1 << 30) == ref
     assert _run(1, 1 << 30) == ref
