@@ -8,8 +8,10 @@
 #include <stdint.h>
 
 #include <functional>
+#include <memory>
 #include <set>
 #include <string>
+#include <utility>
 #include <vector>
 
 namespace cpnp {
@@ -34,13 +36,34 @@ bool load_fasta(const std::string& path, std::vector<Row>& out, std::string& err
 // MultiSequence::WriteMFA, 60 columns (Sequence.h:281-303).
 void write_mfa(std::string& out, const Profile& p, int columns = 60);
 
+// std::allocator whose resize leaves the elements uninitialised: buffers
+// that a copy fills right after (C3's row pointers are 210 MB)
+template <class T>
+struct NoInitAlloc : std::allocator<T> {
+  template <class U>
+  struct rebind {
+    using other = NoInitAlloc<U>;
+  };
+  NoInitAlloc() = default;
+  template <class U>
+  NoInitAlloc(const NoInitAlloc<U>&) {}
+  template <class U>
+  void construct(U* p) noexcept {
+    ::new ((void*)p) U;
+  }
+  template <class U, class... A>
+  void construct(U* p, A&&... a) {
+    ::new ((void*)p) U(std::forward<A>(a)...);
+  }
+};
+
 // Canonical sparse set of libmlpgpu (include/mlpgpu.h): pair (a < b) has
 // row_ptr[rp_off[p] .. + L_a + 2) and entries from ent_off[p].
 struct SparseSet {
   int n = 0;
   std::vector<int> lens;
   std::vector<int64_t> rp_off, ent_off;
-  std::vector<int32_t> row_ptr;
+  std::vector<int32_t, NoInitAlloc<int32_t>> row_ptr;  // (filled by mlp_csr_export)
   std::vector<uint16_t> cols;
   std::vector<float> vals;
   int64_t pair(int a, int b) const {  // a < b, row-major (CPNP/MSA.cpp:907-919)
