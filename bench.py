@@ -41,6 +41,15 @@ VALU_PEAK_WAVE_INSTS = 256 * 4 * 2.4e9 / 2
 # stream local f (4); the merge reads f5, local f, local b, PF posterior (16).
 ALGO_BYTES = {'forward': 16, 'backward': 24, 'local_totals': 4, 'merge_mea_sparsify': 16}
 STAGE_BYTES = 56  # pid 0/1 algorithmic bytes per pair-cell
+# mlprobs --trace stages in pipeline order (tools/c5_attribution.py) and the
+# committed per-family cause of every C5 family whose output differs from the
+# reference CLIs' multi-threaded runs
+C5_STAGES = ('features_line', 'class1', 'col_score', 'regions', 'realigned', 'output')
+C5_ATTRIBUTION = 'r05_c5_attribution_recheck.json'
+# the printed line stays far below what the driver parses (round 5's 20 KB
+# line was not parsed); the full record goes to DETAIL_PATH
+LINE_LIMIT = 8000
+DETAIL_PATH = os.environ.get('MLP_BENCH_DETAIL', os.path.join(ROOT, 'gpurun_out', 'bench_detail.json'))
 
 
 def parse():
@@ -376,7 +385,7 @@ def relax_leg(fam, args, n, lens, total_cells):
                        'kernels_ms': {k: v['ms'] for k, v in kt.items() if v['launches']}})
         if it == 0:
             hash1 = store_hash(fam)
-            k_ms = kt['relax']['ms']
+            k_ms = kt['relax']['ms'] or dt * 1e3  # host contexts (--host) time no kernels
             k_launch = max(kt['relax']['launches'], 1)
             if not args.no_cpu:
                 store1 = [a.copy() for a in fam.export()]
@@ -755,8 +764,13 @@ def c5_pipeline(args):
         # every 8th family below 5e7 pair-cells: the reference CLIs take 100-110 s on each of the five
         # families above it (profiles/r04i_c5_full.json holds the run over every family)
         ref_names = {k for k in names[::8] if fams[k]['cells'] < 5e7}
+    attribution = {}
+    att_path = os.path.join(ROOT, 'profiles', C5_ATTRIBUTION)
+    if os.path.exists(att_path):
+        with open(att_path) as fh:
+            attribution = {r['family']: r['cause'] for r in json.load(fh)['rows'] if r.get('cause')}
     last_log = time.perf_counter()
-    recs, calls, paths, fails, same = [], 0, {}, 0, 0
+    recs, calls, paths, fails, same, differ = [], 0, {}, 0, 0, []
     sp_o, sp_r, sp_p, tc_o, tc_r = [], [], [], [], []
     env_ref = dict(os.environ, OMP_NUM_THREADS=str(args.cpu_threads), OMP_WAIT_POLICY='passive')
     t_start = time.perf_counter()
@@ -790,14 +804,23 @@ def c5_pipeline(args):
                 tc_o.append(tc_score(mine, pub[name]))
             if with_ref and name in ref_names:
                 log(f'c5 {name}: ours {rec["s"]:.2f} s, reference CLIs ...') if e['cells'] > 2e7 else None
-                out2 = os.path.join(td, 'r.msa')
+                out2, trace2 = os.path.join(td, 'r.msa'), os.path.join(td, 'rt.json')
                 t0 = time.perf_counter()
-                subprocess.run([bin_, '-q', '--cpnp', ref_cp, '--quickprobs', f'{ref_qp} -t {args.cpu_threads}',
-                                '--tmp', td, fa, out2], capture_output=True, timeout=1800, env=env_ref)
+                subprocess.run([bin_, '-q', '--trace', trace2, '--cpnp', ref_cp, '--quickprobs',
+                                f'{ref_qp} -t {args.cpu_threads}', '--tmp', td, fa, out2],
+                               capture_output=True, timeout=1800, env=env_ref)
                 rec['ref_s'] = time.perf_counter() - t0
                 with open(out2, encoding='latin-1') as fh:
                     refo = fh.read()
                 same += refo == mine
+                if refo != mine:
+                    # where the two runs part (mlprobs --trace stages) and the
+                    # cause committed for this family by tools/c5_attribution.py
+                    with open(trace2) as fh:
+                        tr2 = json.load(fh)
+                    stage = next((s for s in C5_STAGES[:-1] if tr.get(s) != tr2.get(s)), 'output')
+                    differ.append({'name': name, 'path': tr['path'], 'first_stage': stage,
+                                   'cause': attribution.get(name, 'unattributed')})
                 sp_r.append(sp_score(refo))
                 if name in pub:
                     tc_r.append(tc_score(refo, pub[name]))
@@ -846,6 +869,7 @@ def c5_pipeline(args):
         res['speedup_mean'] = res['all'].get('speedup_mean')
         res['speedup_median'] = res['all'].get('speedup_median')
         res['identical_to_reference_clis'] = same
+        res['differing'] = differ
         res['reference_clis_families'] = len(sp_r)
         res['reference_clis_sp_un_sp_mean'] = mean(sp_r)
         res['reference_clis_tc_vs_published_mean'] = mean(tc_r)
@@ -892,6 +916,144 @@ def quickprobs_stage(fam, fam_in, total_cells, args):
     return res
 
 
+def _r(x, sig=4):
+    """Floats to `sig` significant digits, recursively (the printed line)."""
+    if isinstance(x, float):
+        return float(f'{x:.{sig}g}')
+    if isinstance(x, dict):
+        return {k: _r(v, sig) for k, v in x.items()}
+    if isinstance(x, (list, tuple)):
+        return [_r(v, sig) for v in x]
+    return x
+
+
+def _pick(d, *keys):
+    return {k: d[k] for k in keys if d is not None and k in d}
+
+
+def compact_e2e(e2e):
+    """Per end-to-end leg: median / max / every run's wall seconds, the median
+    run's stage split, the drop-in's posterior stage and the output check."""
+    out = {}
+    for tag, rec in e2e.items():
+        c = _pick(rec, 'median_s', 'max_s', 'runs_s', 'exit')
+        c['stages_s'] = {k: v for k, v in rec.get('stages_s', {}).items() if v >= 0.005}
+        if rec.get('outliers'):
+            c['outliers'] = [_pick(o, 'run', 's', 'stage') for o in rec['outliers']]
+        if 'posterior_stage' in rec:
+            c['posterior_stage'] = _pick(rec['posterior_stage'], 'median_s', 'pair_cells_per_s')
+        if 'reference_output' in rec:
+            c['reference_output'] = _pick(rec['reference_output'], 'identical', 'tc_vs_reference')
+        if 'reference_cpu' in rec:
+            c['reference_cpu'] = _pick(rec['reference_cpu'], 'seconds', 'threads', 'identical_output')
+        out[tag] = c
+    return out
+
+
+def compact_c5(c5):
+    c = _pick(c5, 'families', 'failed', 'device_path_families', 'host_path_families', 'quickprobs_region_calls',
+              'paths', 'speedup_mean', 'speedup_median', 'identical_to_reference_clis', 'reference_clis_families',
+              'sp_un_sp_mean', 'published_sp_un_sp_mean', 'tc_vs_published_mean',
+              'reference_clis_tc_vs_published_mean', 'wall_s', 'devices', 'scaling')
+    for k in ('all', 'device_path', 'host_path'):
+        if k in c5:
+            s = dict(c5[k].get('s_per_family', {}))
+            r = c5[k].get('reference_clis_s_per_family')
+            if r:
+                s['reference_clis_mean'] = r['mean']
+                s['ours_mean_on_reference_families'] = r['ours_on_these']['mean']
+            c[k] = s
+    if 'differing' in c5:
+        d = c5['differing']
+        causes = {}
+        for x in d:
+            causes[x['cause']] = causes.get(x['cause'], 0) + 1
+        c['differing'] = {'n': len(d), 'causes': causes,
+                          'first_stage': {s: sum(x['first_stage'] == s for x in d) for s in C5_STAGES
+                                          if any(x['first_stage'] == s for x in d)},
+                          'unattributed': [x['name'] for x in d if x['cause'] == 'unattributed'][:12]}
+    return c
+
+
+def compact_relax(rx):
+    c = _pick(rx, 'rounds', 'seconds', 'nnz_per_round', 'speedup_vs_cpu')
+    c['per_round'] = [{'s': r['seconds'], 'relax_ms': r.get('kernels_ms', {}).get('relax'),
+                       'nnz_out': r['nnz_out']} if 'ranks' not in r else
+                      {'s': r['seconds'], 'gather_ms': r['gather_ms'], 'nnz_out': r['nnz_out'],
+                       'ranks': [{'rank': q['rank'], 's': q['seconds'], 'relax_ms': q['relax_kernel_ms'],
+                                  'gather_ms': q['gather_ms'], 'store_hash': q['store_hash'][:16]}
+                                 for q in r['ranks']]}
+                      for r in rx.get('per_round', [])]
+    if 'round1' in rx:
+        c['round1'] = _pick(rx['round1'], 'kernel_ms', 'macs_reference', 'mac_per_s')
+    if 'roofline' in rx:
+        c['roofline'] = _pick(rx['roofline'], 'bound', 'kernel', 'achieved', 'peak', 'unit', 'frac', 'traffic',
+                              'avg_launch_ms', 'frac_of_measured')
+    if 'cpu_baseline' in rx:
+        c['cpu_baseline'] = rx['cpu_baseline']
+    if 'parity' in rx:
+        c['parity'] = _pick(rx['parity'], 'pairs', 'max_rel_err', 'violations', 'bit_exact')
+    return c
+
+
+def compact_line(out):
+    """The one JSON line the driver parses: the headline keys, config,
+    roofline, cpu_baseline, parity and summaries of every leg; the per-run
+    and per-family detail stays in the side file (DETAIL_PATH).  Sections
+    are dropped, least important first, if the line would pass LINE_LIMIT."""
+    line = {k: v for k, v in out.items() if k not in ('e2e', 'c5_pipeline', 'relax', 'ranks', 'hbm_stream',
+                                                       'virtual_shards', 'parity')}
+    if out.get('parity'):
+        line['parity'] = _pick(out['parity'], 'pairs', 'max_rel_err', 'violations', 'inexact',
+                               'symmetric_difference', 'distance_max_rel_err', 'bit_exact')
+    if out.get('hbm_stream') and 'peak_GBps' in out['hbm_stream']:
+        line['hbm_stream'] = _pick(out['hbm_stream'], 'read_gbps', 'write_gbps', 'copy_gbps')
+    if out.get('relax'):
+        line['relax'] = compact_relax(out['relax'])
+    if out.get('virtual_shards'):
+        line['virtual_shards'] = {k: v for k, v in out['virtual_shards'].items() if k not in ('note', 'store_bytes')}
+    if out.get('ranks'):
+        line['ranks'] = [{'rank': r['rank'], 'pairs': r['pairs'], 'step_ms': r['step_ms'],
+                          'gather_ms': r['gather_ms'], 'gather_GBps': r['gather_GBps'],
+                          'gather_bytes_in': r['gather_bytes_in'],
+                          'roofline_frac': (r.get('roofline') or {}).get('frac'),
+                          'store_hash': r['store_hash'][:16]} for r in out['ranks']]
+    if out.get('c5_pipeline'):
+        line['c5_pipeline'] = compact_c5(out['c5_pipeline'])
+    if out.get('e2e'):
+        line['e2e'] = compact_e2e(out['e2e'])
+    line['detail'] = os.path.relpath(DETAIL_PATH, ROOT) if DETAIL_PATH.startswith(ROOT) else DETAIL_PATH
+    line = dict(_r(line), value=out['value'], ms_per_step=out['ms_per_step'])
+    for drop in ('hbm_stream', 'e2e', 'c5_pipeline', 'virtual_shards', 'quickprobs', 'ranks'):
+        if len(json.dumps(line)) <= LINE_LIMIT:
+            break
+        log(f'bench line over {LINE_LIMIT} bytes: {drop} left to {line["detail"]}')
+        line.pop(drop, None)
+    return line
+
+
+def emit(out):
+    """Full record to the side file, its summaries to stderr, the compact line
+    to stdout."""
+    os.makedirs(os.path.dirname(DETAIL_PATH), exist_ok=True)
+    with open(DETAIL_PATH, 'w') as fh:
+        json.dump(out, fh)
+    for tag, rec in (out.get('e2e') or {}).items():
+        log(f'e2e {tag}: runs ' + ', '.join(f"{x['s']:.2f}" for x in rec.get('runs', [])) + ' s; median stages ' +
+            ', '.join(f'{k} {v:.3f}' for k, v in rec.get('stages_s', {}).items() if v >= 0.01))
+    c5 = out.get('c5_pipeline')
+    if c5:
+        for x in c5.get('slowest', []):
+            log(f"c5 slow: {x['name']} {x['s']:.2f} s ({x['cells']:.3g} pair-cells)")
+        for x in c5.get('differing', []):
+            log(f"c5 differs from the reference CLIs: {x['name']} ({x['path']}): first at {x['first_stage']}, "
+                f"cause {x['cause']}")
+    line = compact_line(out)
+    s = json.dumps(line)
+    log(f'bench line {len(s)} bytes; full record {DETAIL_PATH}')
+    print(s, flush=True)
+
+
 def main():
     args = parse()
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -913,7 +1075,11 @@ def main():
     # follows a large release waits for the driver to clear that memory)
     log('start')
     if args.only_c5:
-        print(json.dumps({'c5_pipeline': c5_pipeline(args)}))
+        c5 = c5_pipeline(args)
+        print(json.dumps({'c5_pipeline': _r(compact_c5(c5))}))
+        os.makedirs(os.path.dirname(DETAIL_PATH), exist_ok=True)
+        with open(DETAIL_PATH, 'w') as fh:
+            json.dump({'c5_pipeline': c5}, fh)
         return
     stream = hbm_stream() if (world == 1 and not args.host) else None
     e2e = e2e_families(args) if (not args.no_e2e and world == 1) else None
@@ -1092,7 +1258,7 @@ def main():
                 out['relax'] = relax_multi
             if args.host:
                 out['data'] = 'synthetic (host contexts over gloo: CPU dry run, not a GPU measurement)'
-        print(json.dumps(out))
+        emit(out)
     if fam is not None:
         fam.close()
     if world > 1:

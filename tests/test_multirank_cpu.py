@@ -298,7 +298,9 @@ def test_bench_two_ranks_dry_run():
            '--no-shards', '--relax', '2']
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd='/tmp')
     assert r.returncode == 0, r.stderr[-3000:]
-    d = json.loads(r.stdout.strip().splitlines()[-1])
+    last = r.stdout.strip().splitlines()[-1]
+    assert len(last) < 10000
+    d = json.loads(last)
     assert d['n_gpus'] == 2 and len(d['ranks']) == 2
     assert d['gather_ms'] > 0 and d['gather_GBps'] > 0
     assert all(x['gather_bytes_in'] > 0 and x['pairs'] > 0 for x in d['ranks'])
@@ -316,9 +318,10 @@ def test_bench_two_ranks_dry_run():
     f = Family(seqs, host=True)
     try:
         f.posteriors(0, DELTA)
-        assert d['ranks'][0]['store_hash'] == hsh(f)
+        # the line carries each hash's first 16 hex digits
+        assert d['ranks'][0]['store_hash'] == hsh(f)[:16]
         for rr in d['relax']['per_round']:
             f.relax(1)
-            assert rr['ranks'][0]['store_hash'] == hsh(f)
+            assert rr['ranks'][0]['store_hash'] == hsh(f)[:16]
     finally:
         f.close()
