@@ -222,7 +222,9 @@ int mlp_profile_gather(mlp_ctx *ctx, int64_t n, const int64_t *cells, float *val
  * column 0 unused) made the context's device-resident matrix, as if a
  * deferred mlp_profile_posterior* had computed it: for callers that build
  * the profile posterior elsewhere, and for testing mlp_profile_mea on any
- * matrix.  MLP_ERR_STATE on a host context. */
+ * matrix.  Every entry must be finite and >= +0 (a posterior's range; the
+ * device MEA's hand-off and choices rely on it): MLP_ERR_ARG otherwise.
+ * MLP_ERR_STATE on a host context. */
 int mlp_profile_set(mlp_ctx *ctx, int L1, int L2, const float *post);
 
 /* Evaluation only (not a drop-in path): the consistency transform of the
@@ -256,7 +258,7 @@ int mlp_relax_shard_plan(int n, const int32_t *lens, const int64_t *pair_nnz, in
  * its output range): all-gather the CSR store and the per-pair scalars so
  * every rank holds the whole family (RCCL grouped broadcasts of each rank's
  * block into its global place).  Without a communicator, or at one rank, a
- * no-op; MLP_ALLGATHER_FORCE=1 runs the grouped body at one rank too (the
+ * no-op; MLP_TEST_ALLGATHER_FORCE=1 runs the grouped body at one rank too (the
  * test hook that exercises it on a one-GPU box). */
 int mlp_allgather(mlp_ctx *ctx);
 /* One C_P_NP_Aln consistency round (as mlp_relax, CPNP/MSA.cpp:1172-1360)
@@ -271,7 +273,10 @@ int mlp_relax_range(mlp_ctx *ctx, int64_t r0, int64_t r1);
 int mlp_synchronize(mlp_ctx *ctx);
 
 /* Per-kernel device time accumulated since the last reset (HIP events on
- * the context stream), enabled by mlp_profile(ctx, 1).  Kernel ids:
+ * the context stream), enabled by mlp_profile(ctx, 1).  One launch per
+ * group and posterior batch; a group whose kernels run in parts (the local
+ * totals: the forward chains beside the backward sweeps, the backward chains
+ * after them) sums its parts' device time into that launch.  Kernel ids:
  * 0 forward, 1 backward, 2 local totals, 3 merge/MEA/sparsify, 4 compact,
  * 5 relax, 6 transpose, 7 filter, 8 allgather, 9 viterbi. */
 #define MLP_NKERNELS 10

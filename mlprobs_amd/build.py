@@ -15,11 +15,11 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, 'csrc')
 LIBDIR = os.path.join(HERE, 'lib')
 LIB = os.path.join(LIBDIR, 'libmlpgpu.so')
-SOURCES = ['posterior.hip', 'totals.hip', 'viterbi.hip', 'relax.hip', 'relax_mfma.hip', 'profile.hip',
+SOURCES = ['posterior.hip', 'totals.hip', 'viterbi.hip', 'relax.hip', 'relax_mfma.hip', 'profile.hip', 'mlp_knobs.cpp',
            'mlp_context.cpp', 'mlp_planner.cpp', 'mlp_posteriors.cpp', 'mlp_profile_rt.cpp', 'mlp_shards.cpp',
            'mlp_relax_rt.cpp', 'host_backend.cpp']
 HEADERS = ['mlp_kernels.h', 'mlp_numerics.h', 'mlp_chain.h', 'mlp_params_default.inc', 'mlp_params_qp.inc',
-           'host_backend.h', 'mlp_runtime.h']
+           'host_backend.h', 'mlp_runtime.h', 'mlp_knobs.h']
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 # -fno-slp-vectorize: the SLP pass packs adjacent f32 adds/multiplies of the
 # DP cell updates into v_pk_*_f32 and pays for it in register moves; without

@@ -305,47 +305,6 @@ int run_cpnp(std::vector<Row> seqs, bool just_features, bool progressive, cpnp::
         check(ctx, mrc, "MEA", 1);
         path.resize(np);
         check(ctx, mlp_profile_defer(ctx, 0), "profile posterior", 1);
-        if (getenv("MLP_MEA_CHECK")) {   // diagnosis: the same posterior's host MEA beside the device's
-          const int64_t ncell = (int64_t)(L1 + 1) * (L2 + 1);
-          std::vector<int64_t> all(ncell);
-          for (int64_t k = 0; k < ncell; k++) all[k] = k;
-          std::vector<float> dpost(ncell);   // the deferred posterior the device MEA read
-          check(ctx, mlp_profile_gather(ctx, ncell, all.data(), dpost.data()), "gather", 1);
-          check(ctx, mlp_profile_posterior_cpnp(ctx, w, (int)a.size(), lab1.data(), L1, map1.data(), (int)b.size(),
-                                                lab2.data(), L2, map2.data(), nullptr),
-                "profile posterior", 1);
-          const float* hpost = mlp_profile_result(ctx);
-          const bool post_same = !memcmp(hpost, dpost.data(), ncell * 4);
-          float hs = 0;
-          const std::string hp = cpnp::mea_path(L1, L2, hpost, &hs);
-          size_t k = 0;
-          while (k < hp.size() && k < path.size() && hp[k] == path[k]) k++;
-          static int nbad = 0, ncall = 0;
-          ncall++;
-          if (hp != path || hs != *score) {
-            std::string again;
-            for (int rep = 0; rep < 3; rep++) {   // the device MEA again on the same (recomputed) matrix
-              std::string p2(L1 + L2, ' ');
-              int32_t n2 = 0;
-              float s2 = 0;
-              const int rc2 = mlp_profile_mea(ctx, &p2[0], &n2, &s2);
-              p2.resize(n2);
-              again += rc2 ? " rc" + std::to_string(rc2) : p2 == hp && s2 == hs ? " =host" : p2 == path ? " =first" : " other";
-            }
-            fprintf(stderr, "[meacheck] call %d: %d x %d (%zu x %zu rows) posterior %s, path %s at %zu of %zu/%zu, score %a dev %a; again:%s\n",
-                    ncall, L1, L2, a.size(), b.size(), post_same ? "same" : "DIFFERS", hp == path ? "same" : "DIFFERS", k,
-                    hp.size(), path.size(), hs, *score, again.c_str());
-            if (const char* d = getenv("MLP_MEA_DUMP"); d && ncell * 4 < (16 << 20) && nbad++ < 2) {
-              const std::string f = std::string(d) + "/mea_" + std::to_string(nbad) + ".bin";
-              if (FILE* fh = fopen(f.c_str(), "wb")) {
-                const int32_t dims[2] = {L1, L2};
-                fwrite(dims, 4, 2, fh);
-                fwrite(hpost, 4, ncell, fh);
-                fclose(fh);
-              }
-            }
-          }
-        }
         return true;
       });
       struct Unset {  // the backends capture this frame: clear them on every exit

@@ -12,6 +12,7 @@
 // All of it is plain host C++ (no HIP call), compiled without FMA
 // contraction like the reference's scalar SSE build.
 #include "host_backend.h"
+#include "mlp_knobs.h"
 
 #include <math.h>
 
@@ -452,8 +453,7 @@ inline float fixed16(float v) { return (float)(uint32_t)(uint16_t)(v * 65535.0f)
 
 int threads_for(int64_t units) {
   static const int hw = [] {
-    const char* e = getenv("MLP_HOST_THREADS");
-    int t = e ? atoi(e) : (int)std::thread::hardware_concurrency();
+    const int t = (int)mlp::knob("MLP_HOST_THREADS", (double)std::thread::hardware_concurrency());
     return std::max(1, std::min(t, 16));
   }();
   return (int)std::max<int64_t>(1, std::min<int64_t>(hw, units));

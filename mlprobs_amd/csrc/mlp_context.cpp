@@ -72,8 +72,10 @@ void flush_timers(mlp_ctx* c) {
       hipEventElapsedTime(&ms, r.e0, r.e1);
     }
     c->kms[r.id] += ms;
-    c->klaunch[r.id] += 1;
-    c->kcells[r.id] += r.cells;
+    if (!r.cont) {
+      c->klaunch[r.id] += 1;
+      c->kcells[r.id] += r.cells;
+    }
   }
   c->tpend.clear();
   c->evused = 0;
@@ -196,7 +198,11 @@ int mlp_ctx_create(int device, mlp_ctx** out) {
   }
   if (hipStreamCreateWithFlags(&c->side.st, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->side.fork, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->side.join, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&c->side.join, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_done[0], hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_done[1], hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_tot, hipEventDisableTiming) != hipSuccess) {
     delete c;
     return MLP_ERR_HIP;
   }
@@ -223,7 +229,7 @@ int mlp_ctx_create(int device, mlp_ctx** out) {
     const size_t reserve = std::max<size_t>(16ull << 30, total / 100 * 7);
     c->scratch_budget = usable > 2 * reserve ? usable - reserve : usable / 2;
   }
-  if (const char* s = getenv("MLP_SCRATCH_GB")) c->scratch_budget = (size_t)(atof(s) * (1ull << 30));
+  if (knob_set("MLP_SCRATCH_GB")) c->scratch_budget = (size_t)(knob("MLP_SCRATCH_GB", 0) * (1ull << 30));
   *out = c;
   return MLP_OK;
 }
@@ -274,7 +280,7 @@ void mlp_ctx_destroy(mlp_ctx* c) {
                   c->d_rowptr, c->d_ent_off, c->d_cols, c->d_vals};
   for (void* p : ptrs)
     if (p) hipFree(p);
-  DevBuf* bufs[] = {&c->scratch, &c->scratch2, &c->r_trowptr, &c->r_tcols, &c->r_tvals, &c->r_raw, &c->r_newrp,
+  DevBuf* bufs[] = {&c->scratch, &c->r_trowptr, &c->r_tcols, &c->r_tvals, &c->r_raw, &c->r_newrp,
                     &c->r_newcols, &c->r_newvals, &c->r_tasks_p, &c->r_tasks_r, &c->r_pairs,
                     &c->r_nnz, &c->r_newoff, &c->r_img, &c->r_imgoff, &c->r_tiles, &c->r_nwords, &c->r_weights,
                     &c->r_seldist, &c->r_profile, &c->r_mea, &c->ag_cols, &c->ag_vals};
@@ -282,7 +288,7 @@ void mlp_ctx_destroy(mlp_ctx* c) {
     if (b->p && !b->lent) hipFree(b->p);
   if (c->comm) ncclCommDestroy(c->comm);
   for (hipEvent_t e : c->evpool) hipEventDestroy(e);
-  if (getenv("MLP_PROFILE_TIMES") && (c->prof_t[0] > 0 || c->prof_t[1] > 0))
+  if (knob_set("MLP_LOG_PROFILE") && (c->prof_t[0] > 0 || c->prof_t[1] > 0))
     fprintf(stderr, "[profile posterior] host preparation %.3f s, device round trips %.3f s\n", c->prof_t[0],
             c->prof_t[1]);
   if (c->h_prof_in) hipHostFree(c->h_prof_in);
@@ -301,6 +307,9 @@ void mlp_ctx_destroy(mlp_ctx* c) {
     hipStreamDestroy(c->side.st);
     hipEventDestroy(c->side.fork);
     hipEventDestroy(c->side.join);
+  }
+  for (hipEvent_t e : {c->ev_done[0], c->ev_done[1], c->ev_fork, c->ev_tot}) {
+    if (e) hipEventDestroy(e);
   }
   delete c;
 }

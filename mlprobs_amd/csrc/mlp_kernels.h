@@ -6,6 +6,8 @@
 
 #include <string>
 
+#include "mlp_knobs.h"
+
 namespace mlp {
 
 constexpr int kWave = 64;        // CDNA wavefront

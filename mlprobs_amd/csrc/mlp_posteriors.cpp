@@ -66,6 +66,7 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
   HIPCHK(c, hipMemcpyAsync(c->d_tables, &c->h_tables, sizeof(Tables), hipMemcpyHostToDevice, c->stream));
   const int models = model_set_for_pid(pid);
   SeqSet seqs{c->d_res, c->d_off, c->d_len};
+  hipStream_t st = c->stream;
 
   // step-diagonal bytes per slot of the models this pid runs: f5 (5-state),
   // fl + bl (local), zm + pg (partition function)
@@ -75,9 +76,9 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
   // the price of a strided read in the merge.  C3 at the CLIs' 16 GB:
   // posteriors 0.94 s against 1.01 s; at the bench's ~140 GB the batches are
   // large anyway and the merge's extra bytes cost 17 ms a step (690 vs
-  // 679 ms; profiles/r03d_ab_tottr_pg.txt).  MLP_PG_SEPARATE=0 / 1 forces it.
-  static const char* pg_env = getenv("MLP_PG_SEPARATE");
-  const bool pg_in_zm = pg_env ? atoi(pg_env) == 0 : c->scratch_budget <= (48ull << 30);
+  // 679 ms; profiles/r03d_ab_tottr_pg.txt).  MLP_TEST_PG_SEPARATE=0 / 1 forces it.
+  const double pg_knob = knob("MLP_TEST_PG_SEPARATE", -1);
+  const bool pg_in_zm = pg_knob >= 0 ? pg_knob == 0 : c->scratch_budget <= (48ull << 30);
   const int slot_bytes =
       ((models & kHmm5) ? 4 : 0) + ((models & kLocal) ? 8 : 0) + ((models & kPF) ? (pg_in_zm ? 8 : 12) : 0);
   auto pair_bytes = [&](int64_t q) {
@@ -92,11 +93,10 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
   // at C3: 0.81 s vs 0.75 s, the smaller batches lose more to their tails
   // than the overlap wins); the host plans batch b + 1 while batch b's
   // kernels run, and finishes batch b (entry offsets from its pair records,
-  // compaction into the store) before batch b + 1 reuses the scratch.
-  const bool two = getenv("MLP_TWO") && atoi(getenv("MLP_TWO")) > 0;  // experiment hook
-  const SideStream* side = two ? nullptr : &c->side;
+  // compaction into the store) while batch b + 1's sweeps run.
+  const SideStream* side = &c->side;
   // model sets whose sweeps run as two kernels: the partition function's on the side stream
-  const bool side_used = side && (models & kPF) && models != kPF;
+  const bool side_used = (models & kPF) && models != kPF;
   // k_local_totals: persistent waves, each with 64 candidate rows as wide as
   // the family's widest chain row (<= 1 GB of lists), sized once per call so
   // every batch carves the same bytes (no reallocation between batches) and
@@ -114,53 +114,43 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
   // the HMM stream's critical path: under the CLIs' small budgets (PF
   // posterior in the Zm slots, ~38 batches at C3) the one-wave-per-pair
   // k_local_totals after both sweeps runs shorter (C3 drop-in posteriors
-  // 0.92 against 1.03 s, profiles/r05b_cli_lanefold.txt).  MLP_TOT_LANEFOLD=0
-  // / 1 forces either
-  static const char* lf_env = getenv("MLP_TOT_LANEFOLD");
-  const bool lanefold = (models & kLocal) && (lf_env ? atoi(lf_env) != 0 : !pg_in_zm);
+  // 0.92 against 1.03 s, profiles/r05b_cli_lanefold.txt).
+  // MLP_TEST_TOT_LANEFOLD=0 / 1 forces either
+  const double lf_knob = knob("MLP_TEST_TOT_LANEFOLD", -1);
+  const bool lanefold = (models & kLocal) && (lf_knob >= 0 ? lf_knob != 0 : !pg_in_zm);
   // the side stream joins before the merge (the partition function's sweeps
   // run on without a join between them: the lane fold does not wait for them)
   SideStream side_lf;
-  if (side && lanefold && side_used) {
+  if (lanefold && side_used) {
     side_lf = *side;
     side_lf.join_mode = 2;
     side = &side_lf;
   }
   // the one-wave fold's listing bound: the folded chunk maxima of the rows
-  // before (k_local_bounds) instead of their maximum (MLP_TOT_FOLDBOUND=0 / 1)
-  static const char* fb_env = getenv("MLP_TOT_FOLDBOUND");
-  const bool foldbound = (models & kLocal) && !lanefold && (fb_env ? atoi(fb_env) != 0 : true);
+  // before (k_local_bounds) instead of their maximum (MLP_TEST_TOT_FOLDBOUND=0 / 1)
+  const bool foldbound = (models & kLocal) && !lanefold && knob("MLP_TEST_TOT_FOLDBOUND", 1) != 0;
   // the one-wave fold's forward chains on stream2 beside the backward sweeps
   // (they read only what the forward sweep wrote), the backward chains after
-  // them on the context stream (MLP_TOT_BESIDE=0 / 1 / 2, 2 the default: the partition function's sweeps
-  // joined before the merge only, so the HMM backward starts right after
-  // the HMM forward).  C3 drop-in posteriors at 16 GB: 0.90 s after the
-  // sweeps, 0.83 beside, 0.82 with the late join, 0.77 with the totals
-  // kernels at wave priority 3 (profiles/r05z_cli_totals_beside.txt)
-  static const char* tb_env = getenv("MLP_TOT_BESIDE");
-  const int tb_mode = tb_env ? atoi(tb_env) : 2;
-  const bool tot_beside = (models & kLocal) && !lanefold && !two && tb_mode != 0;
-  if (side && tot_beside && side_used && tb_mode == 2) {
+  // them on the context stream (MLP_TEST_TOT_BESIDE=0 / 1 / 2, 2 the default:
+  // the partition function's sweeps joined before the merge only, so the HMM
+  // backward starts right after the HMM forward).  C3 drop-in posteriors at
+  // 16 GB: 0.90 s after the sweeps, 0.83 beside, 0.82 with the late join, 0.77
+  // with the totals kernels at wave priority 3 (profiles/r05z_cli_totals_beside.txt)
+  const int tb_mode = (int)knob("MLP_TEST_TOT_BESIDE", 2);
+  const bool tot_beside = (models & kLocal) && !lanefold && tb_mode != 0;
+  if (tot_beside && side_used && tb_mode == 2) {
     side_lf = *side;
     side_lf.join_mode = 2;
     side = &side_lf;
   }
   auto budget_for = [&](size_t b) { return std::max<size_t>(b > clist_bytes ? b - clist_bytes : 0, 32u << 20); };
-  size_t batch_target =
-      batch_target_for(c, p0, p1, pair_bytes, budget_for(two ? c->scratch_budget / 2 : c->scratch_budget));
+  size_t batch_target = batch_target_for(c, p0, p1, pair_bytes, budget_for(c->scratch_budget));
   int64_t all_cells = 0, done_cells = 0;
   for (int64_t k = p0; k < p1; k++) all_cells += pair_cost_cells(c, k);
   const int64_t base_total = c->store_total;
-  hipStream_t streams[2] = {c->stream, c->stream2};
-  DevBuf* scr[2] = {&c->scratch, &c->scratch2};
-  if (two) {  // stream2 must not run ahead of the tables upload on stream
-    hipEvent_t e = pool_event(c);
-    HIPCHK(c, hipEventRecord(e, c->stream));
-    HIPCHK(c, hipStreamWaitEvent(c->stream2, e, 0));
-  }
+  // a launched batch whose host part and compaction are still to come
   struct Pending {
     bool live = false;
-    int slot = 0;
     int64_t p = 0, q = 0, np = 0, bcells = 0;
     std::vector<int64_t> order;
     const PairRec* rec = nullptr;  // the records' host copy (pinned, c->h_rec[parity])
@@ -170,30 +160,38 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
     PairMeta pm;
     Scratch sc;
     PairRec* d_rec = nullptr;
-    hipEvent_t done = nullptr;  // after the merge and the records' copy to the host
-  };
-  Pending pend[2];
-  // Deferred finish (one slot): batch b + 1's sweeps are launched before the
-  // host finishes batch b (entry offsets, store growth, its compaction), so
-  // that host work overlaps the sweeps instead of idling the device between
+  } B;
+  // Deferred finish: batch b + 1's sweeps are launched before the host
+  // finishes batch b (entry offsets, store growth, its compaction), so that
+  // host work overlaps the sweeps instead of idling the device between
   // batches; batch b + 1's merge follows b's compaction in stream order.  What
   // b's compaction reads (plan, records, entry bases, ELL rows) lives in a
   // front region the sweeps never write: plan and records twice (batch
-  // parity), ELL rows once (written only by the merges).  MLP_DEFER_FINISH=0
-  // finishes each batch before the next is launched.
-  static const char* df_env = getenv("MLP_DEFER_FINISH");
-  const bool defer = !two && (df_env ? atoi(df_env) != 0 : true);
+  // parity), ELL rows once (written only by the merges).
+  // MLP_TEST_DEFER_FINISH=0 finishes each batch before the next is launched.
+  const bool defer = knob("MLP_TEST_DEFER_FINISH", 1) != 0;
   struct Front {
     bool set = false;
     int64_t np = 0, nch = 0, ell = 0;  // capacities
   } front;
+  // the front a batch of plan P is carved with: the current one, or (first
+  // batch, or one that needs more) the widened one, 5% slack
+  auto front_for = [&](const ChainPlan& P) {
+    Front f = front;
+    if (!f.set || P.np > f.np || P.nch > f.nch || P.ell_rows > f.ell) {
+      f.set = true;
+      f.np = std::max<int64_t>(f.np, P.np + P.np / 20 + 64);
+      f.nch = std::max<int64_t>(f.nch, P.nch + P.nch / 20 + 64);
+      f.ell = std::max<int64_t>(f.ell, P.ell_rows + P.ell_rows / 20 + 1024);
+    }
+    return f;
+  };
   int par = 0;
-  // host part + compaction of a launched batch
-  auto finish = [&](Pending& B) -> int {
+  // host part + compaction of the launched batch
+  auto finish = [&]() -> int {
     if (!B.live) return MLP_OK;
     B.live = false;
-    hipStream_t st = streams[B.slot];
-    HIPCHK(c, B.done ? hipEventSynchronize(B.done) : hipStreamSynchronize(st));
+    HIPCHK(c, hipEventSynchronize(c->ev_done[B.par]));
     const int64_t np = B.np;
     for (int64_t s = 0; s < np; s++) {
       if (B.rec[s].flags & 1) {
@@ -239,7 +237,7 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
     // the set's final size, extrapolated from the pairs done so far (+10%)
     const int64_t want = run + (int64_t)((double)(run - base_total) / (double)done_cells *
                                          (double)(all_cells - done_cells) * 1.1);
-    if ((rc = grow_store(c, run, c->store_total, want, two))) return rc;
+    if ((rc = grow_store(c, run, c->store_total, want, false))) return rc;
     HIPCHK(c, hipMemcpyAsync(B.base + B.o_entb, h_entb, np * 8, hipMemcpyHostToDevice, st));
     HIPCHK(c, hipMemcpyAsync(B.base + B.o_rpb, h_rpb, np * 8, hipMemcpyHostToDevice, st));
     {
@@ -252,30 +250,30 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
     return MLP_OK;
   };
   int64_t p = p0;
-  int slot = 0;
   ChainPlan P;
-  // a batch's scratch layout (256-byte aligned sub-buffers); returns the bytes
+  // a batch's scratch layout (256-byte aligned sub-buffers) under front `fr`
+  // (its region first, this batch's parity); returns the bytes
   struct BatchOffs {
     size_t f5, fl, bl, pg, zm, cmf, cmb, tn, cl, crb, rep, lfc, b5, bnl, bz, be, bm, bc, ec, ev, en, entb, rpb, rec;
     PlanDev pd;
   };
-  auto carve = [&](const ChainPlan& P, BatchOffs& o) -> size_t {
+  auto carve = [&](const ChainPlan& P, const Front& fr, BatchOffs& o) -> size_t {
     Carver cv;
     const int64_t np = P.np;
     const bool h5 = models & kHmm5, lo = models & kLocal, pf = models & kPF;
-    if (defer && front.set) {  // the front region (capacities), this batch's parity
+    if (defer) {
       ChainPlan cap;
-      cap.np = front.np;
-      cap.nch = front.nch;
+      cap.np = fr.np;
+      cap.nch = fr.nch;
       const PlanDev pd0 = carve_plan(cv, cap), pd1 = carve_plan(cv, cap);
-      const size_t r0 = cv.take(front.np * sizeof(PairRec)), r1 = cv.take(front.np * sizeof(PairRec));
+      const size_t r0 = cv.take(fr.np * sizeof(PairRec)), r1 = cv.take(fr.np * sizeof(PairRec));
       o.pd = par ? pd1 : pd0;
       o.rec = par ? r1 : r0;
-      o.entb = cv.take(front.np * 8);
-      o.rpb = cv.take(front.np * 8);
-      o.ec = cv.take(front.ell * kEll * 2);
-      o.ev = cv.take(front.ell * kEll * 4);
-      o.en = cv.take(front.ell * 4);
+      o.entb = cv.take(fr.np * 8);
+      o.rpb = cv.take(fr.np * 8);
+      o.ec = cv.take(fr.ell * kEll * 2);
+      o.ev = cv.take(fr.ell * kEll * 4);
+      o.en = cv.take(fr.ell * 4);
     }
     o.f5 = cv.take(h5 ? P.cells * 4 : 0);
     o.fl = cv.take(lo ? P.cells * 4 : 0);
@@ -295,7 +293,7 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
     o.be = cv.take(P.bnd * 4);
     o.bm = cv.take(P.bnd * 4);
     o.bc = cv.take(P.bnd * 4);
-    if (!(defer && front.set)) {
+    if (!defer) {
       o.ec = cv.take(P.ell_rows * kEll * 2);
       o.ev = cv.take(P.ell_rows * kEll * 4);
       o.en = cv.take(P.ell_rows * 4);
@@ -311,7 +309,6 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
     int64_t q;
     int rc;
     if ((rc = next_batch(c, p, p1, batch_target, pair_bytes, &q))) return rc;
-    Pending& B = pend[slot];
     plan_chains(c, p, q, P);          // host planning overlaps the previous batch's kernels
     if (!calibrated) {
       // pair_bytes bounds each pair as if alone in a chain of a wider member;
@@ -322,90 +319,80 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
       BatchOffs o;
       size_t bound = 0;
       for (int64_t k = p; k < q; k++) bound += pair_bytes(k);
-      const size_t got = carve(P, o);
+      const size_t got = carve(P, front_for(P), o);
       const double r = (double)(got > clist_bytes ? got - clist_bytes : 0) / (double)std::max<size_t>(bound, 1);
       if (q < p1 && r > 0.1 && r < 0.97) {
-        const size_t slot_budget = two ? c->scratch_budget / 2 : c->scratch_budget;
-        batch_target = batch_target_for(c, p, p1, pair_bytes,
-                                        std::max<size_t>((size_t)((double)budget_for(slot_budget) / r * 0.99), 32u << 20));
+        batch_target = batch_target_for(
+            c, p, p1, pair_bytes, std::max<size_t>((size_t)((double)budget_for(c->scratch_budget) / r * 0.99), 32u << 20));
         if ((rc = next_batch(c, p, p1, batch_target, pair_bytes, &q))) return rc;
         plan_chains(c, p, q, P);
       }
     }
-    {  // a batch over its slot's budget (the ratio varies with the pairs): fewer pairs
-      const size_t slot_budget = two ? c->scratch_budget / 2 : c->scratch_budget;
+    {  // a batch over the budget (the ratio varies with the pairs), carved as it will be: fewer pairs
       BatchOffs o;
-      while (q - p > 1 && carve(P, o) > slot_budget) {
+      while (q - p > 1 && carve(P, front_for(P), o) > c->scratch_budget) {
         q = p + std::max<int64_t>(1, (q - p) * 97 / 100);
         plan_chains(c, p, q, P);
       }
     }
     if (defer) {
-      // front capacities from the first batch with 5% slack; a batch that
-      // needs more finishes the pending one first (nothing then reads the old
-      // front) and widens them
-      if (!front.set || P.np > front.np || P.nch > front.nch || P.ell_rows > front.ell) {
-        if ((rc = finish(B))) return rc;
-        front.set = true;
-        front.np = std::max<int64_t>(front.np, P.np + P.np / 20 + 64);
-        front.nch = std::max<int64_t>(front.nch, P.nch + P.nch / 20 + 64);
-        front.ell = std::max<int64_t>(front.ell, P.ell_rows + P.ell_rows / 20 + 1024);
+      // a batch that needs a wider front finishes the pending one first
+      // (nothing then reads the old front) and widens it
+      const Front f = front_for(P);
+      if (!front.set || f.np != front.np || f.nch != front.nch || f.ell != front.ell) {
+        if ((rc = finish())) return rc;
+        front = f;
       }
-    } else if ((rc = finish(B))) {  // this slot's previous batch
+    } else if ((rc = finish())) {  // the previous batch
       return rc;
     }
-    hipStream_t st = streams[slot];
     const int64_t np = P.np, nch = P.nch;
     // ---- carve scratch
     BatchOffs o;
-    const size_t need = carve(P, o);
+    const size_t need = carve(P, front, o);
     const PlanDev& pd = o.pd;
-    const size_t o_f5 = o.f5, o_fl = o.fl, o_bl = o.bl, o_pg = o.pg, o_zm = o.zm, o_cmf = o.cmf, o_cmb = o.cmb,
-                 o_tn = o.tn, o_cl = o.cl, o_crb = o.crb, o_rep = o.rep, o_b5 = o.b5, o_bnl = o.bnl, o_bz = o.bz,
-                 o_be = o.be, o_bm = o.bm, o_bc = o.bc, o_ec = o.ec, o_ev = o.ev, o_en = o.en, o_entb = o.entb,
-                 o_rpb = o.rpb, o_rec = o.rec;
-    // with more batches to come, 3% headroom (capped at the slot's budget):
-    // they are planned to the same bytes, and one that needs a little more
-    // would otherwise reallocate the scratch
-    const size_t slot_budget = two ? c->scratch_budget / 2 : c->scratch_budget;
-    const size_t want = q < p1 && scr[slot]->bytes < need ? std::max(need, std::min(slot_budget, need + need / 32)) : need;
-    if (scr[slot]->bytes < want && (rc = finish(B))) return rc;  // a reallocation: nothing may still read the old one
-    if ((rc = ensure(c, *scr[slot], want))) {
+    // with more batches to come, 3% headroom (capped at the budget): they are
+    // planned to the same bytes, and one that needs a little more would
+    // otherwise reallocate the scratch
+    const size_t want =
+        q < p1 && c->scratch.bytes < need ? std::max(need, std::min(c->scratch_budget, need + need / 32)) : need;
+    if (c->scratch.bytes < want && (rc = finish())) return rc;  // a reallocation: nothing may still read the old one
+    if ((rc = ensure(c, c->scratch, want))) {
       if (rc != MLP_ERR_MEMORY || c->scratch_budget < (64u << 20)) return rc;
       c->scratch_budget /= 2;  // the device is shared: plan smaller batches and retry
-      batch_target =
-          batch_target_for(c, p, p1, pair_bytes, budget_for(two ? c->scratch_budget / 2 : c->scratch_budget));
+      batch_target = batch_target_for(c, p, p1, pair_bytes, budget_for(c->scratch_budget));
       calibrated = false;
+      front = Front();
       continue;
     }
-    char* base = (char*)scr[slot]->p;
+    char* base = (char*)c->scratch.p;
     Scratch sc{};
-    sc.f5 = (float*)(base + o_f5);
-    sc.fl = (float*)(base + o_fl);
-    sc.pg = pg_in_zm ? (float*)(base + o_zm) : (float*)(base + o_pg);
+    sc.f5 = (float*)(base + o.f5);
+    sc.fl = (float*)(base + o.fl);
+    sc.pg = pg_in_zm ? (float*)(base + o.zm) : (float*)(base + o.pg);
     sc.pg_stride = pg_in_zm ? 2 : 1;
-    sc.zm = (double*)(base + o_zm);
-    sc.bl = (float*)(base + o_bl);
-    sc.cmf = (float*)(base + o_cmf);
-    sc.cmb = (float*)(base + o_cmb);
-    sc.clist = (float*)(base + o_cl);
+    sc.zm = (double*)(base + o.zm);
+    sc.bl = (float*)(base + o.bl);
+    sc.cmf = (float*)(base + o.cmf);
+    sc.cmb = (float*)(base + o.cmb);
+    sc.clist = (float*)(base + o.cl);
     sc.clist_row = tot_row;
-    sc.tot_next = (int32_t*)(base + o_tn);
-    sc.crb = lanefold || foldbound ? (float*)(base + o_crb) : nullptr;
-    sc.rep = (int32_t*)(base + o_rep);
-    static const bool force_repair = getenv("MLP_TOT_FORCE_REPAIR") != nullptr;  // test hook
+    sc.tot_next = (int32_t*)(base + o.tn);
+    sc.crb = lanefold || foldbound ? (float*)(base + o.crb) : nullptr;
+    sc.rep = (int32_t*)(base + o.rep);
+    static const bool force_repair = knob_set("MLP_TEST_TOT_FORCE_REPAIR");
     sc.force_repair = force_repair ? 1 : 0;
-    sc.bnd5 = (float*)(base + o_b5);
-    sc.bndl = (float*)(base + o_bnl);
-    sc.bndz = (double*)(base + o_bz);
-    sc.bnde = (int32_t*)(base + o_be);
-    sc.bndm = (float*)(base + o_bm);
-    sc.bndc = (int32_t*)(base + o_bc);
-    sc.ell_col = (uint16_t*)(base + o_ec);
-    sc.ell_val = (float*)(base + o_ev);
-    sc.ell_cnt = (int32_t*)(base + o_en);
+    sc.bnd5 = (float*)(base + o.b5);
+    sc.bndl = (float*)(base + o.bnl);
+    sc.bndz = (double*)(base + o.bz);
+    sc.bnde = (int32_t*)(base + o.be);
+    sc.bndm = (float*)(base + o.bm);
+    sc.bndc = (int32_t*)(base + o.bc);
+    sc.ell_col = (uint16_t*)(base + o.ec);
+    sc.ell_val = (float*)(base + o.ev);
+    sc.ell_cnt = (int32_t*)(base + o.en);
     sc.lf_cnt = lanefold && defer ? (int32_t*)(base + o.lfc) : sc.ell_cnt;
-    PairRec* d_rec = (PairRec*)(base + o_rec);
+    PairRec* d_rec = (PairRec*)(base + o.rec);
     PairMeta pm;
     ChainMeta cm;
     {  // the plan through this parity's pinned staging (its last batch is finished)
@@ -431,19 +418,19 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
       fwd_ref = t.e0;
       HIPCHK(c, launch_forward(models, ms, c->d_tables, seqs, pm, cm, d_rec, sc, nch, lds_seq, st, side));
     }
+    // the local totals group times once per batch: its kernels' device time,
+    // the parts after the first (another stream, or after the backward sweep)
+    // adding to the batch's one launch
     if (lanefold) {  // the forward chains, beside the partition function's sweeps
       Timer t(c, KTOT, bcells, st);
       HIPCHK(c, launch_local_fwd_lanefold(seqs, pm, cm, d_rec, sc, np, tot_waves, st));
     }
-    hipEvent_t tot_done = nullptr;
     if (tot_beside) {  // the forward chains on stream2, beside the backward sweeps
-      hipEvent_t e = pool_event(c);
-      HIPCHK(c, hipEventRecord(e, st));
-      HIPCHK(c, hipStreamWaitEvent(c->stream2, e, 0));
+      HIPCHK(c, hipEventRecord(c->ev_fork, st));
+      HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev_fork, 0));
       Timer t(c, KTOT, bcells, c->stream2);
       HIPCHK(c, launch_local_totals(ms, c->d_tables, seqs, pm, cm, d_rec, sc, np, tot_waves, c->stream2, kTotFwd));
-      tot_done = pool_event(c);
-      HIPCHK(c, hipEventRecord(tot_done, c->stream2));
+      HIPCHK(c, hipEventRecord(c->ev_tot, c->stream2));
     }
     {
       Timer t(c, KBWD, bcells, st);
@@ -453,24 +440,25 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
     if (models & kLocal) {
       Timer t(c, KTOT, bcells, st);
       if (lanefold) {
+        t.cont = true;
         HIPCHK(c, launch_local_bwd_lanefold(ms, c->d_tables, seqs, pm, cm, d_rec, sc, np, tot_waves, st));
       } else if (tot_beside) {
+        t.cont = true;
         HIPCHK(c, launch_local_totals(ms, c->d_tables, seqs, pm, cm, d_rec, sc, np, tot_waves, st, kTotBwd));
-        HIPCHK(c, hipStreamWaitEvent(st, tot_done, 0));
+        HIPCHK(c, hipStreamWaitEvent(st, c->ev_tot, 0));
       } else {
         HIPCHK(c, launch_local_totals(ms, c->d_tables, seqs, pm, cm, d_rec, sc, np, tot_waves, st));
       }
     }
     // the previous batch: its host part while this batch's sweeps run, its
     // compaction before this batch's merge overwrites the ELL rows
-    if (defer && (rc = finish(B))) return rc;
-    if (side && side->join_mode != 0) HIPCHK(c, hipStreamWaitEvent(st, side->join, 0));  // deferred join
+    if (defer && (rc = finish())) return rc;
+    if (side->join_mode != 0) HIPCHK(c, hipStreamWaitEvent(st, side->join, 0));  // deferred join
     {
       Timer t(c, KMERGE, bcells, st);
       HIPCHK(c, launch_merge(models, pid, ms, seqs, pm, cm, d_rec, sc, nch, lds_seq, st));
     }
     B.live = true;
-    B.slot = slot;
     B.p = p;
     B.q = q;
     B.np = np;
@@ -490,27 +478,18 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
     B.rec = c->h_rec[par];
     B.par = par;
     B.base = base;
-    B.o_entb = o_entb;
-    B.o_rpb = o_rpb;
+    B.o_entb = o.entb;
+    B.o_rpb = o.rpb;
     B.pm = pm;
     B.sc = sc;
     B.d_rec = d_rec;
     HIPCHK(c, hipMemcpyAsync(c->h_rec[par], d_rec, np * sizeof(PairRec), hipMemcpyDeviceToHost, st));
-    B.done = nullptr;
-    if (defer) {
-      B.done = pool_event(c);
-      HIPCHK(c, hipEventRecord(B.done, st));
-    }
-    // the other slot's batch (launched before this one) compacts now, in pair
-    // order, while this batch's sweeps run
-    if ((rc = finish(pend[slot ^ 1]))) return rc;
-    if (two) slot ^= 1;
+    HIPCHK(c, hipEventRecord(c->ev_done[par], st));  // (its last waiter, finish(), has run)
     par ^= 1;
     p = q;
   }
   int rc;
-  if ((rc = finish(pend[slot ^ 1]))) return rc;
-  if ((rc = finish(pend[slot]))) return rc;
+  if ((rc = finish())) return rc;
   HIPCHK(c, hipStreamSynchronize(c->stream2));
   HIPCHK(c, hipMemcpyAsync(c->d_ent_off, c->ent_off.data(), sizeof(int64_t) * (c->P + 1),
                            hipMemcpyHostToDevice, c->stream));

@@ -271,9 +271,9 @@ int mlp_profile_mea(mlp_ctx* c, char* path, int32_t* path_len, float* score) {
   a.L1 = L1;
   a.L2 = L2;
   a.work = (uint8_t*)c->r_mea.p;
-  // MLP_MEA_SPINS: test hook (0 makes a waiting strip give up at once: the
-  // caller's host fallback)
-  static const int spins = getenv("MLP_MEA_SPINS") ? atoi(getenv("MLP_MEA_SPINS")) : (1 << 22);
+  // MLP_TEST_MEA_SPINS: test hook (0 makes a waiting strip give up at once:
+  // the caller's host fallback)
+  static const int spins = (int)knob("MLP_TEST_MEA_SPINS", 1 << 22);
   a.spin_limit = spins;
   HIPCHK(c, launch_profile_mea(a, c->stream));
   HIPCHK(c, hipMemcpyAsync(c->h_mea, c->r_mea.p, back, hipMemcpyDeviceToHost, c->stream));
@@ -324,8 +324,17 @@ int mlp_profile_mea(mlp_ctx* c, char* path, int32_t* path_len, float* score) {
 int mlp_profile_set(mlp_ctx* c, int L1, int L2, const float* post) {
   if (!c || L1 < 0 || L2 < 0 || !post) return MLP_ERR_ARG;
   if (c->host) return MLP_ERR_STATE;
+  // the device MEA's preconditions: its hand-off polls for non-NaN values,
+  // and its choices (max3, the D / L-over-U flags) match ChooseBestOfThree
+  // on finite entries >= +0 only
+  const int64_t ncell = (int64_t)(L1 + 1) * (L2 + 1);
+  for (int64_t k = 0; k < ncell; k++)
+    if (!(post[k] >= 0.f) || std::isinf(post[k]) || std::signbit(post[k])) {
+      c->err = "mlp_profile_set: entries must be finite and >= +0";
+      return MLP_ERR_ARG;
+    }
   hipSetDevice(c->device);
-  const size_t b_out = (size_t)(L1 + 1) * (L2 + 1) * 4;
+  const size_t b_out = (size_t)ncell * 4;
   int rc;
   // the same guards as a computed posterior: the MEA's row windows read past its rows
   if ((rc = ensure(c, c->r_profile, kMeaGuard + ((b_out + 255) & ~(size_t)255) + kMeaGuard))) return rc;

@@ -195,9 +195,9 @@ static int relax_one(mlp_ctx* c, const QpRelax& qp, bool last) {
   }
   const int64_t nout = r1 - r0;
   int rc;
-  // MLP_RELAX_LOG=1: wall time of the round's phases on stderr (each mark
+  // MLP_LOG_RELAX=1: wall time of the round's phases on stderr (each mark
   // drains the stream first, so the phases do not overlap while logging)
-  static const bool rlog = getenv("MLP_RELAX_LOG") != nullptr;
+  static const bool rlog = knob_set("MLP_LOG_RELAX");
   auto rl_t = std::chrono::steady_clock::now();
   auto mark = [&](const char* what) {
     if (!rlog) return;
@@ -242,12 +242,12 @@ static int relax_one(mlp_ctx* c, const QpRelax& qp, bool last) {
     }
     mark("transpose");
     // Tiled path (k_relax_tile) for every output pair whose blocks fit the
-    // LDS tile; the row-task kernel for the rest (MLP_RELAX=tasks: all).
+    // LDS tile; the row-task kernel for the rest (MLP_TEST_RELAX_PATH=tasks: all).
     int64_t LDS_MAX = 160 * 1024 / kRelaxGroupsPerCU;
-    if (const char* e = getenv("MLP_RELAX_LDS_KB")) LDS_MAX = std::max(32, std::min(160, atoi(e))) * 1024;  // tuning hook
-    const char* mode = getenv("MLP_RELAX");
-    const char* tenv = getenv("MLP_RELAX_TILE");  // test hook: outputs per tile, 1..kTileMax
-    const int tmax = tenv ? std::max(1, std::min(kTileMax, atoi(tenv))) : kTileMax;
+    if (knob_set("MLP_TEST_RELAX_LDS_KB"))
+      LDS_MAX = std::max(32, std::min(160, (int)knob("MLP_TEST_RELAX_LDS_KB", 0))) * 1024;
+    const char* mode = knob_str("MLP_TEST_RELAX_PATH");
+    const int tmax = std::max(1, std::min(kTileMax, (int)knob("MLP_TEST_RELAX_TILE", kTileMax)));
     bool tasks_only = (mode && !strcmp(mode, "tasks")) || c->max_len > 8000 || c->P >= (1LL << 31);
     std::vector<int32_t> nwords(2 * c->P, 0);
     if ((rc = ensure_tmp(c, c->r_nwords, sizeof(int32_t) * std::max<int64_t>(2 * c->P, 1)))) return rc;
@@ -305,20 +305,21 @@ static int relax_one(mlp_ctx* c, const QpRelax& qp, bool last) {
     const int64_t budget = std::min<int64_t>(LDS_MAX - zs, tile_relax_max_cap()) & ~(int64_t)15;
     int64_t small_budget = std::min<int64_t>(budget, (80 * 1024 - zs) & ~(int64_t)15);
     if (LDS_MAX < 160 * 1024) small_budget = 0;
-    if (const char* e = getenv("MLP_RELAX_SMALL_KB"))  // test hook: a small staging area for the small class
-      small_budget = std::min(budget, std::max<int64_t>(64, (int64_t)atoi(e) * 1024 - zs)) & ~(int64_t)15;
+    if (knob_set("MLP_TEST_RELAX_SMALL_KB"))  // a small staging area for the small class
+      small_budget =
+          std::min(budget, std::max<int64_t>(64, (int64_t)knob("MLP_TEST_RELAX_SMALL_KB", 0) * 1024 - zs)) & ~(int64_t)15;
     const int n = c->n;
     const bool exact = !tasks_only && n <= 2048;
     const int64_t kSmallCells = 8 * (int64_t)kRelaxThreads;  // 8 slots: the 64-VGPR budget of 8 waves per SIMD
     // z's per tile whose images may exceed the staging area (staged in passes)
-    const int max_over = getenv("MLP_RELAX_SPLIT_Z") ? atoi(getenv("MLP_RELAX_SPLIT_Z")) : n / 16;
+    const int max_over = (int)knob("MLP_TEST_RELAX_SPLIT_Z", n / 16);
     // z's on which a small-class output's image may not fit beside C even
     // alone (the kernel reads that image in place from HBM on those z's);
     // 0: such outputs go to the one-workgroup class.  No limit by default: at
     // C3 round 1 every output has such z's, and the small class with images
     // read in place runs 1.32 s against 1.60 s for the one-workgroup class
     // (limits of 8 / 32 z's: 1.60 / 1.55 s)
-    const int max_glob = getenv("MLP_RELAX_GLOBAL_Z") ? atoi(getenv("MLP_RELAX_GLOBAL_Z")) : n;
+    const int max_glob = (int)knob("MLP_TEST_RELAX_GLOBAL_Z", n);
     std::vector<int32_t> isz;  // image bytes of P(s, z), s's residues as rows: isz[s * n + z]
     if (exact) {
       isz.assign((size_t)n * n, 0);
@@ -502,7 +503,7 @@ static int relax_one(mlp_ctx* c, const QpRelax& qp, bool last) {
     }
     mark("order, images");
     const int64_t nt = (int64_t)tp.size();
-    if (getenv("MLP_PLAN_LOG")) {
+    if (knob_set("MLP_LOG_PLAN")) {
       int64_t mx = 0;
       for (int i = 0; i < c->n; i++) mx = std::max(mx, maxI[i]);
       fprintf(stderr,
@@ -513,7 +514,7 @@ static int relax_one(mlp_ctx* c, const QpRelax& qp, bool last) {
               (long long)mx, (long long)n_hbm_outputs.load());
     }
     if (mode && !strcmp(mode, "pairs") && nt) {  // test hook: the pair-resident path must cover all
-      c->err = "MLP_RELAX=pairs: " + std::to_string(nt) + " row tasks fell back";
+      c->err = "MLP_TEST_RELAX_PATH=pairs: " + std::to_string(nt) + " row tasks fell back";
       return MLP_ERR_STATE;
     }
     if ((rc = ensure_tmp(c, c->r_tasks_p, sizeof(int64_t) * std::max<int64_t>(nt, 1)))) return rc;

@@ -49,7 +49,7 @@ struct mlp_ctx {
   bool host = false;                  // mlp_ctx_create_host: every stage on the CPU, no HIP call
   mlph::Store hs;                     // the host context's canonical CSR store
   hipStream_t stream = nullptr;
-  hipStream_t stream2 = nullptr;   // second posterior batch stream (pipelined batches)
+  hipStream_t stream2 = nullptr;      // the local totals' forward chains beside the backward sweeps
   SideStream side{};                  // concurrent second sweep kernel of a batch (mlp_kernels.h)
   std::string err;
   // parameter tables
@@ -107,7 +107,10 @@ struct mlp_ctx {
   std::vector<uint8_t> vit_path;      // forward order, 0 = B, 1 = X, 2 = Y (when kept)
   bool vit_done = false, vit_paths = false;
   // batch scratch
-  DevBuf scratch, scratch2;        // batch scratch of the two posterior streams
+  DevBuf scratch;                     // batch scratch of the posterior stage
+  // the posterior stage's synchronisation events, created once: a batch's
+  // records on the host (by batch parity), the fork to stream2 and its join
+  hipEvent_t ev_done[2] = {nullptr, nullptr}, ev_fork = nullptr, ev_tot = nullptr;
   size_t scratch_budget = 0;
   // relaxation buffers
   bool arena_on = false;               // relax_one: temporaries come from the batch scratch
@@ -137,7 +140,8 @@ struct mlp_ctx {
   // e0 / e1 on the timed stream; e0b / e1b (optional) on the side stream, the
   // group's span then runs from the earlier start to the later end, measured
   // from eref (recorded on the context stream before both)
-  struct TimerRec { int id; int64_t cells; hipEvent_t e0, e1, e0b, e1b, eref; };
+  // cont: a later part of the group's launch (time added, launch and cells counted once)
+  struct TimerRec { int id; int64_t cells; bool cont; hipEvent_t e0, e1, e0b, e1b, eref; };
   std::vector<TimerRec> tpend;
   std::vector<hipEvent_t> evpool;
   size_t evused = 0;
@@ -187,6 +191,7 @@ struct Timer {
   int64_t cells;
   hipStream_t st;
   hipEvent_t e0 = nullptr;
+  bool cont = false;  // continues the group's previous launch (TimerRec::cont)
   hipStream_t sb = nullptr;
   hipEvent_t e0b = nullptr, eref = nullptr;
   Timer(mlp_ctx* c_, int id_, int64_t cells_, hipStream_t st_ = nullptr)
@@ -216,7 +221,7 @@ struct Timer {
       e1b = pool_event(c);
       hipEventRecord(e1b, sb);
     }
-    c->tpend.push_back({id, cells, e0, e1, e0b, e1b, eref});
+    c->tpend.push_back({id, cells, cont, e0, e1, e0b, e1b, eref});
   }
 };
 MLP_HIDDEN void flush_timers(mlp_ctx* c);

@@ -33,11 +33,10 @@ int shard_count(mlp_ctx* c) {
   return cells >= kShardMinCells ? (int)devs.size() : 1;
 }
 
-// MLP_FORCE_PEER=1 (test hook): peer copies even between contexts on one
+// MLP_TEST_FORCE_PEER=1 (test hook): peer copies even between contexts on one
 // device, so virtual shards exercise the xGMI branch
 static bool force_peer() {
-  const char* e = getenv("MLP_FORCE_PEER");
-  return e && atoi(e) > 0;
+  return knob("MLP_TEST_FORCE_PEER", 0) > 0;
 }
 
 static hipError_t copy_on(hipStream_t st, mlp_ctx* dst, void* d, const mlp_ctx* src, const void* s, size_t bytes) {
@@ -366,8 +365,8 @@ int mlp_comm_init(mlp_ctx* c, const unsigned char id[128], int nranks, int rank)
 // gather every rank holds [0, P) in canonical layout.
 int mlp_allgather(mlp_ctx* c) {
   if (!c) return MLP_ERR_ARG;
-  // MLP_ALLGATHER_FORCE=1: the grouped body at one rank as well (test hook)
-  static const bool force = getenv("MLP_ALLGATHER_FORCE") && atoi(getenv("MLP_ALLGATHER_FORCE")) > 0;
+  // MLP_TEST_ALLGATHER_FORCE=1: the grouped body at one rank as well (test hook)
+  static const bool force = knob("MLP_TEST_ALLGATHER_FORCE", 0) > 0;
   if (!c->comm || (c->nranks == 1 && !force)) return MLP_OK;
   hipSetDevice(c->device);
   const int R = c->nranks;

@@ -467,16 +467,14 @@ hipError_t launch_profile_posterior(const ProfileArgs& a_in, hipStream_t st) {
   if (a_in.L1 <= 0) return hipSuccess;
   ProfileArgs a = a_in;
   // test hook: a smaller stage reaches the partial-run and long-row branches
-  // with small profiles (MLP_PROFILE_STAGE, 1..kProfStage)
-  a.stage = kProfStage;
-  if (const char* e = getenv("MLP_PROFILE_STAGE")) a.stage = std::max(1, std::min(kProfStage, atoi(e)));
+  // with small profiles (MLP_TEST_PROFILE_STAGE, 1..kProfStage)
+  a.stage = std::max(1, std::min(kProfStage, (int)knob("MLP_TEST_PROFILE_STAGE", kProfStage)));
   hipLaunchKernelGGL(k_profile_inv, dim3((unsigned)((a.map1_len + 255) / 256)), dim3(256), 0, st, a);
   // column ranges per row: only rows too few to give every CU a wave are
   // split (at C3 refinement, one range per row measured fastest: 376 ms of
   // profile kernels against 393 / 466 ms for 2 / 4 ranges); ranges of at
-  // least 64 columns (MLP_PROFILE_SPLIT overrides, for measurement)
-  int k = (256 + a.L1 - 1) / a.L1;
-  if (const char* e = getenv("MLP_PROFILE_SPLIT")) k = atoi(e);
+  // least 64 columns (MLP_TEST_PROFILE_SPLIT overrides, for measurement)
+  int k = (int)knob("MLP_TEST_PROFILE_SPLIT", (256 + a.L1 - 1) / a.L1);
   k = std::max(1, std::min(k, std::min(16, (a.L2 + 1 + 63) / 64)));
   const size_t lds = profile_lds_cols((a.L2 + 1 + k - 1) / k);
   (void)hipFuncSetAttribute((const void*)k_profile_post, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

@@ -837,10 +837,10 @@ static hipError_t launch_tiles_kp(const TileRelaxArgs& a, int slots, size_t lds,
 hipError_t launch_relax_tiles(const TileRelaxArgs& a, int slots, bool one_per_cu, hipStream_t st) {
   if (a.ntiles <= 0) return hipSuccess;
   const size_t lds = tile_relax_lds(a.cap);
-  const char* kp = getenv("MLP_RELAX_KP");  // test hook: force the large-prefetch variant
   hipError_t e;
   const int kpv = tile_relax_prefetch(a.cap);
-  switch (kp ? atoi(kp) : (one_per_cu && kpv ? 9 : kpv)) {
+  // MLP_TEST_RELAX_KP: force the large-prefetch variant
+  switch ((int)knob("MLP_TEST_RELAX_KP", one_per_cu && kpv ? 9 : kpv)) {
     case 5: e = a.qp.on ? launch_tiles_kp<5, true>(a, slots, lds, st) : launch_tiles_kp<5, false>(a, slots, lds, st); break;
     case 9: e = a.qp.on ? launch_tiles_kp<9, true>(a, slots, lds, st) : launch_tiles_kp<9, false>(a, slots, lds, st); break;
     default: return hipErrorInvalidValue;

@@ -50,7 +50,7 @@ def test_cli_profile_posterior_on_gpu(name, flags, suffix, mea):
     if mea.startswith('device'):
         env['MLP_MEA_GPU_MIN'] = '0'
         if mea == 'device-gives-up':   # every device MEA may give up: the host fallback
-            env['MLP_MEA_SPINS'] = '0'
+            env['MLP_TEST_MEA_SPINS'] = '0'
     else:
         env['MLP_MEA_GPU_MIN'] = str(1 << 40)
     r = subprocess.run([BIN, *(flags or ('-p', '0')), os.path.join(GOLDEN, 'cli', f'{name}.fa')], capture_output=True,
@@ -210,10 +210,10 @@ def test_quickprobs_config_families(name):
 @pytest.mark.parametrize('name', ['qp_div60', 'qp_big210'])
 def test_quickprobs_device_mea_gives_up(name):
     """A device MEA strip that gives up waiting for the one above
-    (MLP_MEA_SPINS=0: at the first poll that finds it not ready) returns
+    (MLP_TEST_MEA_SPINS=0: at the first poll that finds it not ready) returns
     MLP_ERR_STATE and the drop-in computes that MEA on the host: still the
     reference's bytes, nothing on stderr."""
-    env = dict(ENV, MLP_MEA_SPINS='0', MLP_MEA_GPU_MIN='0')
+    env = dict(ENV, MLP_TEST_MEA_SPINS='0', MLP_MEA_GPU_MIN='0')
     r = subprocess.run([QP_BIN, os.path.join(GOLDEN, 'cli', f'{name}.fa')], capture_output=True, text=True,
                        timeout=300, env=env)
     assert r.returncode == 0 and r.stderr == '', r.stderr

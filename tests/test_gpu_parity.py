@@ -244,9 +244,9 @@ def test_family_features_cli_golden(name):
 # small-class tiles (two workgroups per CU) whose staging area is too small
 # for some outputs' images beside C: those are read in place from HBM on those
 # z's (with and without passes over output subsets on the others)
-_HBM_IMAGE_MODES = [{'MLP_RELAX': 'pairs', 'MLP_RELAX_SMALL_KB': '14', 'MLP_RELAX_GLOBAL_Z': '100000'},
-                    {'MLP_RELAX': 'pairs', 'MLP_RELAX_SMALL_KB': '16', 'MLP_RELAX_GLOBAL_Z': '100000',
-                     'MLP_RELAX_SPLIT_Z': '100000'}]
+_HBM_IMAGE_MODES = [{'MLP_TEST_RELAX_PATH': 'pairs', 'MLP_TEST_RELAX_SMALL_KB': '14', 'MLP_TEST_RELAX_GLOBAL_Z': '100000'},
+                    {'MLP_TEST_RELAX_PATH': 'pairs', 'MLP_TEST_RELAX_SMALL_KB': '16', 'MLP_TEST_RELAX_GLOBAL_Z': '100000',
+                     'MLP_TEST_RELAX_SPLIT_Z': '100000'}]
 
 
 def _relax_both_paths(seqs, pid, iters, tag):
@@ -265,12 +265,12 @@ def _relax_both_paths(seqs, pid, iters, tag):
     # tiled kernel with up to 4 outputs per tile, one output per tile, the
     # large-prefetch instantiation, and the row-task kernel
     # and tiles over a 48 KB staging area whose oversize z's are staged in
-    # passes over subsets of the outputs (MLP_RELAX_SPLIT_Z: no limit), and
+    # passes over subsets of the outputs (MLP_TEST_RELAX_SPLIT_Z: no limit), and
     # small-class tiles over a tiny staging area, whose outputs' images are
     # read in place from HBM on the z's where they do not fit beside C
-    modes = [{'MLP_RELAX': 'pairs'}, {'MLP_RELAX': 'pairs', 'MLP_RELAX_TILE': '1'},
-             {'MLP_RELAX': 'pairs', 'MLP_RELAX_KP': '9'}, {'MLP_RELAX': 'tasks'},
-             {'MLP_RELAX_LDS_KB': '48', 'MLP_RELAX_SPLIT_Z': '100000'}] + _HBM_IMAGE_MODES
+    modes = [{'MLP_TEST_RELAX_PATH': 'pairs'}, {'MLP_TEST_RELAX_PATH': 'pairs', 'MLP_TEST_RELAX_TILE': '1'},
+             {'MLP_TEST_RELAX_PATH': 'pairs', 'MLP_TEST_RELAX_KP': '9'}, {'MLP_TEST_RELAX_PATH': 'tasks'},
+             {'MLP_TEST_RELAX_LDS_KB': '48', 'MLP_TEST_RELAX_SPLIT_Z': '100000'}] + _HBM_IMAGE_MODES
     for env in modes:
         os.environ.update(env)
         try:
@@ -315,8 +315,8 @@ def test_relax_hbm_images_exercised(capfd):
     ref = orc.relax([len(x) for x in seqs], [(r.astype(np.int32), c.astype(np.int32), v) for r, c, v in cur])
     seen = 0
     for kb in (14, 16, 20, 24, 32):
-        env = {'MLP_RELAX': 'pairs', 'MLP_RELAX_SMALL_KB': str(kb), 'MLP_RELAX_GLOBAL_Z': '100000',
-               'MLP_PLAN_LOG': '1'}
+        env = {'MLP_TEST_RELAX_PATH': 'pairs', 'MLP_TEST_RELAX_SMALL_KB': str(kb), 'MLP_TEST_RELAX_GLOBAL_Z': '100000',
+               'MLP_LOG_PLAN': '1'}
         os.environ.update(env)
         try:
             fam.import_csr(rp, eo, cols, vals)
@@ -395,8 +395,8 @@ def test_qp_ragged_chains():
 
 
 # ---- QuickProbs consistency (QP/Alignment/Multiple/ConsistencyStage.cpp:90-258)
-_RELAX_MODES = [{'MLP_RELAX': 'pairs'}, {'MLP_RELAX': 'pairs', 'MLP_RELAX_TILE': '1'},
-                {'MLP_RELAX': 'pairs', 'MLP_RELAX_KP': '9'}, {'MLP_RELAX': 'tasks'}] + _HBM_IMAGE_MODES
+_RELAX_MODES = [{'MLP_TEST_RELAX_PATH': 'pairs'}, {'MLP_TEST_RELAX_PATH': 'pairs', 'MLP_TEST_RELAX_TILE': '1'},
+                {'MLP_TEST_RELAX_PATH': 'pairs', 'MLP_TEST_RELAX_KP': '9'}, {'MLP_TEST_RELAX_PATH': 'tasks'}] + _HBM_IMAGE_MODES
 
 
 def _import(fam, csrs):
@@ -586,9 +586,9 @@ def test_profile_posterior_stage_branches(stage, split):
     (fewer than 64 pairs), and forced column ranges per row."""
     env = {}
     if stage:
-        env['MLP_PROFILE_STAGE'] = stage
+        env['MLP_TEST_PROFILE_STAGE'] = stage
     if split:
-        env['MLP_PROFILE_SPLIT'] = split
+        env['MLP_TEST_PROFILE_SPLIT'] = split
     _profile_case(83, 9, 70, 0.7, [0, 3, 5, 8], [1, 2, 6], env)
 
 
@@ -655,11 +655,31 @@ def test_profile_mea_any_matrix(L1, L2, kind):
         fam.close()
 
 
+def test_profile_set_rejects_non_posteriors():
+    """mlp_profile_set takes finite entries >= +0 only (the device MEA polls
+    for non-NaN hand-offs and its choices assume that range): NaN, -0, a
+    negative value or infinity is MLP_ERR_ARG, and a valid matrix still works."""
+    fam = Family([x for _, x in synth.family(3, 20, 0.5, seed=1)])
+    try:
+        for bad in (np.nan, -0.0, -1e-30, np.inf):
+            post = np.zeros((6, 9), np.float32)
+            post[3, 4] = bad
+            with pytest.raises(RuntimeError, match='bad argument'):
+                fam.profile_set(post)
+        post = np.zeros((6, 9), np.float32)
+        post[1:, 1:] = 0.25
+        fam.profile_set(post)
+        path, score = fam.profile_mea(5, 8)
+        assert score == np.float32(orc.mea(5, 8, post, with_path=True)[0])
+    finally:
+        fam.close()
+
+
 def test_profile_posterior_many_sequences():
     """More than 64 sequences in profile A: the column compaction runs in
     several 64-sequence chunks (and with a small stage, partial runs)."""
     _profile_case(84, 72, 30, 0.5, list(range(0, 72, 1))[:66], [66, 68, 71])
-    _profile_case(85, 72, 30, 0.5, list(range(3, 72))[:67], [0, 1], {'MLP_PROFILE_STAGE': '40'})
+    _profile_case(85, 72, 30, 0.5, list(range(3, 72))[:67], [0, 1], {'MLP_TEST_PROFILE_STAGE': '40'})
 
 
 # ---- npdoAlign's pair body (MLP_PID_NPDO: ArrangePosteriorProbs,

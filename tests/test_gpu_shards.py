@@ -63,10 +63,10 @@ def test_virtual_shards_quickprobs(k):
 
 @pytest.mark.parametrize('k', [2, 8])
 def test_virtual_shards_forced_peer_copies(k, monkeypatch):
-    """MLP_FORCE_PEER=1: the all-gather's copies take the hipMemcpyPeerAsync
+    """MLP_TEST_FORCE_PEER=1: the all-gather's copies take the hipMemcpyPeerAsync
     branch even between shards of one device (the xGMI path of a real
     multi-GPU box)."""
-    monkeypatch.setenv('MLP_FORCE_PEER', '1')
+    monkeypatch.setenv('MLP_TEST_FORCE_PEER', '1')
     seqs = [s for _, s in synth.family(40, 150, 0.7, seed=93)]
     one = Family(seqs)
     many = Family(seqs, shards=k)
@@ -138,7 +138,7 @@ def test_rccl_allgather_grouped_body_one_rank():
     """The one-process-per-GPU path's RCCL all-gather (mlp_comm_init +
     mlp_allgather's grouped broadcasts, per-rank entry placement, scalar
     exchange, ent_off rebuild) at one rank, forced past the one-rank early
-    return (MLP_ALLGATHER_FORCE=1): the store, distances and MEA scores after
+    return (MLP_TEST_ALLGATHER_FORCE=1): the store, distances and MEA scores after
     the gather equal the context's own, after the posterior stage and after a
     relaxation round.  In a child process: the hook is read once per
     process."""
@@ -147,7 +147,7 @@ def test_rccl_allgather_grouped_body_one_rank():
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     r = subprocess.run([sys.executable, '-c', _RCCL_CHILD, root], capture_output=True, text=True, timeout=300,
-                       env=dict(os.environ, MLP_ALLGATHER_FORCE='1'))
+                       env=dict(os.environ, MLP_TEST_ALLGATHER_FORCE='1'))
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
     assert 'rccl allgather ok' in r.stdout
 

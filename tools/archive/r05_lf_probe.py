@@ -28,7 +28,7 @@ if len(sys.argv) > 1:   # child: dump every family's arrays
 res = {}
 for v in ('0', '1'):
     out = f'/tmp/lfp_{v}.npz'
-    subprocess.run([sys.executable, __file__, out], check=True, env=dict(os.environ, MLP_DEFER_FINISH=v, MLP_TOT_LANEFOLD='1'))
+    subprocess.run([sys.executable, __file__, out], check=True, env=dict(os.environ, MLP_TEST_DEFER_FINISH=v, MLP_TEST_TOT_LANEFOLD='1'))
     res[v] = np.load(out)
 for k in range(len(FAMS)):
     row = []

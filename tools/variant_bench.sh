@@ -1,7 +1,7 @@
 #!/bin/bash
 # Posterior-stage timing of experiment builds (tools/build_variants.py) on the
 # GPU box: tools/variant_bench.sh base v1 v2 ... -> gpurun_out/variants/summary.txt
-# An entry may carry one environment setting: base:MLP_TOT_LANEFOLD=1
+# An entry may carry one environment setting: base:MLP_TEST_TOT_LANEFOLD=1
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/variants
