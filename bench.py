@@ -814,13 +814,26 @@ def c5_pipeline(args):
                     refo = fh.read()
                 same += refo == mine
                 if refo != mine:
-                    # where the two runs part (mlprobs --trace stages) and the
-                    # cause committed for this family by tools/c5_attribution.py
+                    # where the two runs part (mlprobs --trace stages); the
+                    # reference CLIs run twice more on the family: outputs
+                    # that disagree with each other (or one equal to ours)
+                    # show the reference's own multi-threaded races (DESIGN.md
+                    # section 2); else the cause committed for the family by
+                    # tools/c5_attribution.py, if any
                     with open(trace2) as fh:
                         tr2 = json.load(fh)
                     stage = next((s for s in C5_STAGES[:-1] if tr.get(s) != tr2.get(s)), 'output')
-                    differ.append({'name': name, 'path': tr['path'], 'first_stage': stage,
-                                   'cause': attribution.get(name, 'unattributed')})
+                    reruns = []
+                    for _ in range(2):
+                        subprocess.run([bin_, '-q', '--cpnp', ref_cp, '--quickprobs', f'{ref_qp} -t {args.cpu_threads}',
+                                        '--tmp', td, fa, out2], capture_output=True, timeout=1800, env=env_ref)
+                        with open(out2, encoding='latin-1') as fh:
+                            reruns.append(fh.read())
+                    if any(x != refo for x in reruns):
+                        cause = 'race: reference reruns ' + ('equal ours' if mine in reruns else 'disagree')
+                    else:
+                        cause = attribution.get(name, 'unexplained: reference reproducible')
+                    differ.append({'name': name, 'path': tr['path'], 'first_stage': stage, 'cause': cause})
                 sp_r.append(sp_score(refo))
                 if name in pub:
                     tc_r.append(tc_score(refo, pub[name]))
@@ -971,7 +984,7 @@ def compact_c5(c5):
         c['differing'] = {'n': len(d), 'causes': causes,
                           'first_stage': {s: sum(x['first_stage'] == s for x in d) for s in C5_STAGES
                                           if any(x['first_stage'] == s for x in d)},
-                          'unattributed': [x['name'] for x in d if x['cause'] == 'unattributed'][:12]}
+                          'unexplained': [x['name'] for x in d if x['cause'].startswith('unexplained')][:12]}
     return c
 
 

@@ -18,12 +18,32 @@
 //   -q                no progress lines
 // Exit status 0; 1 where the reference pipeline raises a Python exception
 // (no output written).
+//
+//   mlprobs --batch LIST [--devices D0,D1,..] [--report FILE] [options]
+//
+// runs many families (the reference's harness loops over a benchmark's
+// families, one MLProbs.py process each: script.py:38-62): LIST holds one
+// family per line, "in.fa out.msa [trace.json]" (whitespace separated).  One
+// worker process per entry of --devices (default 0; an id may repeat) is
+// forked before any GPU call, sees only its device (HIP_VISIBLE_DEVICES),
+// keeps one device context for all its families and takes the next family,
+// largest first, from a counter shared with the others.  Each family's
+// output (and trace) is written exactly as a separate run writes it.  The
+// report (JSON: per family seconds, status, worker, device runs; the wall
+// time) goes to FILE or stdout.  Exit status 0 when every family succeeded.
 #include <limits.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <sys/wait.h>
 #include <unistd.h>
 
+#include <algorithm>
+#include <chrono>
+#include <numeric>
+#include <sstream>
 #include <string>
 
 #include "pipeline.h"
@@ -173,8 +193,170 @@ static int probe(const std::string& mode, const std::string& arg, const std::str
   return 2;
 }
 
+// pair-cells of a family as the aligners read it (0 when it cannot be read)
+static double family_cells(const std::string& path) {
+  std::vector<cpnp::Row> rows;
+  std::string err;
+  if (!cpnp::load_fasta(path, rows, err)) return 0;
+  std::vector<int> lens;
+  for (const cpnp::Row& r : rows) lens.push_back(r.length());
+  return mlpr::pair_cells(lens);
+}
+
+// one family of a run: the pipeline, its output file and trace
+static int run_family(const std::string& in, const std::string& out, const std::string& trace, mlpp::Tools& tools,
+                      const mlpp::Models& M, const mlpr::Session& session, bool verbose) {
+  std::string result, err;
+  mlpp::Trace tr;
+  const bool ok = mlpp::run_pipeline(in, tools, M, result, tr, err, verbose);
+  if (!trace.empty()) write_trace(trace, tr, tools.name(), session);
+  if (!ok) {
+    fprintf(stderr, "mlprobs: %s: %s\n", in.c_str(), err.c_str());
+    return 1;
+  }
+  FILE* f = fopen(out.c_str(), "wb");
+  if (!f) {
+    fprintf(stderr, "mlprobs: cannot write %s\n", out.c_str());
+    return 1;
+  }
+  fwrite(result.data(), 1, result.size(), f);
+  fclose(f);
+  return 0;
+}
+
+struct BatchSlot {   // one family's record in the workers' shared memory
+  double seconds;
+  int status, worker, device_runs, done;
+};
+
+static int run_batch(const std::string& list, const std::string& devices, const std::string& report,
+                     const std::string& models, const std::string& cpnp_cmd, const std::string& qp_cmd,
+                     const std::string& tmp, bool verbose) {
+  struct Fam { std::string in, out, trace; double cells; };
+  std::vector<Fam> fams;
+  {
+    FILE* f = fopen(list.c_str(), "rb");
+    if (!f) {
+      fprintf(stderr, "mlprobs: cannot read %s\n", list.c_str());
+      return 2;
+    }
+    char line[8192];
+    while (fgets(line, sizeof line, f)) {
+      std::istringstream ss(line);
+      Fam x;
+      if (!(ss >> x.in >> x.out)) continue;
+      ss >> x.trace;
+      fams.push_back(x);
+    }
+    fclose(f);
+  }
+  std::vector<int> devs;
+  {
+    std::stringstream ss(devices);
+    std::string tok;
+    while (std::getline(ss, tok, ',')) devs.push_back(atoi(tok.c_str()));
+    if (devs.empty()) devs.push_back(0);
+  }
+  const int n = (int)fams.size(), nw = (int)devs.size();
+  for (Fam& x : fams) x.cells = family_cells(x.in);
+  std::vector<int> order(n);
+  std::iota(order.begin(), order.end(), 0);
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return fams[a].cells > fams[b].cells; });
+  const double host_max = mlpr::Session().host_max();
+  // the shared counter and per-family records (anonymous shared memory,
+  // mapped before the fork)
+  const size_t bytes = 64 + sizeof(BatchSlot) * (size_t)std::max(n, 1);
+  void* shm = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_ANONYMOUS, -1, 0);
+  if (shm == MAP_FAILED) {
+    perror("mlprobs: mmap");
+    return 2;
+  }
+  int* next = (int*)shm;
+  BatchSlot* slot = (BatchSlot*)((char*)shm + 64);
+  memset(shm, 0, bytes);
+  const auto t0 = std::chrono::steady_clock::now();
+  std::vector<pid_t> kids;
+  for (int w = 0; w < nw; w++) {
+    fflush(nullptr);
+    const pid_t pid = fork();
+    if (pid < 0) {
+      perror("mlprobs: fork");
+      return 2;
+    }
+    if (pid > 0) {
+      kids.push_back(pid);
+      continue;
+    }
+    // ---- worker w: its device only (nothing above touched the GPU); the
+    // worker's scope ends (its context torn down) before the process exits
+    setenv("HIP_VISIBLE_DEVICES", std::to_string(devs[w]).c_str(), 1);
+    const int code = [&]() {
+      mlpr::Session session;
+      std::unique_ptr<mlpp::Tools> tools;
+      const std::string wtmp = tmp + "/w" + std::to_string(w);
+      if (!cpnp_cmd.empty()) {
+        mkdir(wtmp.c_str(), 0755);
+        tools = mlpp::external_tools(cpnp_cmd, qp_cmd, wtmp);
+      } else {
+        tools = mlpp::in_process_tools(&session);
+        if (n && fams[order[0]].cells > host_max) session.prewarm();   // overlaps the models' load
+      }
+      mlpp::Models M;
+      std::string err;
+      if (!M.load(models, err)) {
+        fprintf(stderr, "mlprobs: %s\n", err.c_str());
+        return 2;
+      }
+      for (int k; (k = __atomic_fetch_add(next, 1, __ATOMIC_RELAXED)) < n;) {
+        const Fam& x = fams[order[k]];
+        const int dev0 = session.device_runs;
+        const auto f0 = std::chrono::steady_clock::now();
+        const int st = run_family(x.in, x.out, x.trace, *tools, M, session, verbose);
+        BatchSlot& r = slot[order[k]];
+        r.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - f0).count();
+        r.status = st;
+        r.worker = w;
+        r.device_runs = session.device_runs - dev0;
+        __atomic_store_n(&r.done, 1, __ATOMIC_RELEASE);
+      }
+      return 0;
+    }();
+    fflush(nullptr);
+    exit(code);
+  }
+  int bad = 0;
+  for (pid_t p : kids) {
+    int ws = 0;
+    waitpid(p, &ws, 0);
+    if (!WIFEXITED(ws) || WEXITSTATUS(ws) != 0) bad++;
+  }
+  const double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  std::string j = "{\"families\": " + std::to_string(n) + ", \"workers\": " + std::to_string(nw) +
+                  ", \"devices\": " + json_str(devices) + ", \"wall_s\": " + json_num(wall) + ", \"runs\": [";
+  int failed = 0;
+  for (int i = 0; i < n; i++) {
+    const BatchSlot& r = slot[i];
+    const bool done = __atomic_load_n(&r.done, __ATOMIC_ACQUIRE) != 0;
+    if (!done || r.status) failed++;
+    j += std::string(i ? ", " : "") + "{\"in\": " + json_str(fams[i].in) + ", \"cells\": " + json_num(fams[i].cells) +
+         ", \"s\": " + json_num(done ? r.seconds : -1) + ", \"status\": " + std::to_string(done ? r.status : -1) +
+         ", \"worker\": " + std::to_string(done ? r.worker : -1) + ", \"device_runs\": " +
+         std::to_string(done ? r.device_runs : 0) + "}";
+  }
+  j += "], \"failed\": " + std::to_string(failed) + ", \"workers_failed\": " + std::to_string(bad) + "}\n";
+  munmap(shm, bytes);
+  if (report.empty()) {
+    fwrite(j.data(), 1, j.size(), stdout);
+  } else if (FILE* f = fopen(report.c_str(), "wb")) {
+    fwrite(j.data(), 1, j.size(), f);
+    fclose(f);
+  }
+  return failed || bad ? 1 : 0;
+}
+
 int main(int argc, char** argv) {
-  std::string models = self_dir() + "/../classifier", cpnp_cmd, qp_cmd, tmp = "/tmp", trace;
+  std::string models = self_dir() + "/../classifier", cpnp_cmd, qp_cmd, tmp = "/tmp", trace, batch, devices = "0",
+              report;
   bool verbose = true;
   std::vector<std::string> pos;
   for (int i = 1; i < argc; i++) {
@@ -191,52 +373,45 @@ int main(int argc, char** argv) {
     else if (a == "--quickprobs") qp_cmd = val();
     else if (a == "--tmp") tmp = val();
     else if (a == "--trace") trace = val();
+    else if (a == "--batch") batch = val();
+    else if (a == "--devices") devices = val();
+    else if (a == "--report") report = val();
     else if (a == "-q") verbose = false;
     else if (a == "--classify" || a == "--scores") {
       const std::string v = val();
       return probe(a, v, models);
     } else if (a == "--regions") return probe(a, "", models);
     else if (a == "-h" || a == "--help") {
-      printf("usage: mlprobs [--models DIR] [--cpnp CMD --quickprobs CMD] [--tmp DIR] [--trace FILE] [-q] in.fa [out.msa]\n");
+      printf("usage: mlprobs [--models DIR] [--cpnp CMD --quickprobs CMD] [--tmp DIR] [--trace FILE] [-q] in.fa [out.msa]\n"
+             "       mlprobs --batch LIST [--devices D0,D1,..] [--report FILE] [options]\n");
       return 0;
     } else pos.push_back(a);
   }
+  if ((!cpnp_cmd.empty()) != (!qp_cmd.empty())) {
+    fprintf(stderr, "mlprobs: --cpnp and --quickprobs go together\n");
+    return 2;
+  }
+  if (!batch.empty()) return run_batch(batch, devices, report, models, cpnp_cmd, qp_cmd, tmp, verbose);
   if (pos.empty()) {
     fprintf(stderr, "usage: mlprobs [options] in.fa [out.msa]\n");
     return 2;
   }
   const std::string in = pos[0], out = pos.size() > 1 ? pos[1] : "result.msa";
+  mlpr::Session session;
+  std::unique_ptr<mlpp::Tools> tools;
+  if (!cpnp_cmd.empty()) {
+    tools = mlpp::external_tools(cpnp_cmd, qp_cmd, tmp);
+  } else {
+    tools = mlpp::in_process_tools(&session);
+    // a family the aligners run on the device: its context starts while the
+    // models are read (the first stage, the -G line, needs it)
+    if (family_cells(in) > session.host_max()) session.prewarm();
+  }
   mlpp::Models M;
   std::string err;
   if (!M.load(models, err)) {
     fprintf(stderr, "mlprobs: %s\n", err.c_str());
     return 1;
   }
-  mlpr::Session session;
-  std::unique_ptr<mlpp::Tools> tools;
-  if (!cpnp_cmd.empty() || !qp_cmd.empty()) {
-    if (cpnp_cmd.empty() || qp_cmd.empty()) {
-      fprintf(stderr, "mlprobs: --cpnp and --quickprobs go together\n");
-      return 2;
-    }
-    tools = mlpp::external_tools(cpnp_cmd, qp_cmd, tmp);
-  } else {
-    tools = mlpp::in_process_tools(&session);
-  }
-  std::string result;
-  mlpp::Trace tr;
-  const bool ok = mlpp::run_pipeline(in, *tools, M, result, tr, err, verbose);
-  if (!trace.empty()) write_trace(trace, tr, tools->name(), session);
-  if (!ok) {
-    fprintf(stderr, "mlprobs: %s\n", err.c_str());
-    return 1;
-  }
-  FILE* f = fopen(out.c_str(), "wb");
-  if (!f) {
-    fprintf(stderr, "mlprobs: cannot write %s\n", out.c_str());
-    return 1;
-  }
-  fwrite(result.data(), 1, result.size(), f);
-  fclose(f);
-  return 0;
+  return run_family(in, out, trace, *tools, M, session, verbose);
 }

@@ -40,6 +40,9 @@ int open_device(mlp_ctx** ctx) {
   return mlp_ctx_create(0, ctx);
 }
 
+// the batch scratch of the drop-ins' device contexts (one family per process)
+constexpr size_t kDefaultScratch = 16ull << 30;
+
 // The context one run uses: a fresh host context for a small family, else
 // the session's device context (or a fresh one without a session).
 struct Ctx {
@@ -58,6 +61,7 @@ struct Ctx {
       return;
     }
     if (s) s->device_runs++;
+    if (s) s->ready();
     if (s && s->dev) {
       c = s->dev;
       return;
@@ -79,7 +83,29 @@ struct Ctx {
 }  // namespace
 
 Session::~Session() {
+  ready();
   if (dev) mlp_ctx_destroy(dev);
+}
+
+void Session::prewarm() {
+  if (dev || warm.joinable()) return;
+  const size_t scratch = scratch_bytes ? scratch_bytes : kDefaultScratch;
+  warm = std::thread([this, scratch]() {
+    mlp_ctx* c = nullptr;
+    if (open_device(&c) != MLP_OK) {
+      if (c) mlp_ctx_destroy(c);
+      return;   // the first device run opens (and reports) it again
+    }
+    if (!getenv("MLP_SCRATCH_GB")) mlp_set_scratch(c, scratch);
+    dev = c;
+  });
+}
+
+void Session::ready() {
+  if (warm.joinable()) {
+    warm.join();
+    stage("device init (prewarmed)");
+  }
 }
 
 double Session::host_max() const {
@@ -169,7 +195,7 @@ int run_cpnp(std::vector<Row> seqs, bool just_features, bool progressive, cpnp::
     // one family per process: a 16 GB batch scratch, like quickprobs (C3
     // -p 0 back to back after a large process: 3.1-3.3 s every run at 16 GB;
     // at 24 / 32 GB 3 of 4 and 2 of 4 runs stalled 4-6 s; profiles/r03d_*)
-    cx.open(session, pair_cells(lens), 16ull << 30, 1);
+    cx.open(session, pair_cells(lens), kDefaultScratch, 1);
     mlp_ctx* ctx = cx.c;
     std::string res;
     std::vector<int64_t> off(1, 0);
@@ -365,7 +391,7 @@ int run_qp(std::vector<qph::Seq> seqs, const qph::Options& opt, int threads, Ses
       for (const qph::Seq& s : seqs) lens.push_back(s.length());
       // one family per process: a 16 GB batch scratch (C3 posteriors 0.82 s
       // at 16 GB vs 6.9-7.2 s at 64 GB in a fresh process, 1.16 s at 8 GB)
-      cx.open(session, pair_cells(lens), 16ull << 30, 255);
+      cx.open(session, pair_cells(lens), kDefaultScratch, 255);
       mlp_ctx* ctx = cx.c;
       std::string res;
       std::vector<int64_t> off(1, 0);

@@ -7,6 +7,7 @@
 // process, sharing one device context through a Session.
 #pragma once
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "mlpgpu.h"
@@ -21,11 +22,18 @@ namespace mlpr {
 // use (device 0; MLP_DEVICES=<mask> opts in to the multi-GPU context).
 struct Session {
   mlp_ctx* dev = nullptr;
-  size_t scratch_bytes = 0;   // 0: the caller's default (32 GB c_p_np_aln, 16 GB quickprobs)
+  size_t scratch_bytes = 0;   // 0: the caller's default (16 GB, both aligners)
   double host_max_cells = -1; // < 0: MLP_HOST_MAX_CELLS or 4e6
   int device_runs = 0, host_runs = 0;  // aligner runs per context kind (the pipeline's trace)
   ~Session();
   double host_max() const;
+  // Start creating the device context now, on a thread: HIP's start-up
+  // (~0.2 s a process) overlaps the caller's host work (reading the models,
+  // the family); the first run that needs the device waits for it.  A failed
+  // creation is reported by that run, as without the prewarm.
+  void prewarm();
+  void ready();
+  std::thread warm;
 };
 
 // A failed run: the exit status the reference CLI would return and the

@@ -172,23 +172,33 @@ __device__ ChainView stage_chain(uint8_t* dyn, int lds_seq, int64_t ch, SeqSet s
 
 // Where one lane is in the chain: stacked row g (idle outside [0, rows)),
 // column j, member q and its row i, plus the member's values the sweeps need.
+// The per-row thresholds turn the sweeps' per-step edge and end tests into
+// one compare of j each (set when the lane enters a row, i.e. once per W
+// steps): a forward cell takes every recurrence (i >= 1, j >= 1, not (1, 1))
+// iff j >= jlo; a backward cell is inside its pair (not the last row or
+// column) iff j < jhi; the pair's last cell is j == jend; the backward's
+// first-cell records (rows 0 and 1, columns 0 and 1) need j <= jfirst.
 struct Cursor {
   int g, j, q, i, L1, L2;
   int ca;          // LDS offset of column residue j (padded column seq + j)
   int c1, c1n;     // residues i and i + 1 of the row sequence (0 outside)
+  int c1x, c1nx;   // 26 c1, 26 c1n: the rows of the match table
   float ins1, ins1n;
   int slot;
   int64_t rm, ell;
   float T5, TL;
   double zmant, rzmant;
   int zexp;
+  int jlo, jhi, jend, jfirst, jact;   // jact: L2 (an active row) or -1 (idle)
+  int jpf;   // PF backward: the cell is off rows 1, L1 and columns 1, L2 iff 2 <= j < jpf
 };
 
 __device__ __forceinline__ void locate(Cursor& c, const ChainView& C, const float* __restrict__ ins) {
   if (c.g < 0 || c.g >= C.rows) {
-    c.q = -1; c.i = -1; c.L1 = -1; c.L2 = -1; c.c1 = 0; c.c1n = 0;
+    c.q = -1; c.i = -1; c.L1 = -1; c.L2 = -1; c.c1 = 0; c.c1n = 0; c.c1x = 0; c.c1nx = 0;
     c.ca = c.j;   // the zero area
     c.ins1 = ins[0]; c.ins1n = ins[0];
+    c.jlo = 1 << 30; c.jhi = 0; c.jend = -1; c.jfirst = -1; c.jact = -1; c.jpf = 2;
     return;
   }
   int q = c.q < 0 ? 0 : c.q;
@@ -210,8 +220,16 @@ __device__ __forceinline__ void locate(Cursor& c, const ChainView& C, const floa
   c.zexp = m.zexp;
   c.c1 = C.seq[m.roff + c.i];
   c.c1n = C.seq[m.roff + c.i + 1];
+  c.c1x = 26 * c.c1;
+  c.c1nx = 26 * c.c1n;
   c.ins1 = ins[c.c1];
   c.ins1n = ins[c.c1n];
+  c.jlo = c.i >= 2 ? 1 : c.i == 1 ? 2 : 1 << 30;
+  c.jhi = c.i < c.L1 ? c.L2 : 0;
+  c.jend = c.i == c.L1 ? c.L2 : -1;
+  c.jfirst = c.i <= 1 ? 1 : -1;
+  c.jact = c.L2;
+  c.jpf = c.i >= 2 && c.i < c.L1 && c.L2 > 2 ? c.L2 : 2;
 }
 
 // forward-order cursor at step 0: lane r at u = -r
@@ -221,12 +239,18 @@ __device__ __forceinline__ void cursor_start_fwd(Cursor& c, const ChainView& C, 
   c.j = lane == 0 ? 0 : C.W - lane;
   locate(c, C, ins);
 }
-__device__ __forceinline__ void cursor_next(Cursor& c, const ChainView& C, const float* ins) {
+// on_row(): the sweep's own per-row state, after the lane entered its next row
+struct NoRowState {
+  __device__ void operator()() const {}
+};
+template <class F = NoRowState>
+__device__ __forceinline__ void cursor_next(Cursor& c, const ChainView& C, const float* ins, F on_row = F()) {
   ++c.ca;
   if (++c.j == C.W) {
     c.j = 0;
     c.g += 64;
     locate(c, C, ins);
+    on_row();
   }
 }
 // reverse-order cursor at step tau (u = tau - lane >= 0)
@@ -237,14 +261,50 @@ __device__ __forceinline__ void cursor_start_bwd(Cursor& c, const ChainView& C, 
   c.j = u % C.W;
   locate(c, C, ins);
 }
-__device__ __forceinline__ void cursor_prev(Cursor& c, const ChainView& C, const float* ins) {
+template <class F = NoRowState>
+__device__ __forceinline__ void cursor_prev(Cursor& c, const ChainView& C, const float* ins, F on_row = F()) {
   --c.ca;
   if (--c.j < 0) {
     c.j = C.W - 1;
     c.g -= 64;
     locate(c, C, ins);
+    on_row();
   }
 }
+
+// ---- scalar-addressed buffer access: a wave-uniform base built on the
+// scalar unit (a raw buffer resource; word 3 = 0x00020000, the gfx9
+// family's 32-bit data format) plus a loop-invariant per-lane byte offset,
+// so the sweeps' per-step loads and stores cost no VALU address arithmetic
+// (global stores took one or two 64-bit adds each)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wave_rsrc(const void* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, 0x7fffffff, 0x00020000);
+}
+typedef unsigned mlp_u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void bstore(const float* base, uint32_t boff, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), wave_rsrc(base), boff, 0, 0);
+}
+__device__ __forceinline__ void bstore(const int32_t* base, uint32_t boff, int32_t v) {
+  __builtin_amdgcn_raw_buffer_store_b32((unsigned)v, wave_rsrc(base), boff, 0, 0);
+}
+__device__ __forceinline__ void bstore(const double* base, uint32_t boff, double v) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(mlp_u32x2, v), wave_rsrc(base), boff, 0, 0);
+}
+__device__ __forceinline__ float bload(const float* base, uint32_t boff) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(wave_rsrc(base), boff, 0, 0));
+}
+__device__ __forceinline__ double bload(const double* base, uint32_t boff) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(wave_rsrc(base), boff, 0, 0));
+}
+
+// A chain's boundary rows are stored component-major: component k of column
+// j at base + k W + j, base = the chain's bnd_off times the components per
+// column, so a chunk's load is one coalesced access per component.  The one
+// lane that crosses the strip stores its column: the column of that lane at
+// a step is wave-uniform (a scalar counter), so the store's whole address is
+// scalar.
+template <class T>
+__device__ __forceinline__ void bnd_put(const T* comp, int j_uniform, T v) { bstore(comp + j_uniform, 0, v); }
 
 // Boundary row of the neighbouring strip, read 64 columns at a time (one per
 // lane) and double-buffered: the sweeps switch buffers between 64-step
@@ -261,19 +321,22 @@ struct BoundaryChunks {
   // back: lanes the chunk is loaded shifted up by, so that lane 63 holds the
   // segment's first column (the backward sweep's partial segments)
   __device__ __forceinline__ void load_next(const Scratch& sc, int64_t bo, int W, int col0, int lane, int back = 0) {
-    const int64_t bi = bo + min(max(col0 + lane - back, 0), W - 1);
+    const uint32_t col = (uint32_t)min(max(col0 + lane - back, 0), W - 1);
     if constexpr ((M & kHmm5) != 0) {
+      const float* b5 = sc.bnd5 + bo * 5;
 #pragma unroll
-      for (int k = 0; k < 5; ++k) n5[k] = sc.bnd5[bi * 5 + k];
+      for (int k = 0; k < 5; ++k) n5[k] = b5[k * W + col];
     }
     if constexpr ((M & kLocal) != 0) {
+      const float* bl = sc.bndl + bo * 3;
 #pragma unroll
-      for (int k = 0; k < 3; ++k) nl[k] = sc.bndl[bi * 3 + k];
+      for (int k = 0; k < 3; ++k) nl[k] = bl[k * W + col];
     }
     if constexpr ((M & kPF) != 0) {
+      const double* bz = sc.bndz + bo * 3;
 #pragma unroll
-      for (int k = 0; k < 3; ++k) nz[k] = sc.bndz[bi * 3 + k];
-      ne = sc.bnde[bi];
+      for (int k = 0; k < 3; ++k) nz[k] = bz[k * W + col];
+      ne = sc.bnde[bo + col];
     }
   }
   __device__ __forceinline__ void advance() {

@@ -75,6 +75,14 @@ __device__ __forceinline__ float mlp_log_add_t(float x, float y, const float4* _
   return (d >= 7.5f) ? hi : r;
 }
 
+// max of two non-NaN floats as one v_max_f32 (fmaxf canonicalises both
+// inputs first: two more instructions)
+__device__ __forceinline__ float mlp_max(float a, float b) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
 // LOG_ADD(LOG_ZERO, y) == max(LOG_ZERO, y) exactly: above LOG_ZERO the sentinel
 // returns y; below it the gap to LOG_ZERO exceeds the float spacing at 2e20
 // (1.6e13) and thus the 7.5 cutoff.

@@ -123,12 +123,38 @@ __global__ __launch_bounds__(256, SweepWaves<M>::fwd) void k_forward(ModelScalar
   const int lane = threadIdx.x & 63;
   const ChainView C = stage_chain<kStageFwd>(dyn, lds_seq, ch, sq, pm, cm, rec);
   const int W = C.W, S = C.S;
-  const int64_t base = cm.cell_off[ch] + 64 + lane;   // slot of step tau: base + tau * 64
+  // slot of step tau, lane l: cell0 + tau * 64 + l (a wave-uniform row
+  // pointer per step plus the lane: scalar-addressed stores, no per-step
+  // 64-bit lane arithmetic)
+  const int64_t cell0 = cm.cell_off[ch] + 64;
+  const uint32_t ul4 = (uint32_t)lane * 4;   // the lane's byte offset in a step's fp32 slots
   const int64_t bo = cm.bnd_off[ch];
+  // lane 63's column (the strip's last row, stored into the boundary row):
+  // W - 63 at step 0 (idle until step 63), one column per step, wrapping at W
+  int j63 = W - 63;
+  float* const b5 = sc.bnd5 + bo * 5;
+  float* const bl = sc.bndl + bo * 3;
+  double* const bz = sc.bndz + bo * 3;
+  int32_t* const be = sc.bnde + bo;
   const float rt1 = ms.rt1, two_rt1 = 2 * ms.rt1;
   const double pfo = ms.pf_open, pfe = ms.pf_ext;
   Cursor c;
+  // the local chain's chunk maxima (CPNP/ProbabilisticModel.h:438-447, for
+  // k_local_totals' exact skip test): per lane the column that ends its
+  // current 64-column chunk (a multiple of 64, or L2; -1 on rows without
+  // chunks) and that chunk's element of cmf; set when the lane enters a row
+  int jst = -1;
+  int64_t cmo = 0;
+  float cmx = -INFINITY;   // the chunk's running maximum (row 0 / column 0 hold LZ: no effect)
+  auto local_row = [&]() {
+    if constexpr ((M & kLocal) != 0) {
+      jst = c.q >= 0 && c.i >= 1 ? min(64, c.L2) : -1;
+      cmo = c.rm + (int64_t)(c.i - 1) * local_chunks(c.L2);
+      cmx = -INFINITY;
+    }
+  };
   cursor_start_fwd(c, C, T_.ins, lane);
+  local_row();
   // per-lane state: Lx = own cell at j-1, Ux = cell (i-1, j), Dx = (i-1, j-1)
   float L5[5], U5[5], D5[5];
   float LL[3], UL[3], DL[3];
@@ -138,7 +164,6 @@ __global__ __launch_bounds__(256, SweepWaves<M>::fwd) void k_forward(ModelScalar
   for (int k = 0; k < 5; ++k) L5[k] = U5[k] = D5[k] = LZ;
 #pragma unroll
   for (int k = 0; k < 3; ++k) LL[k] = UL[k] = DL[k] = LZ;
-  float cmx = LZ;   // running maximum of the local chain elements in the current 64-column chunk
   BoundaryChunks<M> bc;
   const int nseg = (W + 63) >> 6;
 
@@ -160,12 +185,11 @@ __global__ __launch_bounds__(256, SweepWaves<M>::fwd) void k_forward(ModelScalar
       for (int u = 0; u < 4; ++u) {
         const int t = t0 + u;
         const int i = c.i, j = c.j, L1 = c.L1, L2 = c.L2;
-        const bool act = c.q >= 0 && j <= L2;
         const bool gen = i > 1 || j > 1;
         // wave-uniform: no lane on an initial cell, row 0 or column 0 (the
         // common case away from the pairs' edges), so the recurrences' values
         // are taken as they are, without the per-lane selects of the edges
-        const bool interior = wave_none(!(i >= 1 && j >= 1 && gen));
+        const bool interior = wave_none(j < c.jlo);
         const int c1 = c.c1;
         const int c2 = C.seq[c.ca];          // residue j (0 at j = 0 and past L2)
         const float ins1 = c.ins1;
@@ -186,10 +210,10 @@ __global__ __launch_bounds__(256, SweepWaves<M>::fwd) void k_forward(ModelScalar
         // idle tail -- so whatever the chunk holds is harmless): one form of
         // the shift, no branch joining two register assignments
         bc.template shift<true, true>(t - t_lo, L5, U5, LL, UL, LZm, LZe, LZf, Le, UZm, UZe, UZf, Ue);
-        const int64_t idx = base + (int64_t)t * 64;
+        const int64_t tcell = cell0 + (int64_t)t * 64;   // wave-uniform
         // ------------------------------------------------ 5-state forward
         if constexpr ((M & kHmm5) != 0) {
-          const float mt = T_.match[c1 * 26 + c2];
+          const float mt = T_.match[c.c1x + c2];
           const float ins2 = T_.ins[c2];
           // CPNP/ProbabilisticModel.h:213-256
           float vm = D5[0] + ms.t[0][0];
@@ -218,8 +242,8 @@ __global__ __launch_bounds__(256, SweepWaves<M>::fwd) void k_forward(ModelScalar
               if (j > 0) { Cc[2] = vy1; Cc[4] = vy2; }
             }
           }
-          sc.f5[idx] = Cc[0];   // every lane: values of idle cells are never used
-          if (act && i == L1 && j == L2) {  // CPNP/ProbabilisticModel.h:415-419 (forward half)
+          bstore(sc.f5 + tcell, ul4, Cc[0]);   // every lane: values of idle cells are never used
+          if (j == c.jend) {  // CPNP/ProbabilisticModel.h:415-419 (forward half)
             float tf = LZ;
 #pragma unroll
             for (int k5 = 0; k5 < 5; ++k5) tf = mlp_log_add_t(tf, Cc[k5] + ms.init[k5], lk);
@@ -227,14 +251,14 @@ __global__ __launch_bounds__(256, SweepWaves<M>::fwd) void k_forward(ModelScalar
           }
           if (lane == 63) {
 #pragma unroll
-            for (int k5 = 0; k5 < 5; ++k5) sc.bnd5[(bo + j) * 5 + k5] = Cc[k5];
+            for (int k5 = 0; k5 < 5; ++k5) bnd_put(b5 + k5 * W, j63, Cc[k5]);
           }
 #pragma unroll
           for (int k5 = 0; k5 < 5; ++k5) L5[k5] = Cc[k5];
         }
         // ------------------------------------------------ local forward
         if constexpr ((M & kLocal) != 0) {
-          const float mt = T_.match[c1 * 26 + c2];
+          const float mt = T_.match[c.c1x + c2];
           const float ins2 = T_.ins[c2];
           const float bs = mt - ins1 - ins2;
           float vm = bs - two_rt1;
@@ -254,18 +278,20 @@ __global__ __launch_bounds__(256, SweepWaves<M>::fwd) void k_forward(ModelScalar
               if (j > 0) Cy = vy;
             }
           }
-          sc.fl[idx] = Cm;
+          bstore(sc.fl + tcell, ul4, Cm);
           if (lane == 63) {
-            sc.bndl[(bo + j) * 3 + 0] = Cm;
-            sc.bndl[(bo + j) * 3 + 1] = Cx;
-            sc.bndl[(bo + j) * 3 + 2] = Cy;
+            bnd_put(bl + 0 * W, j63, Cm);
+            bnd_put(bl + 1 * W, j63, Cx);
+            bnd_put(bl + 2 * W, j63, Cy);
           }
-          // the chain total's input (CPNP/ProbabilisticModel.h:438-447): the
-          // largest f_M of each 64-column chunk of the row, for
-          // k_local_totals' exact skip test
-          if (act && i >= 1 && j >= 1) {
-            cmx = ((j - 1) & 63) == 0 ? Cm : fmaxf(cmx, Cm);
-            if ((j & 63) == 0 || j == L2) sc.cmf[c.rm + (int64_t)(i - 1) * local_chunks(L2) + ((j - 1) >> 6)] = cmx;
+          // the chain total's input: the largest f_M of each 64-column chunk
+          // of the row (from column 0, whose LZ never exceeds a real value)
+          cmx = mlp_max(cmx, Cm);
+          if (j == jst) {
+            sc.cmf[cmo] = cmx;
+            ++cmo;
+            jst = min(jst + 64, L2);
+            cmx = -INFINITY;
           }
           LL[0] = Cm; LL[1] = Cx; LL[2] = Cy;
         }
@@ -295,27 +321,27 @@ __global__ __launch_bounds__(256, SweepWaves<M>::fwd) void k_forward(ModelScalar
             Zm = ((M & kQP) != 0 ? (dZm + dZf) + dZe : (dZm + dZe) + dZf) * score;
             pf_rescale_fast(Zm, Ze, Zf, E);
           }
-          sc.zm[idx] = mlp_pf_pack(Zm, E);
-          if (act) {
-            // QuickProbs' plain double has no such stop; frames past 2^50000 are
-            // ours.  Frames reach 81 (2^16200) only near overflow: the
-            // three-way maximum runs only when some lane's frame got there
-            if (!wave_none(E > ((M & kQP) != 0 ? 250 : 80)))
-              if ((M & kQP) != 0 ? E > 250 : mlp_pf_ldbl_overflow(Zm, Ze, Zf, E)) atomicOr(&rec[c.slot].flags, 1);
-            if (i == L1 && j == L2) {  // CPNP/MSAPartProbs.cpp:591,612; QP/PartitionFunction.cpp:132,155
-              rec[c.slot].zmant = (M & kQP) != 0 ? (Zm + Zf) + Ze : (Zm + Ze) + Zf;
-              rec[c.slot].zexp = E;
-            }
+          bstore(sc.zm + tcell, 2 * ul4, mlp_pf_pack(Zm, E));
+          // QuickProbs' plain double has no such stop; frames past 2^50000 are
+          // ours.  Frames reach 81 (2^16200) only near overflow: the
+          // three-way maximum runs only when some active lane's frame got there
+          if (!wave_none(E > ((M & kQP) != 0 ? 250 : 80) && j <= c.jact))
+            if (j <= c.jact && ((M & kQP) != 0 ? E > 250 : mlp_pf_ldbl_overflow(Zm, Ze, Zf, E)))
+              atomicOr(&rec[c.slot].flags, 1);
+          if (j == c.jend) {  // CPNP/MSAPartProbs.cpp:591,612; QP/PartitionFunction.cpp:132,155
+            rec[c.slot].zmant = (M & kQP) != 0 ? (Zm + Zf) + Ze : (Zm + Ze) + Zf;
+            rec[c.slot].zexp = E;
           }
           if (lane == 63) {
-            sc.bndz[(bo + j) * 3 + 0] = Zm;
-            sc.bndz[(bo + j) * 3 + 1] = Ze;
-            sc.bndz[(bo + j) * 3 + 2] = Zf;
-            sc.bnde[bo + j] = E;
+            bnd_put(bz + 0 * W, j63, Zm);
+            bnd_put(bz + 1 * W, j63, Ze);
+            bnd_put(bz + 2 * W, j63, Zf);
+            bnd_put(be, j63, E);
           }
           LZm = Zm; LZe = Ze; LZf = Zf; Le = E;
         }
-        cursor_next(c, C, T_.ins);
+        cursor_next(c, C, T_.ins, local_row);
+        j63 = j63 + 1 == W ? 0 : j63 + 1;
       }
     }
   }
@@ -339,13 +365,36 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
   const int lane = threadIdx.x & 63;
   const ChainView C = stage_chain<kStageBwd>(dyn, lds_seq, ch, sq, pm, cm, rec);
   const int W = C.W, S = C.S;
-  const int64_t base = cm.cell_off[ch] + 64 + lane;
+  const int64_t cell0 = cm.cell_off[ch] + 64;   // slot of step tau, lane l: cell0 + tau * 64 + l
+  const uint32_t ul4 = (uint32_t)lane * 4;     // the lane's byte offset in a step's fp32 slots
   const int64_t bo = cm.bnd_off[ch];
+  float* const b5 = sc.bnd5 + bo * 5;
+  float* const bl = sc.bndl + bo * 3;
+  double* const bz = sc.bndz + bo * 3;
+  int32_t* const be = sc.bnde + bo;
   const float rt1 = ms.rt1, two_rt1 = 2 * ms.rt1;
   const double pfo = ms.pf_open, pfe = ms.pf_ext;
   const int top = S * W + 62;   // last step with an active lane (lane 63, column W-1)
+  // lane 0's column (the strip's first row, stored into the boundary row):
+  // top mod W at the first step, one column less per step, wrapping to W - 1
+  int j0 = top % W;
   Cursor c;
+  // the local chain's chunk maxima, columns descending: a chunk starts at
+  // its top column (L2 or a multiple of 64) and ends at 64 c + 1, where its
+  // element of cmb is stored; per lane the next such column (-1 on rows
+  // without chunks) and its element, set when the lane enters a row (every
+  // active lane enters at column W - 1)
+  int jsb = -1;
+  int64_t cmob = 0;
+  float cmx = -INFINITY;
+  auto local_row = [&]() {
+    if constexpr ((M & kLocal) != 0) {
+      jsb = c.q >= 0 && c.i >= 1 ? ((c.L2 - 1) & ~63) + 1 : -1;
+      cmob = c.rm + (int64_t)(c.i - 1) * local_chunks(c.L2) + ((c.L2 - 1) >> 6);
+    }
+  };
   cursor_start_bwd(c, C, T_.ins, lane, top);
+  local_row();
   // Rx = own cell (i, j+1), Nx = (i+1, j), Gx = (i+1, j+1)
   float R5[5], N5[5], G5[5];
   float RL[3], NL[3], GL[3];
@@ -355,7 +404,6 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
   for (int k = 0; k < 5; ++k) R5[k] = N5[k] = G5[k] = LZ;
 #pragma unroll
   for (int k = 0; k < 3; ++k) RL[k] = NL[k] = GL[k] = LZ;
-  float cmx = LZ;   // running maximum of the local chain elements in the current 64-column chunk
   BoundaryChunks<M> bc;
   const int nseg = (W + 63) >> 6;
   // the step-t loads of f5 / zm are issued kPrefetch steps earlier into
@@ -366,9 +414,9 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
   double qz[kPrefetch] = {};
 #pragma unroll
   for (int k = 0; k < kPrefetch; ++k) {
-    const int64_t at = base + (int64_t)(top - k) * 64;
-    if constexpr ((M & kHmm5) != 0) q5[k] = sc.f5[at];
-    if constexpr ((M & kPF) != 0) qz[k] = sc.zm[at];
+    const int64_t at = cell0 + (int64_t)(top - k) * 64;
+    if constexpr ((M & kHmm5) != 0) q5[k] = bload(sc.f5 + at, ul4);
+    if constexpr ((M & kPF) != 0) qz[k] = bload(sc.zm + at, 2 * ul4);
   }
 
   // segments, in processing order: lane 63's 64-column chunks of strip k
@@ -397,11 +445,10 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
       for (int u = 0; u < kPrefetch; ++u) {
         const int t = t0 - u;
         const int i = c.i, j = c.j, L1 = c.L1, L2 = c.L2;
-        const bool act = c.q >= 0 && j <= L2;
         const bool in_i = i < L1, in_j = j < L2;
         // wave-uniform: every lane inside its pair (not the last row, column
         // or cell), so the recurrences run without the edge selects
-        const bool interior = wave_none(!(in_i && in_j && !(i == L1 && j == L2)));
+        const bool interior = wave_none(j >= c.jhi);
         const float f5v = q5[u];
         const double zmv = qz[u];
         const int c1 = c.c1, c1n = c.c1n;
@@ -423,11 +470,11 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
         // (one form of the shift: lane 63's down value is unused in the last
         // strip -- the chain's last row, in_i false -- and in the skew head)
         bc.template shift<false, true>(t - t_lo, R5, N5, RL, NL, RZm, RZe, RZf, Re, NZm, NZe, NZf, Ne);
-        const int64_t idx = base + (int64_t)t * 64;
+        const int64_t tcell = cell0 + (int64_t)t * 64;   // wave-uniform
         // ------------------------------------------------ 5-state backward
         if constexpr ((M & kHmm5) != 0) {
           const float ins2n = T_.ins[c2n];
-          const float mn = T_.match[c1n * 26 + c2n];
+          const float mn = T_.match[c.c1nx + c2n];
           float B[5];
           // CPNP/ProbabilisticModel.h:310-313, 340-378
           const float pxy = G5[0] + mn;
@@ -460,15 +507,15 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
             B[4] = mlp_log_add_t(B[4], R5[4] + ins2n + ms.t[4][4], lk);
           }
           }  // !interior
-          sc.f5[idx] = f5v + B[0];   // f + b (CPNP/ProbabilisticModel.h:484)
-          if (act) {
+          bstore(sc.f5 + tcell, ul4, f5v + B[0]);   // f + b (CPNP/ProbabilisticModel.h:484)
+          if (j <= c.jfirst) {   // rows 0 and 1, columns 0 and 1 of an active pair
             if (i == 1 && j == 1) rec[c.slot].b5[0] = B[0];
             if (i == 1 && j == 0) { rec[c.slot].b5[1] = B[1]; rec[c.slot].b5[3] = B[3]; }
             if (i == 0 && j == 1) { rec[c.slot].b5[2] = B[2]; rec[c.slot].b5[4] = B[4]; }
           }
           if (lane == 0) {
 #pragma unroll
-            for (int k5 = 0; k5 < 5; ++k5) sc.bnd5[(bo + j) * 5 + k5] = B[k5];
+            for (int k5 = 0; k5 < 5; ++k5) bnd_put(b5 + k5 * W, j0, B[k5]);
           }
 #pragma unroll
           for (int k5 = 0; k5 < 5; ++k5) R5[k5] = B[k5];
@@ -476,7 +523,7 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
         // ------------------------------------------------ local backward
         if constexpr ((M & kLocal) != 0) {
           const float ins2n = T_.ins[c2n];
-          const float mn = T_.match[c1n * 26 + c2n];
+          const float mn = T_.match[c.c1nx + c2n];
           float Bm = MLP_LOG_ONE, Bx = LZ, By = LZ;
           if (interior) {
             const float pxy = GL[0] + mn - ins1n - ins2n;
@@ -503,18 +550,25 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
             By = mlp_log_add_t(By, RL[2] + ms.lt[2][2] - rt1, lk);
           }
           }  // !interior
-          sc.bl[idx] = Bm;   // f + b is formed by the merge (the same float add)
+          bstore(sc.bl + tcell, ul4, Bm);   // f + b is formed by the merge (the same float add)
           if (lane == 0) {
-            sc.bndl[(bo + j) * 3 + 0] = Bm;
-            sc.bndl[(bo + j) * 3 + 1] = Bx;
-            sc.bndl[(bo + j) * 3 + 2] = By;
+            bnd_put(bl + 0 * W, j0, Bm);
+            bnd_put(bl + 1 * W, j0, Bx);
+            bnd_put(bl + 2 * W, j0, By);
           }
           // chain element (CPNP/ProbabilisticModel.h:444-445); columns descend,
-          // so a chunk starts at its top column and ends at 64c + 1
-          if (act && i >= 1 && j >= 1) {
-            const float e = Bm + T_.match[c1 * 26 + c2] - ins1 - T_.ins[c2] - two_rt1;
-            cmx = ((j & 63) == 0 || j == L2) ? e : fmaxf(cmx, e);
-            if (((j - 1) & 63) == 0) sc.cmb[c.rm + (int64_t)(i - 1) * local_chunks(L2) + ((j - 1) >> 6)] = cmx;
+          // so a chunk starts at its top column (L2: idle columns above it are
+          // dropped there; or a multiple of 64: reset by the store before it)
+          // and ends at 64c + 1
+          {
+            const float e = Bm + T_.match[c.c1x + c2] - ins1 - T_.ins[c2] - two_rt1;
+            cmx = j == L2 ? e : mlp_max(cmx, e);
+            if (j == jsb) {
+              sc.cmb[cmob] = cmx;
+              --cmob;
+              jsb -= 64;
+              cmx = -INFINITY;
+            }
           }
           RL[0] = Bm; RL[1] = Bx; RL[2] = By;
         }
@@ -526,7 +580,7 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
           float post = 0.0f;
           const double score = T_.sub[c2 * 26 + c1];
           // wave-uniform: every lane strictly inside rows 2..L1-1, columns 2..L2-1
-          const bool pf_inner = wave_none(!(i >= 2 && i < L1 && j >= 2 && j < L2));
+          const bool pf_inner = wave_none((uint32_t)(j - 2) >= (uint32_t)(c.jpf - 2));
           if (i >= 1 && j >= 1) {
             double nZm = NZm, nZe = NZe, nZf = NZf, rZm = RZm, rZe = RZe, rZf = RZf;
             double gZm = GZm, gZe = GZe, gZf = GZf;
@@ -555,7 +609,7 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
             }
             Zm = ((M & kQP) != 0 ? (gZm + gZe) + gZf : (gZm + gZf) + gZe) * score;  // QP/PartitionFunction.cpp:260
             pf_rescale_fast(Zm, Ze, Zf, E);
-            if (act) {
+            if (j <= c.jact) {
               int ef;
               const double zf = mlp_pf_unpack(zmv, &ef);
               // C_P_NP_Aln (long double in the reference, parity within 1e-4):
@@ -576,21 +630,22 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
               if constexpr ((M & kQP) != 0) post = (post <= 1.0f && post >= 0.001f) ? post : 0.0f;
             }
           }
-          sc.pg[idx * sc.pg_stride] = post;   // after this cell's zm was read (prefetch)
+          bstore(sc.pg + tcell * sc.pg_stride, ul4 * sc.pg_stride, post);   // after this cell's zm was read (prefetch)
           if (lane == 0) {
-            sc.bndz[(bo + j) * 3 + 0] = Zm;
-            sc.bndz[(bo + j) * 3 + 1] = Ze;
-            sc.bndz[(bo + j) * 3 + 2] = Zf;
-            sc.bnde[bo + j] = E;
+            bnd_put(bz + 0 * W, j0, Zm);
+            bnd_put(bz + 1 * W, j0, Ze);
+            bnd_put(bz + 2 * W, j0, Zf);
+            bnd_put(be, j0, E);
           }
           RZm = Zm; RZe = Ze; RZf = Zf; Re = E;
         }
         // refill slot u after its value is dead, so the load reuses the register
         // (a loop-carried copy of a pending load would drain vmcnt)
-        const int64_t at = base + (int64_t)max(t - kPrefetch, -1) * 64;
-        if constexpr ((M & kHmm5) != 0) q5[u] = sc.f5[at];
-        if constexpr ((M & kPF) != 0) qz[u] = sc.zm[at];
-        cursor_prev(c, C, T_.ins);
+        const int64_t at = cell0 + (int64_t)max(t - kPrefetch, -1) * 64;
+        if constexpr ((M & kHmm5) != 0) q5[u] = bload(sc.f5 + at, ul4);
+        if constexpr ((M & kPF) != 0) qz[u] = bload(sc.zm + at, 2 * ul4);
+        cursor_prev(c, C, T_.ins, local_row);
+        j0 = j0 == 0 ? W - 1 : j0 - 1;
       }
     }
   }

@@ -97,10 +97,11 @@ __global__ __launch_bounds__(256) void k_viterbi(ModelScalars ms, const Tables* 
             if (best < tv[k3]) { best = tv[k3]; st = k3; }
           vo.state[c.slot] = st;
         }
-        if (lane == 63) {
-          sc.bndl[(bo + j) * 3 + 0] = V0;
-          sc.bndl[(bo + j) * 3 + 1] = V1;
-          sc.bndl[(bo + j) * 3 + 2] = V2;
+        if (lane == 63) {   // the boundary row, component-major (mlp_chain.h)
+          float* const bl = sc.bndl + bo * 3;
+          (bl + 0 * W)[(uint32_t)j] = V0;
+          (bl + 1 * W)[(uint32_t)j] = V1;
+          (bl + 2 * W)[(uint32_t)j] = V2;
         }
         LV[0] = V0; LV[1] = V1; LV[2] = V2;
         cursor_next(c, C, T_.ins);

@@ -51,7 +51,7 @@ def test_full_single_gpu_record_compacts():
     # round 5's record plus what this round's legs add: the per-family
     # differences of the C5 leg
     out['c5_pipeline']['differing'] = [{'name': f'ox/fam{k:03d}', 'path': 'RIR', 'first_stage': 'features_line',
-                                        'cause': 'race' if k % 3 else 'unattributed'} for k in range(40)]
+                                        'cause': 'race' if k % 3 else 'unexplained: reference reproducible'} for k in range(40)]
     line = b.compact_line(out)
     s = json.dumps(line)
     assert len(s) < b.LINE_LIMIT < LIMIT

@@ -231,3 +231,47 @@ def test_ragged_realignment_raises_like_reference(tmp_path):
     assert r.returncode == 1, r.stderr.decode()
     assert b'IndexError' in r.stderr
     assert not out.exists()
+
+
+def test_batch_two_workers_match_separate_runs(tmp_path):
+    """mlprobs --batch (C5 at family level: one worker process per device,
+    largest family first from a shared counter, one context per worker) with
+    two workers over every fixture family: each family's output and trace
+    equal the reference pipeline's, as the separate per-family runs do."""
+    tags = families()
+    lst = tmp_path / 'list.txt'
+    with open(lst, 'w') as fh:
+        for t in tags:
+            fh.write(f"{os.path.join(FIX, t + '.fa')}\t{tmp_path / (t + '.msa')}\t{tmp_path / (t + '.json')}\n")
+    report = tmp_path / 'report.json'
+    r = subprocess.run([BIN, '-q', '--batch', str(lst), '--devices', '0,0', '--report', str(report)],
+                       capture_output=True, timeout=900, env=ENV)
+    assert r.returncode == 0, r.stderr.decode()[-3000:]
+    with open(report) as fh:
+        rep = json.load(fh)
+    assert rep['families'] == len(tags) and rep['workers'] == 2 and rep['failed'] == 0
+    assert {x['worker'] for x in rep['runs']} == {0, 1}
+    assert all(x['status'] == 0 and x['s'] > 0 for x in rep['runs'])
+    for t in tags:
+        rec = load(t)
+        with open(tmp_path / (t + '.msa'), encoding='latin-1') as fh:
+            assert fh.read() == rec['final'], t
+        with open(tmp_path / (t + '.json')) as fh:
+            check_trace(rec, json.load(fh), t)
+
+
+def test_batch_reports_failed_family(tmp_path):
+    """A family the pipeline rejects fails alone: the others are written and
+    the exit status and report say which one failed."""
+    bad = tmp_path / 'bad.fa'
+    bad.write_text('>only\nACDE\n')   # one sequence: the reference pipeline raises
+    good = families()[0]
+    lst = tmp_path / 'list.txt'
+    lst.write_text(f"{bad}\t{tmp_path / 'bad.msa'}\n{os.path.join(FIX, good + '.fa')}\t{tmp_path / 'good.msa'}\n")
+    r = subprocess.run([BIN, '-q', '--batch', str(lst), '--devices', '0'], capture_output=True, timeout=600, env=ENV)
+    assert r.returncode == 1
+    rep = json.loads(r.stdout)
+    st = {os.path.basename(x['in']): x['status'] for x in rep['runs']}
+    assert st['bad.fa'] != 0 and st[good + '.fa'] == 0 and rep['failed'] == 1
+    with open(tmp_path / 'good.msa', encoding='latin-1') as fh:
+        assert fh.read() == load(good)['final']
