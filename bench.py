@@ -742,6 +742,7 @@ def c5_pipeline(args):
     reference CLIs' (the reference's multi-threaded quickprobs and
     time-seeded -p 1 make this informative only; byte parity at every stage
     is pinned by tests/test_pipeline.py and tests/test_heavy_gpu.py)."""
+    import hashlib
     import lzma
     bin_ = os.path.join(ROOT, 'mlprobs_amd', 'cli', 'mlprobs')
     ref_cp = os.path.join(ROOT, 'oracle', '_ref', 'c_p_np_aln')
@@ -796,6 +797,7 @@ def c5_pipeline(args):
             with open(trace) as fh:
                 tr = json.load(fh)
             rec['device'] = tr.get('device_runs', 0) > 0
+            rec['sha1'] = hashlib.sha1(mine.encode('latin-1')).hexdigest()
             calls += tr['quickprobs_calls']
             paths[tr['path']] = paths.get(tr['path'], 0) + 1
             sp_o.append(sp_score(mine))
@@ -886,9 +888,71 @@ def c5_pipeline(args):
         res['reference_clis_families'] = len(sp_r)
         res['reference_clis_sp_un_sp_mean'] = mean(sp_r)
         res['reference_clis_tc_vs_published_mean'] = mean(tc_r)
-    if args.only_c5:
-        res['runs'] = recs
+    res['runs'] = recs
     log(f"c5: {len(recs)} families in {res['wall_s']:.0f} s, {len(dev)} on the device")
+    return res
+
+
+def c5_batch(args, devices, per_process=None):
+    """C5 at family level over the GPUs (`mlprobs --batch`): one worker
+    process per device, forked before any GPU call, each keeping one device
+    context for all its families and taking the next family, largest first,
+    from a shared counter; every TEST/ox + TEST/sabre family, outputs written
+    as separate runs write them.  Wall time of the whole benchmark and the
+    per-family seconds inside the workers; with the per-process leg's records
+    (per_process), how many outputs are byte-identical to those runs'."""
+    import hashlib
+    import lzma
+    bin_ = os.path.join(ROOT, 'mlprobs_amd', 'cli', 'mlprobs')
+    if not os.path.exists(bin_):
+        return None
+    with lzma.open(os.path.join(ROOT, 'tests', 'golden', 'sweep.json.xz'), 'rt') as fh:
+        fams = json.load(fh)
+    names = [k for k in sorted(fams) if k.split('/')[0] in ('ox', 'sabre')]
+    if args.c5_stride > 1:
+        names = names[::args.c5_stride]
+    with tempfile.TemporaryDirectory() as td:
+        lines = []
+        for k, name in enumerate(names):
+            fa = os.path.join(td, f'f{k}.fa')
+            with open(fa, 'wb') as fh:
+                fh.write(fams[name]['fa'].encode('latin-1'))
+            lines.append(f"{fa}\t{os.path.join(td, f'f{k}.msa')}\n")
+        lst, rep = os.path.join(td, 'list.txt'), os.path.join(td, 'report.json')
+        with open(lst, 'w') as fh:
+            fh.writelines(lines)
+        log(f'c5 batch: {len(names)} families over devices {devices}')
+        t0 = time.perf_counter()
+        r = subprocess.run([bin_, '-q', '--batch', lst, '--devices', devices, '--report', rep], capture_output=True,
+                           timeout=1800)
+        wall = time.perf_counter() - t0
+        if not os.path.exists(rep):
+            return {'error': r.stderr.decode(errors='replace')[-400:]}
+        with open(rep) as fh:
+            report = json.load(fh)
+        sha = {}
+        for k, name in enumerate(names):
+            p = os.path.join(td, f'f{k}.msa')
+            if os.path.exists(p):
+                with open(p, 'rb') as fh:
+                    sha[name] = hashlib.sha1(fh.read()).hexdigest()
+    runs = report['runs']
+    secs = [x['s'] for x in runs if x['status'] == 0]
+    dev = [x['s'] for x in runs if x['status'] == 0 and x['device_runs'] > 0]
+    res = {'families': len(names), 'devices': devices, 'workers': report['workers'], 'failed': report['failed'],
+           'wall_s': wall, 'wall_s_inside': report['wall_s'],
+           's_per_family': {'median': float(np.median(secs)), 'mean': float(np.mean(secs)),
+                            'total': float(np.sum(secs))} if secs else None,
+           'device_path': {'families': len(dev), 'median': float(np.median(dev)), 'mean': float(np.mean(dev))}
+           if dev else None,
+           'mode': 'mlprobs --batch: one worker process per device, one context per worker, largest family first'}
+    if per_process:
+        pp = {x['name']: x.get('sha1') for x in per_process}
+        both = [n for n in names if n in sha and pp.get(n)]
+        res['identical_to_per_process'] = sum(sha[n] == pp[n] for n in both)
+        res['compared'] = len(both)
+    log(f"c5 batch: {len(names)} families in {wall:.1f} s ({report['workers']} workers), "
+        f"{res.get('identical_to_per_process')} of {res.get('compared')} identical to the per-process runs")
     return res
 
 
@@ -1014,8 +1078,8 @@ def compact_line(out):
     roofline, cpu_baseline, parity and summaries of every leg; the per-run
     and per-family detail stays in the side file (DETAIL_PATH).  Sections
     are dropped, least important first, if the line would pass LINE_LIMIT."""
-    line = {k: v for k, v in out.items() if k not in ('e2e', 'c5_pipeline', 'relax', 'ranks', 'hbm_stream',
-                                                       'virtual_shards', 'parity')}
+    line = {k: v for k, v in out.items() if k not in ('e2e', 'c5_pipeline', 'c5_batch', 'relax', 'ranks',
+                                                       'hbm_stream', 'virtual_shards', 'parity')}
     if out.get('parity'):
         line['parity'] = _pick(out['parity'], 'pairs', 'max_rel_err', 'violations', 'inexact',
                                'symmetric_difference', 'distance_max_rel_err', 'bit_exact')
@@ -1033,6 +1097,8 @@ def compact_line(out):
                           'store_hash': r['store_hash'][:16]} for r in out['ranks']]
     if out.get('c5_pipeline'):
         line['c5_pipeline'] = compact_c5(out['c5_pipeline'])
+    if out.get('c5_batch'):
+        line['c5_batch'] = {k: v for k, v in out['c5_batch'].items() if k != 'mode'}
     if out.get('e2e'):
         line['e2e'] = compact_e2e(out['e2e'])
     line['detail'] = os.path.relpath(DETAIL_PATH, ROOT) if DETAIL_PATH.startswith(ROOT) else DETAIL_PATH
@@ -1097,6 +1163,8 @@ def main():
     stream = hbm_stream() if (world == 1 and not args.host) else None
     e2e = e2e_families(args) if (not args.no_e2e and world == 1) else None
     c5 = c5_pipeline(args) if (not args.no_e2e and not args.no_c5 and world == 1 and rank == 0) else None
+    c5b = c5_batch(args, '0', c5.get('runs') if c5 else None) \
+        if (not args.no_e2e and not args.no_c5 and world == 1 and rank == 0 and not args.host) else None
     if args.relax < 0:
         args.relax = 4 if world == 1 else 1
     fam_in = synth.family(args.n, args.len, args.s, seed=args.seed)
@@ -1194,6 +1262,16 @@ def main():
         fam = None
         log('virtual shards')
         shards_info = shard_gather(args, seqs, post_hash, relax_info['round1_hash'] if relax_info else None)
+    if world > 1 and not args.host and not args.no_c5 and not args.no_e2e:
+        # C5 at family level over all N GPUs: the ranks release their
+        # contexts first, then rank 0's workers take one device each
+        fam.close()
+        fam = None
+        barrier_host = dist.barrier
+        barrier_host()
+        if rank == 0:
+            c5b = c5_batch(args, ','.join(str(d) for d in range(world)))
+        barrier_host()
     out = None
     if rank == 0:
         cpu, parity = None, None
@@ -1253,6 +1331,8 @@ def main():
             out['e2e'] = e2e
         if c5 is not None:
             out['c5_pipeline'] = c5
+        if c5b is not None:
+            out['c5_batch'] = c5b
         if qp_info is not None:
             out['quickprobs'] = qp_info
         if shards_info is not None:

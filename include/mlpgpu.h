@@ -269,6 +269,18 @@ int mlp_allgather(mlp_ctx *ctx);
  * plus mlp_csr_import. */
 int mlp_relax_range(mlp_ctx *ctx, int64_t r0, int64_t r1);
 
+/* The process's device memory pool (per device): contexts take their
+ * large buffers (batch scratch, CSR store, relaxation and gather buffers)
+ * from blocks the process keeps, and a destroyed context's buffers go back
+ * to the pool, not to the driver -- a fresh allocation right after a large
+ * release can wait seconds while the driver clears it, so a context created
+ * after another (a new family, the shards of a mask) reuses its memory.
+ * mlp_pool_info: bytes held in blocks and the part of them free;
+ * mlp_pool_trim: blocks with nothing in use back to the driver (also done
+ * automatically when an allocation fails). */
+int mlp_pool_info(int device, uint64_t *held, uint64_t *free_bytes);
+int mlp_pool_trim(int device);
+
 /* Wait for all device work of the context. */
 int mlp_synchronize(mlp_ctx *ctx);
 

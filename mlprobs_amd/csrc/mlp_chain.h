@@ -20,23 +20,24 @@ template <bool H> struct LdsHmmPart {
   float match[26 * 26];
 };
 template <> struct LdsHmmPart<false> {};
-template <bool P> struct LdsPfPart { double sub[26 * 26], rsub[26 * 26]; };
+template <bool P> struct LdsPfPart { double sub[26 * 26]; };
 template <> struct LdsPfPart<false> {};
-template <bool H, bool P>
-struct LdsTablesT : LdsHmmPart<H>, LdsPfPart<P> {
+template <bool R> struct LdsPfRecip { double rsub[26 * 26]; };   // the PF backward's quotient only
+template <> struct LdsPfRecip<false> {};
+template <bool H, bool P, bool R = false>
+struct LdsTablesT : LdsHmmPart<H>, LdsPfPart<P>, LdsPfRecip<R> {
   float ins[26];   // row insert emissions (every cursor)
 };
-template <int M>
-using LdsTablesFor = LdsTablesT<(M & (kHmm5 | kLocal)) != 0, (M & kPF) != 0>;
+// RECIP: the PF backward sweep, which also reads the reciprocals
+template <int M, bool RECIP = false>
+using LdsTablesFor = LdsTablesT<(M & (kHmm5 | kLocal)) != 0, (M & kPF) != 0, RECIP && (M & kPF) != 0>;
 
-template <bool H, bool P>
-__device__ __forceinline__ void stage_tables(LdsTablesT<H, P>& L, const Tables* __restrict__ tab) {
+template <bool H, bool P, bool R>
+__device__ __forceinline__ void stage_tables(LdsTablesT<H, P, R>& L, const Tables* __restrict__ tab) {
   for (int k = threadIdx.x; k < 26 * 26; k += blockDim.x) {
     if constexpr (H) L.match[k] = tab->match[k];
-    if constexpr (P) {
-      L.sub[k] = tab->sub[k];
-      L.rsub[k] = tab->rsub[k];
-    }
+    if constexpr (P) L.sub[k] = tab->sub[k];
+    if constexpr (R) L.rsub[k] = tab->rsub[k];
   }
   if (threadIdx.x < 26) L.ins[threadIdx.x] = tab->ins[threadIdx.x];
   if constexpr (H) {
@@ -44,8 +45,8 @@ __device__ __forceinline__ void stage_tables(LdsTablesT<H, P>& L, const Tables* 
   }
   __syncthreads();
 }
-template <bool H, bool P>
-__device__ __forceinline__ const float4* lookup_of(const LdsTablesT<H, P>& L) {
+template <bool H, bool P, bool R>
+__device__ __forceinline__ const float4* lookup_of(const LdsTablesT<H, P, R>& L) {
   if constexpr (H) return L.lk;
   else return nullptr;
 }
@@ -191,6 +192,8 @@ struct Cursor {
   int zexp;
   int jlo, jhi, jend, jfirst, jact;   // jact: L2 (an active row) or -1 (idle)
   int jpf;   // PF backward: the cell is off rows 1, L1 and columns 1, L2 iff 2 <= j < jpf
+  int jm;    // merge: a cell of the pair (i >= 1, 1 <= j <= L2) iff (unsigned)(j - 1) < jm
+  int64_t ellx;   // merge: the row's first ELL slot, (ell + i - 1) * kEll
 };
 
 __device__ __forceinline__ void locate(Cursor& c, const ChainView& C, const float* __restrict__ ins) {
@@ -198,7 +201,7 @@ __device__ __forceinline__ void locate(Cursor& c, const ChainView& C, const floa
     c.q = -1; c.i = -1; c.L1 = -1; c.L2 = -1; c.c1 = 0; c.c1n = 0; c.c1x = 0; c.c1nx = 0;
     c.ca = c.j;   // the zero area
     c.ins1 = ins[0]; c.ins1n = ins[0];
-    c.jlo = 1 << 30; c.jhi = 0; c.jend = -1; c.jfirst = -1; c.jact = -1; c.jpf = 2;
+    c.jlo = 1 << 30; c.jhi = 0; c.jend = -1; c.jfirst = -1; c.jact = -1; c.jpf = 2; c.jm = 0; c.ellx = 0;
     return;
   }
   int q = c.q < 0 ? 0 : c.q;
@@ -230,6 +233,8 @@ __device__ __forceinline__ void locate(Cursor& c, const ChainView& C, const floa
   c.jfirst = c.i <= 1 ? 1 : -1;
   c.jact = c.L2;
   c.jpf = c.i >= 2 && c.i < c.L1 && c.L2 > 2 ? c.L2 : 2;
+  c.jm = c.i >= 1 ? c.L2 : 0;
+  c.ellx = (c.ell + c.i - 1) * kEll;
 }
 
 // forward-order cursor at step 0: lane r at u = -r
@@ -339,6 +344,8 @@ struct BoundaryChunks {
       ne = sc.bnde[bo + col];
     }
   }
+  uint8_t* area = nullptr;   // (interface of LdsBoundaryChunks; unused)
+  __device__ __forceinline__ void advance(int) { advance(); }
   __device__ __forceinline__ void advance() {
 #pragma unroll
     for (int k = 0; k < 5; ++k) c5[k] = n5[k];
@@ -390,6 +397,111 @@ struct BoundaryChunks {
         Zf = SHR ? mlp_shr1zd(sZf) : mlp_shl1zd(sZf);
         e = SHR ? mlp_shr1zi(se) : mlp_shl1zi(se);
       }
+    }
+  }
+};
+
+// The same boundary chunk staged in LDS (the posterior sweeps): at a
+// segment's start every lane writes its column of the chunk loaded a segment
+// earlier into this wave's 64-column area, and each step all lanes read the
+// step's column (one address: a broadcast) into the register the DPP shift
+// keeps in the vacated lane.  Against the rotating chunk registers this
+// drops one DPP move per component and step (8 per step in the 5-state +
+// local sweeps, 7 in the partition function's) for two LDS reads.
+template <int M>
+struct LdsChunkLayout {
+  static constexpr int raw = ((M & kHmm5) ? 20 : 0) + ((M & kLocal) ? 12 : 0) + ((M & kPF) ? 28 : 0);
+  static constexpr int bytes = (raw + 15) & ~15;   // per column
+  static constexpr int o5 = 0, ol = (M & kHmm5) ? 20 : 0, oz = ol + ((M & kLocal) ? 12 : 0), oe = oz + 24;
+};
+template <int M>
+struct LdsBoundaryChunks {
+  using Lay = LdsChunkLayout<M>;
+  float n5[5] = {}, nl[3] = {};   // (the first segment's chunk is never read by an active cell)
+  double nz[3] = {};
+  int ne = 0;
+  uint8_t* area;   // this wave's 64 x Lay::bytes
+  __device__ __forceinline__ void load_next(const Scratch& sc, int64_t bo, int W, int col0, int lane, int back = 0) {
+    const uint32_t col = (uint32_t)min(max(col0 + lane - back, 0), W - 1);
+    if constexpr ((M & kHmm5) != 0) {
+      const float* b5 = sc.bnd5 + bo * 5;
+#pragma unroll
+      for (int k = 0; k < 5; ++k) n5[k] = b5[k * W + col];
+    }
+    if constexpr ((M & kLocal) != 0) {
+      const float* bl = sc.bndl + bo * 3;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) nl[k] = bl[k * W + col];
+    }
+    if constexpr ((M & kPF) != 0) {
+      const double* bz = sc.bndz + bo * 3;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) nz[k] = bz[k * W + col];
+      ne = sc.bnde[bo + col];
+    }
+  }
+  // the loaded chunk becomes the current one: this lane's column into LDS
+  // (the wave's reads of the previous chunk precede it in LDS order)
+  __device__ __forceinline__ void advance(int lane) {
+    uint32_t w[Lay::bytes / 4] = {};
+    if constexpr ((M & kHmm5) != 0) {
+#pragma unroll
+      for (int k = 0; k < 5; ++k) w[Lay::o5 / 4 + k] = __float_as_uint(n5[k]);
+    }
+    if constexpr ((M & kLocal) != 0) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) w[Lay::ol / 4 + k] = __float_as_uint(nl[k]);
+    }
+    if constexpr ((M & kPF) != 0) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const uint64_t b = (uint64_t)__double_as_longlong(nz[k]);
+        w[Lay::oz / 4 + 2 * k] = (uint32_t)b;
+        w[Lay::oz / 4 + 2 * k + 1] = (uint32_t)(b >> 32);
+      }
+      w[Lay::oe / 4] = (uint32_t)ne;
+    }
+    uint4* dst = reinterpret_cast<uint4*>(area + lane * Lay::bytes);
+#pragma unroll
+    for (int k = 0; k < Lay::bytes / 16; ++k) dst[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+  }
+  // as BoundaryChunks::shift; col: the LDS address of the chunk column this
+  // step takes (the caller forms it once per group of unrolled steps, the
+  // steps' offsets then fold into the reads)
+  template <bool SHR>
+  __device__ __forceinline__ void shift_at(const uint8_t* col, const float* S5, float* X5, const float* SL,
+                                           float* XL, double sZm, double sZe, double sZf, int se, double& Zm,
+                                           double& Ze, double& Zf, int& e) {
+    uint32_t w[Lay::bytes / 4];
+    const uint4* src = reinterpret_cast<const uint4*>(col);
+#pragma unroll
+    for (int k = 0; k < Lay::bytes / 16; ++k) {
+      const uint4 v = src[k];
+      w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
+    }
+    if constexpr ((M & kHmm5) != 0) {
+#pragma unroll
+      for (int k = 0; k < 5; ++k) {
+        const float o = __uint_as_float(w[Lay::o5 / 4 + k]);
+        X5[k] = SHR ? mlp_shr1(S5[k], o) : mlp_shl1(S5[k], o);
+      }
+    }
+    if constexpr ((M & kLocal) != 0) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const float o = __uint_as_float(w[Lay::ol / 4 + k]);
+        XL[k] = SHR ? mlp_shr1(SL[k], o) : mlp_shl1(SL[k], o);
+      }
+    }
+    if constexpr ((M & kPF) != 0) {
+      double o[3];
+#pragma unroll
+      for (int k = 0; k < 3; ++k)
+        o[k] = __longlong_as_double((long long)(((uint64_t)w[Lay::oz / 4 + 2 * k + 1] << 32) | w[Lay::oz / 4 + 2 * k]));
+      Zm = SHR ? mlp_shr1d(sZm, o[0]) : mlp_shl1d(sZm, o[0]);
+      Ze = SHR ? mlp_shr1d(sZe, o[1]) : mlp_shl1d(sZe, o[1]);
+      Zf = SHR ? mlp_shr1d(sZf, o[2]) : mlp_shl1d(sZf, o[2]);
+      e = SHR ? mlp_shr1i(se, (int)w[Lay::oe / 4]) : mlp_shl1i(se, (int)w[Lay::oe / 4]);
     }
   }
 };

@@ -5,6 +5,223 @@
 // and are bit-identical to the reference's (tests/test_oracle_golden.py).
 #include "mlp_runtime.h"
 
+// ------------------------------------------------------------------ device pool
+namespace {
+
+// One device's blocks.  A block is one hipMalloc; its free ranges are kept
+// by offset (coalesced on release); live allocations map base -> (block,
+// bytes).  First fit over the blocks in allocation order.
+struct PoolBlock {
+  char* base;
+  size_t bytes;
+  std::map<size_t, size_t> free;   // offset -> length
+};
+struct DevicePool {
+  std::mutex mu;
+  int contexts = 0;   // live device contexts on the device
+  std::vector<PoolBlock> blocks;
+  std::map<char*, std::pair<size_t, size_t>> live;   // ptr -> (block index, bytes); kOwn: a small allocation
+};
+constexpr size_t kPoolAlign = 2u << 20;
+// below this a buffer is a plain allocation of its own (a small release does
+// not stall the next allocation, and small buffers would fragment the blocks)
+constexpr size_t kPoolMin = 64u << 20;
+constexpr size_t kOwn = SIZE_MAX;
+thread_local hipError_t pool_last_error = hipSuccess;
+
+DevicePool& pool_of(int device) {
+  static std::mutex mu;
+  static std::map<int, std::unique_ptr<DevicePool>> pools;
+  std::lock_guard<std::mutex> g(mu);
+  std::unique_ptr<DevicePool>& p = pools[device];
+  if (!p) p.reset(new DevicePool());
+  return *p;
+}
+
+// the blocks with nothing live in them back to the driver (caller holds mu)
+size_t pool_trim_locked(DevicePool& P) {
+  size_t freed = 0;
+  std::vector<PoolBlock> keep;
+  std::vector<size_t> remap(P.blocks.size(), SIZE_MAX);
+  for (size_t b = 0; b < P.blocks.size(); b++) {
+    PoolBlock& B = P.blocks[b];
+    if (B.free.size() == 1 && B.free.begin()->first == 0 && B.free.begin()->second == B.bytes) {
+      hipFree(B.base);
+      freed += B.bytes;
+    } else {
+      remap[b] = keep.size();
+      keep.push_back(std::move(B));
+    }
+  }
+  for (auto& kv : P.live)
+    if (kv.second.first != kOwn) kv.second.first = remap[kv.second.first];
+  P.blocks = std::move(keep);
+  return freed;
+}
+
+// empty blocks back to the driver, largest first, until the pool holds at
+// most `keep` bytes (caller holds mu)
+void pool_shrink_locked(DevicePool& P, size_t keep) {
+  size_t held = 0;
+  for (const PoolBlock& B : P.blocks) held += B.bytes;
+  while (held > keep) {
+    size_t best = SIZE_MAX;
+    for (size_t b = 0; b < P.blocks.size(); b++) {
+      const PoolBlock& B = P.blocks[b];
+      const bool empty = B.free.size() == 1 && B.free.begin()->first == 0 && B.free.begin()->second == B.bytes;
+      if (empty && (best == SIZE_MAX || B.bytes > P.blocks[best].bytes)) best = b;
+    }
+    if (best == SIZE_MAX) return;
+    hipFree(P.blocks[best].base);
+    held -= P.blocks[best].bytes;
+    P.blocks.erase(P.blocks.begin() + best);
+    for (auto& kv : P.live)
+      if (kv.second.first != kOwn && kv.second.first > best) kv.second.first--;
+  }
+}
+
+}  // namespace
+
+// A process without live contexts on a device keeps at most MLP_POOL_KEEP_GB
+// (default 32 GiB) of blocks there: the next context (a new family, the next
+// mask of shards) reuses them, while other processes on the device -- the
+// drop-in CLIs a pipeline starts beside a library user -- get the rest back.
+void pool_ctx_opened(int device) {
+  DevicePool& P = pool_of(device);
+  std::lock_guard<std::mutex> g(P.mu);
+  P.contexts++;
+}
+
+void pool_ctx_closed(int device) {
+  DevicePool& P = pool_of(device);
+  std::lock_guard<std::mutex> g(P.mu);
+  if (--P.contexts > 0) return;
+  P.contexts = 0;
+  int cur = device;
+  hipGetDevice(&cur);
+  if (cur != device) hipSetDevice(device);
+  pool_shrink_locked(P, (size_t)(knob("MLP_POOL_KEEP_GB", 32.0) * double(1ull << 30)));
+  if (cur != device) hipSetDevice(cur);
+}
+
+void* pool_alloc(int device, size_t bytes) {
+  DevicePool& P = pool_of(device);
+  const bool own = bytes < kPoolMin;
+  const size_t need = own ? std::max<size_t>(bytes, 256) : (bytes + kPoolAlign - 1) & ~(kPoolAlign - 1);
+  std::lock_guard<std::mutex> g(P.mu);
+  if (!own) {   // best fit over the blocks' free ranges
+    size_t bb = SIZE_MAX, boff = 0, blen = SIZE_MAX;
+    for (size_t b = 0; b < P.blocks.size(); b++)
+      for (const auto& kv : P.blocks[b].free)
+        if (kv.second >= need && kv.second < blen) {
+          bb = b;
+          boff = kv.first;
+          blen = kv.second;
+        }
+    if (bb != SIZE_MAX) {
+      PoolBlock& B = P.blocks[bb];
+      B.free.erase(boff);
+      if (blen > need) B.free[boff + need] = blen - need;
+      P.live[B.base + boff] = {bb, need};
+      return B.base + boff;
+    }
+  }
+  void* p = nullptr;
+  int cur = device;
+  hipGetDevice(&cur);
+  if (cur != device) hipSetDevice(device);
+  hipError_t e = hipMalloc(&p, need);
+  if (e != hipSuccess) {
+    hipGetLastError();
+    if (pool_trim_locked(P)) e = hipMalloc(&p, need);
+    if (e != hipSuccess) hipGetLastError();
+  }
+  if (cur != device) hipSetDevice(cur);
+  pool_last_error = e;
+  if (e != hipSuccess) return nullptr;
+  if (own) {
+    P.live[(char*)p] = {kOwn, need};
+    return p;
+  }
+  P.blocks.push_back(PoolBlock{(char*)p, need, {}});
+  P.live[(char*)p] = {P.blocks.size() - 1, need};
+  return p;
+}
+
+void pool_free(int device, void* p) {
+  if (!p) return;
+  DevicePool& P = pool_of(device);
+  std::lock_guard<std::mutex> g(P.mu);
+  auto lv = P.live.find((char*)p);
+  if (lv == P.live.end()) return;
+  if (lv->second.first == kOwn) {
+    P.live.erase(lv);
+    hipFree(p);
+    return;
+  }
+  PoolBlock& B = P.blocks[lv->second.first];
+  size_t off = (size_t)((char*)p - B.base), len = lv->second.second;
+  P.live.erase(lv);
+  auto next = B.free.lower_bound(off);
+  if (next != B.free.end() && next->first == off + len) {   // coalesce with the range after
+    len += next->second;
+    next = B.free.erase(next);
+  }
+  if (next != B.free.begin()) {   // and the one before
+    auto prev = std::prev(next);
+    if (prev->first + prev->second == off) {
+      off = prev->first;
+      len += prev->second;
+      B.free.erase(prev);
+    }
+  }
+  B.free[off] = len;
+}
+
+extern "C" int mlp_pool_info(int device, uint64_t* held, uint64_t* free_bytes) {
+  DevicePool& P = pool_of(device);
+  std::lock_guard<std::mutex> g(P.mu);
+  uint64_t h = 0, f = 0;
+  for (const PoolBlock& B : P.blocks) {
+    h += B.bytes;
+    for (const auto& kv : B.free) f += kv.second;
+  }
+  if (held) *held = h;
+  if (free_bytes) *free_bytes = f;
+  return MLP_OK;
+}
+
+extern "C" int mlp_pool_trim(int device) {
+  DevicePool& P = pool_of(device);
+  std::lock_guard<std::mutex> g(P.mu);
+  pool_trim_locked(P);
+  return MLP_OK;
+}
+
+size_t pool_free_bytes(int device) {
+  DevicePool& P = pool_of(device);
+  std::lock_guard<std::mutex> g(P.mu);
+  size_t n = 0;
+  for (const PoolBlock& B : P.blocks)
+    for (const auto& kv : B.free) n += kv.second;
+  return n;
+}
+
+std::string pool_failure(int device, size_t bytes) {
+  uint64_t held = 0, pfree = 0;
+  mlp_pool_info(device, &held, &pfree);
+  size_t freeb = 0, total = 0;
+  int cur = device;
+  hipGetDevice(&cur);
+  if (cur != device) hipSetDevice(device);
+  if (hipMemGetInfo(&freeb, &total) != hipSuccess) hipGetLastError();
+  if (cur != device) hipSetDevice(cur);
+  const auto mb = [](uint64_t b) { return std::to_string(b >> 20); };
+  return "device allocation failed (" + std::to_string(bytes) + " bytes: " + hipGetErrorName(pool_last_error) +
+         "; device " + std::to_string(device) + " free " + mb(freeb) + " of " + mb(total) + " MB, pool holds " +
+         mb(held) + " MB, " + mb(pfree) + " MB of it free)";
+}
+
 // ------------------------------------------------------------------ helpers
 
 int ensure(mlp_ctx* c, DevBuf& b, size_t bytes) {
@@ -14,13 +231,15 @@ int ensure(mlp_ctx* c, DevBuf& b, size_t bytes) {
     b.lent = false;
   }
   if (b.bytes >= bytes) return MLP_OK;
-  if (b.p) hipFree(b.p);
+  if (b.p) {   // as hipFree would: nothing in flight may still use it when it is handed out again
+    hipDeviceSynchronize();
+    pool_free(c->device, b.p);
+  }
   b.p = nullptr;
   b.bytes = 0;
-  size_t want = std::max<size_t>(bytes, 256);
-  if (hipMalloc(&b.p, want) != hipSuccess) {
-    c->err = "hipMalloc failed (" + std::to_string(want) + " bytes)";
-    b.p = nullptr;
+  const size_t want = std::max<size_t>(bytes, 256);
+  if (!(b.p = pool_alloc(c->device, want))) {
+    c->err = pool_failure(c->device, want);
     return MLP_ERR_MEMORY;
   }
   b.bytes = want;
@@ -36,7 +255,7 @@ int ensure(mlp_ctx* c, DevBuf& b, size_t bytes) {
 int ensure_tmp(mlp_ctx* c, DevBuf& b, size_t bytes) {
   const size_t need = (std::max<size_t>(bytes, 256) + 255) & ~(size_t)255;
   if (c->arena_on && c->scratch.p && c->arena_off + need <= c->scratch.bytes) {
-    if (b.p && !b.lent) hipFree(b.p);
+    if (b.p && !b.lent) pool_free(c->device, b.p);
     b.p = (char*)c->scratch.p + c->arena_off;
     b.bytes = need;
     b.lent = true;
@@ -225,11 +444,12 @@ int mlp_ctx_create(int device, mlp_ctx** out) {
   // process gets smaller batches, never an oversubscription); an allocation
   // that still fails halves the budget and retries.
   {
-    const size_t usable = freeb;
+    const size_t usable = freeb + pool_free_bytes(device);   // the pool's free ranges serve it too
     const size_t reserve = std::max<size_t>(16ull << 30, total / 100 * 7);
     c->scratch_budget = usable > 2 * reserve ? usable - reserve : usable / 2;
   }
   if (knob_set("MLP_SCRATCH_GB")) c->scratch_budget = (size_t)(knob("MLP_SCRATCH_GB", 0) * (1ull << 30));
+  pool_ctx_opened(device);
   *out = c;
   return MLP_OK;
 }
@@ -276,16 +496,17 @@ void mlp_ctx_destroy(mlp_ctx* c) {
   hipStreamSynchronize(c->stream);
   hipStreamSynchronize(c->stream2);
   if (c->side.st) hipStreamSynchronize(c->side.st);
-  void* ptrs[] = {c->d_tables, c->d_res, c->d_off, c->d_len, c->d_rp_off, c->d_trp_off,
-                  c->d_rowptr, c->d_ent_off, c->d_cols, c->d_vals};
-  for (void* p : ptrs)
-    if (p) hipFree(p);
+  if (c->d_tables) hipFree(c->d_tables);
+  // the family's arrays and the store: back to the pool
+  void* ptrs[] = {c->d_res, c->d_off, c->d_len, c->d_rp_off, c->d_trp_off, c->d_rowptr, c->d_ent_off,
+                  c->d_cols, c->d_vals};
+  for (void* p : ptrs) pool_free(c->device, p);
   DevBuf* bufs[] = {&c->scratch, &c->r_trowptr, &c->r_tcols, &c->r_tvals, &c->r_raw, &c->r_newrp,
                     &c->r_newcols, &c->r_newvals, &c->r_tasks_p, &c->r_tasks_r, &c->r_pairs,
                     &c->r_nnz, &c->r_newoff, &c->r_img, &c->r_imgoff, &c->r_tiles, &c->r_nwords, &c->r_weights,
                     &c->r_seldist, &c->r_profile, &c->r_mea, &c->ag_cols, &c->ag_vals};
   for (DevBuf* b : bufs)
-    if (b->p && !b->lent) hipFree(b->p);
+    if (b->p && !b->lent) pool_free(c->device, b->p);
   if (c->comm) ncclCommDestroy(c->comm);
   for (hipEvent_t e : c->evpool) hipEventDestroy(e);
   if (knob_set("MLP_LOG_PROFILE") && (c->prof_t[0] > 0 || c->prof_t[1] > 0))
@@ -311,7 +532,9 @@ void mlp_ctx_destroy(mlp_ctx* c) {
   for (hipEvent_t e : {c->ev_done[0], c->ev_done[1], c->ev_fork, c->ev_tot}) {
     if (e) hipEventDestroy(e);
   }
+  const int device = c->device;
   delete c;
+  pool_ctx_closed(device);
 }
 
 const char* mlp_last_error(const mlp_ctx* c) { return c ? c->err.c_str() : "null context"; }
@@ -413,12 +636,11 @@ int grow_store(mlp_ctx* c, int64_t need, int64_t keep, int64_t want, bool sync2)
   // `want`: the caller's estimate of the final size, so a growing store is
   // reallocated (and copied) once rather than every 1.5x
   int64_t cap = std::max<int64_t>(std::max<int64_t>(need, want), c->ent_cap + c->ent_cap / 2);
-  uint16_t* nc = nullptr;
-  float* nv = nullptr;
-  if (hipMalloc((void**)&nc, sizeof(uint16_t) * cap) != hipSuccess ||
-      hipMalloc((void**)&nv, sizeof(float) * cap) != hipSuccess) {
-    if (nc) hipFree(nc);
-    c->err = "hipMalloc (CSR store) failed";
+  uint16_t* nc = (uint16_t*)pool_alloc(c->device, sizeof(uint16_t) * cap);
+  float* nv = nc ? (float*)pool_alloc(c->device, sizeof(float) * cap) : nullptr;
+  if (!nv) {
+    pool_free(c->device, nc);
+    c->err = "device allocation (CSR store) failed";
     return MLP_ERR_MEMORY;
   }
   if (keep > 0) {
@@ -426,8 +648,8 @@ int grow_store(mlp_ctx* c, int64_t need, int64_t keep, int64_t want, bool sync2)
     HIPCHK(c, hipMemcpyAsync(nv, c->d_vals, sizeof(float) * keep, hipMemcpyDeviceToDevice, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
   }
-  if (c->d_cols) hipFree(c->d_cols);
-  if (c->d_vals) hipFree(c->d_vals);
+  pool_free(c->device, c->d_cols);
+  pool_free(c->device, c->d_vals);
   c->d_cols = nc;
   c->d_vals = nv;
   c->ent_cap = cap;

@@ -11,7 +11,7 @@ namespace {
 
 const char* const kKnobs[] = {
     // settings
-    "MLP_SCRATCH_GB", "MLP_HOST_THREADS",
+    "MLP_SCRATCH_GB", "MLP_HOST_THREADS", "MLP_POOL_KEEP_GB",
     // test hooks
     "MLP_TEST_PG_SEPARATE", "MLP_TEST_TOT_LANEFOLD", "MLP_TEST_TOT_FOLDBOUND", "MLP_TEST_TOT_BESIDE",
     "MLP_TEST_TOT_FORCE_REPAIR", "MLP_TEST_DEFER_FINISH", "MLP_TEST_FORCE_PEER", "MLP_TEST_ALLGATHER_FORCE",

@@ -5,6 +5,8 @@
 //   MLP_SCRATCH_GB            cap of a device context's batch scratch, GiB (default:
 //                             free HBM less max(16 GiB, 7%); mlp_set_scratch overrides)
 //   MLP_HOST_THREADS          threads of a host context (default: hardware threads)
+//   MLP_POOL_KEEP_GB          device pool bytes a process keeps once its last context on
+//                             the device closes, GiB (default 32)
 // Test hooks (MLP_TEST_*): force one side of a decision the library makes by
 // itself, so the GPU suite checks both sides bit-identical:
 //   MLP_TEST_PG_SEPARATE      0/1: PF posterior in the Zm slots / its own array

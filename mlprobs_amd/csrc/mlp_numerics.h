@@ -37,6 +37,21 @@ __device__ __forceinline__ float mlp_log_add(float x, float y) {
   return (lo == MLP_LOG_ZERO || d >= 7.5f) ? hi : r;
 }
 
+// max / min of two non-NaN floats as one v_max_f32 / v_min_f32 (fmaxf /
+// fminf canonicalise inputs the compiler cannot prove canonical first).
+// Only where the operands come from loads or DPP moves: inside LOG_ADD the
+// opaque asm costs the scheduler more than the canonicalisation it saves
+__device__ __forceinline__ float mlp_max(float a, float b) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ float mlp_min(float a, float b) {
+  float r;
+  asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
 // LDS-table form of LOOKUP.  The interval is found from
 // q = floor(min(d * (2 - 2^-23), 15)): q <= 1 <=> d <= 1, q <= 4 <=> d <= 2.5,
 // q <= 8 <=> d <= 4.5 for every float d >= 0 (checked exhaustively on [0, 8);
@@ -73,14 +88,6 @@ __device__ __forceinline__ float mlp_log_add_t(float x, float y, const float4* _
   const float4 c = *(const float4*)((const char*)lk + (q16 & 0xf0));
   const float r = (((c.x * d + c.y) * d + c.z) * d + c.w) + lo;
   return (d >= 7.5f) ? hi : r;
-}
-
-// max of two non-NaN floats as one v_max_f32 (fmaxf canonicalises both
-// inputs first: two more instructions)
-__device__ __forceinline__ float mlp_max(float a, float b) {
-  float r;
-  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-  return r;
 }
 
 // LOG_ADD(LOG_ZERO, y) == max(LOG_ZERO, y) exactly: above LOG_ZERO the sentinel

@@ -328,9 +328,10 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
         plan_chains(c, p, q, P);
       }
     }
-    {  // a batch over the budget (the ratio varies with the pairs), carved as it will be: fewer pairs
+    {  // a batch over the budget (the ratio varies with the pairs), carved as it will be, or
+       // whose chunk maxima pass the sweeps' 32-bit buffer offsets: fewer pairs
       BatchOffs o;
-      while (q - p > 1 && carve(P, front_for(P), o) > c->scratch_budget) {
+      while (q - p > 1 && (carve(P, front_for(P), o) > c->scratch_budget || P.rm_total * 4 >= (1ll << 31))) {
         q = p + std::max<int64_t>(1, (q - p) * 97 / 100);
         plan_chains(c, p, q, P);
       }

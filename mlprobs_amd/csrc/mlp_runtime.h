@@ -20,6 +20,9 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
 #include <numeric>
 #include <string>
 #include <thread>
@@ -165,16 +168,34 @@ struct mlp_ctx {
     }                                                                              \
   } while (0)
 
+// ---- the process's device memory pool (mlp_context.cpp): large buffers
+// (batch scratch, CSR stores, relaxation and gather buffers) are carved from
+// blocks the process keeps; a released buffer goes back to its block, not to
+// the driver.  A fresh allocation right after a large release can wait
+// seconds while the driver clears what was released,
+// so contexts created one after another (the shards of a mask, a new family's
+// context) reuse what the last one held.  Blocks go back to the driver only
+// when an allocation fails or on mlp_pool_trim.
+MLP_HIDDEN void* pool_alloc(int device, size_t bytes);   // nullptr on failure
+MLP_HIDDEN void pool_free(int device, void* p);
+MLP_HIDDEN size_t pool_free_bytes(int device);           // reusable bytes held
+MLP_HIDDEN void pool_ctx_opened(int device);             // a device context's lifetime:
+MLP_HIDDEN void pool_ctx_closed(int device);             // the last close shrinks the pool
+// the error text for a failed pool_alloc: the request, the driver's error
+// and what the device and the pool held at the time
+MLP_HIDDEN std::string pool_failure(int device, size_t bytes);
+
 // ---- device buffers, timers (mlp_context.cpp)
 MLP_HIDDEN int ensure(mlp_ctx* c, DevBuf& b, size_t bytes);
 MLP_HIDDEN int ensure_tmp(mlp_ctx* c, DevBuf& b, size_t bytes);
+// the family's arrays, from the pool as well (a relaxation round swaps the
+// row pointers with a pooled buffer)
 template <class T>
 inline int dalloc(mlp_ctx* c, T** p, size_t count) {
-  if (*p) hipFree(*p);
-  *p = nullptr;
-  if (hipMalloc((void**)p, std::max<size_t>(count, 1) * sizeof(T)) != hipSuccess) {
-    c->err = "hipMalloc failed";
-    *p = nullptr;
+  pool_free(c->device, *p);
+  *p = (T*)pool_alloc(c->device, std::max<size_t>(count, 1) * sizeof(T));
+  if (!*p) {
+    c->err = pool_failure(c->device, std::max<size_t>(count, 1) * sizeof(T));
     return MLP_ERR_MEMORY;
   }
   return MLP_OK;

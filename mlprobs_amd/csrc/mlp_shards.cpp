@@ -391,11 +391,11 @@ int mlp_allgather(mlp_ctx* c) {
   }
   const int64_t total = ebase[R];
   // 2. new entry arrays; my block moves to its global place
-  uint16_t* nc = nullptr;
-  float* nv = nullptr;
-  if (hipMalloc((void**)&nc, sizeof(uint16_t) * std::max<int64_t>(total, 1)) != hipSuccess ||
-      hipMalloc((void**)&nv, sizeof(float) * std::max<int64_t>(total, 1)) != hipSuccess) {
-    c->err = "hipMalloc (gather) failed";
+  uint16_t* nc = (uint16_t*)pool_alloc(c->device, sizeof(uint16_t) * std::max<int64_t>(total, 1));
+  float* nv = nc ? (float*)pool_alloc(c->device, sizeof(float) * std::max<int64_t>(total, 1)) : nullptr;
+  if (!nv) {
+    pool_free(c->device, nc);
+    c->err = "device allocation (gather) failed";
     return MLP_ERR_MEMORY;
   }
   // per-pair scalars through device memory
@@ -430,8 +430,8 @@ int mlp_allgather(mlp_ctx* c) {
   HIPCHK(c, hipStreamSynchronize(c->stream));
   hipFree(d_sc);
   hipFree(d_nz);
-  if (c->d_cols) hipFree(c->d_cols);
-  if (c->d_vals) hipFree(c->d_vals);
+  pool_free(c->device, c->d_cols);
+  pool_free(c->device, c->d_vals);
   c->d_cols = nc;
   c->d_vals = nv;
   c->ent_cap = std::max<int64_t>(total, 1);

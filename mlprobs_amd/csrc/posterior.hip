@@ -144,12 +144,12 @@ __global__ __launch_bounds__(256, SweepWaves<M>::fwd) void k_forward(ModelScalar
   // current 64-column chunk (a multiple of 64, or L2; -1 on rows without
   // chunks) and that chunk's element of cmf; set when the lane enters a row
   int jst = -1;
-  int64_t cmo = 0;
+  uint32_t cmo4 = 0;       // byte offset of that element (cmf < 2 GB: cells / 16 bytes of a batch)
   float cmx = -INFINITY;   // the chunk's running maximum (row 0 / column 0 hold LZ: no effect)
   auto local_row = [&]() {
     if constexpr ((M & kLocal) != 0) {
       jst = c.q >= 0 && c.i >= 1 ? min(64, c.L2) : -1;
-      cmo = c.rm + (int64_t)(c.i - 1) * local_chunks(c.L2);
+      cmo4 = (uint32_t)(c.rm + (int64_t)(c.i - 1) * local_chunks(c.L2)) * 4u;
       cmx = -INFINITY;
     }
   };
@@ -164,7 +164,9 @@ __global__ __launch_bounds__(256, SweepWaves<M>::fwd) void k_forward(ModelScalar
   for (int k = 0; k < 5; ++k) L5[k] = U5[k] = D5[k] = LZ;
 #pragma unroll
   for (int k = 0; k < 3; ++k) LL[k] = UL[k] = DL[k] = LZ;
-  BoundaryChunks<M> bc;
+  __shared__ __align__(16) uint8_t chunk_lds[kWavesPerBlock * 64 * LdsChunkLayout<M>::bytes];
+  LdsBoundaryChunks<M> bc;
+  bc.area = chunk_lds + (threadIdx.x >> 6) * 64 * LdsChunkLayout<M>::bytes;
   const int nseg = (W + 63) >> 6;
 
   // segments: lane 0's 64-column chunks of strip k; k == S: the skew tail
@@ -175,17 +177,18 @@ __global__ __launch_bounds__(256, SweepWaves<M>::fwd) void k_forward(ModelScalar
       const int t_hi = k < S ? min(t_lo + 64, (k + 1) * W) : t_lo + 64;
       if (k < S) {
         boundary_fence();
-        bc.advance();
+        bc.advance(lane);
         bc.load_next(sc, bo, W, m + 1 < nseg ? 64 * (m + 1) : 0, lane);
       }
       // unrolled by 4 (segments hold multiples of 8 steps) so the rotating
       // left/up/diagonal roles stay in fixed registers
-      for (int t0 = t_lo; t0 < t_hi; t0 += 4)
+      for (int t0 = t_lo; t0 < t_hi; t0 += 4) {
+      // the chunk column of step t0 + u: bc.area + (t0 + u - t_lo) * bytes
+      const uint8_t* const colp = bc.area + (t0 - t_lo) * LdsChunkLayout<M>::bytes;
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int t = t0 + u;
         const int i = c.i, j = c.j, L1 = c.L1, L2 = c.L2;
-        const bool gen = i > 1 || j > 1;
         // wave-uniform: no lane on an initial cell, row 0 or column 0 (the
         // common case away from the pairs' edges), so the recurrences' values
         // are taken as they are, without the per-lane selects of the edges
@@ -209,7 +212,8 @@ __global__ __launch_bounds__(256, SweepWaves<M>::fwd) void k_forward(ModelScalar
         // skew tail lane 0's up value is unused -- row 0 of the chain, the
         // idle tail -- so whatever the chunk holds is harmless): one form of
         // the shift, no branch joining two register assignments
-        bc.template shift<true, true>(t - t_lo, L5, U5, LL, UL, LZm, LZe, LZf, Le, UZm, UZe, UZf, Ue);
+        bc.template shift_at<true>(colp + u * LdsChunkLayout<M>::bytes, L5, U5, LL, UL, LZm, LZe, LZf, Le, UZm, UZe,
+                                   UZf, Ue);
         const int64_t tcell = cell0 + (int64_t)t * 64;   // wave-uniform
         // ------------------------------------------------ 5-state forward
         if constexpr ((M & kHmm5) != 0) {
@@ -230,16 +234,19 @@ __global__ __launch_bounds__(256, SweepWaves<M>::fwd) void k_forward(ModelScalar
           if (interior) {  // every lane's cell takes all five recurrences
             Cc[0] = vm; Cc[1] = vx1; Cc[2] = vy1; Cc[3] = vx2; Cc[4] = vy2;
           } else {
+            // (the edge tests only here: kept from being hoisted into the interior path)
+            int ie = i, je = j;
+            asm volatile("" : "+v"(ie), "+v"(je));
 #pragma unroll
             for (int k5 = 0; k5 < 5; ++k5) Cc[k5] = LZ;
             // CPNP/ProbabilisticModel.h:173-183 initial cells
-            if (i == 1 && j == 1) Cc[0] = ms.init[0] + mt;
-            if (i == 1 && j == 0) { Cc[1] = ms.init[1] + ins1; Cc[3] = ms.init[3] + ins1; }
-            if (i == 0 && j == 1) { Cc[2] = ms.init[2] + ins2; Cc[4] = ms.init[4] + ins2; }
-            if (gen) {
-              if (i > 0 && j > 0) Cc[0] = vm;
-              if (i > 0) { Cc[1] = vx1; Cc[3] = vx2; }
-              if (j > 0) { Cc[2] = vy1; Cc[4] = vy2; }
+            if (ie == 1 && je == 1) Cc[0] = ms.init[0] + mt;
+            if (ie == 1 && je == 0) { Cc[1] = ms.init[1] + ins1; Cc[3] = ms.init[3] + ins1; }
+            if (ie == 0 && je == 1) { Cc[2] = ms.init[2] + ins2; Cc[4] = ms.init[4] + ins2; }
+            if (ie > 1 || je > 1) {
+              if (ie > 0 && je > 0) Cc[0] = vm;
+              if (ie > 0) { Cc[1] = vx1; Cc[3] = vx2; }
+              if (je > 0) { Cc[2] = vy1; Cc[4] = vy2; }
             }
           }
           bstore(sc.f5 + tcell, ul4, Cc[0]);   // every lane: values of idle cells are never used
@@ -271,11 +278,13 @@ __global__ __launch_bounds__(256, SweepWaves<M>::fwd) void k_forward(ModelScalar
           if (interior) {
             Cm = vm; Cx = vx; Cy = vy;
           } else {
-            if (i == 1 && j == 1) Cm = bs - two_rt1;
-            if (gen) {
-              if (i > 0 && j > 0) Cm = vm;
-              if (i > 0) Cx = vx;
-              if (j > 0) Cy = vy;
+            int ie = i, je = j;
+            asm volatile("" : "+v"(ie), "+v"(je));
+            if (ie == 1 && je == 1) Cm = bs - two_rt1;
+            if (ie > 1 || je > 1) {
+              if (ie > 0 && je > 0) Cm = vm;
+              if (ie > 0) Cx = vx;
+              if (je > 0) Cy = vy;
             }
           }
           bstore(sc.fl + tcell, ul4, Cm);
@@ -288,8 +297,8 @@ __global__ __launch_bounds__(256, SweepWaves<M>::fwd) void k_forward(ModelScalar
           // of the row (from column 0, whose LZ never exceeds a real value)
           cmx = mlp_max(cmx, Cm);
           if (j == jst) {
-            sc.cmf[cmo] = cmx;
-            ++cmo;
+            bstore(sc.cmf, cmo4, cmx);
+            cmo4 += 4;
             jst = min(jst + 64, L2);
             cmx = -INFINITY;
           }
@@ -343,6 +352,7 @@ __global__ __launch_bounds__(256, SweepWaves<M>::fwd) void k_forward(ModelScalar
         cursor_next(c, C, T_.ins, local_row);
         j63 = j63 + 1 == W ? 0 : j63 + 1;
       }
+      }
     }
   }
 }
@@ -356,7 +366,7 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
                                                   SeqSet sq, PairMeta pm, ChainMeta cm,
                                                   PairRec* __restrict__ rec, Scratch sc,
                                                   int64_t nchains, int lds_seq) {
-  __shared__ LdsTablesFor<M> T_;
+  __shared__ LdsTablesFor<M, true> T_;
   extern __shared__ __align__(16) uint8_t dyn[];
   stage_tables(T_, tab);
   const int64_t ch = wave_index();
@@ -385,12 +395,12 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
   // without chunks) and its element, set when the lane enters a row (every
   // active lane enters at column W - 1)
   int jsb = -1;
-  int64_t cmob = 0;
+  uint32_t cmob4 = 0;   // byte offset of that element in cmb
   float cmx = -INFINITY;
   auto local_row = [&]() {
     if constexpr ((M & kLocal) != 0) {
       jsb = c.q >= 0 && c.i >= 1 ? ((c.L2 - 1) & ~63) + 1 : -1;
-      cmob = c.rm + (int64_t)(c.i - 1) * local_chunks(c.L2) + ((c.L2 - 1) >> 6);
+      cmob4 = (uint32_t)(c.rm + (int64_t)(c.i - 1) * local_chunks(c.L2) + ((c.L2 - 1) >> 6)) * 4u;
     }
   };
   cursor_start_bwd(c, C, T_.ins, lane, top);
@@ -404,7 +414,9 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
   for (int k = 0; k < 5; ++k) R5[k] = N5[k] = G5[k] = LZ;
 #pragma unroll
   for (int k = 0; k < 3; ++k) RL[k] = NL[k] = GL[k] = LZ;
-  BoundaryChunks<M> bc;
+  __shared__ __align__(16) uint8_t chunk_lds[kWavesPerBlock * 64 * LdsChunkLayout<M>::bytes];
+  LdsBoundaryChunks<M> bc;
+  bc.area = chunk_lds + (threadIdx.x >> 6) * 64 * LdsChunkLayout<M>::bytes;
   const int nseg = (W + 63) >> 6;
   // the step-t loads of f5 / zm are issued kPrefetch steps earlier into
   // fixed registers: slot u serves steps t0 - u (segments hold whole groups
@@ -429,7 +441,7 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
         t_lo = k * W + 63 + 64 * m;
         t_hi = k * W + 63 + min(64 * m + 63, W - 1);
         boundary_fence();
-        bc.advance();
+        bc.advance(lane);
         // chunk before (k, m): (k, m-1) or (k-1, last); holds stacked row 64k+64
         {
           const int col0 = m > 0 ? 64 * (m - 1) : 64 * (nseg - 1);
@@ -440,15 +452,26 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
         t_lo = -1;
         t_hi = 62;
       }
-      for (int t0 = t_hi; t0 >= t_lo; t0 -= kPrefetch)
+      for (int t0 = t_hi; t0 >= t_lo; t0 -= kPrefetch) {
+      // the chunk column of step t0 - u is 63 - (t_hi - t0 + u): the group's
+      // lowest (u = kPrefetch - 1) plus kPrefetch - 1 - u columns
+      const uint8_t* const colp = bc.area + (63 - (t_hi - t0) - (kPrefetch - 1)) * LdsChunkLayout<M>::bytes;
 #pragma unroll
       for (int u = 0; u < kPrefetch; ++u) {
         const int t = t0 - u;
         const int i = c.i, j = c.j, L1 = c.L1, L2 = c.L2;
-        const bool in_i = i < L1, in_j = j < L2;
         // wave-uniform: every lane inside its pair (not the last row, column
         // or cell), so the recurrences run without the edge selects
         const bool interior = wave_none(j >= c.jhi);
+        // the edge tests, for the edge paths only (kept from being hoisted
+        // into the interior path)
+        auto edges = [&](bool& in_i, bool& in_j, bool& last) {
+          int ie = i, je = j;
+          asm volatile("" : "+v"(ie), "+v"(je));
+          in_i = ie < L1;
+          in_j = je < L2;
+          last = ie == L1 && je == L2;
+        };
         const float f5v = q5[u];
         const double zmv = qz[u];
         const int c1 = c.c1, c1n = c.c1n;
@@ -469,7 +492,10 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
         if constexpr ((M & kPF) != 0) { GZm = NZm; GZe = NZe; GZf = NZf; Ge = Ne; }
         // (one form of the shift: lane 63's down value is unused in the last
         // strip -- the chain's last row, in_i false -- and in the skew head)
-        bc.template shift<false, true>(t - t_lo, R5, N5, RL, NL, RZm, RZe, RZf, Re, NZm, NZe, NZf, Ne);
+        // the chunk's column for this step: lane 63 held the segment's first
+        // (the load's shift), each step one lane below
+        bc.template shift_at<false>(colp + (kPrefetch - 1 - u) * LdsChunkLayout<M>::bytes, R5, N5, RL, NL, RZm, RZe,
+                                    RZf, Re, NZm, NZe, NZf, Ne);
         const int64_t tcell = cell0 + (int64_t)t * 64;   // wave-uniform
         // ------------------------------------------------ 5-state backward
         if constexpr ((M & kHmm5) != 0) {
@@ -478,7 +504,6 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
           float B[5];
           // CPNP/ProbabilisticModel.h:310-313, 340-378
           const float pxy = G5[0] + mn;
-          const bool last = (i == L1 && j == L2);
           if (interior) {  // every lane: in_i, in_j, not the last cell -- no per-lane selects
 #pragma unroll
             for (int k5 = 0; k5 < 5; ++k5) B[k5] = mlp_log_add_from_zero(pxy + ms.t[k5][0]);
@@ -491,6 +516,8 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
             B[0] = mlp_log_add_t(B[0], R5[4] + ins2n + ms.t[0][4], lk);
             B[4] = mlp_log_add_t(B[4], R5[4] + ins2n + ms.t[4][4], lk);
           } else {
+          bool in_i, in_j, last;
+          edges(in_i, in_j, last);
 #pragma unroll
           for (int k5 = 0; k5 < 5; ++k5)
             B[k5] = last ? ms.init[k5] : ((in_i && in_j) ? mlp_log_add_from_zero(pxy + ms.t[k5][0]) : LZ);
@@ -535,6 +562,8 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
             Bm = mlp_log_add_t(Bm, RL[2] + ms.lt[0][2] - rt1, lk);
             By = mlp_log_add_t(By, RL[2] + ms.lt[2][2] - rt1, lk);
           } else {
+          bool in_i, in_j, last;
+          edges(in_i, in_j, last);
           if (in_i && in_j) {
             const float pxy = GL[0] + mn - ins1n - ins2n;
             Bm = mlp_log_add_t(Bm, pxy + ms.lt[0][0] - two_rt1, lk);
@@ -564,8 +593,8 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
             const float e = Bm + T_.match[c.c1x + c2] - ins1 - T_.ins[c2] - two_rt1;
             cmx = j == L2 ? e : mlp_max(cmx, e);
             if (j == jsb) {
-              sc.cmb[cmob] = cmx;
-              --cmob;
+              bstore(sc.cmb, cmob4, cmx);
+              cmob4 -= 4;
               jsb -= 64;
               cmx = -INFINITY;
             }
@@ -647,6 +676,7 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
         cursor_prev(c, C, T_.ins, local_row);
         j0 = j0 == 0 ? W - 1 : j0 - 1;
       }
+      }
     }
   }
 }
@@ -680,8 +710,10 @@ __global__ __launch_bounds__(256, NP && M == (kHmm5 | kLocal | kPF) ? 5 : MLP_ME
   const int lane = threadIdx.x & 63;
   const ChainView C = stage_chain<kStageMerge>(dyn, lds_seq, ch, sq, pm, cm, rec);
   const int W = C.W, S = C.S;
-  const int64_t base = cm.cell_off[ch] + 64 + lane;
+  const int64_t cell0 = cm.cell_off[ch] + 64;   // slot of step tau, lane l: cell0 + tau * 64 + l
+  const uint32_t ul4 = (uint32_t)lane * 4;
   const int64_t bo = cm.bnd_off[ch];
+  int j63 = W - 63;   // lane 63's column (scalar; see k_forward)
   const int last = S * W + 63;   // last step with an active lane
   Cursor c;
   cursor_start_fwd(c, C, noins, lane);
@@ -698,10 +730,10 @@ __global__ __launch_bounds__(256, NP && M == (kHmm5 | kLocal | kPF) ? 5 : MLP_ME
   float q5[QD] = {}, ql[QD] = {}, qb[QD] = {}, qg[QD] = {};
 #pragma unroll
   for (int k = 0; k < QD; ++k) {
-    const int64_t at = base + (int64_t)k * 64;
-    if constexpr ((M & kHmm5) != 0) q5[k] = sc.f5[at];
-    if constexpr ((M & kLocal) != 0) { ql[k] = sc.fl[at]; qb[k] = sc.bl[at]; }
-    if constexpr ((M & kPF) != 0) qg[k] = sc.pg[at * sc.pg_stride];
+    const int64_t at = cell0 + (int64_t)k * 64;
+    if constexpr ((M & kHmm5) != 0) q5[k] = bload(sc.f5 + at, ul4);
+    if constexpr ((M & kLocal) != 0) { ql[k] = bload(sc.fl + at, ul4); qb[k] = bload(sc.bl + at, ul4); }
+    if constexpr ((M & kPF) != 0) qg[k] = bload(sc.pg + at * sc.pg_stride, ul4 * sc.pg_stride);
   }
   const int nseg = (W + 63) >> 6;
   for (int k = 0; k <= S; ++k) {
@@ -736,7 +768,7 @@ __global__ __launch_bounds__(256, NP && M == (kHmm5 | kLocal | kPF) ? 5 : MLP_ME
           Uc = take_bnd ? mlp_shr1i(Lc, cch) : mlp_shr1zi(Lc);
           if (take_bnd) cch = mlp_shl1zi(cch);
         }
-        const bool act = c.q >= 0 && i >= 1 && j >= 1 && j <= L2;
+        const bool act = (uint32_t)(j - 1) < (uint32_t)c.jm;   // q >= 0, i >= 1, 1 <= j <= L2
         float P = 0.f;
         if (act) {
           if constexpr (PID == 2) {
@@ -764,16 +796,15 @@ __global__ __launch_bounds__(256, NP && M == (kHmm5 | kLocal | kPF) ? 5 : MLP_ME
         int Cc = 0;
         if (act) {
           const float x1 = P + Dv, x2 = Lv, x3 = Uv;
-          Cv = fmaxf(fmaxf(x1, x2), x3);
+          Cv = mlp_max(mlp_max(x1, x2), x3);
           if constexpr (NP)  // ChooseBestOfThree's pick (ScoreType.h:347-366): D, else L, else U
             Cc = (x1 >= x2 && x1 >= x3) ? Dc + 1 : (x1 < x2 && x2 >= x3) ? Lc : Uc;
-          const int64_t erow = c.ell + (i - 1);
           if (P >= 0.01f) {  // POSTERIOR_CUTOFF (CPNP/SparseMatrix.h:14)
             if (cnt < kEll) {
-              sc.ell_col[erow * kEll + cnt] = (uint16_t)j;
+              sc.ell_col[c.ellx + cnt] = (uint16_t)j;
               // QuickProbs keeps 16-bit fixed point: (uint16)(P * 65535), read back
               // as q / 65535 (QP/DataStructures/SparseEntry.h:31-32)
-              sc.ell_val[erow * kEll + cnt] =
+              sc.ell_val[c.ellx + cnt] =
                   PID == kPidQP ? (float)(uint32_t)(uint16_t)(P * 65535.0f) / 65535.0f : P;
             } else {
               atomicOr(&rec[c.slot].flags, 2);
@@ -781,7 +812,7 @@ __global__ __launch_bounds__(256, NP && M == (kHmm5 | kLocal | kPF) ? 5 : MLP_ME
             ++cnt;
           }
           if (j == L2) {   // row complete
-            sc.ell_cnt[erow] = cnt;
+            sc.ell_cnt[c.ell + (i - 1)] = cnt;
             atomicAdd(reinterpret_cast<unsigned long long*>(&rec[c.slot].nnz), (unsigned long long)cnt);
             cnt = 0;
             if (i == L1) {
@@ -793,18 +824,19 @@ __global__ __launch_bounds__(256, NP && M == (kHmm5 | kLocal | kPF) ? 5 : MLP_ME
             }
           }
         }
-        if (lane == 63) sc.bndm[bo + j] = Cv;
+        if (lane == 63) bnd_put(sc.bndm + bo, j63, Cv);
         Lv = Cv;
         if constexpr (NP) {
-          if (lane == 63) sc.bndc[bo + j] = Cc;
+          if (lane == 63) bnd_put(sc.bndc + bo, j63, Cc);
           Lc = Cc;
         }
         // refill slot u once its value is dead (see k_backward)
-        const int64_t at = base + (int64_t)min(t + QD, last) * 64;
-        if constexpr ((M & kHmm5) != 0) q5[u] = sc.f5[at];
-        if constexpr ((M & kLocal) != 0) { ql[u] = sc.fl[at]; qb[u] = sc.bl[at]; }
-        if constexpr ((M & kPF) != 0) qg[u] = sc.pg[at * sc.pg_stride];
+        const int64_t at = cell0 + (int64_t)min(t + QD, last) * 64;
+        if constexpr ((M & kHmm5) != 0) q5[u] = bload(sc.f5 + at, ul4);
+        if constexpr ((M & kLocal) != 0) { ql[u] = bload(sc.fl + at, ul4); qb[u] = bload(sc.bl + at, ul4); }
+        if constexpr ((M & kPF) != 0) qg[u] = bload(sc.pg + at * sc.pg_stride, ul4 * sc.pg_stride);
         cursor_next(c, C, noins);
+        j63 = j63 + 1 == W ? 0 : j63 + 1;
       }
     }
   }

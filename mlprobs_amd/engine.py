@@ -101,6 +101,9 @@ def lib():
         L.mlp_profile_mea.argtypes = [P, C.c_char_p, C.POINTER(C.c_int32), C.POINTER(C.c_float)]
         L.mlp_profile_gather.argtypes = [P, C.c_int64, I64P, F32P]
         L.mlp_profile_set.argtypes = [P, C.c_int, C.c_int, F32P]
+        if hasattr(L, 'mlp_pool_info'):   # (experiment builds of older sources lack it)
+            L.mlp_pool_info.argtypes = [C.c_int, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+            L.mlp_pool_trim.argtypes = [C.c_int]
         _LIB = L
     return _LIB
 
@@ -113,7 +116,20 @@ EXPORTED = ['mlp_ctx_create', 'mlp_ctx_destroy', 'mlp_last_error', 'mlp_set_scra
             'mlp_shard_range', 'mlp_shard_plan', 'mlp_gather_layout', 'mlp_allgather', 'mlp_synchronize', 'mlp_profile',
             'mlp_kernel_times', 'mlp_profile_reset', 'mlp_ctx_create_mask', 'mlp_set_shards', 'mlp_shard_count',
             'mlp_relax_shard_plan', 'mlp_ctx_create_host', 'mlp_ctx_is_host', 'mlp_relax_blockmfma_eval',
-            'mlp_profile_defer', 'mlp_profile_mea', 'mlp_profile_gather', 'mlp_relax_range', 'mlp_profile_set']
+            'mlp_profile_defer', 'mlp_profile_mea', 'mlp_profile_gather', 'mlp_relax_range', 'mlp_profile_set',
+            'mlp_pool_info', 'mlp_pool_trim']
+
+
+def pool_info(device=0):
+    """(held, free) bytes of the process's device memory pool (mlp_pool_info)."""
+    h, f = C.c_uint64(), C.c_uint64()
+    lib().mlp_pool_info(int(device), C.byref(h), C.byref(f))
+    return h.value, f.value
+
+
+def pool_trim(device=0):
+    """Blocks of the pool with nothing in use back to the driver (mlp_pool_trim)."""
+    lib().mlp_pool_trim(int(device))
 
 
 def shard_plan(lens, nranks, rank):

@@ -199,3 +199,39 @@ def test_virtual_shards_default_budget():
     _same(one, many, 'default budget relax round')
     one.close()
     many.close()
+
+
+def test_device_pool_reuse_across_contexts():
+    """The process's device pool (mlp_pool_info / mlp_pool_trim): a closed
+    context's batch scratch and store go back to the pool, the next context
+    (a new family, then 4 virtual shards over it) is carved from the same
+    blocks, and its results equal a run after
+    the pool was trimmed (fresh allocations)."""
+    from mlprobs_amd import engine
+    seqs = [s for _, s in synth.family(40, 150, 0.7, seed=95)]
+    a = Family(seqs)
+    a.set_scratch(2 << 30)
+    a.posteriors(0, 0.132548)
+    a.relax(1)
+    ref = [x.copy() for x in a.export()] + [x.copy() for x in a.results()]
+    a.close()
+    held, free = engine.pool_info(0)
+    assert held > 0 and free == held           # everything back in the pool, nothing returned to the driver
+    b = Family(seqs, shards=4)
+    b.posteriors(0, 0.132548)
+    b.relax(1)
+    got = list(b.export()) + list(b.results())
+    held2, free2 = engine.pool_info(0)
+    b.close()
+    assert engine.pool_info(0)[0] <= 32 << 30  # the last close shrinks the pool (MLP_POOL_KEEP_GB)
+    assert held2 >= held and free2 < held      # carved from the same blocks (and more if they needed it)
+    for x, y in zip(ref, got):
+        np.testing.assert_array_equal(x, y)
+    engine.pool_trim(0)
+    assert engine.pool_info(0) == (0, 0)
+    c = Family(seqs)
+    c.posteriors(0, 0.132548)
+    c.relax(1)
+    for x, y in zip(ref, list(c.export()) + list(c.results())):
+        np.testing.assert_array_equal(x, y)
+    c.close()
