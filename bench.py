@@ -46,6 +46,8 @@ STAGE_BYTES = 56  # pid 0/1 algorithmic bytes per pair-cel
 # reference CLIs' multi-threaded runs
 C5_STAGES = ('features_line', 'class1', 'col_score', 'regions', 'realigned', 'output')
 C5_ATTRIBUTION = 'r05_c5_attribution_recheck.json'
+# the clock every C5 run reads (the -p 1 refinement's srand(time(0)), CPNP/MSA.cpp:1896)
+C5_CLOCK = '1700000000'
 # the printed line stays far below what the driver parses (round 5's 20 KB
 # line was not parsed); the full record goes to DETAIL_PATH
 LINE_LIMIT = 8000
@@ -739,13 +741,20 @@ def c5_pipeline(args):
     `device_runs`).  Readouts: MLProbs' SP score (un_sp) of each final MSA and
     TC against the published MLProbs output of the family (output4evaluation/,
     tests/golden/c5_published.json.xz), and how many outputs equal the
-    reference CLIs' (the reference's multi-threaded quickprobs and
-    time-seeded -p 1 make this informative only; byte parity at every stage
-    is pinned by tests/test_pipeline.py and tests/test_heavy_gpu.py)."""
+    reference CLIs' (the reference's multi-threaded quickprobs makes this
+    informative only; byte parity at every stage is pinned by
+    tests/test_pipeline.py and tests/test_heavy_gpu.py).  The -p 1
+    refinement reseeds rand() with srand(time(0)) (CPNP/MSA.cpp:1896), so
+    every run here -- ours, the reference CLIs', the batch leg's -- reads
+    one fixed clock (C5_CLOCK: MLP_SRAND_TIME for ours, the reference built
+    with oracle/fixtime.c as _ref/c_p_np_aln_ft); at the wall clock two runs
+    of the same family a second apart differ on -p 1 families."""
     import hashlib
     import lzma
     bin_ = os.path.join(ROOT, 'mlprobs_amd', 'cli', 'mlprobs')
-    ref_cp = os.path.join(ROOT, 'oracle', '_ref', 'c_p_np_aln')
+    ref_cp = os.path.join(ROOT, 'oracle', '_ref', 'c_p_np_aln_ft')
+    if not os.path.exists(ref_cp):
+        ref_cp = os.path.join(ROOT, 'oracle', '_ref', 'c_p_np_aln')
     ref_qp = os.path.join(ROOT, 'oracle', '_ref', 'quickprobs')
     if not os.path.exists(bin_):
         return None
@@ -773,7 +782,9 @@ def c5_pipeline(args):
     last_log = time.perf_counter()
     recs, calls, paths, fails, same, differ = [], 0, {}, 0, 0, []
     sp_o, sp_r, sp_p, tc_o, tc_r = [], [], [], [], []
-    env_ref = dict(os.environ, OMP_NUM_THREADS=str(args.cpu_threads), OMP_WAIT_POLICY='passive')
+    env_ref = dict(os.environ, OMP_NUM_THREADS=str(args.cpu_threads), OMP_WAIT_POLICY='passive',
+                   REF_FIXED_TIME=C5_CLOCK)
+    env_ours = dict(os.environ, MLP_SRAND_TIME=C5_CLOCK)
     t_start = time.perf_counter()
     with tempfile.TemporaryDirectory() as td:
         for k, name in enumerate(names):
@@ -786,7 +797,7 @@ def c5_pipeline(args):
                 fh.write(e['fa'].encode('latin-1'))
             out, trace = os.path.join(td, 'o.msa'), os.path.join(td, 't.json')
             t0 = time.perf_counter()
-            r = subprocess.run([bin_, '-q', '--trace', trace, fa, out], capture_output=True, timeout=900)
+            r = subprocess.run([bin_, '-q', '--trace', trace, fa, out], capture_output=True, timeout=900, env=env_ours)
             rec = {'name': name, 'cells': e['cells'], 's': time.perf_counter() - t0, 'device': False, 'ref_s': None}
             recs.append(rec)
             if r.returncode != 0:
@@ -876,8 +887,9 @@ def c5_pipeline(args):
            'sp_un_sp_mean': mean(sp_o), 'published_sp_un_sp_mean': mean(sp_p),
            'tc_vs_published_mean': mean(tc_o), 'wall_s': time.perf_counter() - t_start}
     res['s_per_family'] = res['all'].get('s_per_family')
+    res['clock'] = C5_CLOCK
     if with_ref:
-        res['reference_clis'] = ('the same orchestration driving oracle/_ref/c_p_np_aln (its own thread count, '
+        res['reference_clis'] = (f'the same orchestration driving oracle/_ref/{os.path.basename(ref_cp)} (its own thread count, '
                                  f'passive OpenMP waits) and oracle/_ref/quickprobs -t {args.cpu_threads} as external '
                                  f'commands, on {"every family" if args.c5_ref == "all" else "every 8th family below 5e7 pair-cells"} '
                                  '(speed-ups over the families both ran)')
@@ -924,7 +936,7 @@ def c5_batch(args, devices, per_process=None):
         log(f'c5 batch: {len(names)} families over devices {devices}')
         t0 = time.perf_counter()
         r = subprocess.run([bin_, '-q', '--batch', lst, '--devices', devices, '--report', rep], capture_output=True,
-                           timeout=1800)
+                           timeout=1800, env=dict(os.environ, MLP_SRAND_TIME=C5_CLOCK))
         wall = time.perf_counter() - t0
         if not os.path.exists(rep):
             return {'error': r.stderr.decode(errors='replace')[-400:]}
@@ -951,6 +963,7 @@ def c5_batch(args, devices, per_process=None):
         both = [n for n in names if n in sha and pp.get(n)]
         res['identical_to_per_process'] = sum(sha[n] == pp[n] for n in both)
         res['compared'] = len(both)
+        res['differing_from_per_process'] = [n for n in both if sha[n] != pp[n]][:20]
     log(f"c5 batch: {len(names)} families in {wall:.1f} s ({report['workers']} workers), "
         f"{res.get('identical_to_per_process')} of {res.get('compared')} identical to the per-process runs")
     return res
@@ -1031,7 +1044,7 @@ def compact_c5(c5):
     c = _pick(c5, 'families', 'failed', 'device_path_families', 'host_path_families', 'quickprobs_region_calls',
               'paths', 'speedup_mean', 'speedup_median', 'identical_to_reference_clis', 'reference_clis_families',
               'sp_un_sp_mean', 'published_sp_un_sp_mean', 'tc_vs_published_mean',
-              'reference_clis_tc_vs_published_mean', 'wall_s', 'devices', 'scaling')
+              'reference_clis_tc_vs_published_mean', 'wall_s', 'devices', 'scaling', 'clock')
     for k in ('all', 'device_path', 'host_path'):
         if k in c5:
             s = dict(c5[k].get('s_per_family', {}))
