@@ -1101,7 +1101,7 @@ def compact_line(out):
     if out.get('relax'):
         line['relax'] = compact_relax(out['relax'])
     if out.get('virtual_shards'):
-        line['virtual_shards'] = {k: v for k, v in out['virtual_shards'].items() if k not in ('note', 'store_bytes')}
+        line['virtual_shards'] = {k: v for k, v in out['virtual_shards'].items() if k not in ('note', 'store_bytes', 'pool')}
     if out.get('ranks'):
         line['ranks'] = [{'rank': r['rank'], 'pairs': r['pairs'], 'step_ms': r['step_ms'],
                           'gather_ms': r['gather_ms'], 'gather_GBps': r['gather_GBps'],
@@ -1270,11 +1270,23 @@ def main():
     shards_info = None
     if world == 1 and not args.no_shards and not args.host:
         # the main context's batch scratch (most of the device) goes first: the
-        # 8 shard contexts need their own
+        # 8 shard contexts need their own.  The bench is a long-lived caller
+        # creating one context after another, so the process pool keeps the
+        # closing family's blocks for the shards (MLP_POOL_KEEP_GB; the
+        # default 32 GiB cap would hand them to the driver and the shards'
+        # first allocations would wait for it to clear them, DESIGN.md
+        # section 3), and gives them back after the leg
+        from mlprobs_amd import engine
+        os.environ['MLP_POOL_KEEP_GB'] = '1000000'
         fam.close()
         fam = None
         log('virtual shards')
-        shards_info = shard_gather(args, seqs, post_hash, relax_info['round1_hash'] if relax_info else None)
+        try:
+            shards_info = shard_gather(args, seqs, post_hash, relax_info['round1_hash'] if relax_info else None)
+        finally:
+            os.environ.pop('MLP_POOL_KEEP_GB', None)
+            engine.pool_trim(0)
+        shards_info['pool'] = 'the main family\'s blocks kept for the shard contexts'
     if world > 1 and not args.host and not args.no_c5 and not args.no_e2e:
         # C5 at family level over all N GPUs: the ranks release their
         # contexts first, then rank 0's workers take one device each
