@@ -89,7 +89,8 @@ def groups(o, d):
                 b = json.loads(line)
                 cells = b['config']['pair_cells'] * (b['steps'] + b['warmup'])
                 if b.get('relax') and b['relax']['rounds'] == 1:
-                    nnz_in = b['relax']['per_round'][0]['nnz_in']
+                    r0 = b['relax']['per_round'][0]
+                    nnz_in = r0['nnz_in'] if 'nnz_in' in r0 else b['relax']['nnz_per_round'][0]
         if cells:
             break
     out = {'_source': os.path.basename(os.path.normpath(d)), '_pair_cells': cells,
