@@ -83,9 +83,19 @@ __device__ __forceinline__ float mlp_log_add_t(float x, float y, const float4* _
   // table index were two half-rate instructions per LOG_ADD: C3 forward
   // 184 -> 180.5, backward 243.7 -> 237, local totals 97-100 -> 83-92 ms a
   // step, profiles/r05o_ab_lookup_byteoff.txt)
-  int q16;
-  asm("v_cvt_i32_f32 %0, %1" : "=v"(q16) : "v"(d * 0x1.fffffep4f));
-  const float4 c = *(const float4*)((const char*)lk + (q16 & 0xf0));
+  // Round 6: the integer floor(fl(d * 16M)) without the half-rate convert:
+  // fma(d, 16M, -0.5) + 1.5 * 2^23 rounds to it in the float's low mantissa
+  // bits (a tie, fl(d * 16M) an integer, goes to the even one, which keeps
+  // every multiple of 16 in its row), two full-rate instructions for a
+  // full-rate multiply and a half-rate convert; the same row on every float
+  // d in [0, 7.5) (tools/check_lookup_rows.py, exhaustive; sampled in
+  // tests/test_numerics_lookup_rows.py)
+  // (asm: the compiler's v_fma_f32 takes 16M from an SGPR, a half-rate
+  // operand; v_fmamk_f32 carries it as a literal, -0.5 in a VGPR)
+  float t;
+  asm("v_fmamk_f32 %0, %1, 0x41ffffff, %2" : "=v"(t) : "v"(d), "v"(-0.5f));
+  const float u = t + 12582912.0f;
+  const float4 c = *(const float4*)((const char*)lk + (__float_as_int(u) & 0xf0));
   const float r = (((c.x * d + c.y) * d + c.z) * d + c.w) + lo;
   return (d >= 7.5f) ? hi : r;
 }
