@@ -66,6 +66,15 @@ __global__ __launch_bounds__(256) void k_rate(uint32_t a, uint32_t b, uint32_t* 
       if constexpr (KIND == 27) OP2("v_xor_b32");
       if constexpr (KIND == 28) OP3("v_lshl_or_b32");
       if constexpr (KIND == 29) asm volatile("v_max3_f32 %0, %1, %2, %0" : "+v"(x[k]) : "v"(a), "v"(b));
+      if constexpr (KIND == 30) asm volatile("v_add_co_u32_e32 %0, vcc, %1, %0" : "+v"(x[k]) : "v"(a) : "vcc");  // carry out to VCC
+      if constexpr (KIND == 31) asm volatile("v_sub_co_u32_e32 %0, vcc, %0, %1" : "+v"(x[k]) : "v"(a) : "vcc");
+      if constexpr (KIND == 32) {  // carry out to an SGPR pair
+        uint64_t c_;
+        asm volatile("v_add_co_u32_e64 %0, %1, %2, %0" : "+v"(x[k]), "=s"(c_) : "v"(a));
+      }
+      if constexpr (KIND == 33) OP2("v_mul_u32_u24");
+      if constexpr (KIND == 34) asm volatile("v_cmp_ne_u32_e32 vcc, %1, %0" : : "v"(x[k]), "v"(a) : "vcc");
+      if constexpr (KIND == 35) OP2("v_lshlrev_b16");
     }
   }
   uint32_t s = 0;
@@ -126,7 +135,8 @@ int main() {
                            "v_cvt_i32_f32", "v_fma_f32_sgpr", "v_mul_f32_sgpr",
                            "v_lshlrev_b32", "v_sub_f32", "v_min_f32", "v_mov_b32", "v_mad_u32_u24", "v_add3_u32",
                            "v_cmp_e32+v_cndmask_vcc_pair", "v_cmp_le_f32_vcc", "v_max_u32", "v_xor_b32", "v_lshl_or_b32",
-                           "v_max3_f32"};
+                           "v_max3_f32", "v_add_co_u32_vcc", "v_sub_co_u32_vcc", "v_add_co_u32_sgpr_pair",
+                           "v_mul_u32_u24", "v_cmp_ne_u32_vcc", "v_lshlrev_b16"};
   const char* names64[] = {"v_add_f64", "v_fma_f64", "v_pk_add_f32", "v_pk_fma_f32"};
   const int waves[] = {1, 2, 4, 8};
   auto report = [&](const char* name, int W, double chains, float ms) {
@@ -186,6 +196,16 @@ int main() {
     run32(k_rate<27>, names32[27]);
     run32(k_rate<28>, names32[28]);
     run32(k_rate<29>, names32[29]);
+  }
+  if (getenv("VALU_RATE_CARRY")) {
+    run32(k_rate<30>, names32[30]);
+    run32(k_rate<31>, names32[31]);
+    run32(k_rate<32>, names32[32]);
+    run32(k_rate<33>, names32[33]);
+    run32(k_rate<34>, names32[34]);
+    run32(k_rate<35>, names32[35]);
+    run32(k_rate<3>, names32[3]);
+    run32(k_rate<5>, names32[5]);
   }
   run64(k_rate64<0>, names64[0]);
   run64(k_rate64<1>, names64[1]);
