@@ -97,6 +97,7 @@ struct ChainView {
   const ChainPair* P;   // K + 1 entries, P[K].row0 = rows
   const uint8_t* seq;   // residues of all members
   int K, W, rows, S;
+  int64_t ell0;         // the first member's first ELL row (members' rows follow in slot order)
 };
 
 enum StageKind { kStageFwd = 0, kStageBwd = 1, kStageMerge = 2 };
@@ -168,6 +169,7 @@ __device__ ChainView stage_chain(uint8_t* dyn, int lds_seq, int64_t ch, SeqSet s
   v.W = W;
   v.rows = cm.rows[ch];
   v.S = chain_strips(v.rows);
+  v.ell0 = pm.ell_row[first];
   return v;
 }
 
@@ -193,7 +195,7 @@ struct Cursor {
   int jlo, jhi, jend, jfirst, jact;   // jact: L2 (an active row) or -1 (idle)
   int jpf;   // PF backward: the cell is off rows 1, L1 and columns 1, L2 iff 2 <= j < jpf
   int jm;    // merge: a cell of the pair (i >= 1, 1 <= j <= L2) iff (unsigned)(j - 1) < jm
-  int64_t ellx;   // merge: the row's first ELL slot, (ell + i - 1) * kEll
+  uint32_t ellr;  // merge: the row's first ELL slot from the chain's first, (ell - ell0 + i - 1) * kEll
 };
 
 __device__ __forceinline__ void locate(Cursor& c, const ChainView& C, const float* __restrict__ ins) {
@@ -201,7 +203,7 @@ __device__ __forceinline__ void locate(Cursor& c, const ChainView& C, const floa
     c.q = -1; c.i = -1; c.L1 = -1; c.L2 = -1; c.c1 = 0; c.c1n = 0; c.c1x = 0; c.c1nx = 0;
     c.ca = c.j;   // the zero area
     c.ins1 = ins[0]; c.ins1n = ins[0];
-    c.jlo = 1 << 30; c.jhi = 0; c.jend = -1; c.jfirst = -1; c.jact = -1; c.jpf = 2; c.jm = 0; c.ellx = 0;
+    c.jlo = 1 << 30; c.jhi = 0; c.jend = -1; c.jfirst = -1; c.jact = -1; c.jpf = 2; c.jm = 0; c.ellr = 0;
     return;
   }
   int q = c.q < 0 ? 0 : c.q;
@@ -234,7 +236,7 @@ __device__ __forceinline__ void locate(Cursor& c, const ChainView& C, const floa
   c.jact = c.L2;
   c.jpf = c.i >= 2 && c.i < c.L1 && c.L2 > 2 ? c.L2 : 2;
   c.jm = c.i >= 1 ? c.L2 : 0;
-  c.ellx = (c.ell + c.i - 1) * kEll;
+  c.ellr = (uint32_t)(c.ell - C.ell0 + c.i - 1) * (uint32_t)kEll;
 }
 
 // forward-order cursor at step 0: lane r at u = -r
@@ -294,6 +296,22 @@ __device__ __forceinline__ void bstore(const int32_t* base, uint32_t boff, int32
 }
 __device__ __forceinline__ void bstore(const double* base, uint32_t boff, double v) {
   __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(mlp_u32x2, v), wave_rsrc(base), boff, 0, 0);
+}
+__device__ __forceinline__ void bstore(const uint16_t* base, uint32_t boff, uint16_t v) {
+  __builtin_amdgcn_raw_buffer_store_b16(v, wave_rsrc(base), boff, 0, 0);
+}
+typedef unsigned mlp_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void bstore4(const float* base, uint32_t boff, float4 v) {
+  const mlp_u32x4 u = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
+  __builtin_amdgcn_raw_buffer_store_b128(u, wave_rsrc(base), boff, 0, 0);
+}
+__device__ __forceinline__ void bstore4(const uint16_t* base, uint32_t boff, uint4 v) {
+  const mlp_u32x4 u = {v.x, v.y, v.z, v.w};
+  __builtin_amdgcn_raw_buffer_store_b128(u, wave_rsrc(base), boff, 0, 0);
+}
+__device__ __forceinline__ void bstore2(const uint16_t* base, uint32_t boff, uint2 v) {
+  const mlp_u32x2 u = {v.x, v.y};
+  __builtin_amdgcn_raw_buffer_store_b64(u, wave_rsrc(base), boff, 0, 0);
 }
 __device__ __forceinline__ float bload(const float* base, uint32_t boff) {
   return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(wave_rsrc(base), boff, 0, 0));

@@ -690,6 +690,11 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
 // recurrence: every cell carries the B count of the path its ChooseBestOfThree
 // choice extends (the traceback follows exactly those choices), so the last
 // cell holds the count of the traced path without a traceback matrix.
+#ifndef MLP_ELL_CHUNK
+#define MLP_ELL_CHUNK 8
+#endif
+constexpr int kEllChunk = MLP_ELL_CHUNK;   // staged ELL entries a lane writes at once (4, 8 or 16)
+static_assert(kEllChunk == 4 || kEllChunk == 8 || kEllChunk == 16 || kEllChunk == 32, "ELL chunk: 4, 8, 16 or 32 entries");
 template <int M, int PID, bool NP = false>
 #ifndef MLP_MERGE_WAVES
 #define MLP_MERGE_WAVES 6
@@ -735,6 +740,27 @@ __global__ __launch_bounds__(256, NP && M == (kHmm5 | kLocal | kPF) ? 5 : MLP_ME
     if constexpr ((M & kLocal) != 0) { ql[k] = bload(sc.fl + at, ul4); qb[k] = bload(sc.bl + at, ul4); }
     if constexpr ((M & kPF) != 0) qg[k] = bload(sc.pg + at * sc.pg_stride, ul4 * sc.pg_stride);
   }
+  const uint16_t* const ecol = sc.ell_col + C.ell0 * kEll;   // the chain's ELL rows (wave-uniform)
+  const float* const evals = sc.ell_val + C.ell0 * kEll;
+  // the lane's staged ELL entries (see the cutoff below), kEllChunk of them
+  constexpr int KS = kEllChunk;
+  __shared__ __align__(16) float ell_stv[kWavesPerBlock * 64 * KS];
+  __shared__ __align__(16) uint16_t ell_stc[kWavesPerBlock * 64 * KS];
+  float* const stv = ell_stv + ((threadIdx.x >> 6) * 64 + lane) * KS;
+  uint16_t* const stc = ell_stc + ((threadIdx.x >> 6) * 64 + lane) * KS;
+  // entries k0 .. k0 + KS - 1 of the lane's row (k0 a multiple of KS:
+  // aligned slots of the row's kEll)
+  auto ell_flush = [&](int k0) {
+    const uint32_t e = c.ellr + (uint32_t)k0;
+#pragma unroll
+    for (int q = 0; q < KS / 4; ++q) bstore4(evals, 4u * e + 16u * q, reinterpret_cast<const float4*>(stv)[q]);
+    if constexpr (KS == 4) {
+      bstore2(ecol, 2u * e, *reinterpret_cast<const uint2*>(stc));
+    } else {
+#pragma unroll
+      for (int q = 0; q < KS / 8; ++q) bstore4(ecol, 2u * e + 16u * q, reinterpret_cast<const uint4*>(stc)[q]);
+    }
+  };
   const int nseg = (W + 63) >> 6;
   for (int k = 0; k <= S; ++k) {
     const int segs = k < S ? nseg : 1;
@@ -799,19 +825,24 @@ __global__ __launch_bounds__(256, NP && M == (kHmm5 | kLocal | kPF) ? 5 : MLP_ME
           Cv = mlp_max(mlp_max(x1, x2), x3);
           if constexpr (NP)  // ChooseBestOfThree's pick (ScoreType.h:347-366): D, else L, else U
             Cc = (x1 >= x2 && x1 >= x3) ? Dc + 1 : (x1 < x2 && x2 >= x3) ? Lc : Uc;
-          if (P >= 0.01f) {  // POSTERIOR_CUTOFF (CPNP/SparseMatrix.h:14)
-            if (cnt < kEll) {
-              sc.ell_col[c.ellx + cnt] = (uint16_t)j;
-              // QuickProbs keeps 16-bit fixed point: (uint16)(P * 65535), read back
-              // as q / 65535 (QP/DataStructures/SparseEntry.h:31-32)
-              sc.ell_val[c.ellx + cnt] =
-                  PID == kPidQP ? (float)(uint32_t)(uint16_t)(P * 65535.0f) / 65535.0f : P;
-            } else {
-              atomicOr(&rec[c.slot].flags, 2);
-            }
-            ++cnt;
+          // POSTERIOR_CUTOFF (CPNP/SparseMatrix.h:14).  A row's entries arrive
+          // one per step over ~10-30 steps; stored one by one (2 + 4 bytes) the
+          // rows' lines left L2 partly written several times (1.6 B/cell written
+          // against 0.16, the stores ~20% of the merge).  Staged per lane in
+          // LDS, they go out kEllChunk at a time (aligned 16-byte pieces), the row's
+          // last chunk when it completes (slots past cnt carry stale values
+          // k_compact never reads).  A row past kEll entries keeps counting,
+          // stores nothing more and is flagged when it completes.
+          const bool keep = P >= 0.01f;
+          if (keep && cnt < kEll) {
+            stv[cnt & (KS - 1)] = PID == kPidQP ? (float)(uint32_t)(uint16_t)(P * 65535.0f) / 65535.0f : P;
+            stc[cnt & (KS - 1)] = (uint16_t)j;
+            if ((cnt & (KS - 1)) == KS - 1) ell_flush(cnt - (KS - 1));
           }
+          cnt += keep ? 1 : 0;
           if (j == L2) {   // row complete
+            if ((cnt & (KS - 1)) != 0 && cnt < kEll) ell_flush(cnt & ~(KS - 1));
+            if (cnt > kEll) atomicOr(&rec[c.slot].flags, 2);
             sc.ell_cnt[c.ell + (i - 1)] = cnt;
             atomicAdd(reinterpret_cast<unsigned long long*>(&rec[c.slot].nnz), (unsigned long long)cnt);
             cnt = 0;
