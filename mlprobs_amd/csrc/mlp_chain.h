@@ -320,14 +320,45 @@ __device__ __forceinline__ double bload(const double* base, uint32_t boff) {
   return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(wave_rsrc(base), boff, 0, 0));
 }
 
-// A chain's boundary rows are stored component-major: component k of column
-// j at base + k W + j, base = the chain's bnd_off times the components per
-// column, so a chunk's load is one coalesced access per component.  The one
-// lane that crosses the strip stores its column: the column of that lane at
-// a step is wave-uniform (a scalar counter), so the store's whole address is
-// scalar.
+// A chain's boundary rows are stored column-major, one 32-byte record per
+// column: the HMMs' (bnd5) the 5-state values then the local model's three,
+// the partition function's (bndz) its three doubles then the frame.  The one
+// lane that crosses the strip stores its column's record: the column of that
+// lane at a step is wave-uniform (a scalar counter), so the stores' whole
+// address is scalar, two 16-byte stores a step where one store per component
+// took eight, and consecutive steps fill a line in four steps instead of each
+// component's line in 32 (round 5's component-major rows left L2 lines
+// partly written).  A chunk's load is two 16-byte loads a lane, contiguous
+// across the lanes.
 template <class T>
 __device__ __forceinline__ void bnd_put(const T* comp, int j_uniform, T v) { bstore(comp + j_uniform, 0, v); }
+__device__ __forceinline__ void bnd_put_hmm(const float* recs, int j_uniform, float4 a, float4 b) {
+  bstore4(recs + 8 * j_uniform, 0, a);
+  bstore4(recs + 8 * j_uniform + 4, 0, b);
+}
+__device__ __forceinline__ void bnd_put_pf(const double* recs, int j_uniform, double m, double e, double f, int E) {
+  const uint64_t um = (uint64_t)__double_as_longlong(m), ue = (uint64_t)__double_as_longlong(e);
+  const uint64_t uf = (uint64_t)__double_as_longlong(f);
+  const mlp_u32x4 a = {(uint32_t)um, (uint32_t)(um >> 32), (uint32_t)ue, (uint32_t)(ue >> 32)};
+  const mlp_u32x4 b = {(uint32_t)uf, (uint32_t)(uf >> 32), (uint32_t)E, 0u};
+  __builtin_amdgcn_raw_buffer_store_b128(a, wave_rsrc(recs + 4 * j_uniform), 0, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b128(b, wave_rsrc(recs + 4 * j_uniform + 2), 0, 0, 0);
+}
+// a column's records into the loader's registers
+__device__ __forceinline__ void bnd_get_hmm(const Scratch& sc, int64_t bo, uint32_t col, float* n5, float* nl) {
+  const float4* r = reinterpret_cast<const float4*>(sc.bnd5 + bo * 8) + 2 * (int64_t)col;
+  const float4 a = r[0], b = r[1];
+  n5[0] = a.x; n5[1] = a.y; n5[2] = a.z; n5[3] = a.w; n5[4] = b.x;
+  nl[0] = b.y; nl[1] = b.z; nl[2] = b.w;
+}
+__device__ __forceinline__ void bnd_get_pf(const Scratch& sc, int64_t bo, uint32_t col, double* nz, int& ne) {
+  const uint4* r = reinterpret_cast<const uint4*>(sc.bndz + bo * 4) + 2 * (int64_t)col;
+  const uint4 a = r[0], b = r[1];
+  nz[0] = __longlong_as_double((long long)(((uint64_t)a.y << 32) | a.x));
+  nz[1] = __longlong_as_double((long long)(((uint64_t)a.w << 32) | a.z));
+  nz[2] = __longlong_as_double((long long)(((uint64_t)b.y << 32) | b.x));
+  ne = (int)b.z;
+}
 
 // Boundary row of the neighbouring strip, read 64 columns at a time (one per
 // lane) and double-buffered: the sweeps switch buffers between 64-step
@@ -345,22 +376,8 @@ struct BoundaryChunks {
   // segment's first column (the backward sweep's partial segments)
   __device__ __forceinline__ void load_next(const Scratch& sc, int64_t bo, int W, int col0, int lane, int back = 0) {
     const uint32_t col = (uint32_t)min(max(col0 + lane - back, 0), W - 1);
-    if constexpr ((M & kHmm5) != 0) {
-      const float* b5 = sc.bnd5 + bo * 5;
-#pragma unroll
-      for (int k = 0; k < 5; ++k) n5[k] = b5[k * W + col];
-    }
-    if constexpr ((M & kLocal) != 0) {
-      const float* bl = sc.bndl + bo * 3;
-#pragma unroll
-      for (int k = 0; k < 3; ++k) nl[k] = bl[k * W + col];
-    }
-    if constexpr ((M & kPF) != 0) {
-      const double* bz = sc.bndz + bo * 3;
-#pragma unroll
-      for (int k = 0; k < 3; ++k) nz[k] = bz[k * W + col];
-      ne = sc.bnde[bo + col];
-    }
+    if constexpr ((M & (kHmm5 | kLocal)) != 0) bnd_get_hmm(sc, bo, col, n5, nl);
+    if constexpr ((M & kPF) != 0) bnd_get_pf(sc, bo, col, nz, ne);
   }
   uint8_t* area = nullptr;   // (interface of LdsBoundaryChunks; unused)
   __device__ __forceinline__ void advance(int) { advance(); }
@@ -441,22 +458,8 @@ struct LdsBoundaryChunks {
   uint8_t* area;   // this wave's 64 x Lay::bytes
   __device__ __forceinline__ void load_next(const Scratch& sc, int64_t bo, int W, int col0, int lane, int back = 0) {
     const uint32_t col = (uint32_t)min(max(col0 + lane - back, 0), W - 1);
-    if constexpr ((M & kHmm5) != 0) {
-      const float* b5 = sc.bnd5 + bo * 5;
-#pragma unroll
-      for (int k = 0; k < 5; ++k) n5[k] = b5[k * W + col];
-    }
-    if constexpr ((M & kLocal) != 0) {
-      const float* bl = sc.bndl + bo * 3;
-#pragma unroll
-      for (int k = 0; k < 3; ++k) nl[k] = bl[k * W + col];
-    }
-    if constexpr ((M & kPF) != 0) {
-      const double* bz = sc.bndz + bo * 3;
-#pragma unroll
-      for (int k = 0; k < 3; ++k) nz[k] = bz[k * W + col];
-      ne = sc.bnde[bo + col];
-    }
+    if constexpr ((M & (kHmm5 | kLocal)) != 0) bnd_get_hmm(sc, bo, col, n5, nl);
+    if constexpr ((M & kPF) != 0) bnd_get_pf(sc, bo, col, nz, ne);
   }
   // the loaded chunk becomes the current one: this lane's column into LDS
   // (the wave's reads of the previous chunk precede it in LDS order)

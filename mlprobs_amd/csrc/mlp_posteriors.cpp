@@ -85,7 +85,7 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
     const int L1 = c->lens[c->pa[q]], L2 = c->lens[c->pb[q]];
     const int64_t rmc = (models & kLocal) ? (int64_t)L1 * local_chunks(L2) : 0;
     return (size_t)(pair_slots_bound(c, q) * slot_bytes + rmc * 8) +
-           (size_t)pair_width_bound(c, q) * (5 * 4 + 3 * 4 + 3 * 8 + 4 + 4 + 4) +
+           (size_t)pair_width_bound(c, q) * (32 + 32 + 4 + 4) +
            (size_t)L1 * (kEll * 6 + 4 + 4) + 4 + kPerSlotMeta;  // + the lane fold's row bounds, repair slot
   };
   // Batches run one after another on the context stream (two batches
@@ -287,10 +287,10 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
     o.crb = cv.take(lanefold || foldbound ? P.ell_rows * 4 : 0);
     o.rep = cv.take(lanefold ? (np + 1) * 4 : 0);
     o.lfc = cv.take(lanefold && defer ? P.ell_rows * 4 : 0);  // (else the lane fold counts in ell_cnt)
-    o.b5 = cv.take(P.bnd * 20);
-    o.bnl = cv.take(P.bnd * 12);
-    o.bz = cv.take(P.bnd * 24);
-    o.be = cv.take(P.bnd * 4);
+    o.b5 = cv.take(P.bnd * 32);   // the HMMs' boundary records (mlp_chain.h, bnd_put_hmm)
+    o.bnl = 0;
+    o.bz = cv.take(P.bnd * 32);   // the partition function's
+    o.be = 0;
     o.bm = cv.take(P.bnd * 4);
     o.bc = cv.take(P.bnd * 4);
     if (!defer) {
@@ -384,9 +384,9 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
     static const bool force_repair = knob_set("MLP_TEST_TOT_FORCE_REPAIR");
     sc.force_repair = force_repair ? 1 : 0;
     sc.bnd5 = (float*)(base + o.b5);
-    sc.bndl = (float*)(base + o.bnl);
+    sc.bndl = nullptr;   // (the Viterbi sweep's, mlp_profile_rt.cpp)
     sc.bndz = (double*)(base + o.bz);
-    sc.bnde = (int32_t*)(base + o.be);
+    sc.bnde = nullptr;
     sc.bndm = (float*)(base + o.bm);
     sc.bndc = (int32_t*)(base + o.bc);
     sc.ell_col = (uint16_t*)(base + o.ec);

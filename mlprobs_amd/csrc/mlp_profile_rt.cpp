@@ -392,7 +392,7 @@ int mlp_viterbi(mlp_ctx* c, int64_t p0, int64_t p1, int keep_paths) {
   if (keep_paths && c->vit_path.size() != (size_t)c->vit_off[c->P]) c->vit_path.assign(c->vit_off[c->P], 0);
   auto pair_bytes = [&](int64_t q) {
     const int L1 = c->lens[c->pa[q]], L2 = c->lens[c->pb[q]];
-    return (size_t)pair_slots_bound(c, q) + (size_t)pair_width_bound(c, q) * 12 + (size_t)(L1 + L2) +
+    return (size_t)pair_slots_bound(c, q) + (size_t)pair_width_bound(c, q) * 32 + (size_t)(L1 + L2) +
            kPerSlotMeta + 24;
   };
   const size_t batch_target = batch_target_for(c, p0, p1, pair_bytes);
@@ -410,7 +410,7 @@ int mlp_viterbi(mlp_ctx* c, int64_t p0, int64_t p1, int keep_paths) {
       h_poff[s + 1] = h_poff[s] + c->lens[c->pa[x]] + c->lens[c->pb[x]];
     }
     Carver cv;
-    const size_t o_vt = cv.take(P.cells), o_bl = cv.take(P.bnd * 12), o_path = cv.take(h_poff[np]),
+    const size_t o_vt = cv.take(P.cells), o_bl = cv.take(P.bnd * 32), o_path = cv.take(h_poff[np]),
                  o_poff = cv.take(np * 8), o_plen = cv.take(np * 4), o_match = cv.take(np * 4),
                  o_state = cv.take(np * 4);
     const PlanDev pd = carve_plan(cv, P);
@@ -418,7 +418,7 @@ int mlp_viterbi(mlp_ctx* c, int64_t p0, int64_t p1, int keep_paths) {
     char* base = (char*)c->scratch.p;
     Scratch sc{};
     sc.vt = (uint8_t*)(base + o_vt);
-    sc.bndl = (float*)(base + o_bl);
+    sc.bnd5 = (float*)(base + o_bl);   // the boundary records (mlp_chain.h)
     VitOut vo;
     vo.path = (uint8_t*)(base + o_path);
     vo.path_off = (const int64_t*)(base + o_poff);

@@ -132,10 +132,8 @@ __global__ __launch_bounds__(256, SweepWaves<M>::fwd) void k_forward(ModelScalar
   // lane 63's column (the strip's last row, stored into the boundary row):
   // W - 63 at step 0 (idle until step 63), one column per step, wrapping at W
   int j63 = W - 63;
-  float* const b5 = sc.bnd5 + bo * 5;
-  float* const bl = sc.bndl + bo * 3;
-  double* const bz = sc.bndz + bo * 3;
-  int32_t* const be = sc.bnde + bo;
+  float* const bh = sc.bnd5 + bo * 8;    // boundary records (mlp_chain.h)
+  double* const bz = sc.bndz + bo * 4;
   const float rt1 = ms.rt1, two_rt1 = 2 * ms.rt1;
   const double pfo = ms.pf_open, pfe = ms.pf_ext;
   Cursor c;
@@ -215,6 +213,8 @@ __global__ __launch_bounds__(256, SweepWaves<M>::fwd) void k_forward(ModelScalar
         bc.template shift_at<true>(colp + u * LdsChunkLayout<M>::bytes, L5, U5, LL, UL, LZm, LZe, LZf, Le, UZm, UZe,
                                    UZf, Ue);
         const int64_t tcell = cell0 + (int64_t)t * 64;   // wave-uniform
+        // the HMMs' boundary record of lane 63's column (bnd_put_hmm)
+        float4 bha = make_float4(0.f, 0.f, 0.f, 0.f), bhb = make_float4(0.f, 0.f, 0.f, 0.f);
         // ------------------------------------------------ 5-state forward
         if constexpr ((M & kHmm5) != 0) {
           const float mt = T_.match[c.c1x + c2];
@@ -256,10 +256,8 @@ __global__ __launch_bounds__(256, SweepWaves<M>::fwd) void k_forward(ModelScalar
             for (int k5 = 0; k5 < 5; ++k5) tf = mlp_log_add_t(tf, Cc[k5] + ms.init[k5], lk);
             rec[c.slot].tf5 = tf;
           }
-          if (lane == 63) {
-#pragma unroll
-            for (int k5 = 0; k5 < 5; ++k5) bnd_put(b5 + k5 * W, j63, Cc[k5]);
-          }
+          bha = make_float4(Cc[0], Cc[1], Cc[2], Cc[3]);
+          bhb.x = Cc[4];
 #pragma unroll
           for (int k5 = 0; k5 < 5; ++k5) L5[k5] = Cc[k5];
         }
@@ -288,11 +286,7 @@ __global__ __launch_bounds__(256, SweepWaves<M>::fwd) void k_forward(ModelScalar
             }
           }
           bstore(sc.fl + tcell, ul4, Cm);
-          if (lane == 63) {
-            bnd_put(bl + 0 * W, j63, Cm);
-            bnd_put(bl + 1 * W, j63, Cx);
-            bnd_put(bl + 2 * W, j63, Cy);
-          }
+          bhb.y = Cm; bhb.z = Cx; bhb.w = Cy;
           // the chain total's input: the largest f_M of each 64-column chunk
           // of the row (from column 0, whose LZ never exceeds a real value)
           cmx = mlp_max(cmx, Cm);
@@ -303,6 +297,9 @@ __global__ __launch_bounds__(256, SweepWaves<M>::fwd) void k_forward(ModelScalar
             cmx = -INFINITY;
           }
           LL[0] = Cm; LL[1] = Cx; LL[2] = Cy;
+        }
+        if constexpr ((M & (kHmm5 | kLocal)) != 0) {
+          if (lane == 63) bnd_put_hmm(bh, j63, bha, bhb);
         }
         // ------------------------------------------------ partition function forward
         if constexpr ((M & kPF) != 0) {
@@ -341,12 +338,7 @@ __global__ __launch_bounds__(256, SweepWaves<M>::fwd) void k_forward(ModelScalar
             rec[c.slot].zmant = (M & kQP) != 0 ? (Zm + Zf) + Ze : (Zm + Ze) + Zf;
             rec[c.slot].zexp = E;
           }
-          if (lane == 63) {
-            bnd_put(bz + 0 * W, j63, Zm);
-            bnd_put(bz + 1 * W, j63, Ze);
-            bnd_put(bz + 2 * W, j63, Zf);
-            bnd_put(be, j63, E);
-          }
+          if (lane == 63) bnd_put_pf(bz, j63, Zm, Ze, Zf, E);
           LZm = Zm; LZe = Ze; LZf = Zf; Le = E;
         }
         cursor_next(c, C, T_.ins, local_row);
@@ -378,10 +370,8 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
   const int64_t cell0 = cm.cell_off[ch] + 64;   // slot of step tau, lane l: cell0 + tau * 64 + l
   const uint32_t ul4 = (uint32_t)lane * 4;     // the lane's byte offset in a step's fp32 slots
   const int64_t bo = cm.bnd_off[ch];
-  float* const b5 = sc.bnd5 + bo * 5;
-  float* const bl = sc.bndl + bo * 3;
-  double* const bz = sc.bndz + bo * 3;
-  int32_t* const be = sc.bnde + bo;
+  float* const bh = sc.bnd5 + bo * 8;    // boundary records (mlp_chain.h)
+  double* const bz = sc.bndz + bo * 4;
   const float rt1 = ms.rt1, two_rt1 = 2 * ms.rt1;
   const double pfo = ms.pf_open, pfe = ms.pf_ext;
   const int top = S * W + 62;   // last step with an active lane (lane 63, column W-1)
@@ -497,6 +487,8 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
         bc.template shift_at<false>(colp + (kPrefetch - 1 - u) * LdsChunkLayout<M>::bytes, R5, N5, RL, NL, RZm, RZe,
                                     RZf, Re, NZm, NZe, NZf, Ne);
         const int64_t tcell = cell0 + (int64_t)t * 64;   // wave-uniform
+        // the HMMs' boundary record of lane 0's column (bnd_put_hmm)
+        float4 bha = make_float4(0.f, 0.f, 0.f, 0.f), bhb = make_float4(0.f, 0.f, 0.f, 0.f);
         // ------------------------------------------------ 5-state backward
         if constexpr ((M & kHmm5) != 0) {
           const float ins2n = T_.ins[c2n];
@@ -540,10 +532,8 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
             if (i == 1 && j == 0) { rec[c.slot].b5[1] = B[1]; rec[c.slot].b5[3] = B[3]; }
             if (i == 0 && j == 1) { rec[c.slot].b5[2] = B[2]; rec[c.slot].b5[4] = B[4]; }
           }
-          if (lane == 0) {
-#pragma unroll
-            for (int k5 = 0; k5 < 5; ++k5) bnd_put(b5 + k5 * W, j0, B[k5]);
-          }
+          bha = make_float4(B[0], B[1], B[2], B[3]);
+          bhb.x = B[4];
 #pragma unroll
           for (int k5 = 0; k5 < 5; ++k5) R5[k5] = B[k5];
         }
@@ -580,11 +570,7 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
           }
           }  // !interior
           bstore(sc.bl + tcell, ul4, Bm);   // f + b is formed by the merge (the same float add)
-          if (lane == 0) {
-            bnd_put(bl + 0 * W, j0, Bm);
-            bnd_put(bl + 1 * W, j0, Bx);
-            bnd_put(bl + 2 * W, j0, By);
-          }
+          bhb.y = Bm; bhb.z = Bx; bhb.w = By;
           // chain element (CPNP/ProbabilisticModel.h:444-445); columns descend,
           // so a chunk starts at its top column (L2: idle columns above it are
           // dropped there; or a multiple of 64: reset by the store before it)
@@ -600,6 +586,9 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
             }
           }
           RL[0] = Bm; RL[1] = Bx; RL[2] = By;
+        }
+        if constexpr ((M & (kHmm5 | kLocal)) != 0) {
+          if (lane == 0) bnd_put_hmm(bh, j0, bha, bhb);
         }
         // ------------------------------------------------ partition function reverse
         if constexpr ((M & kPF) != 0) {
@@ -660,12 +649,7 @@ __global__ __launch_bounds__(256, SweepWaves<M>::bwd) void k_backward(ModelScala
             }
           }
           bstore(sc.pg + tcell * sc.pg_stride, ul4 * sc.pg_stride, post);   // after this cell's zm was read (prefetch)
-          if (lane == 0) {
-            bnd_put(bz + 0 * W, j0, Zm);
-            bnd_put(bz + 1 * W, j0, Ze);
-            bnd_put(bz + 2 * W, j0, Zf);
-            bnd_put(be, j0, E);
-          }
+          if (lane == 0) bnd_put_pf(bz, j0, Zm, Ze, Zf, E);
           RZm = Zm; RZe = Ze; RZf = Zf; Re = E;
         }
         // refill slot u after its value is dead, so the load reuses the register

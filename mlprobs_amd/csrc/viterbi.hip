@@ -97,11 +97,9 @@ __global__ __launch_bounds__(256) void k_viterbi(ModelScalars ms, const Tables* 
             if (best < tv[k3]) { best = tv[k3]; st = k3; }
           vo.state[c.slot] = st;
         }
-        if (lane == 63) {   // the boundary row, component-major (mlp_chain.h)
-          float* const bl = sc.bndl + bo * 3;
-          (bl + 0 * W)[(uint32_t)j] = V0;
-          (bl + 1 * W)[(uint32_t)j] = V1;
-          (bl + 2 * W)[(uint32_t)j] = V2;
+        if (lane == 63) {   // the boundary record of the column (mlp_chain.h: the local model's three)
+          float4* const r = reinterpret_cast<float4*>(sc.bnd5 + bo * 8) + 2 * (int64_t)(uint32_t)j;
+          r[1] = make_float4(0.f, V0, V1, V2);
         }
         LV[0] = V0; LV[1] = V1; LV[2] = V2;
         cursor_next(c, C, T_.ins);
