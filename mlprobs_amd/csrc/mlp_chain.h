@@ -327,7 +327,7 @@ __device__ __forceinline__ double bload(const double* base, uint32_t boff) {
 // lane at a step is wave-uniform (a scalar counter), so the stores' whole
 // address is scalar, two 16-byte stores a step where one store per component
 // took eight, and consecutive steps fill a line in four steps instead of each
-// component's line in 32 (round 5's component-major rows left L2 lines
+// component's line in 32 (the component-major rows before left L2 lines
 // partly written).  A chunk's load is two 16-byte loads a lane, contiguous
 // across the lanes.
 template <class T>

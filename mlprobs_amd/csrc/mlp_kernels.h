@@ -141,7 +141,7 @@ struct Scratch {
   int32_t* rep;
   int32_t force_repair;    // test hook (MLP_TOT_FORCE_REPAIR): every pair goes to the repair list
   float* bnd5;             // chain boundary row, HMMs: a 32-byte record per column (5-state, local)
-  float* bndl;             // Viterbi sweep: 3 floats per column (component-major)
+  float* bndl;             // (unused: the Viterbi sweep writes the HMM records in bnd5)
   double* bndz;            // partition function: a 32-byte record per column (3 doubles, frame)
   int32_t* bnde;           // (unused)
   float* bndm;             // MEA boundary: 1 float per column
