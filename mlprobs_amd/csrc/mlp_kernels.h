@@ -227,6 +227,8 @@ hipError_t launch_fold_totals(const ModelScalars& ms, const Tables* tab, SeqSet 
 hipError_t launch_merge(int models, int pid, const ModelScalars& ms, SeqSet seqs, PairMeta pm,
                         ChainMeta cm, PairRec* rec, Scratch sc, int64_t nchains, int lds_seq,
                         hipStream_t st);
+// the pairs' sparse entry counts (PairRec::nnz) from the merge's row counts
+hipError_t launch_pair_nnz(SeqSet seqs, PairMeta pm, PairRec* rec, Scratch sc, int64_t npairs, hipStream_t st);
 hipError_t launch_viterbi(const ModelScalars& ms, const Tables* tab, SeqSet seqs, PairMeta pm,
                           ChainMeta cm, Scratch sc, VitOut vo, int64_t nchains, int lds_seq,
                           int64_t npairs, hipStream_t st);

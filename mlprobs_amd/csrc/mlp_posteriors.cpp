@@ -458,6 +458,7 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
     {
       Timer t(c, KMERGE, bcells, st);
       HIPCHK(c, launch_merge(models, pid, ms, seqs, pm, cm, d_rec, sc, nch, lds_seq, st));
+      HIPCHK(c, launch_pair_nnz(seqs, pm, d_rec, sc, np, st));
     }
     B.live = true;
     B.p = p;

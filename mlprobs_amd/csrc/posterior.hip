@@ -828,7 +828,7 @@ __global__ __launch_bounds__(256, NP && M == (kHmm5 | kLocal | kPF) ? 5 : MLP_ME
             if ((cnt & (KS - 1)) != 0 && cnt < kEll) ell_flush(cnt & ~(KS - 1));
             if (cnt > kEll) atomicOr(&rec[c.slot].flags, 2);
             sc.ell_cnt[c.ell + (i - 1)] = cnt;
-            atomicAdd(reinterpret_cast<unsigned long long*>(&rec[c.slot].nnz), (unsigned long long)cnt);
+            // (the pair's nnz: k_pair_nnz sums these counts after the merge)
             cnt = 0;
             if (i == L1) {
               rec[c.slot].mea = Cv;

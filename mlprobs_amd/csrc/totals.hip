@@ -513,6 +513,24 @@ __global__ __launch_bounds__(256) void k_local_btot(ModelScalars ms, const Table
 }
 
 // =====================================================================
+// Sparse entries per pair: the sum of its rows' counts (k_merge's ell_cnt,
+// overflowing rows included, as the per-row atomics it replaces summed):
+// one wave per pair, after the merge.
+// =====================================================================
+__global__ __launch_bounds__(256) void k_pair_nnz(SeqSet sq, PairMeta pm, PairRec* __restrict__ rec, Scratch sc,
+                                                  int64_t npairs) {
+  const int64_t p = wave_index();
+  if (p >= npairs) return;
+  const int lane = threadIdx.x & 63;
+  const int L1 = sq.len[pm.pa[p]];
+  const int32_t* __restrict__ cn = sc.ell_cnt + pm.ell_row[p];
+  long long s = 0;
+  for (int i = lane; i < L1; i += 64) s += cn[i];
+  for (int o = 32; o; o >>= 1) s += __shfl_xor(s, o);
+  if (lane == 0) rec[p].nnz = s;
+}
+
+// =====================================================================
 // ELL -> CSR compaction: one wave per pair.
 // =====================================================================
 __global__ __launch_bounds__(256) void k_compact(SeqSet sq, PairMeta pm, Scratch sc,
@@ -640,6 +658,12 @@ hipError_t launch_local_bwd_lanefold(const ModelScalars& ms, const Tables* tab, 
   if ((e = hipMemsetAsync(sc.tot_next, 0, sizeof(int32_t), st)) != hipSuccess) return e;
   hipLaunchKernelGGL(k_local_totals, wave_grid(std::min(nwaves, 1024)), dim3(64 * kWavesPerBlock), 0, st, ms, tab, seqs,
                      pm, cm, rec, sc, npairs, (const int32_t*)sc.rep, kTotFwd | kTotBwd);
+  return hipGetLastError();
+}
+
+hipError_t launch_pair_nnz(SeqSet seqs, PairMeta pm, PairRec* rec, Scratch sc, int64_t npairs, hipStream_t st) {
+  if (npairs <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_pair_nnz, wave_grid(npairs), dim3(64 * kWavesPerBlock), 0, st, seqs, pm, rec, sc, npairs);
   return hipGetLastError();
 }
 
