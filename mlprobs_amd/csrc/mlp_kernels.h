@@ -140,10 +140,8 @@ struct Scratch {
   float* crb;
   int32_t* rep;
   int32_t force_repair;    // test hook (MLP_TOT_FORCE_REPAIR): every pair goes to the repair list
-  float* bnd5;             // chain boundary row, HMMs: a 32-byte record per column (5-state, local)
-  float* bndl;             // (unused: the Viterbi sweep writes the HMM records in bnd5)
+  float* bnd5;             // chain boundary row, HMMs (and the Viterbi sweep): a 32-byte record per column (5-state, local)
   double* bndz;            // partition function: a 32-byte record per column (3 doubles, frame)
-  int32_t* bnde;           // (unused)
   float* bndm;             // MEA boundary: 1 float per column
   int32_t* bndc;           // MEA boundary #B counts (npdoAlign distance): 1 int per column
   uint16_t* ell_col;       // [ell row][kEll]

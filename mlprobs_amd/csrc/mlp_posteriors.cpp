@@ -254,7 +254,7 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
   // a batch's scratch layout (256-byte aligned sub-buffers) under front `fr`
   // (its region first, this batch's parity); returns the bytes
   struct BatchOffs {
-    size_t f5, fl, bl, pg, zm, cmf, cmb, tn, cl, crb, rep, lfc, b5, bnl, bz, be, bm, bc, ec, ev, en, entb, rpb, rec;
+    size_t f5, fl, bl, pg, zm, cmf, cmb, tn, cl, crb, rep, lfc, b5, bz, bm, bc, ec, ev, en, entb, rpb, rec;
     PlanDev pd;
   };
   auto carve = [&](const ChainPlan& P, const Front& fr, BatchOffs& o) -> size_t {
@@ -288,9 +288,7 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
     o.rep = cv.take(lanefold ? (np + 1) * 4 : 0);
     o.lfc = cv.take(lanefold && defer ? P.ell_rows * 4 : 0);  // (else the lane fold counts in ell_cnt)
     o.b5 = cv.take(P.bnd * 32);   // the HMMs' boundary records (mlp_chain.h, bnd_put_hmm)
-    o.bnl = 0;
     o.bz = cv.take(P.bnd * 32);   // the partition function's
-    o.be = 0;
     o.bm = cv.take(P.bnd * 4);
     o.bc = cv.take(P.bnd * 4);
     if (!defer) {
@@ -384,9 +382,7 @@ int mlp_posteriors(mlp_ctx* c, int pid, float delta, int64_t p0, int64_t p1) {
     static const bool force_repair = knob_set("MLP_TEST_TOT_FORCE_REPAIR");
     sc.force_repair = force_repair ? 1 : 0;
     sc.bnd5 = (float*)(base + o.b5);
-    sc.bndl = nullptr;   // (the Viterbi sweep's, mlp_profile_rt.cpp)
     sc.bndz = (double*)(base + o.bz);
-    sc.bnde = nullptr;
     sc.bndm = (float*)(base + o.bm);
     sc.bndc = (int32_t*)(base + o.bc);
     sc.ell_col = (uint16_t*)(base + o.ec);
